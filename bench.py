@@ -1,0 +1,222 @@
+"""Benchmark: edges/s of update_all g-SpMM (copy_u + sum, feat = 128).
+
+BASELINE.json metric: "edges/sec on update_all g-SpMM (copy_u+sum, feat=128)
+at 1/2/4/8 GPUs". Workload (config.workload):
+
+* N = 1: the Reddit-shaped graph of BASELINE.json configs[1] (232,965 nodes,
+  114,615,892 edges + self-loops, fp32 features of width 128), synthetic
+  (dgl.data.reddit_like) — the real dataset cannot be downloaded here. One
+  step = ``g.update_all(fn.copy_src('h','m'), fn.sum('m','h_out'))`` through
+  the DGLGraph API (scheduler -> cached CSR -> HIP g-SpMM), inputs resident in
+  HBM.
+* N > 1 (weak scaling): the same generator at N x the nodes and edges, dst
+  rows 1-D partitioned over the ranks (dgl.distributed.PartitionedGraph); one
+  step = RCCL all-gather of the node-feature halo + the local g-SpMM.
+
+Timing: W warm-up steps, then K steps bracketed by barrier + synchronize;
+the max over ranks is reported; value = all edges processed / that time.
+roofline: algorithmic bytes of one g-SpMM launch (SURVEY.md §8d:
+E*(4F+4) + R*(4F+8)) / the kernel's mean duration, measured with hipEvents
+recorded around every launch on its own stream inside the timed region.
+cpu_baseline: the reference's own CPU arithmetic (torch.sparse.mm on the
+uncoalesced COO, python/dgl/backend/pytorch/tensor.py:145-146) on a bounded
+sample of the same graph, rank 0 at N = 1 only.
+
+Run: python bench.py [--gpus N --steps K --warmup W]
+"""
+from __future__ import absolute_import
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "dgl-1_amd"))
+sys.path.insert(0, ROOT)
+
+import dgl  # noqa: E402
+import dgl.function as fn  # noqa: E402
+from dgl import data, kernel  # noqa: E402
+
+FEAT = 128
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def algorithmic_bytes(num_edges, num_rows, feat):
+    """Gather model: each edge reads one int32 column id and one fp32 source
+    row; each row reads its int64 indptr entry and writes one fp32 row."""
+    return num_edges * (4 * feat + 4) + num_rows * (4 * feat + 8)
+
+
+def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
+    """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on the
+    in-edges of the first rows of the graph (bounded sample)."""
+    threads = torch.get_num_threads()
+    torch.set_num_threads(1)  # torch's uncoalesced-COO CPU product is single-threaded
+    try:
+        deg = torch.bincount(dst, minlength=n)
+        cum = torch.cumsum(deg, 0)
+        rows = int(torch.searchsorted(cum, torch.tensor(target_edges))) + 1
+        rows = min(rows, n)
+        sel = dst < rows
+        s, d = src[sel], dst[sel]
+        e = int(s.numel())
+        A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, n))
+        reps, t_total = 0, 0.0
+        while reps < 2 and t_total < seconds_budget:
+            t0 = time.perf_counter()
+            torch.sparse.mm(A, h_cpu)
+            t_total += time.perf_counter() - t0
+            reps += 1
+        eps = e * reps / t_total
+        return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "reference",
+                "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
+                          "edge-id order) over the in-edges of the first %d rows: %d edges x "
+                          "F=%d, %d call(s), torch %s, 1 thread (host has %d cpus)"
+                          % (rows, e, h_cpu.shape[1], reps, torch.__version__,
+                             os.cpu_count() or 0)}
+    finally:
+        torch.set_num_threads(threads)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        dist.init_process_group("nccl", device_id=dev)
+
+    t0 = time.time()
+    src, dst, n = data.reddit_like(scale=world, seed=0, device=dev)
+    num_edges_total = int(src.numel())
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    log("rank %d: graph %d nodes %d edges generated in %.1fs" % (rank, n, num_edges_total,
+                                                                  time.time() - t0))
+
+    if world == 1:
+        g = dgl.DGLGraph((src.cpu(), dst.cpu()))
+        h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+        g.ndata["h"] = h
+        num_local_edges, num_rows = num_edges_total, n
+        t1 = time.time()
+        g.sparse_adjacency(dev)  # build + cache the device CSR (graph ingestion)
+        torch.cuda.synchronize()
+        log("device CSR built in %.1fs" % (time.time() - t1))
+
+        def step():
+            g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
+        parallelism = "single GPU"
+    else:
+        from dgl.distributed import PartitionedGraph, balanced_bounds
+        bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        sel = (dst >= lo) & (dst < hi)
+        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev)
+        h_full = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+        h_local = h_full[lo:hi].contiguous()
+        del h_full, sel
+        num_local_edges, num_rows = pg.num_edges, pg.num_local
+
+        def step():
+            pg.update_all(h_local)
+        parallelism = "%d-way 1-D dst-row partition, RCCL all-gather halo" % world
+    del src, dst
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernel.timing_enable(True)
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kms, launches = kernel.timing_read()
+    kernel.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    value = num_edges_total * args.steps / elapsed
+    kernel_ms = kms / max(launches, 1)
+    bytes_per_launch = algorithmic_bytes(num_local_edges, num_rows, FEAT)
+    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    result = {
+        "metric": "edges/sec on update_all g-SpMM (copy_u+sum, feat=128)",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (seeded Chung-Lu power-law graph of Reddit's shape; random "
+                "U(-1,1) features)",
+        "config": {
+            "workload": "reddit-shaped x%d: %d nodes, %d edges (incl. self-loops), feat=%d"
+                        % (world, n, num_edges_total, FEAT),
+            "global_batch": n,
+            "feat": FEAT,
+            "parallelism": parallelism,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "gspmm_sum_kernel<copy_u> (rank 0)",
+            "kernel_ms": kernel_ms,
+            "bytes_per_launch": bytes_per_launch,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t2 = time.time()
+        gsrc, gdst = g._graph.src(), g._graph.dst()
+        result["cpu_baseline"] = cpu_baseline(gsrc, gdst, n, g.ndata["h"].cpu(),
+                                              args.cpu_sample_edges)
+        log("cpu baseline took %.1fs" % (time.time() - t2))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

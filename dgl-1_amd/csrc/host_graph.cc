@@ -1,0 +1,256 @@
+// Host-side graph ingestion and the CPU device of the engine.
+//
+//  * COO -> CSR with the slot order the reference's sparse product consumes
+//    (replaces Graph::GetAdj, src/graph/graph.cc:506-554, and the CSR built by
+//    ImmutableGraph, src/graph/immutable_graph.cc:206-237).
+//  * degree-descending launch schedule.
+//  * g-SpMM / g-SDDMM on host memory (same numerics contract as the HIP
+//    kernels; this is the CPU device, not the test oracle in oracle/).
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <limits>
+#include <mutex>
+#include <numeric>
+
+#include "../../include/dgl_hip.h"
+#include "common.h"
+
+namespace dglhip {
+
+static thread_local std::string g_last_error;
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+
+int default_num_threads() {
+  for (const char* var : {"DGL_NUM_THREADS", "OMP_NUM_THREADS"}) {
+    if (const char* s = std::getenv(var)) {
+      int v = std::atoi(s);
+      if (v > 0) return std::min(v, 64);
+    }
+  }
+  unsigned hc = std::thread::hardware_concurrency();
+  return static_cast<int>(std::max(1u, std::min(hc, 64u)));
+}
+
+// Stable counting sort of edges by row. Parallel version: rows are split into
+// contiguous ranges of roughly equal nnz; each thread scans the edge list in
+// edge-id order and places only the edges of its own row range, so slot order
+// inside each row is ascending edge id regardless of thread count.
+static void csr_by_eid(int64_t num_rows, int64_t nnz, const int64_t* row,
+                       const int64_t* col, int64_t* indptr, int32_t* indices,
+                       int64_t* eid, int nthreads) {
+  std::vector<int64_t> deg(num_rows + 1, 0);
+  for (int64_t e = 0; e < nnz; ++e) deg[row[e]]++;
+  indptr[0] = 0;
+  for (int64_t r = 0; r < num_rows; ++r) indptr[r + 1] = indptr[r] + deg[r];
+  if (nnz == 0) return;
+  if (nthreads > 1 && nnz >= (int64_t(1) << 20)) {
+    // row-range boundaries balanced by nnz
+    std::vector<int64_t> bounds(nthreads + 1, num_rows);
+    bounds[0] = 0;
+    for (int t = 1; t < nthreads; ++t) {
+      const int64_t target = nnz * t / nthreads;
+      bounds[t] = std::upper_bound(indptr, indptr + num_rows + 1, target) -
+                  indptr - 1;
+      bounds[t] = std::max(bounds[t], bounds[t - 1]);
+    }
+    parallel_for(nthreads, nthreads, [&](int64_t b, int64_t e, int) {
+      for (int64_t t = b; t < e; ++t) {
+        const int64_t r0 = bounds[t], r1 = bounds[t + 1];
+        if (r0 >= r1) continue;
+        std::vector<int64_t> cursor(indptr + r0, indptr + r1);
+        for (int64_t i = 0; i < nnz; ++i) {
+          const int64_t r = row[i];
+          if (r < r0 || r >= r1) continue;
+          const int64_t p = cursor[r - r0]++;
+          indices[p] = static_cast<int32_t>(col[i]);
+          eid[p] = i;
+        }
+      }
+    });
+  } else {
+    std::vector<int64_t> cursor(indptr, indptr + num_rows);
+    for (int64_t i = 0; i < nnz; ++i) {
+      const int64_t p = cursor[row[i]]++;
+      indices[p] = static_cast<int32_t>(col[i]);
+      eid[p] = i;
+    }
+  }
+}
+
+}  // namespace dglhip
+
+using namespace dglhip;
+
+extern "C" {
+
+const char* DGLGetLastError(void) { return g_last_error.c_str(); }
+void DGLAPISetLastError(const char* msg) { g_last_error = msg ? msg : ""; }
+int dglhip_abi_version(void) { return DGLHIP_ABI_VERSION; }
+const char* dglhip_build_info(void) {
+  return "libdgl_hip abi=1 target=gfx950 built " __DATE__ " " __TIME__;
+}
+
+int dglhip_coo_to_csr_host(int64_t num_rows, int64_t num_cols, int64_t nnz,
+                           const int64_t* row, const int64_t* col, int order,
+                           int64_t* indptr, int32_t* indices, int64_t* eid) {
+  API_BEGIN();
+  DGLHIP_CHECK(num_rows >= 0 && num_cols >= 0 && nnz >= 0, "negative size");
+  DGLHIP_CHECK(num_cols <= std::numeric_limits<int32_t>::max(),
+               "num_cols " << num_cols << " exceeds int32 column ids");
+  DGLHIP_CHECK(order == DGLHIP_ORDER_EID || order == DGLHIP_ORDER_COL,
+               "unknown order " << order);
+  DGLHIP_CHECK(indptr != nullptr, "indptr is null");
+  DGLHIP_CHECK(nnz == 0 || (row && col && indices && eid), "null array");
+  for (int64_t e = 0; e < nnz; ++e) {
+    DGLHIP_CHECK(row[e] >= 0 && row[e] < num_rows,
+                 "row id " << row[e] << " of edge " << e << " out of range [0,"
+                           << num_rows << ")");
+    DGLHIP_CHECK(col[e] >= 0 && col[e] < num_cols,
+                 "col id " << col[e] << " of edge " << e << " out of range [0,"
+                           << num_cols << ")");
+  }
+  const int nthreads = default_num_threads();
+  csr_by_eid(num_rows, nnz, row, col, indptr, indices, eid, nthreads);
+  if (order == DGLHIP_ORDER_COL) {
+    parallel_for(num_rows, nthreads, [&](int64_t b, int64_t e, int) {
+      std::vector<std::pair<int32_t, int64_t>> tmp;
+      for (int64_t r = b; r < e; ++r) {
+        const int64_t s = indptr[r], t = indptr[r + 1];
+        if (t - s < 2) continue;
+        tmp.resize(t - s);
+        for (int64_t k = s; k < t; ++k) tmp[k - s] = {indices[k], eid[k]};
+        std::sort(tmp.begin(), tmp.end());  // (col, eid) lexicographic
+        for (int64_t k = s; k < t; ++k) {
+          indices[k] = tmp[k - s].first;
+          eid[k] = tmp[k - s].second;
+        }
+      }
+    });
+  }
+  API_END();
+}
+
+int dglhip_rows_by_degree_host(int64_t num_rows, const int64_t* indptr,
+                               int32_t* row_order) {
+  API_BEGIN();
+  DGLHIP_CHECK(num_rows >= 0 && num_rows <= std::numeric_limits<int32_t>::max(),
+               "num_rows out of int32 range");
+  if (num_rows == 0) return 0;
+  int64_t maxdeg = 0;
+  for (int64_t r = 0; r < num_rows; ++r)
+    maxdeg = std::max(maxdeg, indptr[r + 1] - indptr[r]);
+  if (maxdeg > 8 * num_rows + 1024) {
+    // very skewed: comparison sort is cheaper than a huge histogram
+    std::iota(row_order, row_order + num_rows, 0);
+    std::stable_sort(row_order, row_order + num_rows, [&](int32_t a, int32_t b) {
+      return indptr[a + 1] - indptr[a] > indptr[b + 1] - indptr[b];
+    });
+    return 0;
+  }
+  // counting sort on degree, descending, stable in row id
+  std::vector<int64_t> cnt(maxdeg + 2, 0);
+  for (int64_t r = 0; r < num_rows; ++r) cnt[maxdeg - (indptr[r + 1] - indptr[r])]++;
+  int64_t acc = 0;
+  for (auto& c : cnt) {
+    const int64_t v = c;
+    c = acc;
+    acc += v;
+  }
+  for (int64_t r = 0; r < num_rows; ++r)
+    row_order[cnt[maxdeg - (indptr[r + 1] - indptr[r])]++] = static_cast<int32_t>(r);
+  API_END();
+}
+
+// ---------------------------------------------------------------------------
+// CPU device: g-SpMM / g-SDDMM on host memory.
+// ---------------------------------------------------------------------------
+
+int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
+                      int64_t feat_len, const int64_t* indptr,
+                      const int32_t* indices, const int64_t* eid,
+                      const float* ufeat, const float* efeat,
+                      int64_t efeat_len, float* out, int64_t* arg_out,
+                      int num_threads) {
+  API_BEGIN();
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 2, "unknown reduce op " << reduce_op);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
+  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
+  DGLHIP_CHECK(!use_e || (efeat && (efeat_len == 1 || efeat_len == feat_len)),
+               "edge feature must have length 1 or feat_len, got " << efeat_len);
+  DGLHIP_CHECK(!use_e || eid, "eid is null");
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  const int64_t F = feat_len;
+  parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
+    for (int64_t r = b; r < e; ++r) {
+      float* o = out + r * F;
+      const int64_t s = indptr[r], t = indptr[r + 1];
+      if (reduce_op == DGLHIP_REDUCE_MAX) {
+        for (int64_t f = 0; f < F; ++f) {
+          float best = -std::numeric_limits<float>::infinity();
+          int64_t arg = -1;
+          for (int64_t k = s; k < t; ++k) {
+            float x;
+            const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+            if (msg_op == DGLHIP_MSG_COPY_U) x = ufeat[int64_t(indices[k]) * F + f];
+            else if (msg_op == DGLHIP_MSG_COPY_E) x = er[efeat_len == 1 ? 0 : f];
+            else x = ufeat[int64_t(indices[k]) * F + f] * er[efeat_len == 1 ? 0 : f];
+            if (arg < 0 || x > best) { best = x; arg = k; }
+          }
+          o[f] = arg < 0 ? 0.0f : best;
+          if (arg_out) arg_out[r * F + f] = arg;
+        }
+        continue;
+      }
+      for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
+      for (int64_t k = s; k < t; ++k) {
+        const float* ur = use_u ? ufeat + int64_t(indices[k]) * F : nullptr;
+        const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+        if (msg_op == DGLHIP_MSG_COPY_U) {
+          for (int64_t f = 0; f < F; ++f) o[f] += ur[f];
+        } else if (msg_op == DGLHIP_MSG_COPY_E) {
+          for (int64_t f = 0; f < F; ++f) o[f] += er[efeat_len == 1 ? 0 : f];
+        } else if (efeat_len == 1) {
+          const float w = er[0];
+          for (int64_t f = 0; f < F; ++f) o[f] = std::fma(w, ur[f], o[f]);
+        } else {
+          for (int64_t f = 0; f < F; ++f) o[f] = std::fma(er[f], ur[f], o[f]);
+        }
+      }
+      if (reduce_op == DGLHIP_REDUCE_MEAN && t - s > 1) {
+        const float inv = static_cast<float>(t - s);
+        for (int64_t f = 0; f < F; ++f) o[f] = o[f] / inv;
+      }
+    }
+  });
+  API_END();
+}
+
+int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
+                       const int64_t* indptr, const int32_t* indices,
+                       const int64_t* eid, const float* lhs, const float* rhs,
+                       float* out, int num_threads) {
+  API_BEGIN();
+  DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  const int64_t F = feat_len;
+  parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
+    for (int64_t r = b; r < e; ++r) {
+      const float* a = lhs + r * F;
+      for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
+        const float* c = rhs + int64_t(indices[k]) * F;
+        float acc = 0.0f;
+        for (int64_t f = 0; f < F; ++f) acc = std::fma(a[f], c[f], acc);
+        out[eid[k]] = acc;
+      }
+    }
+  });
+  API_END();
+}
+
+}  // extern "C"

@@ -1,0 +1,196 @@
+"""ctypes binding of libdgl_hip.so (the engine's C-ABI, include/dgl_hip.h).
+
+Mirrors the reference's FFI layer (python/dgl/_ffi/base.py:31-62): the shared
+library is located (``DGL_LIBRARY_PATH`` first, then the in-tree build), loaded
+once, and every call goes through :func:`check_call`, which turns a -1 return
+into ``DGLError(DGLGetLastError())``.
+
+There is no fallback: if the library cannot be loaded every kernel entry
+point raises. Build it with ``make -C dgl-1_amd/csrc`` (or
+``__graft_entry__.build()``).
+"""
+from __future__ import absolute_import
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the HIP runtime torch links against first)
+
+from .base import DGLError
+
+__all__ = ["LIB", "check_call", "lib_path", "tensor_arg", "call_packed", "list_global_names"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBNAME = "libdgl_hip.so"
+
+
+def lib_path():
+    """Candidate location of libdgl_hip.so (python/dgl/_ffi/libinfo.py:7-60)."""
+    cands = []
+    env = os.environ.get("DGL_LIBRARY_PATH")
+    if env:
+        for d in env.split(os.pathsep):
+            cands.append(os.path.join(d, _LIBNAME) if os.path.isdir(d) else d)
+    cands.append(os.path.join(os.path.dirname(_HERE), "lib", _LIBNAME))
+    for c in cands:
+        if os.path.isfile(c):
+            return c
+    raise DGLError("cannot find %s (looked in %s); build it with "
+                   "`make -C dgl-1_amd/csrc`" % (_LIBNAME, ", ".join(cands)))
+
+
+_c_i64 = ctypes.c_int64
+_c_int = ctypes.c_int
+_vp = ctypes.c_void_p
+
+
+def _load():
+    lib = ctypes.CDLL(lib_path(), mode=ctypes.RTLD_GLOBAL)
+    sig = {
+        "DGLGetLastError": (ctypes.c_char_p, []),
+        "dglhip_abi_version": (_c_int, []),
+        "dglhip_build_info": (ctypes.c_char_p, []),
+        "dglhip_coo_to_csr_host": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp, _vp]),
+        "dglhip_rows_by_degree_host": (_c_int, [_c_i64, _vp, _vp]),
+        "dglhip_coo_to_csr_workspace_bytes": (_c_i64, [_c_i64, _c_i64, _c_i64, _c_int]),
+        "dglhip_coo_to_csr_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
+                                              _vp, _vp, _c_i64, _vp]),
+        "dglhip_gspmm_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                         _c_i64, _vp, _vp, _vp, _vp]),
+        "dglhip_gspmm_host": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                       _c_i64, _vp, _vp, _c_int]),
+        "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "dglhip_gsddmm_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_int]),
+        "dglhip_timing_enable": (_c_int, [_c_int]),
+        "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),
+        "DGLFuncGetGlobal": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+        "DGLFuncListGlobalNames": (_c_int, [ctypes.POINTER(_c_int),
+                                            ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))]),
+        "DGLFuncCall": (_c_int, [_vp, _vp, ctypes.POINTER(_c_int), _c_int, _vp, ctypes.POINTER(_c_int)]),
+        "DGLFuncFree": (_c_int, [_vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+class _LazyLib(object):
+    """Loads the library on first use so that `import dgl` works for docs/tests
+    of pure-host logic; any kernel call without the library raises."""
+
+    def __init__(self):
+        self._lib = None
+        self._err = None
+
+    def _get(self):
+        if self._lib is None:
+            if self._err is not None:
+                raise DGLError(self._err)
+            try:
+                self._lib = _load()
+            except (OSError, DGLError) as err:  # pragma: no cover - depends on build
+                self._err = "libdgl_hip.so unavailable: %s" % err
+                raise DGLError(self._err)
+        return self._lib
+
+    def __getattr__(self, name):
+        return getattr(self._get(), name)
+
+    @property
+    def loaded(self):
+        try:
+            self._get()
+            return True
+        except DGLError:
+            return False
+
+
+LIB = _LazyLib()
+
+
+def check_call(ret):
+    """Raise DGLError with the library's last error if ``ret`` != 0."""
+    if ret != 0:
+        raise DGLError(LIB.DGLGetLastError().decode("utf-8", "replace"))
+
+
+def ptr(t):
+    """Raw data pointer of a tensor (None for None)."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+# --------------------------------------------------------------------------
+# PackedFunc calling convention (include/dgl_hip.h, csrc/registry.cc)
+# --------------------------------------------------------------------------
+_TC_INT, _TC_HANDLE, _TC_NULL, _TC_ARRAY = 0, 3, 4, 7
+
+
+class _DGLHipTensor(ctypes.Structure):
+    _fields_ = [("data", _vp), ("device_type", ctypes.c_int32), ("device_id", ctypes.c_int32),
+                ("ndim", ctypes.c_int32), ("dtype_code", ctypes.c_uint8),
+                ("dtype_bits", ctypes.c_uint8), ("dtype_lanes", ctypes.c_uint16),
+                ("shape", ctypes.POINTER(_c_i64)), ("strides", ctypes.POINTER(_c_i64)),
+                ("byte_offset", ctypes.c_uint64)]
+
+
+class _DGLHipValue(ctypes.Union):
+    _fields_ = [("v_int64", _c_i64), ("v_float64", ctypes.c_double), ("v_handle", _vp),
+                ("v_str", ctypes.c_char_p)]
+
+
+_DTYPE_CODE = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32)}
+
+
+def tensor_arg(t):
+    """Wrap a torch tensor as a non-owning DGLHipTensor (src/c_api_common.cc:16-23)."""
+    code, bits = _DTYPE_CODE[t.dtype]
+    shape = (_c_i64 * t.dim())(*t.shape)
+    strides = (_c_i64 * t.dim())(*t.stride())
+    dev = 10 if t.is_cuda else 1
+    st = _DGLHipTensor(t.data_ptr(), dev, t.device.index or 0, t.dim(), code, bits, 1,
+                       shape, strides, 0)
+    st._keep = (shape, strides, t)  # keep alive for the duration of the call
+    return st
+
+
+def list_global_names():
+    """Names registered in the engine's PackedFunc table."""
+    n = _c_int()
+    arr = ctypes.POINTER(ctypes.c_char_p)()
+    check_call(LIB.DGLFuncListGlobalNames(ctypes.byref(n), ctypes.byref(arr)))
+    return [arr[i].decode() for i in range(n.value)]
+
+
+def call_packed(name, *args):
+    """Call a registered function by name with ints, tensors, None or
+    ``("handle", int)`` stream handles — the DGLFuncCall convention."""
+    h = _vp()
+    check_call(LIB.DGLFuncGetGlobal(name.encode(), ctypes.byref(h)))
+    if not h.value:
+        raise DGLError("global function %s is not registered" % name)
+    n = len(args)
+    vals = (_DGLHipValue * max(n, 1))()
+    codes = (_c_int * max(n, 1))()
+    keep = []
+    for i, a in enumerate(args):
+        if a is None:
+            codes[i] = _TC_NULL
+        elif isinstance(a, torch.Tensor):
+            st = tensor_arg(a)
+            keep.append(st)
+            vals[i].v_handle = ctypes.cast(ctypes.pointer(st), _vp)
+            codes[i] = _TC_ARRAY
+        elif isinstance(a, tuple) and a[0] == "handle":
+            vals[i].v_handle = a[1]
+            codes[i] = _TC_HANDLE
+        else:
+            vals[i].v_int64 = int(a)
+            codes[i] = _TC_INT
+    ret = _DGLHipValue()
+    rc = _c_int()
+    check_call(LIB.DGLFuncCall(h, ctypes.cast(vals, _vp), codes, n,
+                               ctypes.cast(ctypes.pointer(ret), _vp), ctypes.byref(rc)))

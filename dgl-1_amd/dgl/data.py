@@ -1,0 +1,132 @@
+"""Synthetic graph generators (offline stand-ins for the reference's datasets).
+
+The reference downloads Cora / Pubmed / Reddit / FB15k from S3
+(python/dgl/data/utils.py:18-27, data/__init__.py:15-25); nothing can be
+fetched here, so benchmarks use seeded synthetic graphs of the same shape
+(SURVEY.md §8d):
+
+* ``reddit_like``: Chung-Lu power-law graph with Reddit's node count,
+  directed edge count (114,615,892, both directions of each undirected pair),
+  mean degree ~492 and max/mean degree ratio ~44 (Reddit's max degree is
+  21,657), symmetric, no duplicates, node ids permuted; GCN self-loops added
+  (examples/pytorch/gcn/gcn_spmv.py:136).
+* ``rmat``: Graph500 R-MAT edges (a, b, c, d) = (0.57, 0.19, 0.19, 0.05),
+  directed, duplicates kept (multigraph), ids permuted.
+
+Generation runs on whatever device is given (torch RNG seeded per call), so a
+1-GPU box builds the 115M-edge graph in seconds. Edge ids are assigned in
+(src, dst) order.
+"""
+from __future__ import absolute_import
+
+import torch
+
+__all__ = ["reddit_like", "chung_lu", "rmat", "REDDIT_NODES", "REDDIT_EDGES"]
+
+REDDIT_NODES = 232965
+REDDIT_EDGES = 114615892
+REDDIT_MAX_OVER_MEAN = 21657.0 / (REDDIT_EDGES / REDDIT_NODES)
+
+
+def _powerlaw_alpha(n, ratio):
+    """alpha with w_i = (i+1)^-alpha and max(w)/mean(w) == ratio (bisection)."""
+    lo, hi = 0.0, 1.5
+    idx = torch.arange(1, n + 1, dtype=torch.float64)
+    for _ in range(60):
+        a = 0.5 * (lo + hi)
+        r = 1.0 / (idx.pow(-a).mean().item())
+        if r < ratio:
+            lo = a
+        else:
+            hi = a
+    return 0.5 * (lo + hi)
+
+
+def reddit_like(scale=1, seed=0, device="cpu", self_loops=True):
+    """(src, dst, num_nodes) int64 tensors on ``device``.
+
+    ``scale`` multiplies nodes and edges (weak-scaling family: scale = number
+    of GPUs); scale=1 is the Reddit-shaped graph of BASELINE.json configs[1].
+    """
+    return chung_lu(REDDIT_NODES * scale, REDDIT_EDGES * scale, REDDIT_MAX_OVER_MEAN,
+                    seed, device, self_loops)
+
+
+def chung_lu(n, num_edges, max_over_mean, seed=0, device="cpu", self_loops=True):
+    """Symmetric power-law graph with ``num_edges`` directed edges (pairs in
+    both directions, no duplicates or self-loops) plus optional self-loops."""
+    device = torch.device(device)
+    target_pairs = num_edges // 2
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    alpha = _powerlaw_alpha(n, max_over_mean)
+    w = torch.arange(1, n + 1, device=device, dtype=torch.float64).pow(-alpha)
+    perm = torch.randperm(n, generator=gen, device=device)
+    weights = torch.empty_like(w)
+    weights[perm] = w
+    cdf = torch.cumsum(weights, 0)
+    cdf = (cdf / cdf[-1]).to(torch.float64)
+    keys = torch.empty(0, dtype=torch.int64, device=device)
+    need = target_pairs
+    for _ in range(8):
+        m = int(need * 1.08) + 1024
+        a = torch.searchsorted(cdf, torch.rand(m, generator=gen, device=device,
+                                               dtype=torch.float64)).clamp_(max=n - 1)
+        b = torch.searchsorted(cdf, torch.rand(m, generator=gen, device=device,
+                                               dtype=torch.float64)).clamp_(max=n - 1)
+        keep = a != b
+        lo_, hi_ = torch.minimum(a[keep], b[keep]), torch.maximum(a[keep], b[keep])
+        keys = torch.unique(torch.cat([keys, lo_ * n + hi_]))
+        del a, b, keep, lo_, hi_
+        if keys.numel() >= target_pairs:
+            break
+        need = target_pairs - keys.numel()
+    if keys.numel() > target_pairs:
+        pick = torch.randperm(keys.numel(), generator=gen, device=device)[:target_pairs]
+        keys = torch.sort(keys[pick])[0]
+    u, v = keys // n, keys % n
+    del keys
+    src = torch.cat([u, v])
+    dst = torch.cat([v, u])
+    del u, v
+    if self_loops:
+        ar = torch.arange(n, device=device)
+        src = torch.cat([src, ar])
+        dst = torch.cat([dst, ar])
+    order = torch.argsort(src * n + dst)
+    return src[order].contiguous(), dst[order].contiguous(), n
+
+
+def rmat(scale, edge_factor=16, seed=0, device="cpu", abcd=(0.57, 0.19, 0.19, 0.05),
+         chunk=1 << 26):
+    """Graph500 R-MAT: (src, dst, num_nodes); 2^scale nodes, edge_factor*2^scale edges."""
+    device = torch.device(device)
+    n = 1 << scale
+    m = edge_factor * n
+    a, b, c, _ = abcd
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    srcs, dsts = [], []
+    for start in range(0, m, chunk):
+        k = min(chunk, m - start)
+        s = torch.zeros(k, dtype=torch.int64, device=device)
+        d = torch.zeros(k, dtype=torch.int64, device=device)
+        for bit in range(scale):
+            r = torch.rand(k, generator=gen, device=device)
+            sbit = (r >= a + b).to(torch.int64)           # quadrants c, d
+            dbit = (((r >= a) & (r < a + b)) | (r >= a + b + c)).to(torch.int64)  # b, d
+            s |= sbit << bit
+            d |= dbit << bit
+        srcs.append(s)
+        dsts.append(d)
+    src, dst = torch.cat(srcs), torch.cat(dsts)
+    perm = torch.randperm(n, generator=gen, device=device)
+    src, dst = perm[src], perm[dst]
+    order = torch.argsort(src * n + dst)
+    return src[order].contiguous(), dst[order].contiguous(), n
+
+
+def expected_reddit_edges(scale=1, self_loops=True):
+    """Edge count reddit_like produces (exact by construction)."""
+    return (REDDIT_EDGES * scale) // 2 * 2 + (REDDIT_NODES * scale if self_loops else 0)
+

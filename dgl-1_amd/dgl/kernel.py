@@ -1,0 +1,387 @@
+"""Sparse adjacency objects and the g-SpMM / g-SDDMM operators.
+
+This module is the engine's replacement for what the reference delegates to
+the tensor framework:
+
+* ``F.sparse_matrix`` + ``F.spmm`` = ``torch.sparse_coo_tensor`` +
+  ``torch.sparse.mm`` (python/dgl/backend/pytorch/tensor.py:45-51,145-146),
+  driven by SPMVExecutor / SPMVWithDataExecutor
+  (python/dgl/runtime/ir/executor.py:452-473,535-566);
+* the adjacency index built by ``Graph::GetAdj`` (src/graph/graph.cc:506-554)
+  and copied to the device on first use (python/dgl/graph_index.py:575-579).
+
+A :class:`SparseAdj` holds a destination-major CSR (rows = reduce targets)
+plus, built lazily, the source-major CSR of the transpose used by the
+backward. Slot order within a row is the order in which torch's CPU sparse
+product consumes the reference's uncoalesced COO (edge-id order for mutable
+graphs), so the HIP kernels reproduce the reference's results bit for bit.
+
+Every compute call goes to libdgl_hip.so (HIP kernels for tensors on a ROCm
+device, the library's host kernels for CPU tensors). There is no other path.
+"""
+from __future__ import absolute_import
+
+import ctypes
+
+import torch
+
+from . import _ffi
+from ._ffi import LIB, check_call, ptr
+from .base import DGLError
+
+__all__ = ["CSR", "SparseAdj", "build_csr", "gspmm", "gsddmm_dot",
+           "MSG_COPY_U", "MSG_U_MUL_E", "MSG_COPY_E", "RED_SUM", "RED_MAX", "RED_MEAN"]
+
+MSG_COPY_U, MSG_U_MUL_E, MSG_COPY_E = 0, 1, 2
+RED_SUM, RED_MAX, RED_MEAN = 0, 1, 2
+ORDER_EID, ORDER_COL = 0, 1
+
+_MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_U_MUL_E,
+              "u_mul_e": MSG_U_MUL_E, "copy_edge": MSG_COPY_E, "copy_e": MSG_COPY_E}
+_RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
+
+
+def _stream_of(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class CSR(object):
+    """CSR matrix: indptr int64[R+1], indices int32[nnz], eid int64[nnz].
+
+    ``row_order`` (int32[R], optional) is the degree-descending launch
+    schedule handed to the HIP kernel.
+    """
+
+    def __init__(self, indptr, indices, eid, num_cols, row_order=None):
+        self.indptr = indptr
+        self.indices = indices
+        self.eid = eid
+        self.num_rows = indptr.numel() - 1
+        self.num_cols = int(num_cols)
+        self.row_order = row_order
+        self._row_ids = None
+
+    @property
+    def nnz(self):
+        return self.indices.numel()
+
+    @property
+    def device(self):
+        return self.indptr.device
+
+    def to(self, device):
+        if self.device == torch.device(device):
+            return self
+        ro = None if self.row_order is None else self.row_order.to(device)
+        return CSR(self.indptr.to(device), self.indices.to(device), self.eid.to(device),
+                   self.num_cols, ro)
+
+    def degrees(self):
+        return self.indptr[1:] - self.indptr[:-1]
+
+    def row_ids(self):
+        """Row id of every slot (COO expansion), cached."""
+        if self._row_ids is None:
+            self._row_ids = torch.repeat_interleave(
+                torch.arange(self.num_rows, device=self.device), self.degrees())
+        return self._row_ids
+
+
+def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedule=True):
+    """Build a CSR over ``num_rows`` rows from COO (row[e], col[e]).
+
+    Slot k of row r holds ``col`` of the k-th edge of r in ``order``; its
+    ``eid`` is that edge's position in the input arrays. On a ROCm device the
+    build runs on the GPU (stable radix sort), on CPU in the library's host
+    builder; both produce identical arrays.
+    """
+    row = torch.as_tensor(row, dtype=torch.int64)
+    col = torch.as_tensor(col, dtype=torch.int64)
+    nnz = row.numel()
+    if col.numel() != nnz:
+        raise DGLError("row/col length mismatch: %d vs %d" % (nnz, col.numel()))
+    device = torch.device(device) if device is not None else row.device
+    if device.type == "cuda":
+        row = row.to(device).contiguous()
+        col = col.to(device).contiguous()
+        if nnz:
+            lo = torch.stack([row.min(), col.min()]).min().item()
+            if lo < 0 or row.max().item() >= num_rows or col.max().item() >= num_cols:
+                raise DGLError("edge endpoints out of range for a %dx%d matrix"
+                               % (num_rows, num_cols))
+        indptr = torch.empty(num_rows + 1, dtype=torch.int64, device=device)
+        indices = torch.empty(nnz, dtype=torch.int32, device=device)
+        eid = torch.empty(nnz, dtype=torch.int64, device=device)
+        ws_bytes = LIB.dglhip_coo_to_csr_workspace_bytes(num_rows, num_cols, nnz, order)
+        if ws_bytes < 0:
+            check_call(-1)
+        ws = torch.empty(max(int(ws_bytes), 1), dtype=torch.uint8, device=device)
+        check_call(LIB.dglhip_coo_to_csr_device(
+            num_rows, num_cols, nnz, ptr(row), ptr(col), order, ptr(indptr), ptr(indices),
+            ptr(eid), ptr(ws), int(ws_bytes), _stream_of(device)))
+        del ws
+        host_indptr = indptr.cpu() if schedule else None
+    else:
+        row = row.cpu().contiguous()
+        col = col.cpu().contiguous()
+        indptr = torch.empty(num_rows + 1, dtype=torch.int64)
+        indices = torch.empty(nnz, dtype=torch.int32)
+        eid = torch.empty(nnz, dtype=torch.int64)
+        check_call(LIB.dglhip_coo_to_csr_host(num_rows, num_cols, nnz, ptr(row), ptr(col),
+                                              order, ptr(indptr), ptr(indices), ptr(eid)))
+        host_indptr = indptr if schedule else None
+    row_order = None
+    if schedule and num_rows > 0:
+        ro = torch.empty(num_rows, dtype=torch.int32)
+        check_call(LIB.dglhip_rows_by_degree_host(num_rows, ptr(host_indptr), ptr(ro)))
+        row_order = ro.to(device)
+    return CSR(indptr, indices, eid, num_cols, row_order)
+
+
+class SparseAdj(object):
+    """A (num_rows x num_cols) sparse matrix for message passing.
+
+    ``fwd`` is the row-major (destination) CSR; ``bwd`` is the transpose
+    (source-major) CSR, built on first use by ``transpose_builder``.
+    ``edge_map`` (optional int64[nnz]) maps the matrix's edge slots
+    (``eid`` values) to positions of the edge-feature tensor; None = identity.
+    Per-device copies are cached.
+    """
+
+    def __init__(self, fwd, transpose_builder, shape):
+        self.fwd = fwd
+        self._tb = transpose_builder
+        self._bwd = None
+        self.shape = tuple(int(s) for s in shape)
+        self._dev = {}
+
+    @property
+    def bwd(self):
+        if self._bwd is None:
+            self._bwd = self._tb(self.fwd.device)
+        return self._bwd
+
+    def to(self, device):
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if self.fwd.device == device:
+            return self
+        key = str(device)
+        if key not in self._dev:
+            other = SparseAdj(self.fwd.to(device), self._tb, self.shape)
+            if self._bwd is not None:
+                other._bwd = self._bwd.to(device)
+            self._dev[key] = other
+        return self._dev[key]
+
+
+def from_coo(num_rows, num_cols, row, col, order=ORDER_EID, device=None):
+    """SparseAdj whose forward CSR groups (row, col) by row and whose backward
+    CSR groups the same edges by col, both in ``order``."""
+    row = torch.as_tensor(row, dtype=torch.int64)
+    col = torch.as_tensor(col, dtype=torch.int64)
+    fwd = build_csr(num_rows, num_cols, row, col, order, device)
+
+    def tb(dev):
+        return build_csr(num_cols, num_rows, col, row, order, dev)
+
+    return SparseAdj(fwd, tb, (num_rows, num_cols))
+
+
+# ---------------------------------------------------------------------------
+# Raw kernel calls
+# ---------------------------------------------------------------------------
+def _efeat_len(efeat, num_edges_hint, feat_len):
+    if efeat is None:
+        return 0
+    per_edge = efeat.numel() // max(efeat.shape[0], 1) if efeat.dim() > 0 else 1
+    if per_edge != 1 and per_edge != feat_len:
+        raise DGLError("edge feature of %d values per edge cannot combine with node feature "
+                       "of %d values" % (per_edge, feat_len))
+    return per_edge
+
+
+def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
+    """ufeat2: (num_cols, F) or None; efeat2: (E, elen) or None. Returns (out, arg)."""
+    dev = (ufeat2 if ufeat2 is not None else efeat2).device
+    if csr.device != dev:
+        raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
+    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
+    arg = None
+    if red == RED_MAX and want_arg:
+        arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
+    if dev.type == "cuda":
+        check_call(LIB.dglhip_gspmm_device(
+            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
+            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
+            _stream_of(dev)))
+    else:
+        check_call(LIB.dglhip_gspmm_host(
+            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
+            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), 0))
+    return out, arg
+
+
+def _run_sddmm_dot(csr, lhs2, rhs2, num_edges):
+    dev = lhs2.device
+    out = torch.zeros(num_edges, dtype=torch.float32, device=dev)
+    F = lhs2.shape[1]
+    if dev.type == "cuda":
+        check_call(LIB.dglhip_gsddmm_device(0, csr.num_rows, F, ptr(csr.indptr), ptr(csr.indices),
+                                            ptr(csr.eid), ptr(lhs2), ptr(rhs2), ptr(out),
+                                            _stream_of(dev)))
+    else:
+        check_call(LIB.dglhip_gsddmm_host(0, csr.num_rows, F, ptr(csr.indptr), ptr(csr.indices),
+                                          ptr(csr.eid), ptr(lhs2), ptr(rhs2), ptr(out), 0))
+    return out
+
+
+def _f32c(t):
+    if t is None:
+        return None
+    if t.dtype != torch.float32:
+        raise DGLError("g-SpMM computes in float32, got %s" % t.dtype)
+    return t.contiguous()
+
+
+class _GSpMM(torch.autograd.Function):
+    """out = REDUCE over in-slots of MSG(ufeat[col], efeat[eid]).
+
+    Backward (SUM/MEAN): dU = the same product over the transposed CSR (the
+    reference's autograd of torch.sparse.mm computes Aᵀ·dC the same way,
+    accumulating over out-edges in edge-id order); dE by g-SDDMM."""
+
+    @staticmethod
+    def forward(ctx, adj, msg, red, feat_len, num_edges, ufeat2, efeat2):
+        elen = 0 if efeat2 is None else efeat2.shape[1]
+        need_arg = red == RED_MAX and (
+            (ufeat2 is not None and ufeat2.requires_grad) or
+            (efeat2 is not None and efeat2.requires_grad))
+        out, arg = _run_gspmm(adj.fwd, msg, red, ufeat2, efeat2, elen, feat_len, need_arg)
+        ctx.adj, ctx.msg, ctx.red, ctx.num_edges = adj, msg, red, num_edges
+        ctx.save_for_backward(ufeat2, efeat2, arg)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        ufeat2, efeat2, arg = ctx.saved_tensors
+        adj, msg, red = ctx.adj, ctx.msg, ctx.red
+        dout = dout.contiguous()
+        fwd = adj.fwd
+        du = de = None
+        need_u = ctx.needs_input_grad[5]
+        need_e = ctx.needs_input_grad[6]
+        F = dout.shape[1]
+        if red == RED_MEAN:
+            deg = fwd.degrees().clamp(min=1).to(dout.dtype).unsqueeze(1)
+            dout = (dout / deg).contiguous()
+            red_b = RED_SUM
+        else:
+            red_b = red
+        if red_b == RED_SUM:
+            if need_u:
+                elen = 0 if efeat2 is None else efeat2.shape[1]
+                du, _ = _run_gspmm(adj.bwd, msg if msg != MSG_COPY_E else MSG_COPY_U, RED_SUM,
+                                   dout, efeat2 if msg == MSG_U_MUL_E else None,
+                                   elen if msg == MSG_U_MUL_E else 0, F, False)
+            if need_e:
+                rows = fwd.row_ids()
+                if msg == MSG_COPY_E:
+                    g = dout.index_select(0, rows)
+                    if efeat2.shape[1] == 1:
+                        g = g.sum(1, keepdim=True)
+                elif efeat2.shape[1] == 1:
+                    g = _run_sddmm_dot(fwd, dout, ufeat2.contiguous(), ctx.num_edges)
+                    de = g.unsqueeze(1)
+                    g = None
+                else:
+                    g = dout.index_select(0, rows) * ufeat2.index_select(0, fwd.indices.long())
+                if g is not None:
+                    de = torch.zeros_like(efeat2)
+                    de.index_copy_(0, fwd.eid, g)
+        else:  # MAX: route each output element's gradient to its argmax slot
+            valid = arg >= 0
+            slots = arg.clamp(min=0)
+            rowsel = valid.nonzero(as_tuple=True)
+            sl = slots[rowsel]
+            g = dout[rowsel]
+            fidx = rowsel[1]
+            if need_u:
+                src = fwd.indices.long()[sl]
+                gu = g
+                if msg == MSG_U_MUL_E:
+                    e = fwd.eid[sl]
+                    gu = g * (efeat2[e, 0] if efeat2.shape[1] == 1 else efeat2[e, fidx])
+                du = torch.zeros_like(ufeat2)
+                du.index_put_((src, fidx), gu, accumulate=True)
+            if need_e:
+                e = fwd.eid[sl]
+                ge = g
+                if msg == MSG_U_MUL_E:
+                    ge = g * ufeat2[fwd.indices.long()[sl], fidx]
+                de = torch.zeros_like(efeat2)
+                if efeat2.shape[1] == 1:
+                    de.index_put_((e, torch.zeros_like(e)), ge, accumulate=True)
+                else:
+                    de.index_put_((e, fidx), ge, accumulate=True)
+        return None, None, None, None, None, du, de
+
+
+def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None):
+    """Generalised SpMM over ``adj`` (a SparseAdj on the features' device).
+
+    ufeat : (num_cols, *fshape) node features or None (copy_e)
+    efeat : (num_edges,) / (num_edges, 1) scalar or (num_edges, *fshape) edge
+            features indexed by the adjacency's eid, or None (copy_u)
+    returns (num_rows, *fshape) float32
+    """
+    msg = _MSG_NAMES.get(msg, msg)
+    red = _RED_NAMES.get(reduce, reduce)
+    if msg != MSG_COPY_E and ufeat is None:
+        raise DGLError("message needs source node features")
+    if msg != MSG_COPY_U and efeat is None:
+        raise DGLError("message needs edge features")
+    if ufeat is not None:
+        fshape = tuple(ufeat.shape[1:])
+    else:
+        fshape = tuple(efeat.shape[1:]) if efeat.dim() > 1 else ()
+        if fshape == (1,):
+            fshape = (1,)
+    F = 1
+    for s in fshape:
+        F *= int(s)
+    dev = (ufeat if ufeat is not None else efeat).device
+    adj = adj.to(dev)
+    u2 = None if ufeat is None else _f32c(ufeat.reshape(ufeat.shape[0], F))
+    e2 = None
+    if efeat is not None:
+        ne = efeat.shape[0]
+        elen = _efeat_len(efeat, ne, F)
+        e2 = _f32c(efeat.reshape(ne, elen))
+    if num_edges is None:
+        num_edges = 0 if e2 is None else e2.shape[0]
+    out = _GSpMM.apply(adj, msg, red, F, num_edges, u2, e2)
+    return out.reshape((adj.shape[0],) + fshape) if fshape else out.reshape(adj.shape[0])
+
+
+def gsddmm_dot(adj, lhs, rhs, num_edges):
+    """out[eid] = <lhs[row], rhs[col]> for every slot of ``adj`` (no autograd)."""
+    dev = lhs.device
+    adj = adj.to(dev)
+    F = lhs[0].numel() if lhs.shape[0] else 0
+    return _run_sddmm_dot(adj.fwd, _f32c(lhs.reshape(lhs.shape[0], -1)),
+                          _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges)
+
+
+def timing_enable(flag=True):
+    """Bracket every g-SpMM/g-SDDMM launch with hipEvents (bench support)."""
+    check_call(LIB.dglhip_timing_enable(1 if flag else 0))
+
+
+def timing_read():
+    """(total kernel ms, launches) since the last timing_enable."""
+    ms = ctypes.c_double()
+    n = ctypes.c_int64()
+    check_call(LIB.dglhip_timing_read(ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value

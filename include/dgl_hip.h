@@ -1,0 +1,223 @@
+/*
+ * dgl_hip.h — C-ABI of the MI355X-native g-SpMM engine (libdgl_hip.so).
+ *
+ * This is the drop-in boundary for the one hot path this project accelerates:
+ * DGLGraph.update_all / send_and_recv / pull / push with the builtin
+ * message/reduce pairs (copy_src|src_mul_edge|copy_edge  x  sum|max|mean).
+ *
+ * In the reference (GaiYu0/dgl-1 = DGL 0.1.3) that path is
+ *   SPMVExecutor.run            python/dgl/runtime/ir/executor.py:452-473
+ *   SPMVWithDataExecutor.run    python/dgl/runtime/ir/executor.py:535-566
+ *   F.spmm = torch.sparse.mm    python/dgl/backend/pytorch/tensor.py:145-146
+ * fed by the adjacency index produced natively by
+ *   _CAPI_DGLGraphGetAdj        src/graph/graph_apis.cc:474-482
+ *   Graph::GetAdj               src/graph/graph.cc:506-554
+ *   ImmutableGraph CSR build    src/graph/immutable_graph.cc:206-237,553-574
+ * and bound from Python through the ctypes PackedFunc FFI
+ *   DGLFuncGetGlobal/DGLFuncCall include/dgl/runtime/c_runtime_api.h:255-260
+ *   error convention            src/runtime/runtime_base.h:13-32 (API_BEGIN/END),
+ *                               src/runtime/c_runtime_api.cc:130-145 (DGLGetLastError)
+ *
+ * Conventions (same as the reference's C API):
+ *   - every int-returning entry point returns 0 on success and -1 on failure;
+ *     the message is then available from DGLGetLastError() (thread-local).
+ *   - plain pointers and sizes only; no framework types cross this boundary.
+ *   - "device" entry points take device pointers and a hipStream_t passed as
+ *     void*; they enqueue work on that stream and never synchronise it.
+ *   - "host" entry points take host pointers and run synchronously on the
+ *     calling thread (parallelised internally with std::thread).
+ *   - CSR layout: indptr int64[num_rows+1], indices int32[nnz] (column ids),
+ *     eid int64[nnz] (original edge id of each CSR slot). Within a row the
+ *     slots keep the order in which the reference's sparse product consumes
+ *     them (see DGLHIP_ORDER_*), which is what makes results bit-exact.
+ *   - dense features are row-major contiguous float32 [rows, feat_len].
+ */
+#ifndef DGL_HIP_H_
+#define DGL_HIP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DGLHIP_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* Error handling / build info                                               */
+/* ------------------------------------------------------------------------ */
+
+/* Replaces DGLGetLastError (src/runtime/c_runtime_api.cc:138-140). */
+const char* DGLGetLastError(void);
+/* Replaces DGLAPISetLastError (src/runtime/c_runtime_api.cc:142-145). */
+void DGLAPISetLastError(const char* msg);
+/* ABI version (DGLHIP_ABI_VERSION) and a human-readable build string. */
+int dglhip_abi_version(void);
+const char* dglhip_build_info(void);
+
+/* ------------------------------------------------------------------------ */
+/* Graph ingestion: COO -> CSR (replaces Graph::GetAdj + the uncoalesced COO  */
+/* that torch.sparse.mm consumes; graph.cc:506-554, graph_index.py:565-583)  */
+/* ------------------------------------------------------------------------ */
+
+/* Slot order inside a CSR row.
+ *  EID    : ascending edge id — the nnz order of the mutable graph's COO
+ *           (graph.cc:509-524 emits [dst..., src...] in edge-id order).
+ *  COL    : ascending (column, edge id) — the order of ImmutableGraph's CSR
+ *           (immutable_graph.cc:206-237 sorts by (dst, src)).            */
+#define DGLHIP_ORDER_EID 0
+#define DGLHIP_ORDER_COL 1
+
+/* Host: build a CSR over `num_rows` rows from COO (row[e], col[e]), e < nnz.
+ * Stable: slots of a row follow `order`. All ids are validated. */
+int dglhip_coo_to_csr_host(int64_t num_rows, int64_t num_cols, int64_t nnz,
+                           const int64_t* row, const int64_t* col, int order,
+                           int64_t* indptr, int32_t* indices, int64_t* eid);
+
+/* Host: rows sorted by descending degree (ties: ascending row id). Used as
+ * the launch schedule so the longest rows start first. */
+int dglhip_rows_by_degree_host(int64_t num_rows, const int64_t* indptr,
+                               int32_t* row_order);
+
+/* Device: the same COO -> CSR build on the GPU (stable LSD radix sort on
+ * (row[, col]) with edge-id as the final tie-break). `workspace` must be at
+ * least dglhip_coo_to_csr_workspace_bytes(...) bytes of device memory. */
+int64_t dglhip_coo_to_csr_workspace_bytes(int64_t num_rows, int64_t num_cols,
+                                          int64_t nnz, int order);
+int dglhip_coo_to_csr_device(int64_t num_rows, int64_t num_cols, int64_t nnz,
+                             const int64_t* row, const int64_t* col, int order,
+                             int64_t* indptr, int32_t* indices, int64_t* eid,
+                             void* workspace, int64_t workspace_bytes,
+                             void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* g-SpMM: out[r,:] = REDUCE_{slot k of row r} MSG(ufeat[indices[k],:],      */
+/*                                                  efeat[eid[k],:])        */
+/* Replaces F.spmm / SPMV / SPMV_WITH_DATA (executor.py:452-473,535-566,    */
+/* backend/pytorch/tensor.py:145-146) and, for max/mean, the degree-bucketing*/
+/* UDF reduce (runtime/degree_bucketing.py:13-190, src/scheduler/scheduler.cc*/
+/* :13-93).                                                                  */
+/* ------------------------------------------------------------------------ */
+
+#define DGLHIP_MSG_COPY_U  0  /* copy_src(src, out)                 message.py:215-235 */
+#define DGLHIP_MSG_U_MUL_E 1  /* src_mul_edge(src, edge, out)       message.py:190-213 */
+#define DGLHIP_MSG_COPY_E  2  /* copy_edge(edge, out)               message.py:237-257 */
+
+#define DGLHIP_REDUCE_SUM  0  /* sum(msg, out)                      reducer.py:52-73   */
+#define DGLHIP_REDUCE_MAX  1  /* max(msg, out)                      reducer.py:75-97   */
+#define DGLHIP_REDUCE_MEAN 2  /* mean: sum / max(deg, 1) (north-star extension) */
+
+/* efeat_len: 0 (no edge feature), 1 (one scalar per edge, broadcast over the
+ * feature row; the only case the reference specialises, message.py:37-44),
+ * or feat_len (one value per edge and feature).
+ * arg_out (int64[num_rows*feat_len], may be NULL): for MAX, the CSR slot that
+ * won each element (-1 for empty rows); needed by the backward.
+ * row_order (int32[num_rows], may be NULL): launch schedule (a permutation);
+ * results never depend on it.
+ * Numerics: SUM/MEAN accumulate per output element in CSR slot order with
+ * one fused multiply-add per slot (acc = fma(w, x, acc); copy: acc += x),
+ * starting from +0.0 — the arithmetic of torch's CPU sparse x dense product
+ * on the reference's uncoalesced COO. Empty rows produce 0. */
+int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
+                        int64_t feat_len, const int64_t* indptr,
+                        const int32_t* indices, const int64_t* eid,
+                        const float* ufeat, const float* efeat,
+                        int64_t efeat_len, float* out, int64_t* arg_out,
+                        const int32_t* row_order, void* stream);
+
+/* Same contract on host memory (the CPU device of the engine; std::thread). */
+int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
+                      int64_t feat_len, const int64_t* indptr,
+                      const int32_t* indices, const int64_t* eid,
+                      const float* ufeat, const float* efeat,
+                      int64_t efeat_len, float* out, int64_t* arg_out,
+                      int num_threads);
+
+/* ------------------------------------------------------------------------ */
+/* g-SDDMM: per-edge products feeding the backward of u_mul_e and the GAT    */
+/* edge attention (gat/train.py:74-96).                                      */
+/*   DOT : out[eid[k]] = sum_f lhs[r,f] * rhs[indices[k],f]   (r = row of k) */
+/* ------------------------------------------------------------------------ */
+#define DGLHIP_SDDMM_DOT 0
+int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
+                         const int64_t* indptr, const int32_t* indices,
+                         const int64_t* eid, const float* lhs,
+                         const float* rhs, float* out, void* stream);
+int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
+                       const int64_t* indptr, const int32_t* indices,
+                       const int64_t* eid, const float* lhs, const float* rhs,
+                       float* out, int num_threads);
+
+/* ------------------------------------------------------------------------ */
+/* Kernel timing (measurement support for bench.py): when enabled, every     */
+/* g-SpMM launch is bracketed by a pair of hipEvents on its own stream.     */
+/* ------------------------------------------------------------------------ */
+int dglhip_timing_enable(int enable);
+/* Synchronises on the recorded events and returns the summed kernel time
+ * (ms) and launch count since the last enable/reset. */
+int dglhip_timing_read(double* total_ms, int64_t* launches);
+
+/* ------------------------------------------------------------------------ */
+/* PackedFunc registry (replaces the TVM-derived runtime's global registry, */
+/* src/runtime/registry.cc:47,137 and c_runtime_api.cc:243-276, so that a    */
+/* ctypes binding written for libdgl finds the engine's kernels by name).   */
+/* ------------------------------------------------------------------------ */
+
+/* Type codes (include/dgl/runtime/c_runtime_api.h:79-95, DLPack kDLInt=0,
+ * kDLUInt=1, kDLFloat=2). */
+#define DGLHIP_TC_INT 0
+#define DGLHIP_TC_UINT 1
+#define DGLHIP_TC_FLOAT 2
+#define DGLHIP_TC_HANDLE 3
+#define DGLHIP_TC_NULL 4
+#define DGLHIP_TC_ARRAY_HANDLE 7
+#define DGLHIP_TC_STR 11
+
+/* DLPack-compatible tensor (same layout as DLTensor with DLContext, which is
+ * what include/dgl/runtime/ndarray.h:114 passes). device_type: 1 = CPU,
+ * 10 = ROCm (kDLROCM, c_runtime_api.cc:36). */
+typedef struct {
+  void* data;
+  int32_t device_type;
+  int32_t device_id;
+  int32_t ndim;
+  uint8_t dtype_code;
+  uint8_t dtype_bits;
+  uint16_t dtype_lanes;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+} DGLHipTensor;
+
+typedef union {
+  int64_t v_int64;
+  double v_float64;
+  void* v_handle;
+  const char* v_str;
+} DGLHipValue;
+
+typedef void* DGLHipFunctionHandle;
+
+int DGLFuncGetGlobal(const char* name, DGLHipFunctionHandle* out);
+int DGLFuncListGlobalNames(int* out_size, const char*** out_array);
+int DGLFuncCall(DGLHipFunctionHandle func, DGLHipValue* arg_values,
+                int* type_codes, int num_args, DGLHipValue* ret_val,
+                int* ret_type_code);
+int DGLFuncFree(DGLHipFunctionHandle func);
+
+/* Registered names (argument lists are documented in csrc/registry.cc):
+ *   "dglhip._CAPI_GSpMM"        (msg, reduce, indptr, indices, eid, ufeat,
+ *                                efeat|null, out, arg_out|null,
+ *                                row_order|null, stream)
+ *   "dglhip._CAPI_GSDDMM"       (op, indptr, indices, eid, lhs, rhs, out,
+ *                                stream)
+ *   "dglhip._CAPI_COOToCSR"     (num_rows, row, col, order, indptr, indices,
+ *                                eid)
+ *   "dglhip._CAPI_RowsByDegree" (indptr, row_order)
+ * Tensors are DGLHipTensor* (type code 7); device is taken from the tensor. */
+
+#ifdef __cplusplus
+}  /* extern "C" */
+#endif
+
+#endif  /* DGL_HIP_H_ */

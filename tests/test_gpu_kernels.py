@@ -1,0 +1,165 @@
+"""HIP kernels through the C-ABI vs the oracle, on the MI355X.
+
+Bit-exact for integer CSR arrays and for the reference-arithmetic products
+(copy_u / u_mul_e + sum, max); tolerance 1e-5 (north_star) for mean and the
+SDDMM dot. Shapes sweep the kernel's (VEC, GROUP) specialisations, empty and
+ragged inputs, multigraph duplicates and a Reddit-degree-scale row set.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import dgl
+from dgl import _ffi, kernel
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cuda():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device("cuda", 0)
+
+
+def rand_graph(rng, n_rows, n_cols, nnz, skew=False):
+    if skew:  # power-law destinations: a few very long rows
+        p = 1.0 / np.arange(1, n_rows + 1) ** 1.1
+        row = rng.choice(n_rows, size=nnz, p=p / p.sum())
+    else:
+        row = rng.integers(0, n_rows, nnz)
+    col = rng.integers(0, n_cols, nnz)
+    return row.astype(np.int64), col.astype(np.int64)
+
+
+@pytest.mark.parametrize("F", [1, 2, 3, 7, 16, 41, 64, 128, 256, 500])
+def test_gspmm_copy_u_sum_exact(cuda, F):
+    rng = np.random.default_rng(F)
+    n = 3000
+    row, col = rand_graph(rng, n, n, 40000, skew=True)
+    H = rng.standard_normal((n, F)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    out = kernel.gspmm(adj, "copy_u", "sum", torch.from_numpy(H).to(cuda))
+    ref = O.spmm_coo(n, row, col, H)
+    assert np.array_equal(out.cpu().numpy().reshape(n, F), ref)
+
+
+@pytest.mark.parametrize("F", [1, 5, 128])
+@pytest.mark.parametrize("edge_len", ["scalar", "vector"])
+def test_gspmm_u_mul_e_sum(cuda, F, edge_len):
+    rng = np.random.default_rng(7)
+    n, m = 500, 20000  # many duplicate (row, col) pairs
+    row, col = rand_graph(rng, n, 60, m)
+    H = rng.standard_normal((60, F)).astype(np.float32)
+    W = rng.standard_normal((m, 1 if edge_len == "scalar" else F)).astype(np.float32)
+    adj = kernel.from_coo(n, 60, row, col, kernel.ORDER_EID, cuda)
+    out = kernel.gspmm(adj, "u_mul_e", "sum", torch.from_numpy(H).to(cuda),
+                       torch.from_numpy(W).to(cuda)).cpu().numpy().reshape(n, F)
+    if edge_len == "scalar":
+        assert np.array_equal(out, O.spmm_coo(n, row, col, H, W[:, 0]))
+    else:
+        ref = np.zeros((n, F), np.float32)
+        for f in range(F):
+            ref[:, f] = O.spmm_coo(n, row, col, H[:, f:f + 1], W[:, f])[:, 0]
+        assert np.array_equal(out, ref)
+
+
+def test_gspmm_max_and_mean(cuda):
+    rng = np.random.default_rng(11)
+    n, F = 700, 33
+    row, col = rand_graph(rng, n, n, 9000, skew=True)
+    H = rng.standard_normal((n, F)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    Hd = torch.from_numpy(H).to(cuda)
+    mx = kernel.gspmm(adj, "copy_u", "max", Hd).cpu().numpy()
+    assert np.array_equal(mx, O.max_mailbox(n, row, H[col]))
+    mn = kernel.gspmm(adj, "copy_u", "mean", Hd).cpu().numpy()
+    np.testing.assert_allclose(mn, O.mean_mailbox(n, row, H[col]), rtol=1e-5, atol=1e-6)
+
+
+def test_empty_and_degenerate(cuda):
+    for n, nnz in ((0, 0), (5, 0), (1, 1)):
+        row = np.zeros(nnz, np.int64)
+        adj = kernel.from_coo(n, max(n, 1), row, row, kernel.ORDER_EID, cuda)
+        H = torch.ones(max(n, 1), 4, device=cuda)
+        out = kernel.gspmm(adj, "copy_u", "sum", H)
+        assert out.shape == (n, 4)
+        assert out.sum().item() == float(nnz * 4)
+
+
+@pytest.mark.parametrize("order", [kernel.ORDER_EID, kernel.ORDER_COL])
+def test_device_csr_builder_matches_host(cuda, order):
+    rng = np.random.default_rng(5)
+    for n_rows, n_cols, nnz in ((1, 1, 0), (10, 7, 100), (5000, 3000, 200000)):
+        row, col = rand_graph(rng, n_rows, n_cols, nnz)
+        h = kernel.build_csr(n_rows, n_cols, row, col, order, "cpu")
+        d = kernel.build_csr(n_rows, n_cols, row, col, order, cuda)
+        assert torch.equal(h.indptr, d.indptr.cpu())
+        assert torch.equal(h.indices, d.indices.cpu())
+        assert torch.equal(h.eid, d.eid.cpu())
+        assert torch.equal(h.row_order, d.row_order.cpu())
+        if order == kernel.ORDER_EID and nnz:
+            ip, ix, pos = O.coo_to_csr(n_rows, row, col)
+            assert np.array_equal(h.indptr.numpy(), ip)
+            assert np.array_equal(h.indices.numpy().astype(np.int64), ix)
+            assert np.array_equal(h.eid.numpy(), pos)
+
+
+def test_backward_transposed(cuda):
+    rng = np.random.default_rng(9)
+    n, F = 2000, 128
+    row, col = rand_graph(rng, n, n, 50000, skew=True)
+    H = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(cuda)
+    G = rng.standard_normal((n, F)).astype(np.float32)
+    W = rng.standard_normal(len(row)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    Hr = H.clone().requires_grad_(True)
+    kernel.gspmm(adj, "copy_u", "sum", Hr).backward(torch.from_numpy(G).to(cuda))
+    assert np.array_equal(Hr.grad.cpu().numpy(), O.spmm_coo(n, col, row, G))
+    Hr = H.clone().requires_grad_(True)
+    Wd = torch.from_numpy(W).to(cuda).requires_grad_(True)
+    kernel.gspmm(adj, "u_mul_e", "sum", Hr, Wd).backward(torch.from_numpy(G).to(cuda))
+    assert np.array_equal(Hr.grad.cpu().numpy(), O.spmm_coo(n, col, row, G, W))
+    np.testing.assert_allclose(Wd.grad.cpu().numpy(),
+                               O.sddmm_dot(row, col, G, H.cpu().numpy()), rtol=1e-5, atol=1e-4)
+
+
+def test_large_reddit_scale_rows(cuda):
+    """Long power-law rows at F=128 (the bench shape): exact vs the OpenMP oracle."""
+    rng = np.random.default_rng(1)
+    n = 200000
+    row, col = rand_graph(rng, n, n, 8_000_000, skew=True)
+    H = rng.uniform(-1, 1, (n, 128)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    out = kernel.gspmm(adj, "copy_u", "sum", torch.from_numpy(H).to(cuda)).cpu().numpy()
+    ip, ix, pos = O.coo_to_csr(n, row, col)
+    assert np.array_equal(out, O.spmm_csr(ip, ix, pos, H, num_threads=16))
+
+
+def test_packed_func_on_device(cuda):
+    rng = np.random.default_rng(2)
+    n = 100
+    row, col = rand_graph(rng, n, n, 1000)
+    csr = kernel.build_csr(n, n, row, col, kernel.ORDER_EID, cuda)
+    H = torch.from_numpy(rng.standard_normal((n, 8)).astype(np.float32)).to(cuda)
+    out = torch.empty(n, 8, device=cuda)
+    stream = torch.cuda.current_stream().cuda_stream
+    _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, csr.indptr, csr.indices, csr.eid, H, None,
+                     out, None, csr.row_order, ("handle", stream))
+    assert np.array_equal(out.cpu().numpy(), O.spmm_coo(n, row, col, H.cpu().numpy()))
+
+
+def test_timing_hooks(cuda):
+    n = 1000
+    row = np.arange(n, dtype=np.int64)
+    adj = kernel.from_coo(n, n, row, row, kernel.ORDER_EID, cuda)
+    H = torch.ones(n, 128, device=cuda)
+    kernel.timing_enable(True)
+    for _ in range(3):
+        kernel.gspmm(adj, "copy_u", "sum", H)
+    ms, launches = kernel.timing_read()
+    kernel.timing_enable(False)
+    assert launches == 3 and ms > 0

@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: gpu tests, smoke, bench, rocprofv3 kernel stats.
+# Stops at the first step that faults / aborts / times out (exit >= 2 or 124/134/137/139).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
+STEPS="${STEPS:-tests smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; tail -5 gpurun_out/pytest_gpu.log; ok $rc || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+      rc=$?; tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json; [ $rc -eq 0 ] || exit $rc ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
+        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/prof.log 2>&1
+      rc=$?; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+  esac
+done
+echo "gpu_check done"
