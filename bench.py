@@ -88,6 +88,42 @@ def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
         torch.set_num_threads(threads)
 
 
+def pmc_traffic():
+    """HBM bytes per g-SpMM launch from two rocprofv3 --pmc passes (FETCH_SIZE,
+    WRITE_SIZE) of a short child run of this script, corrected as
+    MI355X_MICROARCH.md §HBM prescribes (tools/pmc_traffic.py). Runs before
+    this process touches the GPU; returns None if the profiler is unavailable."""
+    import shutil
+    import subprocess
+    import tempfile
+    from tools.pmc_traffic import traffic
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None
+    env = dict(os.environ, TMPDIR="/tmp")
+    out = tempfile.mkdtemp(prefix="dglhip_pmc_", dir="/tmp")
+    csvs = []
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(out, counter)
+        cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
+               sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
+               "--no-cpu-baseline", "--no-traffic"]
+        try:
+            subprocess.run(cmd, cwd="/tmp", env=env, timeout=300, check=True,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        except (subprocess.SubprocessError, OSError) as err:
+            log("pmc pass %s failed: %s" % (counter, err))
+            return None
+        csvs.append(os.path.join(d, "run_counter_collection.csv"))
+    try:
+        return traffic(csvs[0], csvs[1])
+    except (OSError, ValueError, KeyError) as err:
+        log("pmc parse failed: %s" % err)
+        return None
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,10 +131,17 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 PMC passes that fill roofline.traffic")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    pmc = None
+    if world == 1 and not args.no_traffic:
+        t0 = time.time()
+        pmc = pmc_traffic()  # before this process initialises the GPU
+        log("pmc traffic passes took %.1fs" % (time.time() - t0))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
@@ -198,10 +241,12 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": None if pmc is None else pmc["bytes"],
             "kernel": "gspmm_sum_kernel<copy_u> (rank 0)",
             "kernel_ms": kernel_ms,
             "bytes_per_launch": bytes_per_launch,
+            "traffic_source": None if pmc is None else
+            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
         },
         "cpu_baseline": None,
     }

@@ -322,6 +322,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 2, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  if (num_rows == 0 || feat_len == 0) return 0;  // empty tensors may carry null pointers
   DGLHIP_CHECK(indptr != nullptr && out != nullptr, "null indptr/out");
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
@@ -329,7 +330,6 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
   DGLHIP_CHECK(!use_e || efeat_len == 1 || efeat_len == feat_len,
                "edge feature must have length 1 or feat_len, got " << efeat_len);
-  if (num_rows == 0 || feat_len == 0) return 0;
   const bool eb = efeat_len == 1;
   if (reduce_op == DGLHIP_REDUCE_MAX) {
     const int64_t blocks = (num_rows + 3) / 4;

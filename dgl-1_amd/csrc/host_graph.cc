@@ -178,6 +178,7 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 2, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  if (num_rows == 0 || feat_len == 0) return 0;
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");

@@ -61,7 +61,7 @@ def _materialize(g, mfunc, u, v, eid):
     return mfunc(_edge_batch(g, u, v, eid))
 
 
-def _msg_operands(g, mfn, whole_graph, eid):
+def _msg_operands(g, mfn):
     """(ufeat, efeat) for a kernel message on the graph's frames."""
     nf, ef = g._node_frame, g._edge_frame
     ufeat = nf[mfn.src_field] if mfn.kernel_msg != "copy_e" else None
@@ -69,7 +69,21 @@ def _msg_operands(g, mfn, whole_graph, eid):
     return ufeat, efeat
 
 
-def _send_reduce(g, mfunc, rfunc, u, v, eid, recv_nodes, whole_graph):
+class _Edges(object):
+    """The triggered edges (u, v, eid); for update_all they are produced only
+    if messages must be materialised (the kernel path never needs them)."""
+
+    def __init__(self, fn):
+        self._fn = fn
+        self._val = None
+
+    def get(self):
+        if self._val is None:
+            self._val = self._fn()
+        return self._val
+
+
+def _send_reduce(g, mfunc, rfunc, edges, recv_nodes, whole_graph):
     """Returns the reduced feature dict (rows = recv_nodes)."""
     nf, ef = g._node_frame, g._edge_frame
     mfunc = _standardize(mfunc, "message")
@@ -83,6 +97,7 @@ def _send_reduce(g, mfunc, rfunc, u, v, eid, recv_nodes, whole_graph):
             if whole_graph:
                 adj_cache[key] = g._graph.adjacency(dev)
             else:
+                u, v, eid = edges.get()
                 adj_cache[key] = spmv.build_adj_uv(g.number_of_nodes(), u, v, eid, recv_nodes,
                                                    dev)
         return adj_cache[key]
@@ -90,7 +105,7 @@ def _send_reduce(g, mfunc, rfunc, u, v, eid, recv_nodes, whole_graph):
     if is_iterable(mfunc) and is_iterable(rfunc):
         pairs, mfunc, rfunc = spmv.analyze_v2v(mfunc, rfunc, nf, ef)
         for mfn, rfn in pairs:
-            ufeat, efeat = _msg_operands(g, mfn, whole_graph, eid)
+            ufeat, efeat = _msg_operands(g, mfn)
             dev = (ufeat if ufeat is not None else efeat).device
             ir.record("SPMV", msg=mfn.kernel_msg, reduce=rfn.kernel_reduce,
                       src=mfn.src_field, edge=mfn.edge_field, out=rfn.out_field)
@@ -98,6 +113,7 @@ def _send_reduce(g, mfunc, rfunc, u, v, eid, recv_nodes, whole_graph):
                                               rfn.kernel_reduce, ufeat, efeat)
         if not mfunc:
             return out
+    u, v, eid = edges.get()
     msgs = _materialize(g, mfunc, u, v, eid)
     if is_iterable(rfunc):
         for rfn in rfunc:
@@ -144,9 +160,9 @@ def schedule_update_all(g, message_func, reduce_func, apply_func):
         if apply_func is not None:
             schedule_apply_nodes(g, None, apply_func, inplace=False)
         return
-    u, v, eid = g._graph.edges()
+    edges = _Edges(g._graph.edges)
     recv = torch.arange(g.number_of_nodes(), dtype=torch.int64)
-    reduced = _send_reduce(g, message_func, reduce_func, u, v, eid, recv, True)
+    reduced = _send_reduce(g, message_func, reduce_func, edges, recv, True)
     final = _apply_with_accum(g, None, reduced, apply_func)
     ir.record("WRITE_DICT_", keys=sorted(final.keys()))
     g._node_frame.update_rows(None, final)
@@ -155,7 +171,8 @@ def schedule_update_all(g, message_func, reduce_func, apply_func):
 def schedule_snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace):
     """send_and_recv on the given edges."""
     recv = torch.unique(v, sorted=True)
-    reduced = _send_reduce(g, message_func, reduce_func, u, v, eid, recv, False)
+    reduced = _send_reduce(g, message_func, reduce_func, _Edges(lambda: (u, v, eid)), recv,
+                           False)
     final = _apply_with_accum(g, recv, reduced, apply_func)
     ir.record("WRITE_ROW_", num_rows=len(recv), inplace=inplace)
     g._node_frame.update_rows(recv, final, inplace)
@@ -169,7 +186,8 @@ def schedule_pull(g, pull_nodes, message_func, reduce_func, apply_func, inplace)
             schedule_apply_nodes(g, pull_nodes, apply_func, inplace)
         return
     recv = torch.unique(pull_nodes, sorted=True)
-    reduced = _send_reduce(g, message_func, reduce_func, u, v, eid, recv, False)
+    reduced = _send_reduce(g, message_func, reduce_func, _Edges(lambda: (u, v, eid)), recv,
+                           False)
     final = _apply_with_accum(g, recv, reduced, apply_func)
     ir.record("WRITE_ROW_", num_rows=len(recv), inplace=inplace)
     g._node_frame.update_rows(recv, final, inplace)

@@ -20,9 +20,15 @@ for s in $STEPS; do
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline \
+        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic \
         > gpurun_out/prof.log 2>&1
       rc=$?; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      for c in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
+          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > gpurun_out/pmc_$c.log 2>&1
+        rc=$?; tail -2 gpurun_out/pmc_$c.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
   esac
 done
 echo "gpu_check done"
