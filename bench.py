@@ -133,33 +133,67 @@ def main():
     ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
     ap.add_argument("--no-traffic", action="store_true",
                     help="skip the rocprofv3 PMC passes that fill roofline.traffic")
+    ap.add_argument("--graph-scale", type=float, default=1.0,
+                    help="per-GPU graph size as a fraction of Reddit (testing only)")
+    ap.add_argument("--workload", default="reddit", choices=["reddit", "rmat"],
+                    help="reddit: weak-scaled Reddit-shaped graph (default, the driver's line); "
+                         "rmat: one fixed Graph500 R-MAT graph partitioned over the ranks "
+                         "(strong scaling, heavy rows chunked)")
+    ap.add_argument("--rmat-scale", type=int, default=26)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
+                         "to rehearse the multi-rank path")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     pmc = None
-    if world == 1 and not args.no_traffic:
+    if world == 1 and not args.no_traffic and args.workload == "reddit":
         t0 = time.time()
         pmc = pmc_traffic()  # before this process initialises the GPU
         log("pmc traffic passes took %.1fs" % (time.time() - t0))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     t0 = time.time()
-    src, dst, n = data.reddit_like(scale=world, seed=0, device=dev)
+    if args.workload == "rmat":
+        src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
+        kernel.set_row_split("auto")
+        args.no_cpu_baseline = True
+    elif args.graph_scale == 1.0:
+        src, dst, n = data.reddit_like(scale=world, seed=0, device=dev)
+    else:
+        src, dst, n = data.chung_lu(int(data.REDDIT_NODES * world * args.graph_scale),
+                                    int(data.REDDIT_EDGES * world * args.graph_scale),
+                                    data.REDDIT_MAX_OVER_MEAN, seed=0, device=dev)
     num_edges_total = int(src.numel())
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
     log("rank %d: graph %d nodes %d edges generated in %.1fs" % (rank, n, num_edges_total,
                                                                   time.time() - t0))
 
-    if world == 1:
+    if world == 1 and args.workload == "rmat":
+        # 1.07B edges: build the device CSR directly (no host copy of the edge list)
+        adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+        del src, dst
+        src = dst = None
+        h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+        num_local_edges, num_rows = num_edges_total, n
+
+        def step():
+            kernel.gspmm(adj, "copy_u", "sum", h)
+        parallelism = "single GPU (kernel API; heavy rows chunked)"
+    elif world == 1:
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))
         h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         g.ndata["h"] = h
@@ -188,6 +222,8 @@ def main():
         parallelism = "%d-way 1-D dst-row partition, RCCL all-gather halo" % world
     del src, dst
     torch.cuda.synchronize()
+    log("setup done in %.1fs; peak HBM %.1f GB" % (time.time() - t0,
+                                                    torch.cuda.max_memory_allocated(dev) / 1e9))
 
     for _ in range(args.warmup):
         step()
@@ -211,7 +247,7 @@ def main():
         elapsed = float(t.item())
 
     value = num_edges_total * args.steps / elapsed
-    kernel_ms = kms / max(launches, 1)
+    kernel_ms = kms / args.steps  # g-SpMM device time per step (all its launches)
     bytes_per_launch = algorithmic_bytes(num_local_edges, num_rows, FEAT)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     result = {
@@ -223,14 +259,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "weak" if args.workload == "reddit" else "strong",
         "vs_baseline": None,
         "dtype": "fp32",
-        "data": "synthetic (seeded Chung-Lu power-law graph of Reddit's shape; random "
-                "U(-1,1) features)",
+        "data": ("synthetic (seeded Chung-Lu power-law graph of Reddit's shape; random "
+                 "U(-1,1) features)") if args.workload == "reddit" else
+                "synthetic (seeded Graph500 R-MAT 0.57/0.19/0.19/0.05, ids permuted)",
         "config": {
-            "workload": "reddit-shaped x%d: %d nodes, %d edges (incl. self-loops), feat=%d"
-                        % (world, n, num_edges_total, FEAT),
+            "workload": ("reddit-shaped x%d%s: %d nodes, %d edges (incl. self-loops), feat=%d"
+                         % (world, "" if args.graph_scale == 1.0 else
+                            " (graph-scale %g)" % args.graph_scale, n, num_edges_total, FEAT))
+                        if args.workload == "reddit" else
+                        ("rmat-%d: %d nodes, %d edges, feat=%d, row split %s"
+                         % (args.rmat_scale, n, num_edges_total, FEAT, kernel._ROW_SPLIT)),
             "global_batch": n,
             "feat": FEAT,
             "parallelism": parallelism,

@@ -98,52 +98,97 @@ struct SlotLoad {
   }
 };
 
-// Sum-reduce kernel (also MEAN). GROUP lanes per row, VEC floats per lane.
-template <int VEC, int GROUP, int UNROLL, int MSG, bool EB, bool MEAN>
+// Sequential reduction of slots [beg, end) of one row for the VEC features at
+// f0: the fma chain the reference's product runs (see the file header).
+template <int VEC, int UNROLL, int MSG, bool EB>
+__device__ __forceinline__ typename Vec<VEC>::T reduce_range(
+    int64_t beg, int64_t end, int64_t F, int64_t f0, const int32_t* __restrict__ indices,
+    const int64_t* __restrict__ eid, const float* __restrict__ ufeat,
+    const float* __restrict__ efeat) {
+  typedef typename Vec<VEC>::T V;
+  V acc = Vec<VEC>::zero();
+  int64_t k = beg;
+  for (; k + UNROLL <= end; k += UNROLL) {
+    SlotLoad<VEC, MSG, EB> s[UNROLL];
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j)
+      s[j].load(ufeat, efeat, F, f0, indices[k + j],
+                MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j) {
+      if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
+      else if (MSG == DGLHIP_MSG_COPY_E) acc += s[j].e;
+      else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
+    }
+  }
+  for (; k < end; ++k) {
+    SlotLoad<VEC, MSG, EB> s;
+    s.load(ufeat, efeat, F, f0, indices[k], MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+    if (MSG == DGLHIP_MSG_COPY_U) acc += s.u;
+    else if (MSG == DGLHIP_MSG_COPY_E) acc += s.e;
+    else acc = Vec<VEC>::fma(s.e, s.u, acc);
+  }
+  return acc;
+}
+
+// Sum-reduce kernel (also MEAN). GROUP lanes per work item, VEC floats per
+// lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
+// or a slot range [chunk_beg[i], chunk_end[i]) of a heavy row whose partial
+// sum goes to partial[i, :] (CHUNKED = true).
+template <int VEC, int GROUP, int UNROLL, int MSG, bool EB, bool MEAN, bool CHUNKED>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
-    int64_t num_rows, int64_t F, const int64_t* __restrict__ indptr,
+    int64_t num_items, int64_t F, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
-    float* __restrict__ out, const int32_t* __restrict__ row_order) {
+    float* __restrict__ out, const int32_t* __restrict__ row_order,
+    const int64_t* __restrict__ chunk_beg, const int64_t* __restrict__ chunk_end) {
   typedef typename Vec<VEC>::T V;
-  constexpr int ROWS_PER_WAVE = 64 / GROUP;
+  constexpr int ITEMS_PER_WAVE = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   // wave index is uniform; make that explicit so slot data goes through SGPRs
   const int64_t wave =
       int64_t(blockIdx.x) * (blockDim.x >> 6) +
       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  int64_t r = wave * ROWS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
-  if (r >= num_rows) return;
+  const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
+  if (it >= num_items) return;
   const int gl = GROUP == 64 ? lane : (lane % GROUP);
-  int64_t row = row_order ? row_order[r] : r;
-  if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
-  const int64_t beg = indptr[row], end = indptr[row + 1];
+  int64_t row, beg, end;
+  if (CHUNKED) {
+    row = it;
+    beg = chunk_beg[it];
+    end = chunk_end[it];
+  } else {
+    row = row_order ? row_order[it] : it;
+    if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+    beg = indptr[row];
+    end = indptr[row + 1];
+  }
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
-    V acc = Vec<VEC>::zero();
-    int64_t k = beg;
-    for (; k + UNROLL <= end; k += UNROLL) {
-      SlotLoad<VEC, MSG, EB> s[UNROLL];
-#pragma unroll
-      for (int j = 0; j < UNROLL; ++j)
-        s[j].load(ufeat, efeat, F, f0, indices[k + j],
-                  MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
-#pragma unroll
-      for (int j = 0; j < UNROLL; ++j) {
-        if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
-        else if (MSG == DGLHIP_MSG_COPY_E) acc += s[j].e;
-        else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
-      }
-    }
-    for (; k < end; ++k) {
-      SlotLoad<VEC, MSG, EB> s;
-      s.load(ufeat, efeat, F, f0, indices[k],
-             MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
-      if (MSG == DGLHIP_MSG_COPY_U) acc += s.u;
-      else if (MSG == DGLHIP_MSG_COPY_E) acc += s.e;
-      else acc = Vec<VEC>::fma(s.e, s.u, acc);
-    }
-    if (MEAN && end - beg > 1) acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
+    V acc = reduce_range<VEC, UNROLL, MSG, EB>(beg, end, F, f0, indices, eid, ufeat, efeat);
+    if (!CHUNKED && MEAN && end - beg > 1)
+      acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     stv<VEC>(out + row * F + f0, acc);
+  }
+}
+
+// Combine the chunk partials of each heavy row in chunk order:
+// out[row] = ((p0 + p1) + p2) + ... (deterministic), then MEAN scaling.
+template <bool MEAN>
+__global__ __launch_bounds__(256) void gspmm_combine_kernel(
+    int64_t num_heavy, int64_t F, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ heavy_rows, const int64_t* __restrict__ heavy_chunk_ptr,
+    const float* __restrict__ partial, float* __restrict__ out) {
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (wave >= num_heavy) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t row = heavy_rows[wave];
+  const int64_t c0 = heavy_chunk_ptr[wave], c1 = heavy_chunk_ptr[wave + 1];
+  const float deg = static_cast<float>(indptr[row + 1] - indptr[row]);
+  for (int64_t f = lane; f < F; f += 64) {
+    float acc = partial[c0 * F + f];
+    for (int64_t c = c0 + 1; c < c1; ++c) acc += partial[c * F + f];
+    if (MEAN && deg > 1.0f) acc = acc / deg;
+    out[row * F + f] = acc;
   }
 }
 
@@ -265,36 +310,49 @@ static int pick_group(int64_t F, int vec) {
   return g;
 }
 
+struct SumLaunch {
+  int64_t num_items, F;
+  const int64_t* indptr;
+  const int32_t* indices;
+  const int64_t* eid;
+  const float* ufeat;
+  const float* efeat;
+  float* out;
+  const int32_t* row_order;
+  const int64_t* chunk_beg;  // non-null: chunked launch (partials to `out`)
+  const int64_t* chunk_end;
+};
+
 template <int VEC, int GROUP, int MSG, bool EB, bool MEAN>
-static void launch_sum(int64_t num_rows, int64_t F, const int64_t* indptr,
-                       const int32_t* indices, const int64_t* eid,
-                       const float* ufeat, const float* efeat, float* out,
-                       const int32_t* row_order, hipStream_t stream) {
+static void launch_sum(const SumLaunch& a, hipStream_t stream) {
   constexpr int UNROLL = (VEC == 4) ? 4 : 8;
-  constexpr int ROWS_PER_BLOCK = 4 * (64 / GROUP);
-  const int64_t blocks = (num_rows + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  constexpr int ITEMS_PER_BLOCK = 4 * (64 / GROUP);
+  const int64_t blocks = (a.num_items + ITEMS_PER_BLOCK - 1) / ITEMS_PER_BLOCK;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
+  if (blocks == 0) return;
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EB, MEAN>),
-                       dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
-                       num_rows, F, indptr, indices, eid, ufeat, efeat, out,
-                       row_order);
+    if (a.chunk_beg)
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EB, MEAN, true>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         a.num_items, a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.out, a.row_order, a.chunk_beg, a.chunk_end);
+    else
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EB, MEAN, false>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         a.num_items, a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.out, a.row_order, a.chunk_beg, a.chunk_end);
   });
 }
 
 template <int MSG, bool EB, bool MEAN>
-static void dispatch_sum_shape(int64_t num_rows, int64_t F, const int64_t* indptr,
-                               const int32_t* indices, const int64_t* eid,
-                               const float* ufeat, const float* efeat,
-                               float* out, const int32_t* row_order,
-                               hipStream_t stream) {
-  const int vec = pick_vec(F, {ufeat, EB ? nullptr : efeat, out});
+static void dispatch_sum_shape(const SumLaunch& a, hipStream_t stream) {
+  const int64_t F = a.F;
+  const int vec = pick_vec(F, {a.ufeat, EB ? nullptr : a.efeat, a.out});
   const int group = pick_group(F, vec);
-#define DGLHIP_CASE(V, G)                                                     \
-  if (vec == V && group == G) {                                               \
-    launch_sum<V, G, MSG, EB, MEAN>(num_rows, F, indptr, indices, eid, ufeat, \
-                                    efeat, out, row_order, stream);           \
-    return;                                                                   \
+#define DGLHIP_CASE(V, G)                                  \
+  if (vec == V && group == G) {                            \
+    launch_sum<V, G, MSG, EB, MEAN>(a, stream);            \
+    return;                                                \
   }
   DGLHIP_CASE(4, 64)
   DGLHIP_CASE(2, 64) DGLHIP_CASE(2, 32) DGLHIP_CASE(2, 16) DGLHIP_CASE(2, 8)
@@ -303,6 +361,25 @@ static void dispatch_sum_shape(int64_t num_rows, int64_t F, const int64_t* indpt
   DGLHIP_CASE(1, 4) DGLHIP_CASE(1, 2) DGLHIP_CASE(1, 1)
 #undef DGLHIP_CASE
   DGLHIP_CHECK(false, "no kernel for F=" << F << " vec=" << vec << " group=" << group);
+}
+
+static void dispatch_sum(int msg_op, bool eb, bool mean, const SumLaunch& a,
+                         hipStream_t stream) {
+#define DGLHIP_SUM(M, B)                                      \
+  do {                                                        \
+    if (mean) dispatch_sum_shape<M, B, true>(a, stream);      \
+    else dispatch_sum_shape<M, B, false>(a, stream);          \
+  } while (0)
+  if (msg_op == DGLHIP_MSG_COPY_U) {
+    DGLHIP_SUM(DGLHIP_MSG_COPY_U, false);
+  } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
+    if (eb) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, true);
+    else DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, false);
+  } else {
+    if (eb) DGLHIP_SUM(DGLHIP_MSG_COPY_E, true);
+    else DGLHIP_SUM(DGLHIP_MSG_COPY_E, false);
+  }
+#undef DGLHIP_SUM
 }
 
 }  // namespace dglhip
@@ -349,20 +426,61 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
     return 0;
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
-#define DGLHIP_SUM(M, B, MN)                                                     \
-  dispatch_sum_shape<M, B, MN>(num_rows, feat_len, indptr, indices, eid, ufeat, \
-                               efeat, out, row_order, stream)
-  if (msg_op == DGLHIP_MSG_COPY_U) {
-    if (mean) DGLHIP_SUM(DGLHIP_MSG_COPY_U, false, true);
-    else DGLHIP_SUM(DGLHIP_MSG_COPY_U, false, false);
-  } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
-    if (eb) { if (mean) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, true, true); else DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, true, false); }
-    else { if (mean) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, false, true); else DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, false, false); }
-  } else {
-    if (eb) { if (mean) DGLHIP_SUM(DGLHIP_MSG_COPY_E, true, true); else DGLHIP_SUM(DGLHIP_MSG_COPY_E, true, false); }
-    else { if (mean) DGLHIP_SUM(DGLHIP_MSG_COPY_E, false, true); else DGLHIP_SUM(DGLHIP_MSG_COPY_E, false, false); }
+  SumLaunch a{num_rows, feat_len, indptr, indices, eid, ufeat, efeat, out, row_order,
+              nullptr, nullptr};
+  dispatch_sum(msg_op, eb, mean, a, stream);
+  API_END();
+}
+
+int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
+                                const int64_t* indptr, const int32_t* indices,
+                                const int64_t* eid, const float* ufeat,
+                                const float* efeat, int64_t efeat_len, float* out,
+                                int64_t num_light, const int32_t* light_rows,
+                                int64_t num_chunks, const int64_t* chunk_beg,
+                                const int64_t* chunk_end, int64_t num_heavy,
+                                const int32_t* heavy_rows,
+                                const int64_t* heavy_chunk_ptr, float* partial,
+                                void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN,
+               "chunked rows support sum/mean only");
+  DGLHIP_CHECK(num_light >= 0 && num_chunks >= 0 && num_heavy >= 0, "negative size");
+  if (feat_len == 0) return 0;
+  const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
+  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
+  DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
+  DGLHIP_CHECK(!use_e || efeat_len == 1 || efeat_len == feat_len,
+               "edge feature must have length 1 or feat_len, got " << efeat_len);
+  DGLHIP_CHECK(num_chunks == 0 || (partial && chunk_beg && chunk_end), "null chunk plan");
+  const bool eb = efeat_len == 1;
+  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
+  if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
+    SumLaunch c{num_chunks, feat_len, indptr, indices, eid, ufeat, efeat, partial,
+                nullptr, chunk_beg, chunk_end};
+    dispatch_sum(msg_op, eb, false, c, stream);
   }
-#undef DGLHIP_SUM
+  if (num_light > 0) {
+    SumLaunch l{num_light, feat_len, indptr, indices, eid, ufeat, efeat, out, light_rows,
+                nullptr, nullptr};
+    dispatch_sum(msg_op, eb, mean, l, stream);
+  }
+  if (num_heavy > 0) {
+    const int64_t blocks = (num_heavy + 3) / 4;
+    timed_launch(stream, [&] {
+      if (mean)
+        hipLaunchKernelGGL(gspmm_combine_kernel<true>, dim3(static_cast<unsigned>(blocks)),
+                           dim3(256), 0, stream, num_heavy, feat_len, indptr, heavy_rows,
+                           heavy_chunk_ptr, partial, out);
+      else
+        hipLaunchKernelGGL(gspmm_combine_kernel<false>, dim3(static_cast<unsigned>(blocks)),
+                           dim3(256), 0, stream, num_heavy, feat_len, indptr, heavy_rows,
+                           heavy_chunk_ptr, partial, out);
+    });
+  }
   API_END();
 }
 

@@ -22,7 +22,9 @@ device, the library's host kernels for CPU tensors). There is no other path.
 from __future__ import absolute_import
 
 import ctypes
+import os
 
+import numpy as np
 import torch
 
 from . import _ffi
@@ -41,6 +43,29 @@ _MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_
 _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 
 
+# Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device):
+#   "off"  : every row is one sequential chain — bit-exact with the reference (default)
+#   "auto" : rows longer than max(4096, nnz / 12000) slots are split into chunks
+#   <int>  : explicit chunk length
+_ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "off")
+
+
+def set_row_split(policy):
+    """Set the heavy-row policy ("off", "auto" or a chunk length); returns the old one."""
+    global _ROW_SPLIT
+    old = _ROW_SPLIT
+    _ROW_SPLIT = str(policy)
+    return old
+
+
+def _split_threshold(csr):
+    pol = _ROW_SPLIT
+    if pol in ("off", "0", "", "none", "None"):
+        return 0
+    t = max(4096, csr.nnz // 12000) if pol == "auto" else int(pol)
+    return t if csr.max_degree > t else 0
+
+
 def _stream_of(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -52,7 +77,7 @@ class CSR(object):
     schedule handed to the HIP kernel.
     """
 
-    def __init__(self, indptr, indices, eid, num_cols, row_order=None):
+    def __init__(self, indptr, indices, eid, num_cols, row_order=None, host_indptr=None):
         self.indptr = indptr
         self.indices = indices
         self.eid = eid
@@ -60,6 +85,50 @@ class CSR(object):
         self.num_cols = int(num_cols)
         self.row_order = row_order
         self._row_ids = None
+        self._host_indptr = host_indptr
+        self._plans = {}
+
+    @property
+    def host_indptr(self):
+        if self._host_indptr is None:
+            self._host_indptr = self.indptr.cpu()
+        return self._host_indptr
+
+    @property
+    def max_degree(self):
+        if self.num_rows == 0:
+            return 0
+        ip = self.host_indptr
+        return int((ip[1:] - ip[:-1]).max())
+
+    def split_plan(self, threshold):
+        """Launch plan cutting rows longer than ``threshold`` slots into chunks
+        (cached per threshold): dict of device tensors for
+        dglhip_gspmm_chunked_device."""
+        if threshold in self._plans:
+            return self._plans[threshold]
+        ip = self.host_indptr.numpy()
+        deg = ip[1:] - ip[:-1]
+        order = (self.row_order.cpu().numpy().astype(np.int64) if self.row_order is not None
+                 else np.argsort(-deg, kind="stable"))
+        heavy_mask = deg[order] > threshold
+        light = order[~heavy_mask].astype(np.int32)
+        heavy = order[heavy_mask]
+        nchunks = (deg[heavy] + threshold - 1) // threshold
+        ptr = np.concatenate([[0], np.cumsum(nchunks)]).astype(np.int64)
+        rep = np.repeat(np.arange(len(heavy)), nchunks)
+        k = np.arange(int(ptr[-1])) - ptr[rep]
+        beg = ip[heavy][rep] + k * threshold
+        end = np.minimum(beg + threshold, ip[heavy + 1][rep])
+        dev = self.device
+        plan = {"light": torch.from_numpy(light).to(dev),
+                "heavy": torch.from_numpy(heavy.astype(np.int32)).to(dev),
+                "chunk_ptr": torch.from_numpy(ptr).to(dev),
+                "beg": torch.from_numpy(beg.astype(np.int64)).to(dev),
+                "end": torch.from_numpy(end.astype(np.int64)).to(dev),
+                "num_chunks": int(ptr[-1])}
+        self._plans[threshold] = plan
+        return plan
 
     @property
     def nnz(self):
@@ -74,7 +143,7 @@ class CSR(object):
             return self
         ro = None if self.row_order is None else self.row_order.to(device)
         return CSR(self.indptr.to(device), self.indices.to(device), self.eid.to(device),
-                   self.num_cols, ro)
+                   self.num_cols, ro, self._host_indptr)
 
     def degrees(self):
         return self.indptr[1:] - self.indptr[:-1]
@@ -135,7 +204,7 @@ def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedu
         ro = torch.empty(num_rows, dtype=torch.int32)
         check_call(LIB.dglhip_rows_by_degree_host(num_rows, ptr(host_indptr), ptr(ro)))
         row_order = ro.to(device)
-    return CSR(indptr, indices, eid, num_cols, row_order)
+    return CSR(indptr, indices, eid, num_cols, row_order, host_indptr)
 
 
 class SparseAdj(object):
@@ -211,7 +280,16 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
-    if dev.type == "cuda":
+    split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
+    if split:
+        p = csr.split_plan(split)
+        partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
+        check_call(LIB.dglhip_gspmm_chunked_device(
+            msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid), ptr(ufeat2),
+            ptr(efeat2), elen, ptr(out), p["light"].numel(), ptr(p["light"]), p["num_chunks"],
+            ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
+            ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
+    elif dev.type == "cuda":
         check_call(LIB.dglhip_gspmm_device(
             msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),

@@ -107,7 +107,8 @@ class _RemappedAdj(kernel.SparseAdj):
 
 def _remap_csr(csr, eid_map):
     m = eid_map.to(csr.device)
-    return kernel.CSR(csr.indptr, csr.indices, m[csr.eid], csr.num_cols, csr.row_order)
+    return kernel.CSR(csr.indptr, csr.indices, m[csr.eid], csr.num_cols, csr.row_order,
+                      csr._host_indptr)
 
 
 def _remap_eid(adj, eid):

@@ -125,6 +125,26 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
                         int64_t efeat_len, float* out, int64_t* arg_out,
                         const int32_t* row_order, void* stream);
 
+/* Heavy-row variant (sum / mean): rows are split into a launch plan so that
+ * no single sequential chain dominates the kernel on very skewed graphs
+ * (RMAT in-degrees reach ~1e6). Light rows (light_rows[num_light]) run as in
+ * dglhip_gspmm_device. Each heavy row is cut into consecutive slot ranges
+ * [chunk_beg[c], chunk_end[c]); chunk c's sequential partial sum goes to
+ * partial[c, :] (float32[num_chunks, feat_len] workspace), and heavy row
+ * heavy_rows[h] = ((p[c0] + p[c0+1]) + ...) over its chunks
+ * c0 = heavy_chunk_ptr[h] .. heavy_chunk_ptr[h+1]-1. Deterministic; differs
+ * from the single chain only by re-association (fp32 tolerance, not bits). */
+int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
+                                const int64_t* indptr, const int32_t* indices,
+                                const int64_t* eid, const float* ufeat,
+                                const float* efeat, int64_t efeat_len, float* out,
+                                int64_t num_light, const int32_t* light_rows,
+                                int64_t num_chunks, const int64_t* chunk_beg,
+                                const int64_t* chunk_end, int64_t num_heavy,
+                                const int32_t* heavy_rows,
+                                const int64_t* heavy_chunk_ptr, float* partial,
+                                void* stream);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,
