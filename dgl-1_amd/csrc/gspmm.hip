@@ -77,42 +77,50 @@ __device__ __forceinline__ void stv(float* p, typename Vec<VEC>::T v) {
   *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
 }
 
+// Edge-feature layouts (EM template parameter):
+//  EM_FULL   : one value per edge and feature, efeat[e, f]
+//  EM_SCALAR : one scalar per edge broadcast over the row, efeat[e]
+//  EM_HEAD   : one scalar per edge and head, efeat[e, f / D] with D = F / elen
+//              (GAT's (E, H, 1) attention against (N, H, D) features)
+enum { EM_FULL = 0, EM_SCALAR = 1, EM_HEAD = 2 };
+
 // Message for slot k as a vector of VEC features starting at feature f0.
 //  COPY_U : u                     U_MUL_E: w * u (fused into the reducer)
 //  COPY_E : e
-// EB = edge feature is one scalar per edge (broadcast over features).
-template <int VEC, int MSG, bool EB>
+// `eoff` is the edge-feature column of f0 (f0, 0 or f0 / D by EM).
+template <int VEC, int MSG, int EM>
 struct SlotLoad {
   typedef typename Vec<VEC>::T V;
   V u;
   V e;
   __device__ __forceinline__ void load(const float* __restrict__ ufeat,
                                        const float* __restrict__ efeat,
-                                       int64_t F, int64_t f0, int32_t src,
-                                       int64_t edge) {
+                                       int64_t F, int64_t f0, int64_t elen, int64_t eoff,
+                                       int32_t src, int64_t edge) {
     if (MSG != DGLHIP_MSG_COPY_E) u = ldv<VEC>(ufeat + int64_t(src) * F + f0);
     if (MSG != DGLHIP_MSG_COPY_U) {
-      if (EB) e = Vec<VEC>::splat(efeat[edge]);
-      else e = ldv<VEC>(efeat + edge * F + f0);
+      if (EM == EM_FULL) e = ldv<VEC>(efeat + edge * F + f0);
+      else e = Vec<VEC>::splat(efeat[edge * elen + eoff]);
     }
   }
 };
 
 // Sequential reduction of slots [beg, end) of one row for the VEC features at
 // f0: the fma chain the reference's product runs (see the file header).
-template <int VEC, int UNROLL, int MSG, bool EB>
+template <int VEC, int UNROLL, int MSG, int EM>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
-    int64_t beg, int64_t end, int64_t F, int64_t f0, const int32_t* __restrict__ indices,
+    int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen, int64_t eoff,
+    const int32_t* __restrict__ indices,
     const int64_t* __restrict__ eid, const float* __restrict__ ufeat,
     const float* __restrict__ efeat) {
   typedef typename Vec<VEC>::T V;
   V acc = Vec<VEC>::zero();
   int64_t k = beg;
   for (; k + UNROLL <= end; k += UNROLL) {
-    SlotLoad<VEC, MSG, EB> s[UNROLL];
+    SlotLoad<VEC, MSG, EM> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
-      s[j].load(ufeat, efeat, F, f0, indices[k + j],
+      s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
                 MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
@@ -122,8 +130,9 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     }
   }
   for (; k < end; ++k) {
-    SlotLoad<VEC, MSG, EB> s;
-    s.load(ufeat, efeat, F, f0, indices[k], MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+    SlotLoad<VEC, MSG, EM> s;
+    s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
+           MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
     if (MSG == DGLHIP_MSG_COPY_U) acc += s.u;
     else if (MSG == DGLHIP_MSG_COPY_E) acc += s.e;
     else acc = Vec<VEC>::fma(s.e, s.u, acc);
@@ -135,9 +144,9 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 // lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
 // or a slot range [chunk_beg[i], chunk_end[i]) of a heavy row whose partial
 // sum goes to partial[i, :] (CHUNKED = true).
-template <int VEC, int GROUP, int UNROLL, int MSG, bool EB, bool MEAN, bool CHUNKED>
+template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
-    int64_t num_items, int64_t F, const int64_t* __restrict__ indptr,
+    int64_t num_items, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
     float* __restrict__ out, const int32_t* __restrict__ row_order,
@@ -164,7 +173,9 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     end = indptr[row + 1];
   }
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
-    V acc = reduce_range<VEC, UNROLL, MSG, EB>(beg, end, F, f0, indices, eid, ufeat, efeat);
+    const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
+    V acc = reduce_range<VEC, UNROLL, MSG, EM>(beg, end, F, f0, elen, eoff, indices, eid,
+                                               ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     stv<VEC>(out + row * F + f0, acc);
@@ -195,9 +206,9 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
 // Max-reduce kernel with argmax slot (first slot wins ties, like a strict
 // running max over the mailbox). Scalar per lane: max is VALU-light and this
 // path is off the headline metric.
-template <int MSG, bool EB>
+template <int MSG>
 __global__ __launch_bounds__(256) void gspmm_max_kernel(
-    int64_t num_rows, int64_t F, const int64_t* __restrict__ indptr,
+    int64_t num_rows, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
     float* __restrict__ out, int64_t* __restrict__ arg_out,
@@ -215,7 +226,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
       if (MSG == DGLHIP_MSG_COPY_U) {
         x = ufeat[int64_t(indices[k]) * F + f];
       } else {
-        const float e = EB ? efeat[eid[k]] : efeat[eid[k] * F + f];
+        const float e = efeat[eid[k] * elen + f / (F / elen)];
         x = MSG == DGLHIP_MSG_COPY_E ? e : ufeat[int64_t(indices[k]) * F + f] * e;
       }
       if (arg < 0 || x > best) { best = x; arg = k; }
@@ -225,10 +236,12 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
   }
 }
 
-// SDDMM dot: one wave per row, per slot a wave-wide dot product of two
-// feature rows reduced in a fixed butterfly order (deterministic).
+// SDDMM dot: one wave per row. One head (H == 1): per slot a wave-wide fma
+// dot product of two feature rows reduced in a fixed butterfly order. Several
+// heads: lane h computes head h's dot over its D = F / H features as one
+// sequential fma chain. Both orders are fixed, so results are deterministic.
 __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
-    int64_t num_rows, int64_t F, const int64_t* __restrict__ indptr,
+    int64_t num_rows, int64_t F, int64_t H, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs,
     float* __restrict__ out) {
@@ -236,13 +249,22 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   if (wave >= num_rows) return;
   const int lane = threadIdx.x & 63;
   const float* a = lhs + wave * F;
+  const int64_t D = F / H;
   for (int64_t k = indptr[wave]; k < indptr[wave + 1]; ++k) {
     const float* c = rhs + int64_t(indices[k]) * F;
-    float acc = 0.0f;
-    for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
+    if (H == 1) {
+      float acc = 0.0f;
+      for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-    if (lane == 0) out[eid[k]] = acc;
+      for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+      if (lane == 0) out[eid[k]] = acc;
+    } else {
+      for (int64_t h = lane; h < H; h += 64) {
+        float acc = 0.0f;
+        for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);
+        out[eid[k] * H + h] = acc;
+      }
+    }
   }
 }
 
@@ -311,7 +333,7 @@ static int pick_group(int64_t F, int vec) {
 }
 
 struct SumLaunch {
-  int64_t num_items, F;
+  int64_t num_items, F, elen;
   const int64_t* indptr;
   const int32_t* indices;
   const int64_t* eid;
@@ -323,7 +345,7 @@ struct SumLaunch {
   const int64_t* chunk_end;
 };
 
-template <int VEC, int GROUP, int MSG, bool EB, bool MEAN>
+template <int VEC, int GROUP, int MSG, int EM, bool MEAN>
 static void launch_sum(const SumLaunch& a, hipStream_t stream) {
   constexpr int UNROLL = (VEC == 4) ? 4 : 8;
   constexpr int ITEMS_PER_BLOCK = 4 * (64 / GROUP);
@@ -332,26 +354,28 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
   if (blocks == 0) return;
   timed_launch(stream, [&] {
     if (a.chunk_beg)
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EB, MEAN, true>),
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
-                         a.num_items, a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EB, MEAN, false>),
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
-                         a.num_items, a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
   });
 }
 
-template <int MSG, bool EB, bool MEAN>
+template <int MSG, int EM, bool MEAN>
 static void dispatch_sum_shape(const SumLaunch& a, hipStream_t stream) {
   const int64_t F = a.F;
-  const int vec = pick_vec(F, {a.ufeat, EB ? nullptr : a.efeat, a.out});
+  int vec = pick_vec(F, {a.ufeat, EM == EM_FULL ? a.efeat : nullptr, a.out});
+  // per-head weights: a lane's VEC features must stay inside one head
+  while (EM == EM_HEAD && vec > 1 && (F / a.elen) % vec != 0) vec >>= 1;
   const int group = pick_group(F, vec);
 #define DGLHIP_CASE(V, G)                                  \
   if (vec == V && group == G) {                            \
-    launch_sum<V, G, MSG, EB, MEAN>(a, stream);            \
+    launch_sum<V, G, MSG, EM, MEAN>(a, stream);            \
     return;                                                \
   }
   DGLHIP_CASE(4, 64)
@@ -363,21 +387,27 @@ static void dispatch_sum_shape(const SumLaunch& a, hipStream_t stream) {
   DGLHIP_CHECK(false, "no kernel for F=" << F << " vec=" << vec << " group=" << group);
 }
 
-static void dispatch_sum(int msg_op, bool eb, bool mean, const SumLaunch& a,
-                         hipStream_t stream) {
-#define DGLHIP_SUM(M, B)                                      \
+static int edge_mode(int64_t elen, int64_t F) {
+  return elen == F ? EM_FULL : (elen == 1 ? EM_SCALAR : EM_HEAD);
+}
+
+static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
+#define DGLHIP_SUM(M, E)                                      \
   do {                                                        \
-    if (mean) dispatch_sum_shape<M, B, true>(a, stream);      \
-    else dispatch_sum_shape<M, B, false>(a, stream);          \
+    if (mean) dispatch_sum_shape<M, E, true>(a, stream);      \
+    else dispatch_sum_shape<M, E, false>(a, stream);          \
   } while (0)
+  const int em = edge_mode(a.elen, a.F);
   if (msg_op == DGLHIP_MSG_COPY_U) {
-    DGLHIP_SUM(DGLHIP_MSG_COPY_U, false);
+    DGLHIP_SUM(DGLHIP_MSG_COPY_U, EM_SCALAR);
   } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
-    if (eb) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, true);
-    else DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, false);
+    if (em == EM_FULL) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, EM_FULL);
+    else if (em == EM_SCALAR) DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, EM_SCALAR);
+    else DGLHIP_SUM(DGLHIP_MSG_U_MUL_E, EM_HEAD);
   } else {
-    if (eb) DGLHIP_SUM(DGLHIP_MSG_COPY_E, true);
-    else DGLHIP_SUM(DGLHIP_MSG_COPY_E, false);
+    if (em == EM_FULL) DGLHIP_SUM(DGLHIP_MSG_COPY_E, EM_FULL);
+    else if (em == EM_SCALAR) DGLHIP_SUM(DGLHIP_MSG_COPY_E, EM_SCALAR);
+    else DGLHIP_SUM(DGLHIP_MSG_COPY_E, EM_HEAD);
   }
 #undef DGLHIP_SUM
 }
@@ -405,30 +435,27 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
-  DGLHIP_CHECK(!use_e || efeat_len == 1 || efeat_len == feat_len,
-               "edge feature must have length 1 or feat_len, got " << efeat_len);
-  const bool eb = efeat_len == 1;
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
+  const int64_t elen = use_e ? efeat_len : 1;
   if (reduce_op == DGLHIP_REDUCE_MAX) {
     const int64_t blocks = (num_rows + 3) / 4;
     timed_launch(stream, [&] {
-#define DGLHIP_MAX(M, B)                                                         \
-  hipLaunchKernelGGL((gspmm_max_kernel<M, B>), dim3(static_cast<unsigned>(blocks)), \
-                     dim3(256), 0, stream, num_rows, feat_len, indptr, indices,  \
-                     eid, ufeat, efeat, out, arg_out, row_order)
-      if (msg_op == DGLHIP_MSG_COPY_U) DGLHIP_MAX(DGLHIP_MSG_COPY_U, false);
-      else if (msg_op == DGLHIP_MSG_COPY_E) {
-        if (eb) DGLHIP_MAX(DGLHIP_MSG_COPY_E, true); else DGLHIP_MAX(DGLHIP_MSG_COPY_E, false);
-      } else {
-        if (eb) DGLHIP_MAX(DGLHIP_MSG_U_MUL_E, true); else DGLHIP_MAX(DGLHIP_MSG_U_MUL_E, false);
-      }
+#define DGLHIP_MAX(M)                                                          \
+  hipLaunchKernelGGL((gspmm_max_kernel<M>), dim3(static_cast<unsigned>(blocks)), \
+                     dim3(256), 0, stream, num_rows, feat_len, elen, indptr,    \
+                     indices, eid, ufeat, efeat, out, arg_out, row_order)
+      if (msg_op == DGLHIP_MSG_COPY_U) DGLHIP_MAX(DGLHIP_MSG_COPY_U);
+      else if (msg_op == DGLHIP_MSG_COPY_E) DGLHIP_MAX(DGLHIP_MSG_COPY_E);
+      else DGLHIP_MAX(DGLHIP_MSG_U_MUL_E);
 #undef DGLHIP_MAX
     });
     return 0;
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
-  SumLaunch a{num_rows, feat_len, indptr, indices, eid, ufeat, efeat, out, row_order,
+  SumLaunch a{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, row_order,
               nullptr, nullptr};
-  dispatch_sum(msg_op, eb, mean, a, stream);
+  dispatch_sum(msg_op, mean, a, stream);
   API_END();
 }
 
@@ -453,20 +480,20 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
-  DGLHIP_CHECK(!use_e || efeat_len == 1 || efeat_len == feat_len,
-               "edge feature must have length 1 or feat_len, got " << efeat_len);
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   DGLHIP_CHECK(num_chunks == 0 || (partial && chunk_beg && chunk_end), "null chunk plan");
-  const bool eb = efeat_len == 1;
+  const int64_t elen = use_e ? efeat_len : 1;
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
-    SumLaunch c{num_chunks, feat_len, indptr, indices, eid, ufeat, efeat, partial,
+    SumLaunch c{num_chunks, feat_len, elen, indptr, indices, eid, ufeat, efeat, partial,
                 nullptr, chunk_beg, chunk_end};
-    dispatch_sum(msg_op, eb, false, c, stream);
+    dispatch_sum(msg_op, false, c, stream);
   }
   if (num_light > 0) {
-    SumLaunch l{num_light, feat_len, indptr, indices, eid, ufeat, efeat, out, light_rows,
-                nullptr, nullptr};
-    dispatch_sum(msg_op, eb, mean, l, stream);
+    SumLaunch l{num_light, feat_len, elen, indptr, indices, eid, ufeat, efeat, out,
+                light_rows, nullptr, nullptr};
+    dispatch_sum(msg_op, mean, l, stream);
   }
   if (num_heavy > 0) {
     const int64_t blocks = (num_heavy + 3) / 4;
@@ -485,18 +512,20 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
 }
 
 int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
-                         const int64_t* indptr, const int32_t* indices,
+                         int64_t num_heads, const int64_t* indptr, const int32_t* indices,
                          const int64_t* eid, const float* lhs,
                          const float* rhs, float* out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
   const int64_t blocks = (num_rows + 3) / 4;
   timed_launch(stream, [&] {
     hipLaunchKernelGGL(gsddmm_dot_kernel, dim3(static_cast<unsigned>(blocks)),
-                       dim3(256), 0, stream, num_rows, feat_len, indptr,
+                       dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
                        indices, eid, lhs, rhs, out);
   });
   API_END();

@@ -182,11 +182,12 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
-  DGLHIP_CHECK(!use_e || (efeat && (efeat_len == 1 || efeat_len == feat_len)),
-               "edge feature must have length 1 or feat_len, got " << efeat_len);
+  DGLHIP_CHECK(!use_e || (efeat && efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   DGLHIP_CHECK(!use_e || eid, "eid is null");
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
   const int64_t F = feat_len;
+  const int64_t dpe = use_e ? F / efeat_len : 1;  // features per edge value
   parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
     for (int64_t r = b; r < e; ++r) {
       float* o = out + r * F;
@@ -199,8 +200,8 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
             float x;
             const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
             if (msg_op == DGLHIP_MSG_COPY_U) x = ufeat[int64_t(indices[k]) * F + f];
-            else if (msg_op == DGLHIP_MSG_COPY_E) x = er[efeat_len == 1 ? 0 : f];
-            else x = ufeat[int64_t(indices[k]) * F + f] * er[efeat_len == 1 ? 0 : f];
+            else if (msg_op == DGLHIP_MSG_COPY_E) x = er[f / dpe];
+            else x = ufeat[int64_t(indices[k]) * F + f] * er[f / dpe];
             if (arg < 0 || x > best) { best = x; arg = k; }
           }
           o[f] = arg < 0 ? 0.0f : best;
@@ -215,12 +216,12 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
         if (msg_op == DGLHIP_MSG_COPY_U) {
           for (int64_t f = 0; f < F; ++f) o[f] += ur[f];
         } else if (msg_op == DGLHIP_MSG_COPY_E) {
-          for (int64_t f = 0; f < F; ++f) o[f] += er[efeat_len == 1 ? 0 : f];
+          for (int64_t f = 0; f < F; ++f) o[f] += er[f / dpe];
         } else if (efeat_len == 1) {
           const float w = er[0];
           for (int64_t f = 0; f < F; ++f) o[f] = std::fma(w, ur[f], o[f]);
         } else {
-          for (int64_t f = 0; f < F; ++f) o[f] = std::fma(er[f], ur[f], o[f]);
+          for (int64_t f = 0; f < F; ++f) o[f] = std::fma(er[f / dpe], ur[f], o[f]);
         }
       }
       if (reduce_op == DGLHIP_REDUCE_MEAN && t - s > 1) {
@@ -232,22 +233,26 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   API_END();
 }
 
-int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
+int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
                        const int64_t* indptr, const int32_t* indices,
                        const int64_t* eid, const float* lhs, const float* rhs,
                        float* out, int num_threads) {
   API_BEGIN();
   DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
-  const int64_t F = feat_len;
+  const int64_t F = feat_len, H = num_heads, D = feat_len / num_heads;
   parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
     for (int64_t r = b; r < e; ++r) {
       const float* a = lhs + r * F;
       for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k) {
         const float* c = rhs + int64_t(indices[k]) * F;
-        float acc = 0.0f;
-        for (int64_t f = 0; f < F; ++f) acc = std::fma(a[f], c[f], acc);
-        out[eid[k]] = acc;
+        for (int64_t h = 0; h < H; ++h) {
+          float acc = 0.0f;
+          for (int64_t d = 0; d < D; ++d) acc = std::fma(a[h * D + d], c[h * D + d], acc);
+          out[eid[k] * H + h] = acc;
+        }
       }
     }
   });

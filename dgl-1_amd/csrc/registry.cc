@@ -152,26 +152,28 @@ void register_all() {
                                      I32(order, "row_order"), stream));
     }
   };
-  // (op, indptr, indices, eid, lhs, rhs, out, stream)
+  // (op, num_heads, indptr, indices, eid, lhs, rhs, out, stream)
   t["dglhip._CAPI_GSDDMM"] = [](const Args& a) {
     const int op = static_cast<int>(a.i64(0));
-    auto* indptr = a.tensor(1);
-    auto* indices = a.tensor(2);
-    auto* eid = a.tensor(3);
-    auto* lhs = a.tensor(4);
-    auto* rhs = a.tensor(5);
-    auto* out = a.tensor(6);
-    void* stream = a.handle(7);
+    const int64_t heads = a.i64(1);
+    auto* indptr = a.tensor(2);
+    auto* indices = a.tensor(3);
+    auto* eid = a.tensor(4);
+    auto* lhs = a.tensor(5);
+    auto* rhs = a.tensor(6);
+    auto* out = a.tensor(7);
+    void* stream = a.handle(8);
     same_device(out, {indptr, indices, eid, lhs, rhs});
     DGLHIP_CHECK(lhs->ndim == 2, "lhs must be 2-D");
     const int64_t rows = numel(indptr) - 1, F = lhs->shape[1];
+    DGLHIP_CHECK(numel(out) >= heads, "out too small");
     if (out->device_type == kDeviceCPU) {
-      throw_last(dglhip_gsddmm_host(op, rows, F, I64(indptr, "indptr"),
+      throw_last(dglhip_gsddmm_host(op, rows, F, heads, I64(indptr, "indptr"),
                                     I32(indices, "indices"), I64(eid, "eid"),
                                     F32(lhs, "lhs"), F32(rhs, "rhs"),
                                     F32(out, "out"), 0));
     } else {
-      throw_last(dglhip_gsddmm_device(op, rows, F, I64(indptr, "indptr"),
+      throw_last(dglhip_gsddmm_device(op, rows, F, heads, I64(indptr, "indptr"),
                                       I32(indices, "indices"), I64(eid, "eid"),
                                       F32(lhs, "lhs"), F32(rhs, "rhs"),
                                       F32(out, "out"), stream));

@@ -62,8 +62,10 @@ def _load():
                                                  _c_i64, _vp, _vp, _vp, _vp]),
         "dglhip_gspmm_host": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                        _c_i64, _vp, _vp, _c_int]),
-        "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-        "dglhip_gsddmm_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _vp, _c_int]),
+        "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                          _vp, _vp]),
+        "dglhip_gsddmm_host": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                        _vp, _c_int]),
         "dglhip_timing_enable": (_c_int, [_c_int]),
         "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),
         "DGLFuncGetGlobal": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),

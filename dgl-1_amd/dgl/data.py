@@ -130,3 +130,54 @@ def expected_reddit_edges(scale=1, self_loops=True):
     """Edge count reddit_like produces (exact by construction)."""
     return (REDDIT_EDGES * scale) // 2 * 2 + (REDDIT_NODES * scale if self_loops else 0)
 
+
+
+# -- synthetic node-classification datasets (BASELINE.json configs) -----------
+_SHAPES = {
+    # name: (nodes, directed edges without self-loops, features, classes, max/mean degree)
+    "cora": (2708, 10556, 1433, 7, 42.0),
+    "citeseer": (3327, 9228, 3703, 6, 36.0),
+    "pubmed": (19717, 88651, 500, 3, 38.0),
+    "reddit": (REDDIT_NODES, REDDIT_EDGES, 602, 41, REDDIT_MAX_OVER_MEAN),
+}
+
+
+class SyntheticNodeDataset(object):
+    """Shape-matched stand-in for the reference's citation / Reddit datasets
+    (python/dgl/data/citation_graph.py, the Reddit numbers of SURVEY.md §8a):
+    a symmetric Chung-Lu graph with the dataset's node and edge counts and
+    degree skew, row-normalised sparse binary features (dense Gaussian for
+    Reddit), random labels and 140/500/1000-style
+    train/val/test masks. ``graph`` is (src, dst) without self-loops."""
+
+    def __init__(self, name, seed=0, device="cpu"):
+        if name not in _SHAPES:
+            raise ValueError("unknown dataset %s (have %s)" % (name, sorted(_SHAPES)))
+        n, m, nfeat, ncls, ratio = _SHAPES[name]
+        self.name = name
+        src, dst, n = chung_lu(n, m, ratio, seed=seed, device=device, self_loops=False)
+        self.graph = (src, dst)
+        gen = torch.Generator(device=device)
+        gen.manual_seed(seed + 1)
+        if name == "reddit":  # dense embeddings
+            self.features = 0.1 * torch.randn(n, nfeat, generator=gen, device=device)
+        else:  # row-normalised sparse bag-of-words, as the citation loaders produce
+            bow = (torch.rand(n, nfeat, generator=gen, device=device) < 0.0127).float()
+            bow[:, 0] += (bow.sum(1) == 0).float()
+            self.features = bow / bow.sum(1, keepdim=True)
+        self.labels = torch.randint(0, ncls, (n,), generator=gen, device=device)
+        self.num_labels = ncls
+        self.num_nodes = n
+        ntrain = min(20 * ncls, n // 10) if name != "reddit" else int(0.66 * n)
+        perm = torch.randperm(n, generator=gen, device=device)
+        self.train_mask = torch.zeros(n, dtype=torch.bool, device=device)
+        self.val_mask = torch.zeros(n, dtype=torch.bool, device=device)
+        self.test_mask = torch.zeros(n, dtype=torch.bool, device=device)
+        self.train_mask[perm[:ntrain]] = True
+        self.val_mask[perm[ntrain:ntrain + min(500, n // 10)]] = True
+        self.test_mask[perm[-min(1000, n // 5):]] = True
+
+
+def load_data(name, seed=0, device="cpu"):
+    """dgl.data.load_data counterpart (python/dgl/data/__init__.py:15-25), offline."""
+    return SyntheticNodeDataset(name, seed, device)

@@ -87,6 +87,7 @@ class CSR(object):
         self._row_ids = None
         self._host_indptr = host_indptr
         self._plans = {}
+        self._max_degree = None
 
     @property
     def host_indptr(self):
@@ -96,10 +97,10 @@ class CSR(object):
 
     @property
     def max_degree(self):
-        if self.num_rows == 0:
-            return 0
-        ip = self.host_indptr
-        return int((ip[1:] - ip[:-1]).max())
+        if self._max_degree is None:
+            ip = self.host_indptr
+            self._max_degree = int((ip[1:] - ip[:-1]).max()) if self.num_rows else 0
+        return self._max_degree
 
     def split_plan(self, threshold):
         """Launch plan cutting rows longer than ``threshold`` slots into chunks
@@ -261,14 +262,24 @@ def from_coo(num_rows, num_cols, row, col, order=ORDER_EID, device=None):
 # ---------------------------------------------------------------------------
 # Raw kernel calls
 # ---------------------------------------------------------------------------
-def _efeat_len(efeat, num_edges_hint, feat_len):
-    if efeat is None:
-        return 0
-    per_edge = efeat.numel() // max(efeat.shape[0], 1) if efeat.dim() > 0 else 1
-    if per_edge != 1 and per_edge != feat_len:
-        raise DGLError("edge feature of %d values per edge cannot combine with node feature "
-                       "of %d values" % (per_edge, feat_len))
-    return per_edge
+def _edge_len(eshape, fshape):
+    """Values per edge for an edge feature of trailing shape ``eshape`` against
+    node features of trailing shape ``fshape``: 1 (scalar), F (same shape) or
+    H (leading dims of fshape, broadcast over the rest: GAT's (H, 1) vs (H, D))."""
+    eshape, fshape = tuple(eshape), tuple(fshape)
+    F = int(np.prod(fshape)) if fshape else 1
+    if eshape in ((), (1,)):
+        return 1
+    if eshape == fshape:
+        return F
+    k = len(eshape)
+    while k > 0 and eshape[k - 1] == 1:
+        k -= 1
+    if 0 < k < len(fshape) and eshape[:k] == fshape[:k] and \
+            all(d == 1 for d in eshape[k:]) and len(eshape) <= len(fshape):
+        return int(np.prod(fshape[:k]))
+    raise DGLError("edge feature shape %s does not broadcast against node feature shape %s"
+                   % (eshape, fshape))
 
 
 def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
@@ -301,17 +312,19 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
     return out, arg
 
 
-def _run_sddmm_dot(csr, lhs2, rhs2, num_edges):
+def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1):
+    """out[eid, h] = <lhs[row, head h], rhs[col, head h]>; returns (num_edges, heads)."""
     dev = lhs2.device
-    out = torch.zeros(num_edges, dtype=torch.float32, device=dev)
+    out = torch.zeros(num_edges, heads, dtype=torch.float32, device=dev)
     F = lhs2.shape[1]
     if dev.type == "cuda":
-        check_call(LIB.dglhip_gsddmm_device(0, csr.num_rows, F, ptr(csr.indptr), ptr(csr.indices),
-                                            ptr(csr.eid), ptr(lhs2), ptr(rhs2), ptr(out),
-                                            _stream_of(dev)))
+        check_call(LIB.dglhip_gsddmm_device(0, csr.num_rows, F, heads, ptr(csr.indptr),
+                                            ptr(csr.indices), ptr(csr.eid), ptr(lhs2), ptr(rhs2),
+                                            ptr(out), _stream_of(dev)))
     else:
-        check_call(LIB.dglhip_gsddmm_host(0, csr.num_rows, F, ptr(csr.indptr), ptr(csr.indices),
-                                          ptr(csr.eid), ptr(lhs2), ptr(rhs2), ptr(out), 0))
+        check_call(LIB.dglhip_gsddmm_host(0, csr.num_rows, F, heads, ptr(csr.indptr),
+                                          ptr(csr.indices), ptr(csr.eid), ptr(lhs2), ptr(rhs2),
+                                          ptr(out), 0))
     return out
 
 
@@ -369,9 +382,9 @@ class _GSpMM(torch.autograd.Function):
                     g = dout.index_select(0, rows)
                     if efeat2.shape[1] == 1:
                         g = g.sum(1, keepdim=True)
-                elif efeat2.shape[1] == 1:
-                    g = _run_sddmm_dot(fwd, dout, ufeat2.contiguous(), ctx.num_edges)
-                    de = g.unsqueeze(1)
+                elif efeat2.shape[1] < F:  # scalar or per-head weights: g-SDDMM dot
+                    de = _run_sddmm_dot(fwd, dout, ufeat2.contiguous(), ctx.num_edges,
+                                        efeat2.shape[1])
                     g = None
                 else:
                     g = dout.index_select(0, rows) * ufeat2.index_select(0, fwd.indices.long())
@@ -385,12 +398,13 @@ class _GSpMM(torch.autograd.Function):
             sl = slots[rowsel]
             g = dout[rowsel]
             fidx = rowsel[1]
+            dpe = F // efeat2.shape[1] if efeat2 is not None else 1
             if need_u:
                 src = fwd.indices.long()[sl]
                 gu = g
                 if msg == MSG_U_MUL_E:
                     e = fwd.eid[sl]
-                    gu = g * (efeat2[e, 0] if efeat2.shape[1] == 1 else efeat2[e, fidx])
+                    gu = g * efeat2[e, fidx // dpe]
                 du = torch.zeros_like(ufeat2)
                 du.index_put_((src, fidx), gu, accumulate=True)
             if need_e:
@@ -399,10 +413,7 @@ class _GSpMM(torch.autograd.Function):
                 if msg == MSG_U_MUL_E:
                     ge = g * ufeat2[fwd.indices.long()[sl], fidx]
                 de = torch.zeros_like(efeat2)
-                if efeat2.shape[1] == 1:
-                    de.index_put_((e, torch.zeros_like(e)), ge, accumulate=True)
-                else:
-                    de.index_put_((e, fidx), ge, accumulate=True)
+                de.index_put_((e, fidx // dpe), ge, accumulate=True)
         return None, None, None, None, None, du, de
 
 
@@ -435,7 +446,7 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None):
     e2 = None
     if efeat is not None:
         ne = efeat.shape[0]
-        elen = _efeat_len(efeat, ne, F)
+        elen = _edge_len(efeat.shape[1:], fshape) if ufeat is not None else F
         e2 = _f32c(efeat.reshape(ne, elen))
     if num_edges is None:
         num_edges = 0 if e2 is None else e2.shape[0]
@@ -443,13 +454,13 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None):
     return out.reshape((adj.shape[0],) + fshape) if fshape else out.reshape(adj.shape[0])
 
 
-def gsddmm_dot(adj, lhs, rhs, num_edges):
-    """out[eid] = <lhs[row], rhs[col]> for every slot of ``adj`` (no autograd)."""
+def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
+    """out[eid, h] = <lhs[row, h], rhs[col, h]> for every slot of ``adj``
+    (rows of lhs are the adjacency's rows, of rhs its columns; no autograd)."""
     dev = lhs.device
     adj = adj.to(dev)
-    F = lhs[0].numel() if lhs.shape[0] else 0
     return _run_sddmm_dot(adj.fwd, _f32c(lhs.reshape(lhs.shape[0], -1)),
-                          _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges)
+                          _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges, heads)
 
 
 def timing_enable(flag=True):

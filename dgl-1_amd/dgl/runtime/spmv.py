@@ -39,12 +39,12 @@ def kernel_feat_ok(mfn, nf, ef):
         if e.dtype != torch.float32:
             return False
         if name == "u_mul_e":
-            es = tuple(e.shape[1:])
-            us = tuple(nf[mfn.src_field].shape[1:])
-            scalar = len(es) == 0 or es == (1,)
-            if not scalar and es != us:
+            u = nf[mfn.src_field]
+            try:
+                kernel._edge_len(e.shape[1:], u.shape[1:])
+            except DGLError:
                 return False
-            if name == "u_mul_e" and not scalar and (e.device != nf[mfn.src_field].device):
+            if e.device != u.device:
                 return False
     return True
 

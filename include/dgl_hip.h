@@ -109,7 +109,9 @@ int dglhip_coo_to_csr_device(int64_t num_rows, int64_t num_cols, int64_t nnz,
 
 /* efeat_len: 0 (no edge feature), 1 (one scalar per edge, broadcast over the
  * feature row; the only case the reference specialises, message.py:37-44),
- * or feat_len (one value per edge and feature).
+ * feat_len (one value per edge and feature), or any H dividing feat_len (one
+ * value per edge and head, broadcast over the D = feat_len / H consecutive
+ * features of that head: GAT's (E, H, 1) attention x (N, H, D) features).
  * arg_out (int64[num_rows*feat_len], may be NULL): for MAX, the CSR slot that
  * won each element (-1 for empty rows); needed by the backward.
  * row_order (int32[num_rows], may be NULL): launch schedule (a permutation);
@@ -156,17 +158,20 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
 /* ------------------------------------------------------------------------ */
 /* g-SDDMM: per-edge products feeding the backward of u_mul_e and the GAT    */
 /* edge attention (gat/train.py:74-96).                                      */
-/*   DOT : out[eid[k]] = sum_f lhs[r,f] * rhs[indices[k],f]   (r = row of k) */
+/*   DOT : out[eid[k], h] = sum_{d<D} lhs[r, hD+d] * rhs[indices[k], hD+d]   */
+/*         (r = row of slot k, H = num_heads, D = feat_len / H)              */
 /* ------------------------------------------------------------------------ */
 #define DGLHIP_SDDMM_DOT 0
 int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
-                         const int64_t* indptr, const int32_t* indices,
-                         const int64_t* eid, const float* lhs,
-                         const float* rhs, float* out, void* stream);
+                         int64_t num_heads, const int64_t* indptr,
+                         const int32_t* indices, const int64_t* eid,
+                         const float* lhs, const float* rhs, float* out,
+                         void* stream);
 int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
-                       const int64_t* indptr, const int32_t* indices,
-                       const int64_t* eid, const float* lhs, const float* rhs,
-                       float* out, int num_threads);
+                       int64_t num_heads, const int64_t* indptr,
+                       const int32_t* indices, const int64_t* eid,
+                       const float* lhs, const float* rhs, float* out,
+                       int num_threads);
 
 /* ------------------------------------------------------------------------ */
 /* Kernel timing (measurement support for bench.py): when enabled, every     */
@@ -229,8 +234,8 @@ int DGLFuncFree(DGLHipFunctionHandle func);
  *   "dglhip._CAPI_GSpMM"        (msg, reduce, indptr, indices, eid, ufeat,
  *                                efeat|null, out, arg_out|null,
  *                                row_order|null, stream)
- *   "dglhip._CAPI_GSDDMM"       (op, indptr, indices, eid, lhs, rhs, out,
- *                                stream)
+ *   "dglhip._CAPI_GSDDMM"       (op, num_heads, indptr, indices, eid, lhs, rhs,
+ *                                out, stream)
  *   "dglhip._CAPI_COOToCSR"     (num_rows, row, col, order, indptr, indices,
  *                                eid)
  *   "dglhip._CAPI_RowsByDegree" (indptr, row_order)

@@ -1,0 +1,52 @@
+"""The BASELINE config drivers run end to end (few epochs): GCN (configs 0/1)
+and GAT (config 2) on synthetic shape-matched data, on CPU and — under the
+`gpu` marker — on the MI355X."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "examples", "gcn"))
+sys.path.insert(0, os.path.join(ROOT, "examples", "gat"))
+
+import gcn_spmv  # noqa: E402
+import train as gat_train  # noqa: E402
+
+
+def _gpu_arg(device):
+    if device == "cuda":
+        if not torch.cuda.is_available():
+            pytest.skip("no ROCm device")
+        return "0"
+    return "-1"
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_gcn_cora(device):
+    args = gcn_spmv.parser().parse_args(["--dataset", "cora", "--n-epochs", "30",
+                                         "--gpu", _gpu_arg(device)])
+    res = gcn_spmv.run(args)
+    assert res["edges"] == 10556 + 2708
+    assert res["loss"] < 1.95 and torch.isfinite(torch.tensor(res["loss"]))
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_gat_cora(device):
+    args = gat_train.parser().parse_args(["--dataset", "cora", "--epochs", "8",
+                                          "--gpu", _gpu_arg(device)])
+    res = gat_train.run(args)
+    assert torch.isfinite(torch.tensor(res["loss"]))
+
+
+@pytest.mark.gpu
+def test_gcn_reddit_gpu():
+    """configs[1]: 2-layer GCN, hidden 128, Reddit-shaped, full graph on one GPU."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    args = gcn_spmv.parser().parse_args(["--dataset", "reddit", "--n-epochs", "6", "--gpu", "0",
+                                         "--n-hidden", "128"])
+    res = gcn_spmv.run(args)
+    print("reddit gcn epoch", res)
+    assert torch.isfinite(torch.tensor(res["loss"]))

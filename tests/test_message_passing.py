@@ -308,3 +308,35 @@ def test_graph_queries():
     assert g.ndata["x"][:, 0].tolist() == [0, 1, 1, 0]
     g.add_nodes(1)
     assert g.ndata["x"].shape == (5, 2)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_gat_head_broadcast(device):
+    """GAT: update_all(src_mul_edge(ft (N,H,D), a (E,H,1)), sum) fused in the kernel
+    (gat/train.py:77-78) == the materialised UDF path, forward and gradients."""
+    dev = _dev(device)
+    rng = np.random.default_rng(21)
+    n, m, H, D = 300, 4000, 8, 8
+    src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+    ft = torch.from_numpy(rng.standard_normal((n, H, D)).astype(np.float32)).to(dev)
+    a = torch.from_numpy(rng.uniform(0, 1, (m, H, 1)).astype(np.float32)).to(dev)
+    G = torch.from_numpy(rng.standard_normal((n, H, D)).astype(np.float32)).to(dev)
+    outs = []
+    for fused in (True, False):
+        g = dgl.DGLGraph(multigraph=True)
+        g.add_nodes(n)
+        g.add_edges(src, dst)
+        f1, a1 = ft.clone().requires_grad_(True), a.clone().requires_grad_(True)
+        g.ndata["ft"] = f1
+        g.edata["a"] = a1
+        with ir.prog() as p:
+            if fused:
+                g.update_all(fn.src_mul_edge("ft", "a", "m"), fn.sum("m", "o"))
+            else:
+                g.update_all(lambda e: {"m": e.src["ft"] * e.data["a"]},
+                             lambda nd: {"o": nd.mailbox["m"].sum(1)})
+        assert ("SPMV" in p.opcodes()) == fused
+        g.ndata["o"].backward(G)
+        outs.append((g.ndata["o"].detach().cpu(), f1.grad.cpu(), a1.grad.cpu()))
+    for x, y in zip(outs[0], outs[1]):
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)

@@ -29,6 +29,10 @@ for s in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 1 \
         --graph-scale 0.05 --dist-backend gloo > gpurun_out/dist.json 2> gpurun_out/dist.err
       rc=$?; tail -3 gpurun_out/dist.err; cat gpurun_out/dist.json; [ $rc -eq 0 ] || exit $rc ;;
+    rmat)
+      timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
+        --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
+      rc=$?; tail -4 gpurun_out/rmat.err; cat gpurun_out/rmat.json; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
