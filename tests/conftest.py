@@ -25,3 +25,13 @@ def load_golden(name):
 @pytest.fixture
 def golden():
     return load_golden
+
+
+def load_example(relpath, name):
+    """Import an example script by path under a unique module name."""
+    import importlib.util
+    path = os.path.join(ROOT, "examples", relpath)
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod

@@ -60,3 +60,40 @@ def test_balanced_bounds():
     assert b.tolist()[0] == 0 and b.tolist()[-1] == 10
     assert all(x <= y for x, y in zip(b.tolist(), b.tolist()[1:]))
     assert balanced_bounds(torch.zeros(0, dtype=torch.int64), 4).tolist() == [0, 0, 0, 0, 0]
+
+
+def _sage_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dgl-1_amd"), os.path.join(root, "tests")]
+    from conftest import load_example
+    sage = load_example("graphsage/train.py", "sage_train")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        args = sage.parser().parse_args(["--graph", "rmat", "--rmat-scale", "11", "--gpu", "-1",
+                                         "--dist", "--n-epochs", "3", "--in-feats", "16",
+                                         "--n-hidden", "16", "--n-classes", "5"])
+        res = sage.run(args)
+        if rank == 0:
+            q.put({k: v.numpy() for k, v in res["state"].items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graphsage_distributed_matches_single():
+    """Three training steps of GraphSAGE-mean on 2 gloo ranks (halo all-gather,
+    reduce-scatter backward, DDP all-reduce) == the single-process run."""
+    from conftest import load_example
+    sage = load_example("graphsage/train.py", "sage_train")
+    args = sage.parser().parse_args(["--graph", "rmat", "--rmat-scale", "11", "--gpu", "-1",
+                                     "--n-epochs", "3", "--in-feats", "16", "--n-hidden", "16",
+                                     "--n-classes", "5"])
+    single = sage.run(args)["state"]
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.spawn(_sage_worker, args=(2, _free_port(), q), nprocs=2, join=True)
+    multi = q.get()
+    for k, v in single.items():
+        np.testing.assert_allclose(multi[k], v.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)

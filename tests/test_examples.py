@@ -1,18 +1,14 @@
 """The BASELINE config drivers run end to end (few epochs): GCN (configs 0/1)
 and GAT (config 2) on synthetic shape-matched data, on CPU and — under the
 `gpu` marker — on the MI355X."""
-import os
-import sys
-
 import pytest
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(ROOT, "examples", "gcn"))
-sys.path.insert(0, os.path.join(ROOT, "examples", "gat"))
+from conftest import load_example
 
-import gcn_spmv  # noqa: E402
-import train as gat_train  # noqa: E402
+gcn_spmv = load_example("gcn/gcn_spmv.py", "gcn_spmv")
+gat_train = load_example("gat/train.py", "gat_train")
+sage_train = load_example("graphsage/train.py", "sage_train")
 
 
 def _gpu_arg(device):
@@ -49,4 +45,12 @@ def test_gcn_reddit_gpu():
                                          "--n-hidden", "128"])
     res = gcn_spmv.run(args)
     print("reddit gcn epoch", res)
+    assert torch.isfinite(torch.tensor(res["loss"]))
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_graphsage_mean(device):
+    args = sage_train.parser().parse_args(["--dataset", "cora", "--n-epochs", "5",
+                                           "--gpu", _gpu_arg(device), "--n-hidden", "32"])
+    res = sage_train.run(args)
     assert torch.isfinite(torch.tensor(res["loss"]))

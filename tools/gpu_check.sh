@@ -29,6 +29,12 @@ for s in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 1 \
         --graph-scale 0.05 --dist-backend gloo > gpurun_out/dist.json 2> gpurun_out/dist.err
       rc=$?; tail -3 gpurun_out/dist.err; cat gpurun_out/dist.json; [ $rc -eq 0 ] || exit $rc ;;
+    examples)
+      ( timeout -k 10 600 python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 --n-hidden 128 --n-epochs 20 &&
+        timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset cora --gpu 0 --n-epochs 50 &&
+        timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 ) \
+        > gpurun_out/examples.log 2>&1
+      rc=$?; tail -4 gpurun_out/examples.log; [ $rc -eq 0 ] || exit $rc ;;
     rmat)
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
