@@ -140,6 +140,13 @@ def main():
                          "rmat: one fixed Graph500 R-MAT graph partitioned over the ranks "
                          "(strong scaling, heavy rows chunked)")
     ap.add_argument("--rmat-scale", type=int, default=26)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="single-GPU study: build the x N graph, keep rank 0's partition and "
+                         "time its local g-SpMM against the full (all-gathered) feature matrix "
+                         "(no communication; not a driver line)")
+    ap.add_argument("--pipeline-chunks", type=int, default=4,
+                    help="N>1: halo all-gather chunks overlapped with the local g-SpMM "
+                         "(0 = one all-gather, then the kernel; bit-exact rows)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
                          "to rehearse the multi-rank path")
@@ -193,6 +200,26 @@ def main():
         def step():
             kernel.gspmm(adj, "copy_u", "sum", h)
         parallelism = "single GPU (kernel API; heavy rows chunked)"
+    elif world == 1 and args.emulate_world > 1:
+        from dgl.distributed import balanced_bounds
+        del src, dst
+        W = args.emulate_world
+        src, dst, n = data.reddit_like(scale=W, seed=0, device=dev)
+        num_edges_total = int(src.numel())
+        bounds = balanced_bounds(torch.bincount(dst, minlength=n), W)
+        lo, hi = int(bounds[0]), int(bounds[1])
+        sel = (dst >= lo) & (dst < hi)
+        adj = kernel.from_coo(hi - lo, n, dst[sel] - lo, src[sel], kernel.ORDER_EID, dev)
+        num_local_edges, num_rows = int(sel.sum()), hi - lo
+        num_edges_total = num_local_edges  # value = this rank's edges / its time
+        h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+        del sel
+
+        def step():
+            kernel.gspmm(adj, "copy_u", "sum", h)
+        parallelism = "emulated rank 0 of %d (local g-SpMM only, H = %.0f MB)" % (
+            W, n * FEAT * 4 / 1e6)
+        args.no_cpu_baseline = True
     elif world == 1:
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))
         h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
@@ -211,7 +238,8 @@ def main():
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         sel = (dst >= lo) & (dst < hi)
-        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev)
+        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
+                              pipeline_chunks=args.pipeline_chunks)
         h_full = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         h_local = h_full[lo:hi].contiguous()
         del h_full, sel
@@ -219,7 +247,9 @@ def main():
 
         def step():
             pg.update_all(h_local)
-        parallelism = "%d-way 1-D dst-row partition, RCCL all-gather halo" % world
+        parallelism = "%d-way 1-D dst-row partition, RCCL all-gather halo%s" % (
+            world, " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
+            if args.pipeline_chunks > 0 else "")
     del src, dst
     torch.cuda.synchronize()
     log("setup done in %.1fs; peak HBM %.1f GB" % (time.time() - t0,

@@ -109,12 +109,10 @@ struct SlotLoad {
 // f0: the fma chain the reference's product runs (see the file header).
 template <int VEC, int UNROLL, int MSG, int EM>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
-    int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen, int64_t eoff,
-    const int32_t* __restrict__ indices,
+    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen,
+    int64_t eoff, const int32_t* __restrict__ indices,
     const int64_t* __restrict__ eid, const float* __restrict__ ufeat,
     const float* __restrict__ efeat) {
-  typedef typename Vec<VEC>::T V;
-  V acc = Vec<VEC>::zero();
   int64_t k = beg;
   for (; k + UNROLL <= end; k += UNROLL) {
     SlotLoad<VEC, MSG, EM> s[UNROLL];
@@ -142,9 +140,11 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 
 // Sum-reduce kernel (also MEAN). GROUP lanes per work item, VEC floats per
 // lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
-// or a slot range [chunk_beg[i], chunk_end[i]) of a heavy row whose partial
-// sum goes to partial[i, :] (CHUNKED = true).
-template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED>
+// or a slot range [chunk_beg[i], chunk_end[i]) whose sum goes to out[i, :]
+// (CHUNKED = true). With ACCUM the chain continues from the value already in
+// out[i, :] (segment-by-segment evaluation of one sequential chain).
+template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
+          bool ACCUM>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     int64_t num_items, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
@@ -174,8 +174,9 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   }
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
-    V acc = reduce_range<VEC, UNROLL, MSG, EM>(beg, end, F, f0, elen, eoff, indices, eid,
-                                               ufeat, efeat);
+    V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
+    acc = reduce_range<VEC, UNROLL, MSG, EM>(acc, beg, end, F, f0, elen, eoff, indices, eid,
+                                             ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     stv<VEC>(out + row * F + f0, acc);
@@ -343,6 +344,7 @@ struct SumLaunch {
   const int32_t* row_order;
   const int64_t* chunk_beg;  // non-null: chunked launch (partials to `out`)
   const int64_t* chunk_end;
+  bool accumulate;           // chunked launch continuing the chain in `out`
 };
 
 template <int VEC, int GROUP, int MSG, int EM, bool MEAN>
@@ -353,13 +355,18 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
   if (blocks == 0) return;
   timed_launch(stream, [&] {
-    if (a.chunk_beg)
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true>),
+    if (a.chunk_beg && a.accumulate)
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.out, a.row_order, a.chunk_beg, a.chunk_end);
+    else if (a.chunk_beg)
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false>),
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, false>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
@@ -454,7 +461,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   SumLaunch a{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, row_order,
-              nullptr, nullptr};
+              nullptr, nullptr, false};
   dispatch_sum(msg_op, mean, a, stream);
   API_END();
 }
@@ -487,12 +494,12 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
     SumLaunch c{num_chunks, feat_len, elen, indptr, indices, eid, ufeat, efeat, partial,
-                nullptr, chunk_beg, chunk_end};
+                nullptr, chunk_beg, chunk_end, false};
     dispatch_sum(msg_op, false, c, stream);
   }
   if (num_light > 0) {
     SumLaunch l{num_light, feat_len, elen, indptr, indices, eid, ufeat, efeat, out,
-                light_rows, nullptr, nullptr};
+                light_rows, nullptr, nullptr, false};
     dispatch_sum(msg_op, mean, l, stream);
   }
   if (num_heavy > 0) {
@@ -508,6 +515,29 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                            heavy_chunk_ptr, partial, out);
     });
   }
+  API_END();
+}
+
+int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
+                               const int64_t* item_beg, const int64_t* item_end,
+                               int accumulate, const int32_t* indices, const int64_t* eid,
+                               const float* ufeat, const float* efeat, int64_t efeat_len,
+                               float* out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(num_items >= 0 && feat_len >= 0, "negative size");
+  if (num_items == 0 || feat_len == 0) return 0;
+  const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
+  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  DGLHIP_CHECK(item_beg && item_end && out, "null ranges/out");
+  DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
+  DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
+  SumLaunch a{num_items, feat_len, use_e ? efeat_len : 1, nullptr, indices, eid, ufeat, efeat,
+              out, nullptr, item_beg, item_end, accumulate != 0};
+  dispatch_sum(msg_op, false, a, stream);
   API_END();
 }
 

@@ -233,6 +233,38 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   API_END();
 }
 
+int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
+                             const int64_t* item_beg, const int64_t* item_end,
+                             int accumulate, const int32_t* indices, const int64_t* eid,
+                             const float* ufeat, const float* efeat, int64_t efeat_len,
+                             float* out, int num_threads) {
+  API_BEGIN();
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  if (num_items == 0 || feat_len == 0) return 0;
+  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  DGLHIP_CHECK(!use_e || (efeat && eid && efeat_len >= 1 && feat_len % efeat_len == 0),
+               "bad edge feature");
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  const int64_t F = feat_len, dpe = use_e ? F / efeat_len : 1;
+  parallel_for(num_items, nt, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      float* o = out + i * F;
+      if (!accumulate)
+        for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
+      for (int64_t k = item_beg[i]; k < item_end[i]; ++k) {
+        const float* ur = msg_op != DGLHIP_MSG_COPY_E ? ufeat + int64_t(indices[k]) * F : nullptr;
+        const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+        for (int64_t f = 0; f < F; ++f) {
+          if (msg_op == DGLHIP_MSG_COPY_U) o[f] += ur[f];
+          else if (msg_op == DGLHIP_MSG_COPY_E) o[f] += er[f / dpe];
+          else o[f] = std::fma(er[f / dpe], ur[f], o[f]);
+        }
+      }
+    }
+  });
+  API_END();
+}
+
 int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
                        const int64_t* indptr, const int32_t* indices,
                        const int64_t* eid, const float* lhs, const float* rhs,

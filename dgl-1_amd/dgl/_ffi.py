@@ -60,6 +60,10 @@ def _load():
         "dglhip_gspmm_chunked_device": (_c_int, [_c_int, _c_int, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                  _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp,
                                                  _c_i64, _vp, _vp, _vp, _vp]),
+        "dglhip_gspmm_ranges_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
+                                                _vp, _vp, _c_i64, _vp, _vp]),
+        "dglhip_gspmm_ranges_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
+                                              _vp, _vp, _c_i64, _vp, _c_int]),
         "dglhip_gspmm_host": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                        _c_i64, _vp, _vp, _c_int]),
         "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,

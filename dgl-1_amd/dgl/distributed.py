@@ -17,6 +17,16 @@ Column ids of the local CSR are remapped once (at partition time) from global
 node ids to positions in the padded all-gather buffer, so the kernel runs
 unchanged. Row results are bit-identical to the single-GPU product: each
 local row accumulates exactly the same edges in the same edge-id order.
+
+Pipelined forward (``pipeline_chunks = C > 0``, inference / benchmarking):
+each row's slots are grouped into segments — sources this rank owns first,
+then the remote sources of halo chunk 1..C — so the own segment is reduced
+while the halo is still in flight, and each remote segment as soon as its
+chunk's all-gather (on a separate HIP stream) lands. The row's fma chain is
+continued segment by segment (dglhip_gspmm_ranges_device, accumulate), so
+the result is one sequential chain in (segment, edge-id) order: deterministic
+and within fp32 tolerance of the edge-id-order chain (bit-identical when edge
+ids already run in source order, as in bench.py's graphs).
 """
 from __future__ import absolute_import
 
@@ -79,7 +89,7 @@ class PartitionedGraph(object):
     group     : torch.distributed process group (default world)
     """
 
-    def __init__(self, num_nodes, src, dst, bounds, device, group=None):
+    def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
@@ -96,9 +106,37 @@ class PartitionedGraph(object):
         owner = torch.searchsorted(b, src, right=True) - 1
         cols = owner * self.max_rows + (src - b[owner])
         self.num_edges = int(src.numel())
-        self.adj = kernel.from_coo(self.num_local, self.world * self.max_rows, dst - self.lo,
-                                   cols, kernel.ORDER_EID, device)
         self.device = device
+        self.chunks = int(pipeline_chunks)
+        if self.chunks > 0:
+            self._build_pipeline(src, dst, b, owner)
+            self.adj = None
+        else:
+            self.adj = kernel.from_coo(self.num_local, self.world * self.max_rows,
+                                       dst - self.lo, cols, kernel.ORDER_EID, device)
+
+    def _build_pipeline(self, src, dst, b, owner):
+        C, P, R = self.chunks, self.world, self.num_local
+        cr = -(-self.max_rows // C)  # rows per halo chunk
+        self.chunk_rows = cr
+        j = src - b[owner]                      # index inside the owner's block
+        c = j // cr
+        own = owner == self.rank
+        # own sources index h_local directly; remote ones the chunked halo buffer
+        cols = torch.where(own, j, c * (P * cr) + owner * cr + (j - c * cr))
+        seg = torch.where(own, torch.zeros_like(c), c + 1)
+        S = C + 1
+        vrow = (dst - self.lo) * S + seg
+        csr = kernel.build_csr(R * S, max(P * cr * C, R), vrow, cols, kernel.ORDER_EID,
+                               self.device, schedule=False)
+        ip = csr.indptr
+        self.seg_ranges = [(ip[s:R * S:S].contiguous(), ip[s + 1:R * S + 1:S].contiguous())
+                           for s in range(S)]
+        self.pipe_csr = csr
+        self.halo = None
+        # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
+        overlap = self.device.type == "cuda" and dist.get_backend(self.group) == "nccl"
+        self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
 
     def gather_halo(self, h_local):
         """All-gather of the padded row blocks (RCCL all_gather_into_tensor)."""
@@ -106,5 +144,47 @@ class PartitionedGraph(object):
 
     def update_all(self, h_local, msg="copy_u", reduce="sum", efeat=None):
         """Local rows of update_all(msg, reduce) given this rank's node features."""
+        if self.chunks > 0:
+            if msg != "copy_u" or reduce != "sum" or h_local.requires_grad:
+                raise ValueError("the pipelined forward covers copy_u + sum without autograd")
+            return self._pipelined_copy_sum(h_local)
         full = self.gather_halo(h_local)
         return kernel.gspmm(self.adj, msg, reduce, full, efeat)
+
+    def _pipelined_copy_sum(self, h_local):
+        C, P, cr = self.chunks, self.world, self.chunk_rows
+        F = h_local.shape[1]
+        dev = self.device
+        if self.halo is None or self.halo.shape[1] != F:
+            self.halo = torch.empty(C * P * cr, F, device=dev)
+            self.hpad = torch.zeros(C * cr, F, device=dev)
+        self.hpad[:self.num_local].copy_(h_local)
+        out = torch.empty(self.num_local, F, device=dev)
+        ind = self.pipe_csr.indices
+        beg, end = self.seg_ranges[0]
+        events = []
+        if self.comm_stream is not None:
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ready)
+                for c in range(C):
+                    dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
+                                                self.hpad[c * cr:(c + 1) * cr],
+                                                group=self.group)
+                    ev = torch.cuda.Event()
+                    ev.record(self.comm_stream)
+                    events.append(ev)
+        # own sources while the halo is in flight
+        kernel.gspmm_ranges("copy_u", beg, end, False, ind, out, ufeat=h_local.contiguous())
+        for c in range(C):
+            if self.comm_stream is not None:
+                torch.cuda.current_stream(dev).wait_event(events[c])
+            else:
+                dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
+                                            self.hpad[c * cr:(c + 1) * cr], group=self.group)
+            beg, end = self.seg_ranges[c + 1]
+            kernel.gspmm_ranges("copy_u", beg, end, True, ind, out, ufeat=self.halo)
+        if self.comm_stream is not None:
+            self.halo.record_stream(torch.cuda.current_stream(dev))
+        return out

@@ -463,6 +463,23 @@ def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
                           _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges, heads)
 
 
+def gspmm_ranges(msg, beg, end, accumulate, indices, out, ufeat=None, efeat=None, eid=None):
+    """out[i] (=|+=) sum over slots [beg[i], end[i]) of MSG(ufeat[indices[k]], efeat[eid[k]]),
+    each row one sequential chain (continued from ``out`` when ``accumulate``).
+    Raw op without autograd (the pipelined distributed forward)."""
+    msg = _MSG_NAMES.get(msg, msg)
+    dev = out.device
+    F = out.shape[1]
+    elen = 0 if efeat is None else efeat.shape[1]
+    args = (msg, beg.numel(), F, ptr(beg), ptr(end), 1 if accumulate else 0, ptr(indices),
+            ptr(eid), ptr(ufeat), ptr(efeat), elen, ptr(out))
+    if dev.type == "cuda":
+        check_call(LIB.dglhip_gspmm_ranges_device(*(args + (_stream_of(dev),))))
+    else:
+        check_call(LIB.dglhip_gspmm_ranges_host(*(args + (0,))))
+    return out
+
+
 def timing_enable(flag=True):
     """Bracket every g-SpMM/g-SDDMM launch with hipEvents (bench support)."""
     check_call(LIB.dglhip_timing_enable(1 if flag else 0))

@@ -147,6 +147,25 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 const int64_t* heavy_chunk_ptr, float* partial,
                                 void* stream);
 
+/* Range-list g-SpMM (sum): for every item i, out[i, :] = (accumulate ?
+ * out[i, :] : 0) (+)= chain over slots [item_beg[i], item_end[i]) in slot
+ * order. With accumulate the chain of a row can be evaluated segment by
+ * segment (e.g. as its source features arrive over the network) and equals
+ * the single chain over the concatenated segments bit for bit. */
+int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
+                               const int64_t* item_beg, const int64_t* item_end,
+                               int accumulate, const int32_t* indices,
+                               const int64_t* eid, const float* ufeat,
+                               const float* efeat, int64_t efeat_len, float* out,
+                               void* stream);
+
+int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
+                             const int64_t* item_beg, const int64_t* item_end,
+                             int accumulate, const int32_t* indices,
+                             const int64_t* eid, const float* ufeat,
+                             const float* efeat, int64_t efeat_len, float* out,
+                             int num_threads);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,

@@ -97,3 +97,36 @@ def test_graphsage_distributed_matches_single():
     multi = q.get()
     for k, v in single.items():
         np.testing.assert_allclose(multi[k], v.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
+
+
+def _pipe_worker(rank, world, port):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
+    from dgl import data
+    from dgl.distributed import PartitionedGraph, balanced_bounds
+    from oracle import oracle as O
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, F = 2500, 8
+        src, dst, n = data.chung_lu(n, 30 * n, 30.0, seed=5)  # edge ids in (src, dst) order
+        bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        sel = (dst >= lo) & (dst < hi)
+        H = torch.rand(n, F, generator=torch.Generator().manual_seed(2)) * 2 - 1
+        ref = O.spmm_coo(n, dst.numpy(), src.numpy(), H.numpy())[lo:hi]
+        for chunks in (1, 3):
+            pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu", pipeline_chunks=chunks)
+            out = pg.update_all(H[lo:hi].contiguous()).numpy()
+            np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+            # deterministic
+            assert np.array_equal(out, pg.update_all(H[lo:hi].contiguous()).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipelined_forward(world):
+    mp.spawn(_pipe_worker, args=(world, _free_port()), nprocs=world, join=True)

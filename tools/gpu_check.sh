@@ -35,6 +35,17 @@ for s in $STEPS; do
         timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 ) \
         > gpurun_out/examples.log 2>&1
       rc=$?; tail -4 gpurun_out/examples.log; [ $rc -eq 0 ] || exit $rc ;;
+    emul)
+      for w in 2 4 8; do
+        timeout -k 10 600 python bench.py --emulate-world $w --steps 10 --warmup 3 --no-traffic \
+          > gpurun_out/emul_$w.json 2> gpurun_out/emul_$w.err
+        rc=$?; tail -2 gpurun_out/emul_$w.err; cat gpurun_out/emul_$w.json; [ $rc -eq 0 ] || exit $rc
+      done ;;
+    gcnprof)
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gcnprof -o run \
+        --output-format csv -- python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 \
+        --n-hidden 128 --n-epochs 8 > gpurun_out/gcnprof.log 2>&1
+      rc=$?; tail -2 gpurun_out/gcnprof.log; [ $rc -eq 0 ] || exit $rc ;;
     rmat)
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
