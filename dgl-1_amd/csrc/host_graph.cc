@@ -265,6 +265,65 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
   API_END();
 }
 
+int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks, int64_t in_block,
+                                 int64_t out_block, const int64_t* indptr,
+                                 const int32_t* indices, const int64_t* eid,
+                                 const int64_t* etype, const float* ufeat,
+                                 const float* weight, const float* enorm, float* out,
+                                 int num_threads) {
+  API_BEGIN();
+  DGLHIP_CHECK(num_rows >= 0 && num_blocks > 0 && in_block > 0 && out_block > 0, "bad sizes");
+  const int64_t nb = num_blocks, si = in_block, so = out_block;
+  const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  parallel_for(num_rows, nt, [&](int64_t b0, int64_t b1, int) {
+    for (int64_t row = b0; row < b1; ++row) {
+      float* o = out + row * Fo;
+      for (int64_t jg = 0; jg < Fo; ++jg) o[jg] = 0.0f;
+      for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
+        const int64_t e = eid[k];
+        const float* h = ufeat + int64_t(indices[k]) * Fi;
+        const float* w = weight + etype[e] * wr;
+        const float nrm = enorm ? enorm[e] : 1.0f;
+        for (int64_t jg = 0; jg < Fo; ++jg) {
+          const int64_t b = jg / so, j = jg - b * so;
+          float m = 0.0f;
+          for (int64_t i = 0; i < si; ++i) m = std::fma(h[b * si + i], w[b * si * so + i * so + j], m);
+          o[jg] = std::fma(nrm, m, o[jg]);
+        }
+      }
+    }
+  });
+  API_END();
+}
+
+int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks, int64_t in_block,
+                                  int64_t out_block, const int64_t* rel_ptr,
+                                  const int32_t* rel_src, const int64_t* rel_eid,
+                                  const int64_t* edge_dst, const float* ufeat,
+                                  const float* dout, const float* enorm, float* dweight,
+                                  int num_threads) {
+  API_BEGIN();
+  const int64_t nb = num_blocks, si = in_block, so = out_block;
+  const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  parallel_for(num_rels * wr, nt, [&](int64_t b0, int64_t b1, int) {
+    for (int64_t idx = b0; idx < b1; ++idx) {
+      const int64_t r = idx / wr, rem = idx - r * wr;
+      const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
+      float acc = 0.0f;
+      for (int64_t k = rel_ptr[r]; k < rel_ptr[r + 1]; ++k) {
+        const int64_t e = rel_eid[k];
+        const float x = ufeat[int64_t(rel_src[k]) * Fi + b * si + i];
+        const float g = dout[edge_dst[e] * Fo + b * so + j];
+        acc = std::fma(enorm ? enorm[e] * x : x, g, acc);
+      }
+      dweight[idx] = acc;
+    }
+  });
+  API_END();
+}
+
 int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
                        const int64_t* indptr, const int32_t* indices,
                        const int64_t* eid, const float* lhs, const float* rhs,

@@ -1,0 +1,152 @@
+// Typed-edge block-diagonal g-SpMM for R-GCN.
+//
+// Replaces the reference's R-GCN block layer message path
+// (examples/pytorch/rgcn/layers.py:121-132): per edge, gather h[src] and the
+// relation's block-diagonal weight W[type] (num_blocks blocks of
+// in_block x out_block), multiply with torch.bmm into an E x out message
+// tensor, then reduce by destination (builtin sum -> incidence SPMV /
+// degree bucketing). Here the three steps are one kernel over the
+// destination-major CSR: each wave owns a destination row; lanes own output
+// features; per in-edge the wave reads the source row and the relation's
+// weight block (hot in L2: the whole weight tensor of FB15k-237's 474
+// relations x 100 blocks x 5 x 5 is 4.7 MB) and accumulates
+//   out[v, b*so + j] += norm_e * sum_i h[u, b*si + i] * W[r, b, i, j]
+// in CSR-slot order. No E x out message tensor is materialised.
+//
+// The backward runs the same kernel over the transposed CSR with the blocks
+// transposed (dH), and a relation-grouped kernel for dW in which every
+// weight element is one sequential chain over that relation's edges
+// (deterministic; no atomics).
+#include <hip/hip_runtime.h>
+
+#include "../../include/dgl_hip.h"
+#include "common.h"
+
+namespace dglhip {
+
+#define HIP_CALL(expr)                                                        \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    DGLHIP_CHECK(_e == hipSuccess, #expr << " -> " << hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+
+constexpr int kMaxPass = 16;  // output features per lane: 64 * 16 = 1024 max
+
+template <int PASS>
+__global__ __launch_bounds__(256) void typed_block_spmm_kernel(
+    int64_t num_rows, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const int64_t* __restrict__ etype, const float* __restrict__ ufeat,
+    const float* __restrict__ weight, const float* __restrict__ enorm,
+    float* __restrict__ out) {
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) +
+                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (row >= num_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
+  float acc[PASS];
+#pragma unroll
+  for (int t = 0; t < PASS; ++t) acc[t] = 0.0f;
+  for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
+    const int64_t e = eid[k];
+    const float* h = ufeat + int64_t(indices[k]) * Fi;
+    const float* w = weight + etype[e] * wr;
+    const float nrm = enorm ? enorm[e] : 1.0f;
+#pragma unroll
+    for (int t = 0; t < PASS; ++t) {
+      const int64_t jg = lane + 64 * t;
+      if (jg < Fo) {
+        const int64_t b = jg / so, j = jg - b * so;
+        const float* hb = h + b * si;
+        const float* wb = w + b * si * so + j;
+        float m = 0.0f;
+        for (int64_t i = 0; i < si; ++i) m = __builtin_fmaf(hb[i], wb[i * so], m);
+        acc[t] = __builtin_fmaf(nrm, m, acc[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < PASS; ++t) {
+    const int64_t jg = lane + 64 * t;
+    if (jg < Fo) out[row * Fo + jg] = acc[t];
+  }
+}
+
+// dW[r, b, i, j] = sum over edges e of relation r (edge-id order) of
+//   norm_e * h[src_e, b*si + i] * dout[dst_e, b*so + j]
+__global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
+    int64_t num_rels, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ rel_ptr,
+    const int32_t* __restrict__ rel_src, const int64_t* __restrict__ rel_eid,
+    const int64_t* __restrict__ edge_dst, const float* __restrict__ ufeat,
+    const float* __restrict__ dout, const float* __restrict__ enorm, float* __restrict__ dw) {
+  const int64_t wr = nb * si * so;
+  const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (idx >= num_rels * wr) return;
+  const int64_t r = idx / wr, rem = idx - r * wr;
+  const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
+  const int64_t Fi = nb * si, Fo = nb * so;
+  float acc = 0.0f;
+  for (int64_t k = rel_ptr[r]; k < rel_ptr[r + 1]; ++k) {
+    const int64_t e = rel_eid[k];
+    const float x = ufeat[int64_t(rel_src[k]) * Fi + b * si + i];
+    const float g = dout[edge_dst[e] * Fo + b * so + j];
+    acc = __builtin_fmaf(enorm ? enorm[e] * x : x, g, acc);
+  }
+  dw[idx] = acc;
+}
+
+}  // namespace
+}  // namespace dglhip
+
+using namespace dglhip;
+
+extern "C" {
+
+int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t in_block,
+                                   int64_t out_block, const int64_t* indptr,
+                                   const int32_t* indices, const int64_t* eid,
+                                   const int64_t* etype, const float* ufeat,
+                                   const float* weight, const float* enorm, float* out,
+                                   void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && num_blocks > 0 && in_block > 0 && out_block > 0,
+               "bad sizes");
+  const int64_t Fo = num_blocks * out_block;
+  DGLHIP_CHECK(Fo <= 64 * kMaxPass, "output width " << Fo << " exceeds " << 64 * kMaxPass);
+  if (num_rows == 0) return 0;
+  const int64_t pass = (Fo + 63) / 64;
+  const dim3 grid(static_cast<unsigned>((num_rows + 3) / 4)), block(256);
+#define DGLHIP_TB(P)                                                                    \
+  if (pass <= P) {                                                                     \
+    hipLaunchKernelGGL(typed_block_spmm_kernel<P>, grid, block, 0, stream, num_rows,   \
+                       num_blocks, in_block, out_block, indptr, indices, eid, etype,   \
+                       ufeat, weight, enorm, out);                                     \
+    HIP_CALL(hipGetLastError());                                                       \
+    return 0;                                                                          \
+  }
+  DGLHIP_TB(1) DGLHIP_TB(2) DGLHIP_TB(4) DGLHIP_TB(8) DGLHIP_TB(16)
+#undef DGLHIP_TB
+  API_END();
+}
+
+int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks, int64_t in_block,
+                                    int64_t out_block, const int64_t* rel_ptr,
+                                    const int32_t* rel_src, const int64_t* rel_eid,
+                                    const int64_t* edge_dst, const float* ufeat,
+                                    const float* dout, const float* enorm, float* dweight,
+                                    void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  const int64_t total = num_rels * num_blocks * in_block * out_block;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(typed_block_wgrad_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+                     dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
+                     rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);
+  HIP_CALL(hipGetLastError());
+  API_END();
+}
+
+}  // extern "C"

@@ -491,3 +491,86 @@ def timing_read():
     n = ctypes.c_int64()
     check_call(LIB.dglhip_timing_read(ctypes.byref(ms), ctypes.byref(n)))
     return ms.value, n.value
+
+
+# ---------------------------------------------------------------------------
+# Typed-edge block-diagonal g-SpMM (R-GCN block layer)
+# ---------------------------------------------------------------------------
+def _run_typed_block(csr, ufeat2, weight, etype, enorm, nb, si, so):
+    dev = ufeat2.device
+    out = torch.empty(csr.num_rows, nb * so, dtype=torch.float32, device=dev)
+    args = (csr.num_rows, nb, si, so, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
+            ptr(etype), ptr(ufeat2), ptr(weight), ptr(enorm), ptr(out))
+    if dev.type == "cuda":
+        check_call(LIB.dglhip_typed_block_spmm_device(*(args + (_stream_of(dev),))))
+    else:
+        check_call(LIB.dglhip_typed_block_spmm_host(*(args + (0,))))
+    return out
+
+
+class _RelationGroups(object):
+    """Relation-major grouping of an adjacency's edges for the weight gradient."""
+
+    def __init__(self, fwd, etype, num_rels, num_edges):
+        rows = fwd.row_ids()
+        rel_of_slot = etype[fwd.eid]
+        rel = build_csr(num_rels, max(fwd.num_cols, 1), rel_of_slot, fwd.indices.long(),
+                        ORDER_EID, fwd.device, schedule=False)
+        self.ptr = rel.indptr
+        self.src = rel.indices
+        self.eid = fwd.eid[rel.eid]
+        self.edge_dst = torch.zeros(num_edges, dtype=torch.int64, device=fwd.device)
+        self.edge_dst[fwd.eid] = rows
+
+
+class _TypedBlock(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj, etype, num_rels, ufeat2, weight, enorm):
+        R, nb, si, so = weight.shape
+        out = _run_typed_block(adj.fwd, ufeat2, weight, etype, enorm, nb, si, so)
+        ctx.adj, ctx.num_rels = adj, num_rels
+        ctx.save_for_backward(etype, ufeat2, weight, enorm)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        etype, ufeat2, weight, enorm = ctx.saved_tensors
+        adj = ctx.adj
+        R, nb, si, so = weight.shape
+        dout = dout.contiguous()
+        du = dw = None
+        if ctx.needs_input_grad[3]:
+            wt = weight.transpose(2, 3).contiguous()  # (R, nb, so, si)
+            du = _run_typed_block(adj.bwd, dout, wt, etype, enorm, nb, so, si)
+        if ctx.needs_input_grad[4]:
+            if getattr(adj, "_rel_groups", None) is None:
+                adj._rel_groups = _RelationGroups(adj.fwd, etype, R, etype.numel())
+            g = adj._rel_groups
+            dw = torch.empty_like(weight)
+            args = (R, nb, si, so, ptr(g.ptr), ptr(g.src), ptr(g.eid), ptr(g.edge_dst),
+                    ptr(ufeat2), ptr(dout), ptr(enorm), ptr(dw))
+            if dout.is_cuda:
+                check_call(LIB.dglhip_typed_block_wgrad_device(*(args + (_stream_of(dout.device),))))
+            else:
+                check_call(LIB.dglhip_typed_block_wgrad_host(*(args + (0,))))
+        return None, None, None, du, dw, None
+
+
+def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
+    """R-GCN block-diagonal message passing in one kernel:
+    out[v] = sum_{e=(u->v)} enorm[e] * blockdiag(weight[etype[e]]) applied to ufeat[u].
+
+    adj    : SparseAdj (rows = destinations) on the features' device
+    ufeat  : (num_src, nb * si) float32
+    weight : (num_rels, nb, si, so) float32 (autograd)
+    etype  : (num_edges,) int64 relation of each edge id
+    enorm  : optional (num_edges,) float32 per-edge scale (not differentiated)
+    """
+    dev = ufeat.device
+    adj = adj.to(dev)
+    R, nb, si, so = weight.shape
+    if ufeat.shape[1] != nb * si:
+        raise DGLError("ufeat width %d != num_blocks * in_block %d" % (ufeat.shape[1], nb * si))
+    etype = etype.to(device=dev, dtype=torch.int64).contiguous()
+    en = None if enorm is None else _f32c(enorm.to(dev).reshape(-1).detach())
+    return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en)

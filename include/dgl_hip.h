@@ -193,6 +193,42 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
                        int num_threads);
 
 /* ------------------------------------------------------------------------ */
+/* Typed-edge block-diagonal g-SpMM (R-GCN block layer, examples/pytorch/    */
+/* rgcn/layers.py:121-132): with Fi = nb*si, Fo = nb*so,                     */
+/*   out[r, b*so+j] = sum_{slot k of row r} norm[e] *                       */
+/*                    sum_i ufeat[indices[k], b*si+i] * weight[type[e],b,i,j]*/
+/* (e = eid[k]; norm may be NULL = 1). One sequential chain per output      */
+/* element in slot order. weight is float32[R, nb, si, so]; etype int64[E]. */
+/* ------------------------------------------------------------------------ */
+int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks,
+                                   int64_t in_block, int64_t out_block,
+                                   const int64_t* indptr, const int32_t* indices,
+                                   const int64_t* eid, const int64_t* etype,
+                                   const float* ufeat, const float* weight,
+                                   const float* enorm, float* out, void* stream);
+int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks,
+                                 int64_t in_block, int64_t out_block,
+                                 const int64_t* indptr, const int32_t* indices,
+                                 const int64_t* eid, const int64_t* etype,
+                                 const float* ufeat, const float* weight,
+                                 const float* enorm, float* out, int num_threads);
+/* Weight gradient: dweight[r,b,i,j] = sum over the edges of relation r
+ * (relation-major CSR rel_ptr[R+1] / rel_src / rel_eid, edge-id order) of
+ * norm[e] * ufeat[src, b*si+i] * dout[edge_dst[e], b*so+j]. */
+int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks,
+                                    int64_t in_block, int64_t out_block,
+                                    const int64_t* rel_ptr, const int32_t* rel_src,
+                                    const int64_t* rel_eid, const int64_t* edge_dst,
+                                    const float* ufeat, const float* dout,
+                                    const float* enorm, float* dweight, void* stream);
+int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
+                                  int64_t in_block, int64_t out_block,
+                                  const int64_t* rel_ptr, const int32_t* rel_src,
+                                  const int64_t* rel_eid, const int64_t* edge_dst,
+                                  const float* ufeat, const float* dout,
+                                  const float* enorm, float* dweight, int num_threads);
+
+/* ------------------------------------------------------------------------ */
 /* Kernel timing (measurement support for bench.py): when enabled, every     */
 /* g-SpMM launch is bracketed by a pair of hipEvents on its own stream.     */
 /* ------------------------------------------------------------------------ */

@@ -54,3 +54,18 @@ def test_graphsage_mean(device):
                                            "--gpu", _gpu_arg(device), "--n-hidden", "32"])
     res = sage_train.run(args)
     assert torch.isfinite(torch.tensor(res["loss"]))
+
+
+rgcn = load_example("rgcn/link_predict.py", "rgcn_link_predict")
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_rgcn_fused_matches_udf(device):
+    """configs[4] driver: the fused typed-edge kernel and the reference's UDF
+    formulation train to the same loss."""
+    base = ["--n-epochs", "3", "--gpu", _gpu_arg(device), "--n-hidden", "40", "--n-bases",
+            "8", "--graph-batch-size", "3000", "--num-entities", "2000", "--num-rels", "20",
+            "--num-triples", "20000", "--dropout", "0"]
+    fused = rgcn.run(rgcn.parser().parse_args(base))
+    udf = rgcn.run(rgcn.parser().parse_args(base + ["--udf"]))
+    assert abs(fused["loss"] - udf["loss"]) < 1e-4 * max(1.0, abs(udf["loss"]))
