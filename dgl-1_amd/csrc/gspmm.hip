@@ -14,8 +14,8 @@
 //    cross-lane reduction is needed: every output element is a sequential
 //    fma chain over the row's CSR slots — the exact arithmetic of the
 //    reference's CPU product, hence bit-exact parity.
-//  * Memory-level parallelism comes from UNROLL independent row gathers in
-//    flight per wave plus many waves per SIMD (low VGPR count). With a whole
+//  * Memory-level parallelism comes from UNROLL (16) independent row gathers
+//    in flight per wave plus several waves per SIMD. With a whole
 //    wave per row the CSR slot stream is wave-uniform: column ids and edge
 //    weights come through the scalar cache (s_load), not VGPRs.
 //  * Rows are launched in degree-descending order (row_order) so the longest
@@ -138,13 +138,45 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
   return acc;
 }
 
+// Software-pipelined variant of reduce_range (copy_u only): the gathers of
+// batch t+1 are issued before batch t is accumulated, so 2 x UNROLL row
+// reads stay in flight across iterations instead of draining every batch.
+// Same per-element operation order (bit-identical results).
+template <int VEC, int UNROLL>
+__device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
+    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0,
+    const int32_t* __restrict__ indices, const float* __restrict__ ufeat) {
+  typedef typename Vec<VEC>::T V;
+  int64_t k = beg;
+  if (k + UNROLL <= end) {
+    V cur[UNROLL];
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j) cur[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * F + f0);
+    k += UNROLL;
+    for (; k + UNROLL <= end; k += UNROLL) {
+      V nxt[UNROLL];
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j)
+        nxt[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * F + f0);
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j) acc += cur[j];
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j) cur[j] = nxt[j];
+    }
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j) acc += cur[j];
+  }
+  for (; k < end; ++k) acc += ldv<VEC>(ufeat + int64_t(indices[k]) * F + f0);
+  return acc;
+}
+
 // Sum-reduce kernel (also MEAN). GROUP lanes per work item, VEC floats per
 // lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
 // or a slot range [chunk_beg[i], chunk_end[i]) whose sum goes to out[i, :]
 // (CHUNKED = true). With ACCUM the chain continues from the value already in
 // out[i, :] (segment-by-segment evaluation of one sequential chain).
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
-          bool ACCUM>
+          bool ACCUM, bool PIPE = false>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     int64_t num_items, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
@@ -175,8 +207,11 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
     V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
-    acc = reduce_range<VEC, UNROLL, MSG, EM>(acc, beg, end, F, f0, elen, eoff, indices, eid,
-                                             ufeat, efeat);
+    if (PIPE && MSG == DGLHIP_MSG_COPY_U)
+      acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, F, f0, indices, ufeat);
+    else
+      acc = reduce_range<VEC, UNROLL, MSG, EM>(acc, beg, end, F, f0, elen, eoff, indices, eid,
+                                               ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     stv<VEC>(out + row * F + f0, acc);
@@ -347,9 +382,16 @@ struct SumLaunch {
   bool accumulate;           // chunked launch continuing the chain in `out`
 };
 
-template <int VEC, int GROUP, int MSG, int EM, bool MEAN>
+// Tuning override for the copy_u + sum shape (dglhip_set_spmm_variant);
+// 0 = automatic choice.
+static int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
+
+template <int VEC, int GROUP, int MSG, int EM, bool MEAN, int UNROLL_OVERRIDE = 0,
+          bool PIPE = false>
 static void launch_sum(const SumLaunch& a, hipStream_t stream) {
-  constexpr int UNROLL = (VEC == 4) ? 4 : 8;
+  // 16 row gathers in flight per lane group: measured +22% over 8 on HBM-bound
+  // RMAT (tools/kernel_sweep.py), neutral on the MALL-resident Reddit table
+  constexpr int UNROLL = UNROLL_OVERRIDE ? UNROLL_OVERRIDE : ((VEC == 4) ? 8 : 16);
   constexpr int ITEMS_PER_BLOCK = 4 * (64 / GROUP);
   const int64_t blocks = (a.num_items + ITEMS_PER_BLOCK - 1) / ITEMS_PER_BLOCK;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
@@ -366,7 +408,7 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, false>),
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, false, PIPE>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
@@ -374,8 +416,28 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
 }
 
 template <int MSG, int EM, bool MEAN>
+static bool dispatch_variant(const SumLaunch& a, hipStream_t stream) {
+  if (MSG != DGLHIP_MSG_COPY_U || MEAN || g_var_vec == 0) return false;
+  const int v = g_var_vec, gr = g_var_group, u = g_var_unroll, pp = g_var_pipe;
+  if (int64_t(v) * gr < a.F && (a.F % (int64_t(v) * gr)) != 0) return false;
+  if (a.F % v != 0) return false;
+#define DGLHIP_VAR(V, G, U, P)                                                   \
+  if (v == V && gr == G && u == U && pp == P) {                                \
+    launch_sum<V, G, MSG, EM, MEAN, U, P>(a, stream);                          \
+    return true;                                                               \
+  }
+  DGLHIP_VAR(2, 64, 4, 0) DGLHIP_VAR(2, 64, 8, 0) DGLHIP_VAR(2, 64, 16, 0)
+  DGLHIP_VAR(2, 64, 32, 0) DGLHIP_VAR(4, 32, 8, 0) DGLHIP_VAR(4, 32, 16, 0)
+  DGLHIP_VAR(4, 32, 32, 0) DGLHIP_VAR(2, 64, 8, 1) DGLHIP_VAR(2, 64, 16, 1)
+  DGLHIP_VAR(4, 32, 8, 1) DGLHIP_VAR(4, 32, 16, 1)
+#undef DGLHIP_VAR
+  return false;
+}
+
+template <int MSG, int EM, bool MEAN>
 static void dispatch_sum_shape(const SumLaunch& a, hipStream_t stream) {
   const int64_t F = a.F;
+  if (dispatch_variant<MSG, EM, MEAN>(a, stream)) return;
   int vec = pick_vec(F, {a.ufeat, EM == EM_FULL ? a.efeat : nullptr, a.out});
   // per-head weights: a lane's VEC features must stay inside one head
   while (EM == EM_HEAD && vec > 1 && (F / a.elen) % vec != 0) vec >>= 1;
@@ -558,6 +620,19 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                        dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
                        indices, eid, lhs, rhs, out);
   });
+  API_END();
+}
+
+int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {
+  API_BEGIN();
+  DGLHIP_CHECK((vec == 0) || ((vec == 1 || vec == 2 || vec == 4) &&
+                              (group == 32 || group == 64) &&
+                              (unroll == 4 || unroll == 8 || unroll == 16 || unroll == 32)),
+               "unsupported variant " << vec << "," << group << "," << unroll);
+  g_var_vec = vec;
+  g_var_group = group;
+  g_var_unroll = unroll;
+  g_var_pipe = pipelined ? 1 : 0;
   API_END();
 }
 

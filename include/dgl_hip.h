@@ -233,6 +233,11 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
 /* g-SpMM launch is bracketed by a pair of hipEvents on its own stream.     */
 /* ------------------------------------------------------------------------ */
 int dglhip_timing_enable(int enable);
+/* Tuning knob for copy_u + sum: force (vec floats/lane, lanes/row, gathers
+ * per batch, software-pipelined batches) for subsequent launches; vec = 0
+ * restores the automatic choice. Results are identical for every variant
+ * (same per-element chain). */
+int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined);
 /* Synchronises on the recorded events and returns the summed kernel time
  * (ms) and launch count since the last enable/reset. */
 int dglhip_timing_read(double* total_ms, int64_t* launches);

@@ -192,3 +192,21 @@ def test_heavy_row_split(cuda, msg, reduce):
     assert np.array_equal(split1[light], exact[light])
     scale = np.abs(exact).max()
     np.testing.assert_allclose(split1, exact, rtol=1e-5, atol=1e-5 * scale)
+
+
+def test_full_reddit_bench_graph_bit_exact(cuda):
+    """The bench workload at full size (BASELINE configs[1] shape: 232,965 nodes,
+    114.8M edges, F=128) through update_all on the MI355X == the oracle's
+    multi-core restatement, bit for bit."""
+    import dgl.function as fn
+    from dgl import data
+    src, dst, n = data.reddit_like(scale=1, seed=0, device=cuda)
+    gen = torch.Generator(device=cuda).manual_seed(1)
+    h = torch.rand(n, 128, generator=gen, device=cuda) * 2 - 1
+    g = dgl.DGLGraph((src.cpu(), dst.cpu()))
+    g.ndata["h"] = h
+    g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+    out = g.ndata["o"].cpu().numpy()
+    ip, ix, pos = O.coo_to_csr(n, dst.cpu().numpy(), src.cpu().numpy())
+    ref = O.spmm_csr(ip, ix, pos, h.cpu().numpy(), num_threads=16)
+    assert np.array_equal(out, ref)

@@ -49,6 +49,10 @@ for s in $STEPS; do
         --output-format csv -- python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 \
         --n-hidden 128 --n-epochs 8 > gpurun_out/gcnprof.log 2>&1
       rc=$?; tail -2 gpurun_out/gcnprof.log; [ $rc -eq 0 ] || exit $rc ;;
+    sweep)
+      timeout -k 10 600 python tools/kernel_sweep.py > gpurun_out/sweep_reddit.json 2> gpurun_out/sweep.err &&
+      timeout -k 10 600 python tools/kernel_sweep.py --workload rmat --rmat-scale 25 > gpurun_out/sweep_rmat.json 2>> gpurun_out/sweep.err
+      rc=$?; cat gpurun_out/sweep_reddit.json gpurun_out/sweep_rmat.json; [ $rc -eq 0 ] || exit $rc ;;
     rmat)
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
