@@ -304,6 +304,27 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   }
 }
 
+// GAT edge attention, one wave per destination row v (gat/train.py:90-96):
+//   out[eid[k], h] = clamp(exp(leaky_relu(lhs[u, h] + rhs[v, h], alpha)), lo, hi)
+// with u = indices[k]; lanes run over the row's (slot, head) pairs.
+__global__ __launch_bounds__(256) void gsddmm_attention_kernel(
+    int64_t num_rows, int64_t H, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const float* __restrict__ lhs, const float* __restrict__ rhs, float alpha, float lo,
+    float hi, int apply_exp, float* __restrict__ out) {
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= num_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t beg = indptr[row], n = (indptr[row + 1] - beg) * H;
+  for (int64_t idx = lane; idx < n; idx += 64) {
+    const int64_t k = beg + idx / H, h = idx - (idx / H) * H;
+    float x = lhs[int64_t(indices[k]) * H + h] + rhs[row * H + h];
+    x = x > 0.0f ? x : alpha * x;
+    if (apply_exp) x = __expf(x);
+    out[eid[k] * H + h] = fminf(fmaxf(x, lo), hi);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Timing support: hipEvent pairs around each launch, on the launch stream.
 // ---------------------------------------------------------------------------
@@ -633,6 +654,23 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {
   g_var_group = group;
   g_var_unroll = unroll;
   g_var_pipe = pipelined ? 1 : 0;
+  API_END();
+}
+
+int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
+                                   const int64_t* indptr, const int32_t* indices,
+                                   const int64_t* eid, const float* lhs, const float* rhs,
+                                   float alpha, float clamp_lo, float clamp_hi, int apply_exp,
+                                   float* out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && num_heads >= 1, "bad sizes");
+  if (num_rows == 0) return 0;
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(gsddmm_attention_kernel, dim3(static_cast<unsigned>((num_rows + 3) / 4)),
+                       dim3(256), 0, stream, num_rows, num_heads, indptr, indices, eid, lhs,
+                       rhs, alpha, clamp_lo, clamp_hi, apply_exp, out);
+  });
   API_END();
 }
 

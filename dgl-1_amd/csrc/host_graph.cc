@@ -324,6 +324,27 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks, int64_t 
   API_END();
 }
 
+int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads, const int64_t* indptr,
+                                 const int32_t* indices, const int64_t* eid, const float* lhs,
+                                 const float* rhs, float alpha, float clamp_lo,
+                                 float clamp_hi, int apply_exp, float* out,
+                                 int num_threads) {
+  API_BEGIN();
+  const int64_t H = num_heads;
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
+    for (int64_t r = b; r < e; ++r)
+      for (int64_t k = indptr[r]; k < indptr[r + 1]; ++k)
+        for (int64_t h = 0; h < H; ++h) {
+          float x = lhs[int64_t(indices[k]) * H + h] + rhs[r * H + h];
+          x = x > 0.0f ? x : alpha * x;
+          if (apply_exp) x = std::exp(x);
+          out[eid[k] * H + h] = std::min(std::max(x, clamp_lo), clamp_hi);
+        }
+  });
+  API_END();
+}
+
 int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
                        const int64_t* indptr, const int32_t* indices,
                        const int64_t* eid, const float* lhs, const float* rhs,

@@ -68,6 +68,12 @@ def _load():
         "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_c_int]),
         "dglhip_typed_block_wgrad_device": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_vp]),
         "dglhip_typed_block_wgrad_host": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_c_int]),
+        "dglhip_gsddmm_attention_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                                    ctypes.c_float, ctypes.c_float,
+                                                    ctypes.c_float, _c_int, _vp, _vp]),
+        "dglhip_gsddmm_attention_host": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+                                                  ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                  _c_int, _vp, _c_int]),
         "dglhip_gspmm_host": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                        _c_i64, _vp, _vp, _c_int]),
         "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,

@@ -574,3 +574,56 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
     etype = etype.to(device=dev, dtype=torch.int64).contiguous()
     en = None if enorm is None else _f32c(enorm.to(dev).reshape(-1).detach())
     return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en)
+
+
+# ---------------------------------------------------------------------------
+# GAT edge attention (fused u_add_v g-SDDMM + leaky_relu + exp + clamp)
+# ---------------------------------------------------------------------------
+class _EdgeAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, adj, num_edges, alpha, lo, hi, apply_exp, a_src, a_dst):
+        fwd = adj.fwd
+        H = a_src.shape[1]
+        out = torch.empty(num_edges, H, dtype=torch.float32, device=a_src.device)
+        args = (fwd.num_rows, H, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.eid), ptr(a_src),
+                ptr(a_dst), float(alpha), float(lo), float(hi), 1 if apply_exp else 0, ptr(out))
+        if a_src.is_cuda:
+            check_call(LIB.dglhip_gsddmm_attention_device(*(args + (_stream_of(a_src.device),))))
+        else:
+            check_call(LIB.dglhip_gsddmm_attention_host(*(args + (0,))))
+        ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp = adj, alpha, lo, hi, apply_exp
+        ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (out,) = ctx.saved_tensors
+        # d/dx clamp(exp(lrelu(x))): out * lrelu'(x) where not clamped
+        inside = (out > ctx.lo) & (out < ctx.hi)
+        if ctx.apply_exp:
+            # lrelu(x) = log(out); slope alpha where lrelu(x) < 0  <=>  out < 1
+            slope = torch.where(out < 1, torch.full_like(out, ctx.alpha), torch.ones_like(out))
+            g = dout * out * slope
+        else:
+            slope = torch.where(out < 0, torch.full_like(out, ctx.alpha), torch.ones_like(out))
+            g = dout * slope
+        g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
+        adj = ctx.adj
+        # sum the per-edge gradient at the source (transposed CSR) and destination
+        H = g.shape[1]
+        d_src, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False)
+        d_dst, _ = _run_gspmm(adj.fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False)
+        return None, None, None, None, None, None, d_src, d_dst
+
+
+def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
+                   apply_exp=True):
+    """Per-edge, per-head GAT attention in one kernel:
+    clamp(exp(leaky_relu(a_src[u] + a_dst[v], alpha))) for every edge u -> v,
+    returned as (num_edges, H) indexed by edge id. Differentiable in a_src/a_dst."""
+    dev = a_src.device
+    adj = adj.to(dev)
+    H = a_src.reshape(a_src.shape[0], -1).shape[1]
+    return _EdgeAttention.apply(adj, int(num_edges), float(alpha), float(clamp[0]),
+                                float(clamp[1]), bool(apply_exp),
+                                _f32c(a_src.reshape(-1, H)), _f32c(a_dst.reshape(-1, H)))

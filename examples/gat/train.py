@@ -1,8 +1,9 @@
 """Graph Attention Network on the engine (counterpart of the reference's
 examples/pytorch/gat/train.py; BASELINE.json configs[2]: 8 heads on Pubmed).
 
-Per layer: an edge UDF computes the unnormalised attention
-exp(leaky_relu(a_l[src] + a_r[dst])) (E x H x 1), then ONE
+Per layer: the unnormalised attention exp(leaky_relu(a_l[src] + a_r[dst]))
+(E x H x 1) comes from one fused g-SDDMM kernel (dgl.kernel.edge_attention;
+``--udf`` runs the reference's edge UDF instead), then ONE
 ``update_all([src_mul_edge('ft','a_drop','ft'), copy_edge('a','a')],
 [sum('ft','ft'), sum('a','z')])`` — on this engine both pairs are fused
 g-SpMMs (per-head edge weights broadcast over the head's features, and the
@@ -23,14 +24,17 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
                                 "dgl-1_amd"))
 import dgl.function as fn  # noqa: E402
-from dgl import DGLGraph  # noqa: E402
+from dgl import DGLGraph, kernel  # noqa: E402
 from dgl.data import load_data  # noqa: E402
 
 
 class GraphAttention(nn.Module):
-    def __init__(self, g, in_dim, out_dim, num_heads, feat_drop, attn_drop, alpha, residual):
+    def __init__(self, g, in_dim, out_dim, num_heads, feat_drop, attn_drop, alpha, residual,
+                 udf=False):
         super(GraphAttention, self).__init__()
         self.g = g
+        self.udf = udf
+        self.alpha = alpha
         self.num_heads = num_heads
         self.fc = nn.Linear(in_dim, num_heads * out_dim, bias=False)
         self.feat_drop = nn.Dropout(feat_drop) if feat_drop else None
@@ -55,8 +59,16 @@ class GraphAttention(nn.Module):
         a2 = torch.bmm(head_ft, self.attn_r).transpose(0, 1)           # N x H x 1
         if self.feat_drop is not None:
             ft = self.feat_drop(ft)
-        self.g.ndata.update({"ft": ft, "a1": a1.contiguous(), "a2": a2.contiguous()})
-        self.g.apply_edges(self.edge_attention)
+        if self.udf:  # the reference's edge UDF (gat/train.py:90-96)
+            self.g.ndata.update({"ft": ft, "a1": a1.contiguous(), "a2": a2.contiguous()})
+            self.g.apply_edges(self.edge_attention)
+        else:  # fused u_add_v -> leaky_relu -> exp -> clamp g-SDDMM
+            self.g.ndata["ft"] = ft
+            a = kernel.edge_attention(self.g.sparse_adjacency(h.device), a1, a2,
+                                      self.g.number_of_edges(), self.alpha)
+            a = a.unsqueeze(-1)  # E x H x 1
+            a_drop = self.attn_drop(a) if self.attn_drop is not None else a
+            self.g.edata.update({"a": a, "a_drop": a_drop})
         self.g.update_all([fn.src_mul_edge("ft", "a_drop", "ft"), fn.copy_edge("a", "a")],
                           [fn.sum("ft", "ft"), fn.sum("a", "z")])
         ret = self.g.ndata["ft"] / self.g.ndata["z"]
@@ -75,16 +87,16 @@ class GraphAttention(nn.Module):
 
 class GAT(nn.Module):
     def __init__(self, g, num_layers, in_dim, num_hidden, num_classes, heads, activation,
-                 feat_drop, attn_drop, alpha, residual):
+                 feat_drop, attn_drop, alpha, residual, udf=False):
         super(GAT, self).__init__()
         self.activation = activation
         self.layers = nn.ModuleList([GraphAttention(g, in_dim, num_hidden, heads[0], feat_drop,
-                                                    attn_drop, alpha, False)])
+                                                    attn_drop, alpha, False, udf)])
         for i in range(1, num_layers):
             self.layers.append(GraphAttention(g, num_hidden * heads[i - 1], num_hidden, heads[i],
-                                              feat_drop, attn_drop, alpha, residual))
+                                              feat_drop, attn_drop, alpha, residual, udf))
         self.layers.append(GraphAttention(g, num_hidden * heads[-2], num_classes, heads[-1],
-                                          feat_drop, attn_drop, alpha, residual))
+                                          feat_drop, attn_drop, alpha, residual, udf))
 
     def forward(self, h):
         for layer in self.layers[:-1]:
@@ -101,7 +113,7 @@ def run(args):
     torch.manual_seed(args.seed)
     heads = [args.num_heads] * args.num_layers + [args.num_out_heads]
     model = GAT(g, args.num_layers, data.features.shape[1], args.num_hidden, data.num_labels,
-                heads, F.elu, args.in_drop, args.attn_drop, args.alpha, args.residual)
+                heads, F.elu, args.in_drop, args.attn_drop, args.alpha, args.residual, args.udf)
     model = model.to(device)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=args.weight_decay)
     dur = []
@@ -140,6 +152,7 @@ def parser():
     p.add_argument("--weight-decay", type=float, default=5e-4)
     p.add_argument("--alpha", type=float, default=0.2)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--udf", action="store_true", help="reference edge UDF for the attention")
     return p
 
 

@@ -192,6 +192,22 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
                        const float* lhs, const float* rhs, float* out,
                        int num_threads);
 
+/* GAT edge attention (gat/train.py:90-96), fused u_add_v SDDMM + activation:
+ *   out[eid[k], h] = clamp(act(lhs[indices[k], h] + rhs[r, h]), lo, hi),
+ *   act(x) = exp(leaky_relu(x, alpha)) if apply_exp else leaky_relu(x, alpha)
+ * lhs: [num_src, H], rhs: [num_rows, H], out: [num_edges, H]. */
+int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
+                                   const int64_t* indptr, const int32_t* indices,
+                                   const int64_t* eid, const float* lhs,
+                                   const float* rhs, float alpha, float clamp_lo,
+                                   float clamp_hi, int apply_exp, float* out,
+                                   void* stream);
+int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads,
+                                 const int64_t* indptr, const int32_t* indices,
+                                 const int64_t* eid, const float* lhs, const float* rhs,
+                                 float alpha, float clamp_lo, float clamp_hi,
+                                 int apply_exp, float* out, int num_threads);
+
 /* ------------------------------------------------------------------------ */
 /* Typed-edge block-diagonal g-SpMM (R-GCN block layer, examples/pytorch/    */
 /* rgcn/layers.py:121-132): with Fi = nb*si, Fo = nb*so,                     */

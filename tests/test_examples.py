@@ -30,10 +30,12 @@ def test_gcn_cora(device):
 
 @pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
 def test_gat_cora(device):
-    args = gat_train.parser().parse_args(["--dataset", "cora", "--epochs", "8",
-                                          "--gpu", _gpu_arg(device)])
-    res = gat_train.run(args)
-    assert torch.isfinite(torch.tensor(res["loss"]))
+    base = ["--dataset", "cora", "--epochs", "8", "--gpu", _gpu_arg(device), "--in-drop", "0",
+            "--attn-drop", "0"]
+    fused = gat_train.run(gat_train.parser().parse_args(base))
+    udf = gat_train.run(gat_train.parser().parse_args(base + ["--udf"]))
+    assert torch.isfinite(torch.tensor(fused["loss"]))
+    assert abs(fused["loss"] - udf["loss"]) < 1e-4
 
 
 @pytest.mark.gpu

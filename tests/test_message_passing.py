@@ -340,3 +340,31 @@ def test_gat_head_broadcast(device):
         outs.append((g.ndata["o"].detach().cpu(), f1.grad.cpu(), a1.grad.cpu()))
     for x, y in zip(outs[0], outs[1]):
         torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_gat_edge_attention_fused(device):
+    """kernel.edge_attention == the reference's edge UDF (gat/train.py:90-96):
+    exp(leaky_relu(a1[src] + a2[dst])).clamp(-10, 10), forward and gradients."""
+    dev = _dev(device)
+    from dgl import kernel
+    rng = np.random.default_rng(8)
+    n, m, H = 200, 3000, 8
+    src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+    g = dgl.DGLGraph(multigraph=True)
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    a1 = torch.from_numpy(rng.standard_normal((n, H, 1)).astype(np.float32)).to(dev)
+    a2 = torch.from_numpy(rng.standard_normal((n, H, 1)).astype(np.float32)).to(dev) * 2
+    G = torch.from_numpy(rng.standard_normal((m, H)).astype(np.float32)).to(dev)
+    x1, x2 = a1.clone().requires_grad_(True), a2.clone().requires_grad_(True)
+    att = kernel.edge_attention(g.sparse_adjacency(dev), x1, x2, m, alpha=0.2)
+    att.backward(G)
+    y1, y2 = a1.clone().requires_grad_(True), a2.clone().requires_grad_(True)
+    s, d = torch.as_tensor(src).to(dev), torch.as_tensor(dst).to(dev)
+    ref = torch.exp(torch.nn.functional.leaky_relu(y1[s] + y2[d], 0.2)).clamp(-10, 10)
+    ref = ref.reshape(m, H)
+    ref.backward(G)
+    torch.testing.assert_close(att, ref, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(x1.grad, y1.grad, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x2.grad, y2.grad, rtol=1e-5, atol=1e-5)
