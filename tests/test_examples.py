@@ -71,3 +71,15 @@ def test_rgcn_fused_matches_udf(device):
     fused = rgcn.run(rgcn.parser().parse_args(base))
     udf = rgcn.run(rgcn.parser().parse_args(base + ["--udf"]))
     assert abs(fused["loss"] - udf["loss"]) < 1e-4 * max(1.0, abs(udf["loss"]))
+
+
+@pytest.mark.gpu
+def test_gcn_hip_graph_replay_matches_eager():
+    """The captured (HIP graph) training step computes the same losses as eager."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    base = ["--dataset", "cora", "--n-epochs", "20", "--gpu", "0", "--dropout", "0"]
+    eager = gcn_spmv.run(gcn_spmv.parser().parse_args(base))
+    graph = gcn_spmv.run(gcn_spmv.parser().parse_args(base + ["--hip-graph"]))
+    assert graph["hip_graph"]
+    assert abs(graph["loss"] - eager["loss"]) < 1e-4

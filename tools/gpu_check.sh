@@ -32,6 +32,8 @@ for s in $STEPS; do
     examples)
       ( timeout -k 10 600 python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 --n-hidden 128 --n-epochs 20 &&
         timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset cora --gpu 0 --n-epochs 50 &&
+        timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset cora --gpu 0 --n-epochs 50 --hip-graph &&
+        timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 --n-hidden 128 --n-epochs 20 --hip-graph &&
         timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 &&
         timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 --udf &&
         timeout -k 10 300 python examples/graphsage/train.py --dataset reddit --gpu 0 --n-epochs 10 &&
