@@ -209,16 +209,29 @@ def main():
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), W)
         lo, hi = int(bounds[0]), int(bounds[1])
         sel = (dst >= lo) & (dst < hi)
-        adj = kernel.from_coo(hi - lo, n, dst[sel] - lo, src[sel], kernel.ORDER_EID, dev)
         num_local_edges, num_rows = int(sel.sum()), hi - lo
         num_edges_total = num_local_edges  # value = this rank's edges / its time
-        h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
-        del sel
+        if args.pipeline_chunks > 0:
+            from dgl.distributed import PartitionedGraph
+            pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
+                                  pipeline_chunks=args.pipeline_chunks, rank=0, world=W)
+            h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
+            pg.update_all(h_local)  # allocates the halo buffer
+            pg.halo.uniform_(-1, 1)
 
-        def step():
-            kernel.gspmm(adj, "copy_u", "sum", h)
-        parallelism = "emulated rank 0 of %d (local g-SpMM only, H = %.0f MB)" % (
-            W, n * FEAT * 4 / 1e6)
+            def step():
+                pg.update_all(h_local)
+            mode = "pipelined segments (own + %d halo chunks)" % args.pipeline_chunks
+        else:
+            adj = kernel.from_coo(hi - lo, n, dst[sel] - lo, src[sel], kernel.ORDER_EID, dev)
+            h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+
+            def step():
+                kernel.gspmm(adj, "copy_u", "sum", h)
+            mode = "one g-SpMM"
+        del sel
+        parallelism = "emulated rank 0 of %d, %s, no communication (H = %.0f MB)" % (
+            W, mode, n * FEAT * 4 / 1e6)
         args.no_cpu_baseline = True
     elif world == 1:
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))

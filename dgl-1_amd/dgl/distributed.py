@@ -89,10 +89,13 @@ class PartitionedGraph(object):
     group     : torch.distributed process group (default world)
     """
 
-    def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0):
+    def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0,
+                 rank=None, world=None):
         self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
+        # explicit rank/world: single-process studies of one rank's share (no collectives)
+        self.rank = dist.get_rank(group) if rank is None else int(rank)
+        self.world = dist.get_world_size(group) if world is None else int(world)
+        self._emulated = rank is not None
         self.bounds = torch.as_tensor(bounds, dtype=torch.int64).cpu()
         self.lo = int(self.bounds[self.rank])
         self.hi = int(self.bounds[self.rank + 1])
@@ -135,7 +138,8 @@ class PartitionedGraph(object):
         self.pipe_csr = csr
         self.halo = None
         # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
-        overlap = self.device.type == "cuda" and dist.get_backend(self.group) == "nccl"
+        overlap = (not self._emulated and self.device.type == "cuda"
+                   and dist.get_backend(self.group) == "nccl")
         self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
 
     def gather_halo(self, h_local):
@@ -180,7 +184,7 @@ class PartitionedGraph(object):
         for c in range(C):
             if self.comm_stream is not None:
                 torch.cuda.current_stream(dev).wait_event(events[c])
-            else:
+            elif not self._emulated:
                 dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
                                             self.hpad[c * cr:(c + 1) * cr], group=self.group)
             beg, end = self.seg_ranges[c + 1]
