@@ -1,0 +1,86 @@
+"""nn modules vs dense torch formulations of the same layer (CPU and GPU)."""
+import numpy as np
+import pytest
+import torch
+
+import dgl
+from dgl import nn as dglnn
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def graph(device, n=60, m=400, seed=0):
+    rng = np.random.default_rng(seed)
+    src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+    g = dgl.DGLGraph(multigraph=True)
+    g.add_nodes(n)
+    g.add_edges(src, dst)
+    A = torch.zeros(n, n, dtype=torch.float64)
+    A.index_put_((torch.as_tensor(dst), torch.as_tensor(src)),
+                 torch.ones(m, dtype=torch.float64), accumulate=True)
+    return g, A.to(device), torch.as_tensor(src).to(device), torch.as_tensor(dst).to(device)
+
+
+def _dev(device):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device(device)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("fin,fout", [(8, 4), (4, 8)])
+def test_graphconv(device, fin, fout):
+    dev = _dev(device)
+    g, A, _, _ = graph(dev)
+    torch.manual_seed(0)
+    conv = dglnn.GraphConv(fin, fout, norm="both", activation=torch.relu).to(dev)
+    x = torch.randn(60, fin, device=dev)
+    out = conv(g, x)
+    dout = A.sum(0).clamp(min=1).pow(-0.5)  # out-degree of sources
+    din = A.sum(1).clamp(min=1).pow(-0.5)
+    ref = torch.relu((din[:, None] * (A @ (dout[:, None] * x.double())))
+                     @ conv.weight.double() + conv.bias.double())
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_gatconv(device):
+    dev = _dev(device)
+    g, A, src, dst = graph(dev)
+    torch.manual_seed(0)
+    conv = dglnn.GATConv(8, 5, num_heads=3).to(dev)
+    x = torch.randn(60, 8, device=dev)
+    out = conv(g, x)
+    ft = conv.fc(x).view(-1, 3, 5)
+    el, er = (ft * conv.attn_l).sum(-1), (ft * conv.attn_r).sum(-1)
+    e = torch.nn.functional.leaky_relu(el[src] + er[dst], 0.2).exp()  # E x H
+    num = torch.zeros(60, 3, 5, device=dev).index_add(0, dst, e.unsqueeze(-1) * ft[src])
+    den = torch.zeros(60, 3, device=dev).index_add(0, dst, e).clamp(min=1e-20)
+    torch.testing.assert_close(out, num / den.unsqueeze(-1), rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_sageconv(device):
+    dev = _dev(device)
+    g, A, _, _ = graph(dev)
+    torch.manual_seed(0)
+    conv = dglnn.SAGEConv(6, 4).to(dev)
+    x = torch.randn(60, 6, device=dev)
+    mean = (A @ x.double()) / A.sum(1, keepdim=True).clamp(min=1)
+    ref = conv.fc_self(x).double() + conv.fc_neigh(mean.float()).double()
+    torch.testing.assert_close(conv(g, x).double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_relgraphconv(device):
+    dev = _dev(device)
+    g, A, src, dst = graph(dev)
+    torch.manual_seed(0)
+    conv = dglnn.RelGraphConv(8, 6, num_rels=4, num_bases=2).to(dev)
+    x = torch.randn(60, 8, device=dev)
+    et = torch.as_tensor(np.random.default_rng(1).integers(0, 4, 400)).to(dev)
+    out = conv(g, x, et)
+    W = conv.weight  # (R, nb, 4, 3)
+    msg = torch.bmm(x[src].view(-1, 1, 4), W[et].reshape(-1, 4, 3)).view(400, 6)
+    ref = torch.zeros(60, 6, device=dev).index_add(0, dst, msg) + x @ conv.loop_weight + conv.bias
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-5)
