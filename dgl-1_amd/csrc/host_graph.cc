@@ -345,6 +345,55 @@ int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads, const int6
   API_END();
 }
 
+// Degree-bucketing schedule for UDF reduces (replaces sched::DegreeBucketing,
+// src/scheduler/scheduler.cc:13-93). Messages m (0..num_msgs-1) go to
+// receiver position msg_recv[m] in [0, num_recv). Buckets are the distinct
+// non-zero degrees in ascending order; inside a bucket nodes ascend, and each
+// node's messages keep message order. Outputs (caller-allocated, max sizes):
+//   bucket_deg[num_recv], bucket_node_ptr[num_recv+1], nodes[num_recv],
+//   msg_ids[num_msgs]; *num_buckets = number of buckets. Nodes without
+// messages are not listed (the caller fills them with the initializer).
+int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
+                                 int64_t num_recv, int64_t* num_buckets,
+                                 int64_t* bucket_deg, int64_t* bucket_node_ptr,
+                                 int64_t* nodes, int64_t* msg_ids) {
+  API_BEGIN();
+  DGLHIP_CHECK(num_msgs >= 0 && num_recv >= 0, "negative size");
+  std::vector<int64_t> deg(num_recv, 0);
+  for (int64_t m = 0; m < num_msgs; ++m) {
+    DGLHIP_CHECK(msg_recv[m] >= 0 && msg_recv[m] < num_recv, "receiver out of range");
+    deg[msg_recv[m]]++;
+  }
+  // message lists per receiver (stable counting sort)
+  std::vector<int64_t> start(num_recv + 1, 0);
+  for (int64_t v = 0; v < num_recv; ++v) start[v + 1] = start[v] + deg[v];
+  std::vector<int64_t> by_node(num_msgs), cur(start.begin(), start.end() - 1);
+  for (int64_t m = 0; m < num_msgs; ++m) by_node[cur[msg_recv[m]]++] = m;
+  // nodes ordered by (degree, node id), zero degree dropped
+  int64_t maxdeg = 0;
+  for (int64_t v = 0; v < num_recv; ++v) maxdeg = std::max(maxdeg, deg[v]);
+  std::vector<int64_t> cnt(maxdeg + 2, 0);
+  for (int64_t v = 0; v < num_recv; ++v) cnt[deg[v] + 1]++;
+  for (int64_t d = 0; d <= maxdeg; ++d) cnt[d + 1] += cnt[d];
+  std::vector<int64_t> order(num_recv), pos(cnt.begin(), cnt.end() - 1);
+  for (int64_t v = 0; v < num_recv; ++v) order[pos[deg[v]]++] = v;
+  int64_t nb = 0, nn = 0, nm = 0;
+  bucket_node_ptr[0] = 0;
+  for (int64_t d = 1; d <= maxdeg; ++d) {
+    const int64_t b = cnt[d], e = cnt[d + 1];
+    if (b == e) continue;
+    bucket_deg[nb] = d;
+    for (int64_t i = b; i < e; ++i) {
+      const int64_t v = order[i];
+      nodes[nn++] = v;
+      for (int64_t k = start[v]; k < start[v + 1]; ++k) msg_ids[nm++] = by_node[k];
+    }
+    bucket_node_ptr[++nb] = nn;
+  }
+  *num_buckets = nb;
+  API_END();
+}
+
 int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
                        const int64_t* indptr, const int32_t* indices,
                        const int64_t* eid, const float* lhs, const float* rhs,

@@ -74,6 +74,7 @@ def _load():
         "dglhip_gsddmm_attention_host": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                   ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                                   _c_int, _vp, _c_int]),
+        "dglhip_degree_bucketing_host": (_c_int, [_c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_gspmm_host": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                        _c_i64, _vp, _vp, _c_int]),
         "dglhip_gsddmm_device": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,

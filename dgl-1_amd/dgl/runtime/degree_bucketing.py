@@ -10,12 +10,16 @@ ascending degree and the results are merged back in receiving-node order
 (MERGE_ROW, executor.py:600-663); receiving nodes without messages get the
 frame initializer's value (degree_bucketing.py:72-78).
 
-Builtin reducers never come here: they run as g-SpMM kernels.
+Builtin reducers never come here: they run as g-SpMM kernels. The bucket
+schedule itself is computed natively (dglhip_degree_bucketing_host).
 """
 from __future__ import absolute_import
 
+import ctypes
+
 import torch
 
+from .._ffi import LIB, check_call, ptr
 from ..udf import NodeBatch
 
 __all__ = ["bucket_reduce"]
@@ -30,18 +34,25 @@ def bucket_reduce(g, reduce_udf, recv_nodes, msg_dst, msgs, node_frame):
     returns    : dict of reduced features, first dim = len(recv_nodes)
     """
     n_recv = len(recv_nodes)
-    pos = torch.searchsorted(recv_nodes, msg_dst)
-    order = torch.sort(pos, stable=True)[1]
-    deg = torch.bincount(pos, minlength=n_recv)
-    starts = torch.cumsum(deg, 0) - deg
+    pos = torch.searchsorted(recv_nodes, msg_dst).contiguous()
+    n_msgs = pos.numel()
+    nb = ctypes.c_int64()
+    bdeg = torch.empty(max(n_recv, 1), dtype=torch.int64)
+    bptr = torch.empty(n_recv + 1, dtype=torch.int64)
+    bnodes = torch.empty(max(n_recv, 1), dtype=torch.int64)
+    mids_all = torch.empty(max(n_msgs, 1), dtype=torch.int64)
+    check_call(LIB.dglhip_degree_bucketing_host(n_msgs, ptr(pos), n_recv, ctypes.byref(nb),
+                                                ptr(bdeg), ptr(bptr), ptr(bnodes),
+                                                ptr(mids_all)))
     results = {}
     positions = []
     outs = []
-    for d in torch.unique(deg).tolist():
-        if d == 0:
-            continue
-        members = (deg == d).nonzero(as_tuple=True)[0]
-        mids = order[(starts[members].unsqueeze(1) + torch.arange(d)).reshape(-1)]
+    moff = 0
+    for b in range(nb.value):
+        d = int(bdeg[b])
+        members = bnodes[int(bptr[b]):int(bptr[b + 1])]
+        mids = mids_all[moff:moff + d * len(members)]
+        moff += d * len(members)
         nodes = recv_nodes[members]
         mailbox = {}
         for k, t in msgs.items():
@@ -53,7 +64,9 @@ def bucket_reduce(g, reduce_udf, recv_nodes, msg_dst, msgs, node_frame):
         outs.append(out)
     if not outs:
         return results
-    zero_deg = (deg == 0).nonzero(as_tuple=True)[0]
+    has_msg = torch.zeros(n_recv, dtype=torch.bool)
+    has_msg[bnodes[:int(bptr[nb.value])]] = True
+    zero_deg = (~has_msg).nonzero(as_tuple=True)[0]
     allpos = torch.cat(positions + [zero_deg])
     inv = torch.empty_like(allpos)
     inv[allpos] = torch.arange(len(allpos))

@@ -90,6 +90,19 @@ int dglhip_coo_to_csr_device(int64_t num_rows, int64_t num_cols, int64_t nnz,
                              void* workspace, int64_t workspace_bytes,
                              void* stream);
 
+/* Host: degree-bucketing schedule for user-defined reduce functions
+ * (replaces sched::DegreeBucketing, src/scheduler/scheduler.cc:13-93, and
+ * _CAPI_DGLDegreeBucketing*, src/scheduler/scheduler_apis.cc:16-60). Message
+ * m goes to receiver position msg_recv[m]. Buckets = distinct non-zero
+ * degrees, ascending; nodes ascend inside a bucket; a node's messages keep
+ * message order. Outputs are caller-allocated at their maximum sizes:
+ * bucket_deg[num_recv], bucket_node_ptr[num_recv+1], nodes[num_recv],
+ * msg_ids[num_msgs]; *num_buckets receives the bucket count. */
+int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
+                                 int64_t num_recv, int64_t* num_buckets,
+                                 int64_t* bucket_deg, int64_t* bucket_node_ptr,
+                                 int64_t* nodes, int64_t* msg_ids);
+
 /* ------------------------------------------------------------------------ */
 /* g-SpMM: out[r,:] = REDUCE_{slot k of row r} MSG(ufeat[indices[k],:],      */
 /*                                                  efeat[eid[k],:])        */
