@@ -116,10 +116,13 @@ class SAGEConv(nn.Module):
         self.activation = activation
 
     def forward(self, g, feat):
-        g.ndata["_sage_h"] = feat
+        # fc_neigh (no bias) commutes with the mean: aggregate the narrower side
+        pre = self.fc_neigh.in_features > self.fc_neigh.out_features
+        g.ndata["_sage_h"] = self.fc_neigh(feat) if pre else feat
         g.update_all(fn.copy_src("_sage_h", "_sage_m"), fn.mean("_sage_m", "_sage_n"))
         g.ndata.pop("_sage_h")
-        rst = self.fc_self(feat) + self.fc_neigh(g.ndata.pop("_sage_n"))
+        neigh = g.ndata.pop("_sage_n")
+        rst = self.fc_self(feat) + (neigh if pre else self.fc_neigh(neigh))
         return self.activation(rst) if self.activation else rst
 
 

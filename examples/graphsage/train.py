@@ -10,7 +10,10 @@ dgl.distributed:
   each layer all-gathers the feature halo over RCCL and runs the local g-SpMM
   (bit-identical rows); dense-layer gradients are all-reduced by DDP.
 
-Layer: h' = act(fc_self(h) + fc_neigh(mean_{u->v} h_u)).
+Layer: h' = act(fc_self(h) + fc_neigh(mean_{u->v} h_u)). fc_neigh has no bias,
+so it commutes with the mean: when it narrows the features (602 -> 128 on
+Reddit) it is applied before the aggregation, which then moves 4.7x fewer
+bytes through the g-SpMM (same result up to fp32 rounding).
 
   python examples/graphsage/train.py --dataset reddit --gpu 0
   torchrun --nproc-per-node 8 --master-addr 127.0.0.1 examples/graphsage/train.py --dist \\
@@ -40,8 +43,12 @@ class SAGELayer(nn.Module):
         self.fc_neigh = nn.Linear(in_feats, out_feats, bias=False)
         self.activation = activation
 
-    def forward(self, h, neigh):
-        h = self.fc_self(h) + self.fc_neigh(neigh)
+    def forward(self, h, aggregate):
+        if self.fc_neigh.in_features > self.fc_neigh.out_features:
+            neigh = aggregate(self.fc_neigh(h))
+        else:
+            neigh = self.fc_neigh(aggregate(h))
+        h = self.fc_self(h) + neigh
         return self.activation(h) if self.activation else h
 
 
@@ -58,7 +65,7 @@ class SAGE(nn.Module):
         for i, layer in enumerate(self.layers):
             if self.dropout is not None and i > 0:
                 h = self.dropout(h)
-            h = layer(h, aggregate(h))
+            h = layer(h, aggregate)
         return h
 
 

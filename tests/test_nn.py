@@ -64,11 +64,12 @@ def test_sageconv(device):
     dev = _dev(device)
     g, A, _, _ = graph(dev)
     torch.manual_seed(0)
-    conv = dglnn.SAGEConv(6, 4).to(dev)
-    x = torch.randn(60, 6, device=dev)
-    mean = (A @ x.double()) / A.sum(1, keepdim=True).clamp(min=1)
-    ref = conv.fc_self(x).double() + conv.fc_neigh(mean.float()).double()
-    torch.testing.assert_close(conv(g, x).double(), ref, rtol=1e-5, atol=1e-5)
+    for fin, fout in ((6, 4), (4, 6)):
+        conv = dglnn.SAGEConv(fin, fout).to(dev)
+        x = torch.randn(60, fin, device=dev)
+        mean = (A @ x.double()) / A.sum(1, keepdim=True).clamp(min=1)
+        ref = conv.fc_self(x).double() + mean @ conv.fc_neigh.weight.double().t()
+        torch.testing.assert_close(conv(g, x).double(), ref, rtol=1e-5, atol=1e-5)
 
 
 @pytest.mark.parametrize("device", DEVICES)
