@@ -12,6 +12,13 @@ contiguous ranges balanced by in-edge count, one process per GPU
   (``all_gather_into_tensor``, a ring over the xGMI links).
 * Backward: the all-gather's adjoint, a reduce-scatter (sum) of the source
   gradients produced by the local transposed g-SpMM.
+* Graphs with locality (halo below half of N) use a sparse
+  halo instead: each rank receives only the remote rows its CSR references,
+  one all-to-allv (``all_to_all_single`` with split sizes) per layer; the
+  backward is the reverse all-to-allv with sum-on-receive. The request lists
+  are exchanged once, at partition time. ``halo="auto"`` takes the
+  all-to-allv when the largest rank halo is below N/2 (one all-reduce MAX,
+  so every rank decides alike).
 
 Column ids of the local CSR are remapped once (at partition time) from global
 node ids to positions in the padded all-gather buffer, so the kernel runs
@@ -76,6 +83,41 @@ class _AllGatherRows(torch.autograd.Function):
         return out[:ctx.n_local], None, None
 
 
+class _AllToAllRows(torch.autograd.Function):
+    """Sparse halo: rows h_local[send_idx] go to their requesting ranks
+    (send_splits), the rows this rank requested come back in owner order
+    (recv_splits). Backward: reverse all-to-allv, then sum-on-receive one peer
+    at a time (indices are unique within a peer, so the adds are ordered)."""
+
+    @staticmethod
+    def forward(ctx, h_local, send_idx, send_splits, recv_splits, group):
+        ctx.save_for_backward(send_idx)
+        ctx.splits = (send_splits, recv_splits)
+        ctx.group = group
+        ctx.n_local = h_local.shape[0]
+        tail = tuple(h_local.shape[1:])
+        send = h_local.index_select(0, send_idx)
+        recv = h_local.new_empty((sum(recv_splits),) + tail)
+        dist.all_to_all_single(recv, send, recv_splits, send_splits, group=group)
+        return recv
+
+    @staticmethod
+    def backward(ctx, drecv):
+        send_idx, = ctx.saved_tensors
+        send_splits, recv_splits = ctx.splits
+        tail = tuple(drecv.shape[1:])
+        dsend = drecv.new_empty((sum(send_splits),) + tail)
+        dist.all_to_all_single(dsend, drecv.contiguous(), send_splits, recv_splits,
+                               group=ctx.group)
+        dh = drecv.new_zeros((ctx.n_local,) + tail)
+        off = 0
+        for n in send_splits:
+            if n:
+                dh.index_add_(0, send_idx[off:off + n], dsend[off:off + n])
+            off += n
+        return dh, None, None, None, None
+
+
 class PartitionedGraph(object):
     """This rank's shard of a graph for full-graph message passing.
 
@@ -87,10 +129,13 @@ class PartitionedGraph(object):
     bounds    : int64[P+1] row ranges (balanced_bounds)
     device    : where the shard lives
     group     : torch.distributed process group (default world)
+    halo      : "allgather" (padded row blocks of every rank), "alltoall"
+                (only the referenced remote rows) or "auto" (alltoall when
+                the ranks' halos total less than half of N)
     """
 
     def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0,
-                 rank=None, world=None):
+                 rank=None, world=None, halo="auto"):
         self.group = group
         # explicit rank/world: single-process studies of one rank's share (no collectives)
         self.rank = dist.get_rank(group) if rank is None else int(rank)
@@ -111,12 +156,54 @@ class PartitionedGraph(object):
         self.num_edges = int(src.numel())
         self.device = device
         self.chunks = int(pipeline_chunks)
-        if self.chunks > 0:
+        if halo not in ("auto", "allgather", "alltoall"):
+            raise ValueError("halo must be auto, allgather or alltoall")
+        if halo != "allgather" and (self.chunks > 0 or self._emulated):
+            halo = "allgather"  # the pipelined / emulated studies model the all-gather
+        own = owner == self.rank
+        if halo != "allgather":
+            need = torch.unique(src[~own])       # sorted global ids = owner order
+            if halo == "auto":
+                # largest halo over the ranks (one all-reduce: every rank decides alike)
+                top = torch.tensor([need.numel()], dtype=torch.int64, device=self._coll_dev())
+                dist.all_reduce(top, op=dist.ReduceOp.MAX, group=group)
+                halo = "alltoall" if 2 * int(top) < self.num_nodes else "allgather"
+        self.halo_mode = halo
+        if halo == "alltoall":
+            self._build_alltoall(src, dst, b, owner, own, need)
+        elif self.chunks > 0:
             self._build_pipeline(src, dst, b, owner)
             self.adj = None
         else:
             self.adj = kernel.from_coo(self.num_local, self.world * self.max_rows,
                                        dst - self.lo, cols, kernel.ORDER_EID, device)
+
+    def _coll_dev(self):
+        """Device the process group's collectives take tensors on."""
+        return self.device if dist.get_backend(self.group) == "nccl" else torch.device("cpu")
+
+    def _build_alltoall(self, src, dst, b, owner, own, need):
+        P, R = self.world, self.num_local
+        cdev = self._coll_dev()
+        bd = b.to(need.device)
+        need_owner = torch.searchsorted(bd, need, right=True) - 1
+        recv_splits = torch.bincount(need_owner, minlength=P).cpu()
+        # tell every owner how many of its rows this rank needs, then which
+        send_splits = torch.empty(P, dtype=torch.int64, device=cdev)
+        dist.all_to_all_single(send_splits, recv_splits.to(cdev), group=self.group)
+        send_splits = send_splits.cpu()
+        req = torch.empty(int(send_splits.sum()), dtype=torch.int64, device=cdev)
+        dist.all_to_all_single(req, need.to(cdev), send_splits.tolist(),
+                               recv_splits.tolist(), group=self.group)
+        self.send_idx = (req.to(self.device) - self.lo).contiguous()
+        self.send_splits = send_splits.tolist()
+        self.recv_splits = recv_splits.tolist()
+        self.num_halo = int(need.numel())
+        # columns: own sources -> [0, R), remote -> R + position in `need`
+        pos = torch.searchsorted(need, src)
+        cols = torch.where(own, src - self.lo, R + pos)
+        self.adj = kernel.from_coo(R, R + self.num_halo, dst - self.lo, cols,
+                                   kernel.ORDER_EID, self.device)
 
     def _build_pipeline(self, src, dst, b, owner):
         C, P, R = self.chunks, self.world, self.num_local
@@ -143,7 +230,13 @@ class PartitionedGraph(object):
         self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
 
     def gather_halo(self, h_local):
-        """All-gather of the padded row blocks (RCCL all_gather_into_tensor)."""
+        """Source rows the local CSR's columns index: all-gather of the padded
+        row blocks (RCCL all_gather_into_tensor), or [h_local | requested remote
+        rows] through one all-to-allv."""
+        if self.halo_mode == "alltoall":
+            recv = _AllToAllRows.apply(h_local, self.send_idx, self.send_splits,
+                                       self.recv_splits, self.group)
+            return torch.cat([h_local, recv], 0)
         return _AllGatherRows.apply(h_local, self.max_rows, self.group)
 
     def update_all(self, h_local, msg="copy_u", reduce="sum", efeat=None):

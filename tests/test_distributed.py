@@ -17,7 +17,15 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, F):
+def _banded(n, width, seed):
+    """Graph with locality: every source within `width` ids of its destination."""
+    gen = torch.Generator().manual_seed(seed)
+    dst = torch.randint(0, n, (12 * n,), generator=gen)
+    src = (dst + torch.randint(-width, width + 1, dst.shape, generator=gen)).clamp(0, n - 1)
+    return src, dst, n
+
+
+def _worker(rank, world, port, n, F, halo="auto", graph="chung_lu"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
@@ -28,11 +36,19 @@ def _worker(rank, world, port, n, F):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        src, dst, n = data.chung_lu(n, 40 * n, 30.0, seed=3)  # same graph on every rank
+        if graph == "banded":
+            src, dst, n = _banded(n, 40, seed=3)
+        else:
+            src, dst, n = data.chung_lu(n, 40 * n, 30.0, seed=3)  # same graph on every rank
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         sel = (dst >= lo) & (dst < hi)
-        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu")
+        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu", halo=halo)
+        expect = {"auto": "alltoall" if graph == "banded" else "allgather"}.get(halo, halo)
+        assert pg.halo_mode == expect, pg.halo_mode
+        if expect == "alltoall":
+            remote = src[sel][(src[sel] < lo) | (src[sel] >= hi)]
+            assert pg.num_halo == torch.unique(remote).numel()
         gen = torch.Generator().manual_seed(7)
         H = torch.rand(n, F, generator=gen) * 2 - 1
         G = torch.randn(n, F, generator=gen)
@@ -51,6 +67,16 @@ def _worker(rank, world, port, n, F):
 @pytest.mark.parametrize("world", [2, 3])
 def test_partitioned_update_all(world):
     mp.spawn(_worker, args=(world, _free_port(), 3000, 16), nprocs=world, join=True)
+
+
+@pytest.mark.parametrize("world,halo,graph", [(2, "alltoall", "chung_lu"),
+                                              (3, "auto", "banded"),
+                                              (3, "allgather", "banded")])
+def test_partitioned_halo_modes(world, halo, graph):
+    """All-to-allv halo (only the referenced remote rows): forward rows are
+    bit-identical, backward (reverse all-to-allv + sum-on-receive) within
+    1e-5; auto picks it for a banded graph, all-gather for a power-law one."""
+    mp.spawn(_worker, args=(world, _free_port(), 3000, 16, halo, graph), nprocs=world, join=True)
 
 
 def test_balanced_bounds():
