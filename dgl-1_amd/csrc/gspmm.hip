@@ -239,36 +239,86 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
   }
 }
 
-// Max-reduce kernel with argmax slot (first slot wins ties, like a strict
-// running max over the mailbox). Scalar per lane: max is VALU-light and this
-// path is off the headline metric.
-template <int MSG>
+// Max-reduce kernel with argmax slot: first slot wins ties (a strict running
+// max over the mailbox, seeded with the first message), 0 / -1 for rows
+// without slots. Same lane mapping as the sum kernel (GROUP lanes per row,
+// VEC features per lane, UNROLL gathers in flight); the compares then run
+// slot by slot in CSR order, so the argmax is the one the sequential
+// reduction picks.
+template <int VEC, int GROUP, int UNROLL, int MSG, int EM>
 __global__ __launch_bounds__(256) void gspmm_max_kernel(
     int64_t num_rows, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
     float* __restrict__ out, int64_t* __restrict__ arg_out,
     const int32_t* __restrict__ row_order) {
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (wave >= num_rows) return;
+  typedef typename Vec<VEC>::T V;
+  constexpr int ITEMS_PER_WAVE = 64 / GROUP;
   const int lane = threadIdx.x & 63;
-  const int64_t row = row_order ? row_order[wave] : wave;
+  const int64_t wave =
+      int64_t(blockIdx.x) * (blockDim.x >> 6) +
+      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
+  if (it >= num_rows) return;
+  const int gl = GROUP == 64 ? lane : (lane % GROUP);
+  int64_t row = row_order ? row_order[it] : it;
+  if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
   const int64_t beg = indptr[row], end = indptr[row + 1];
-  for (int64_t f = lane; f < F; f += 64) {
-    float best = 0.0f;
-    int64_t arg = -1;
-    for (int64_t k = beg; k < end; ++k) {
-      float x;
-      if (MSG == DGLHIP_MSG_COPY_U) {
-        x = ufeat[int64_t(indices[k]) * F + f];
-      } else {
-        const float e = efeat[eid[k] * elen + f / (F / elen)];
-        x = MSG == DGLHIP_MSG_COPY_E ? e : ufeat[int64_t(indices[k]) * F + f] * e;
-      }
-      if (arg < 0 || x > best) { best = x; arg = k; }
+  auto message = [](const SlotLoad<VEC, MSG, EM>& s) -> V {
+    if (MSG == DGLHIP_MSG_COPY_U) return s.u;
+    if (MSG == DGLHIP_MSG_COPY_E) return s.e;
+    return s.u * s.e;
+  };
+  for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
+    const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
+    V best = Vec<VEC>::zero();
+    int64_t arg[VEC];
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) arg[i] = -1;
+    int64_t k = beg;
+    if (k < end) {
+      SlotLoad<VEC, MSG, EM> s;
+      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
+             MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+      best = message(s);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) arg[i] = k;
+      ++k;
     }
-    out[row * F + f] = best;
-    if (arg_out) arg_out[row * F + f] = arg;
+    for (; k + UNROLL <= end; k += UNROLL) {
+      SlotLoad<VEC, MSG, EM> s[UNROLL];
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j)
+        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
+                  MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j) {
+        const V x = message(s[j]);
+#pragma unroll
+        for (int i = 0; i < VEC; ++i) {
+          const float xi = reinterpret_cast<const float*>(&x)[i];
+          float& bi = reinterpret_cast<float*>(&best)[i];
+          if (xi > bi) { bi = xi; arg[i] = k + j; }
+        }
+      }
+    }
+    for (; k < end; ++k) {
+      SlotLoad<VEC, MSG, EM> s;
+      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
+             MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+      const V x = message(s);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) {
+        const float xi = reinterpret_cast<const float*>(&x)[i];
+        float& bi = reinterpret_cast<float*>(&best)[i];
+        if (xi > bi) { bi = xi; arg[i] = k; }
+      }
+    }
+    stv<VEC>(out + row * F + f0, best);
+    if (arg_out) {
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) arg_out[row * F + f0 + i] = arg[i];
+    }
   }
 }
 
@@ -502,6 +552,61 @@ static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t 
 #undef DGLHIP_SUM
 }
 
+struct MaxLaunch {
+  int64_t num_rows, F, elen;
+  const int64_t* indptr;
+  const int32_t* indices;
+  const int64_t* eid;
+  const float* ufeat;
+  const float* efeat;
+  float* out;
+  int64_t* arg_out;
+  const int32_t* row_order;
+};
+
+template <int MSG, int EM>
+static void dispatch_max_shape(const MaxLaunch& a, hipStream_t stream) {
+  const int64_t F = a.F;
+  int vec = pick_vec(F, {a.ufeat, EM == EM_FULL ? a.efeat : nullptr, a.out});
+  while (EM == EM_HEAD && vec > 1 && (F / a.elen) % vec != 0) vec >>= 1;
+  const int group = pick_group(F, vec);
+#define DGLHIP_CASE(V, G)                                                            \
+  if (vec == V && group == G) {                                                      \
+    constexpr int ITEMS_PER_BLOCK = 4 * (64 / G);                                    \
+    const int64_t blocks = (a.num_rows + ITEMS_PER_BLOCK - 1) / ITEMS_PER_BLOCK;     \
+    DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);                \
+    timed_launch(stream, [&] {                                                       \
+      hipLaunchKernelGGL((gspmm_max_kernel<V, G, 8, MSG, EM>),                       \
+                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,  \
+                         a.num_rows, a.F, a.elen, a.indptr, a.indices, a.eid,        \
+                         a.ufeat, a.efeat, a.out, a.arg_out, a.row_order);           \
+    });                                                                              \
+    return;                                                                          \
+  }
+  DGLHIP_CASE(4, 64)
+  DGLHIP_CASE(2, 64) DGLHIP_CASE(2, 32) DGLHIP_CASE(2, 16) DGLHIP_CASE(2, 8)
+  DGLHIP_CASE(2, 4) DGLHIP_CASE(2, 2)
+  DGLHIP_CASE(1, 64) DGLHIP_CASE(1, 32) DGLHIP_CASE(1, 16) DGLHIP_CASE(1, 8)
+  DGLHIP_CASE(1, 4) DGLHIP_CASE(1, 2) DGLHIP_CASE(1, 1)
+#undef DGLHIP_CASE
+  DGLHIP_CHECK(false, "no max kernel for F=" << F << " vec=" << vec << " group=" << group);
+}
+
+static void dispatch_max(int msg_op, const MaxLaunch& a, hipStream_t stream) {
+  const int em = edge_mode(a.elen, a.F);
+  if (msg_op == DGLHIP_MSG_COPY_U) {
+    dispatch_max_shape<DGLHIP_MSG_COPY_U, EM_SCALAR>(a, stream);
+  } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
+    if (em == EM_FULL) dispatch_max_shape<DGLHIP_MSG_U_MUL_E, EM_FULL>(a, stream);
+    else if (em == EM_SCALAR) dispatch_max_shape<DGLHIP_MSG_U_MUL_E, EM_SCALAR>(a, stream);
+    else dispatch_max_shape<DGLHIP_MSG_U_MUL_E, EM_HEAD>(a, stream);
+  } else {
+    if (em == EM_FULL) dispatch_max_shape<DGLHIP_MSG_COPY_E, EM_FULL>(a, stream);
+    else if (em == EM_SCALAR) dispatch_max_shape<DGLHIP_MSG_COPY_E, EM_SCALAR>(a, stream);
+    else dispatch_max_shape<DGLHIP_MSG_COPY_E, EM_HEAD>(a, stream);
+  }
+}
+
 }  // namespace dglhip
 
 using namespace dglhip;
@@ -529,17 +634,9 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   const int64_t elen = use_e ? efeat_len : 1;
   if (reduce_op == DGLHIP_REDUCE_MAX) {
-    const int64_t blocks = (num_rows + 3) / 4;
-    timed_launch(stream, [&] {
-#define DGLHIP_MAX(M)                                                          \
-  hipLaunchKernelGGL((gspmm_max_kernel<M>), dim3(static_cast<unsigned>(blocks)), \
-                     dim3(256), 0, stream, num_rows, feat_len, elen, indptr,    \
-                     indices, eid, ufeat, efeat, out, arg_out, row_order)
-      if (msg_op == DGLHIP_MSG_COPY_U) DGLHIP_MAX(DGLHIP_MSG_COPY_U);
-      else if (msg_op == DGLHIP_MSG_COPY_E) DGLHIP_MAX(DGLHIP_MSG_COPY_E);
-      else DGLHIP_MAX(DGLHIP_MSG_U_MUL_E);
-#undef DGLHIP_MAX
-    });
+    MaxLaunch m{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, arg_out,
+                row_order};
+    dispatch_max(msg_op, m, stream);
     return 0;
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;

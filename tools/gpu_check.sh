@@ -57,6 +57,9 @@ for s in $STEPS; do
       timeout -k 10 600 python tools/kernel_sweep.py > gpurun_out/sweep_reddit.json 2> gpurun_out/sweep.err &&
       timeout -k 10 600 python tools/kernel_sweep.py --workload rmat --rmat-scale 25 > gpurun_out/sweep_rmat.json 2>> gpurun_out/sweep.err
       rc=$?; cat gpurun_out/sweep_reddit.json gpurun_out/sweep_rmat.json; [ $rc -eq 0 ] || exit $rc ;;
+    reducers)
+      timeout -k 10 600 python tools/reducer_bench.py > gpurun_out/reducers.json 2> gpurun_out/reducers.err
+      rc=$?; cat gpurun_out/reducers.json; tail -3 gpurun_out/reducers.err; [ $rc -eq 0 ] || exit $rc ;;
     rmat)
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err

@@ -1,0 +1,61 @@
+"""Kernel time of each g-SpMM reducer / message on the Reddit-shaped bench
+graph (hipEvent pairs on the launch stream, dglhip_timing_*), with the
+algorithmic bandwidth of each: every slot gathers one source row (4F B) plus
+its 4-B column id (+ 8-B eid and the edge values when the message reads edge
+features), every row writes 4F B (+ 8F B of argmax ids for max).
+
+  python tools/reducer_bench.py [--feat 128] [--iters 10]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dgl-1_amd")]
+from dgl import data, kernel  # noqa: E402
+
+PEAK_GBS = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--feat", type=int, default=128)
+    ap.add_argument("--iters", type=int, default=10)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    src, dst, n = data.reddit_like(device=dev)
+    E = int(src.numel())
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    del src, dst
+    F = args.feat
+    h = torch.rand(n, F, device=dev) * 2 - 1
+    w = torch.rand(E, device=dev)
+    cases = [("copy_u", "sum", None), ("copy_u", "mean", None), ("copy_u", "max", None),
+             ("u_mul_e", "sum", w), ("u_mul_e", "max", w)]
+    res = []
+    for msg, red, e in cases:
+        kernel.gspmm(adj, msg, red, h, e)
+        torch.cuda.synchronize()
+        kernel.timing_enable(True)
+        for _ in range(args.iters):
+            kernel.gspmm(adj, msg, red, h, e)
+        ms, cnt = kernel.timing_read()
+        kernel.timing_enable(False)
+        t = ms / max(cnt, 1)
+        per_edge = 4 * F + 4 + (12 if e is not None else 0)
+        per_row = 4 * F + 8
+        byts = E * per_edge + n * per_row
+        res.append({"msg": msg, "reduce": red, "kernel_ms": round(t, 3),
+                    "edges_per_s": E / (t * 1e-3),
+                    "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
+                    "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
+    print(json.dumps({"graph": "reddit_like", "nodes": n, "edges": E, "feat": F,
+                      "note": "max also writes the (N, F) int64 argmax only under autograd; "
+                              "timed here without it", "cases": res}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
