@@ -107,7 +107,7 @@ struct SlotLoad {
 
 // Sequential reduction of slots [beg, end) of one row for the VEC features at
 // f0: the fma chain the reference's product runs (see the file header).
-template <int VEC, int UNROLL, int MSG, int EM>
+template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen,
     int64_t eoff, const int32_t* __restrict__ indices,
@@ -119,7 +119,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
       s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
-                MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
+                MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k + j] : k + j));
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
       if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
@@ -130,7 +130,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
   for (; k < end; ++k) {
     SlotLoad<VEC, MSG, EM> s;
     s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
-           MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+           MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k] : k));
     if (MSG == DGLHIP_MSG_COPY_U) acc += s.u;
     else if (MSG == DGLHIP_MSG_COPY_E) acc += s.e;
     else acc = Vec<VEC>::fma(s.e, s.u, acc);
@@ -209,9 +209,12 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, F, f0, indices, ufeat);
+    else if (MSG == DGLHIP_MSG_COPY_U || eid != nullptr)  // uniform branch
+      acc = reduce_range<VEC, UNROLL, MSG, EM, true>(acc, beg, end, F, f0, elen, eoff, indices,
+                                                     eid, ufeat, efeat);
     else
-      acc = reduce_range<VEC, UNROLL, MSG, EM>(acc, beg, end, F, f0, elen, eoff, indices, eid,
-                                               ufeat, efeat);
+      acc = reduce_range<VEC, UNROLL, MSG, EM, false>(acc, beg, end, F, f0, elen, eoff, indices,
+                                                      eid, ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     stv<VEC>(out + row * F + f0, acc);
@@ -245,31 +248,24 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
 // VEC features per lane, UNROLL gathers in flight); the compares then run
 // slot by slot in CSR order, so the argmax is the one the sequential
 // reduction picks.
-template <int VEC, int GROUP, int UNROLL, int MSG, int EM>
-__global__ __launch_bounds__(256) void gspmm_max_kernel(
-    int64_t num_rows, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
-    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
-    const float* __restrict__ ufeat, const float* __restrict__ efeat,
-    float* __restrict__ out, int64_t* __restrict__ arg_out,
-    const int32_t* __restrict__ row_order) {
+template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID>
+__device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t beg,
+                                        int64_t end, int64_t F, int64_t elen,
+                                        const int32_t* __restrict__ indices,
+                                        const int64_t* __restrict__ eid,
+                                        const float* __restrict__ ufeat,
+                                        const float* __restrict__ efeat,
+                                        float* __restrict__ out, int64_t* __restrict__ arg_out) {
   typedef typename Vec<VEC>::T V;
-  constexpr int ITEMS_PER_WAVE = 64 / GROUP;
-  const int lane = threadIdx.x & 63;
-  const int64_t wave =
-      int64_t(blockIdx.x) * (blockDim.x >> 6) +
-      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
-  if (it >= num_rows) return;
-  const int gl = GROUP == 64 ? lane : (lane % GROUP);
-  int64_t row = row_order ? row_order[it] : it;
-  if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
-  const int64_t beg = indptr[row], end = indptr[row + 1];
   auto message = [](const SlotLoad<VEC, MSG, EM>& s) -> V {
     if (MSG == DGLHIP_MSG_COPY_U) return s.u;
     if (MSG == DGLHIP_MSG_COPY_E) return s.e;
     return s.u * s.e;
   };
-  for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
+  auto edge = [&](int64_t k) -> int64_t {
+    return MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k] : k);
+  };
+  for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(group) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
     V best = Vec<VEC>::zero();
     int64_t arg[VEC];
@@ -278,8 +274,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
     int64_t k = beg;
     if (k < end) {
       SlotLoad<VEC, MSG, EM> s;
-      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
-             MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k], edge(k));
       best = message(s);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) arg[i] = k;
@@ -289,8 +284,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
       SlotLoad<VEC, MSG, EM> s[UNROLL];
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j)
-        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
-                  MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k + j]);
+        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j], edge(k + j));
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j) {
         const V x = message(s[j]);
@@ -304,8 +298,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
     }
     for (; k < end; ++k) {
       SlotLoad<VEC, MSG, EM> s;
-      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
-             MSG == DGLHIP_MSG_COPY_U ? 0 : eid[k]);
+      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k], edge(k));
       const V x = message(s);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) {
@@ -320,6 +313,32 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
       for (int i = 0; i < VEC; ++i) arg_out[row * F + f0 + i] = arg[i];
     }
   }
+}
+
+template <int VEC, int GROUP, int UNROLL, int MSG, int EM>
+__global__ __launch_bounds__(256) void gspmm_max_kernel(
+    int64_t num_rows, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const float* __restrict__ ufeat, const float* __restrict__ efeat,
+    float* __restrict__ out, int64_t* __restrict__ arg_out,
+    const int32_t* __restrict__ row_order) {
+  constexpr int ITEMS_PER_WAVE = 64 / GROUP;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave =
+      int64_t(blockIdx.x) * (blockDim.x >> 6) +
+      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
+  if (it >= num_rows) return;
+  const int gl = GROUP == 64 ? lane : (lane % GROUP);
+  int64_t row = row_order ? row_order[it] : it;
+  if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  if (MSG == DGLHIP_MSG_COPY_U || eid != nullptr)  // uniform branch
+    max_row<VEC, UNROLL, MSG, EM, true>(row, gl, GROUP, beg, end, F, elen, indices, eid, ufeat,
+                                        efeat, out, arg_out);
+  else
+    max_row<VEC, UNROLL, MSG, EM, false>(row, gl, GROUP, beg, end, F, elen, indices, eid,
+                                         ufeat, efeat, out, arg_out);
 }
 
 // SDDMM dot: one wave per row. One head (H == 1): per slot a wave-wide fma
@@ -629,7 +648,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
-  DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   const int64_t elen = use_e ? efeat_len : 1;
@@ -666,7 +685,7 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
-  DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   DGLHIP_CHECK(num_chunks == 0 || (partial && chunk_beg && chunk_end), "null chunk plan");
@@ -712,7 +731,7 @@ int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(item_beg && item_end && out, "null ranges/out");
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
-  DGLHIP_CHECK(!use_e || (efeat && eid), "efeat/eid is null");
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   SumLaunch a{num_items, feat_len, use_e ? efeat_len : 1, nullptr, indices, eid, ufeat, efeat,
@@ -732,7 +751,9 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
                "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
   const int64_t blocks = (num_rows + 3) / 4;
+  DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
   timed_launch(stream, [&] {
     hipLaunchKernelGGL(gsddmm_dot_kernel, dim3(static_cast<unsigned>(blocks)),
                        dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
@@ -763,6 +784,8 @@ int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && num_heads >= 1, "bad sizes");
   if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
+  DGLHIP_CHECK((num_rows + 3) / 4 <= 0x7fffffff, "grid too large");
   timed_launch(stream, [&] {
     hipLaunchKernelGGL(gsddmm_attention_kernel, dim3(static_cast<unsigned>((num_rows + 3) / 4)),
                        dim3(256), 0, stream, num_rows, num_heads, indptr, indices, eid, lhs,

@@ -184,7 +184,6 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || (efeat && efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
-  DGLHIP_CHECK(!use_e || eid, "eid is null");
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
   const int64_t F = feat_len;
   const int64_t dpe = use_e ? F / efeat_len : 1;  // features per edge value
@@ -198,7 +197,7 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
           int64_t arg = -1;
           for (int64_t k = s; k < t; ++k) {
             float x;
-            const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+            const float* er = use_e ? efeat + (eid ? eid[k] : k) * efeat_len : nullptr;
             if (msg_op == DGLHIP_MSG_COPY_U) x = ufeat[int64_t(indices[k]) * F + f];
             else if (msg_op == DGLHIP_MSG_COPY_E) x = er[f / dpe];
             else x = ufeat[int64_t(indices[k]) * F + f] * er[f / dpe];
@@ -212,7 +211,7 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
       for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
       for (int64_t k = s; k < t; ++k) {
         const float* ur = use_u ? ufeat + int64_t(indices[k]) * F : nullptr;
-        const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+        const float* er = use_e ? efeat + (eid ? eid[k] : k) * efeat_len : nullptr;
         if (msg_op == DGLHIP_MSG_COPY_U) {
           for (int64_t f = 0; f < F; ++f) o[f] += ur[f];
         } else if (msg_op == DGLHIP_MSG_COPY_E) {
@@ -242,7 +241,7 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
   if (num_items == 0 || feat_len == 0) return 0;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
-  DGLHIP_CHECK(!use_e || (efeat && eid && efeat_len >= 1 && feat_len % efeat_len == 0),
+  DGLHIP_CHECK(!use_e || (efeat && efeat_len >= 1 && feat_len % efeat_len == 0),
                "bad edge feature");
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
   const int64_t F = feat_len, dpe = use_e ? F / efeat_len : 1;
@@ -253,7 +252,7 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
         for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
       for (int64_t k = item_beg[i]; k < item_end[i]; ++k) {
         const float* ur = msg_op != DGLHIP_MSG_COPY_E ? ufeat + int64_t(indices[k]) * F : nullptr;
-        const float* er = use_e ? efeat + eid[k] * efeat_len : nullptr;
+        const float* er = use_e ? efeat + (eid ? eid[k] : k) * efeat_len : nullptr;
         for (int64_t f = 0; f < F; ++f) {
           if (msg_op == DGLHIP_MSG_COPY_U) o[f] += ur[f];
           else if (msg_op == DGLHIP_MSG_COPY_E) o[f] += er[f / dpe];

@@ -117,6 +117,9 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t
   const int64_t Fo = num_blocks * out_block;
   DGLHIP_CHECK(Fo <= 64 * kMaxPass, "output width " << Fo << " exceeds " << 64 * kMaxPass);
   if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && eid && etype && ufeat && weight && out,
+               "null pointer argument");
+  DGLHIP_CHECK((num_rows + 3) / 4 <= 0x7fffffff, "grid too large");
   const int64_t pass = (Fo + 63) / 64;
   const dim3 grid(static_cast<unsigned>((num_rows + 3) / 4)), block(256);
 #define DGLHIP_TB(P)                                                                    \
@@ -140,8 +143,13 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks, int64_
                                     void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rels >= 0 && num_blocks >= 0 && in_block >= 0 && out_block >= 0,
+               "bad sizes");
   const int64_t total = num_rels * num_blocks * in_block * out_block;
   if (total == 0) return 0;
+  DGLHIP_CHECK(rel_ptr && rel_src && rel_eid && edge_dst && ufeat && dout && dweight,
+               "null pointer argument");
+  DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
   hipLaunchKernelGGL(typed_block_wgrad_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
                      dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
                      rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);

@@ -88,6 +88,7 @@ class CSR(object):
         self._host_indptr = host_indptr
         self._plans = {}
         self._max_degree = None
+        self._slot_eid = False  # not computed yet
 
     @property
     def host_indptr(self):
@@ -101,6 +102,26 @@ class CSR(object):
             ip = self.host_indptr
             self._max_degree = int((ip[1:] - ip[:-1]).max()) if self.num_rows else 0
         return self._max_degree
+
+    @property
+    def slot_eid(self):
+        """``eid`` for the g-SpMM entry points, or None when the slots already
+        run in edge-id order (eid == arange): the kernels then index edge
+        features by slot and skip the eid indirection (include/dgl_hip.h).
+        Checked once per CSR, in bounded chunks."""
+        if self._slot_eid is False:
+            ident = True
+            n = self.eid.numel()
+            step = 1 << 26
+            for b in range(0, n, step):
+                e = min(n, b + step)
+                if not torch.equal(self.eid[b:e],
+                                   torch.arange(b, e, dtype=self.eid.dtype,
+                                                device=self.eid.device)):
+                    ident = False
+                    break
+            self._slot_eid = None if ident else self.eid
+        return self._slot_eid
 
     def split_plan(self, threshold):
         """Launch plan cutting rows longer than ``threshold`` slots into chunks
@@ -291,23 +312,24 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
+    eid = csr.slot_eid if msg != MSG_COPY_U else None
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     if split:
         p = csr.split_plan(split)
         partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
         check_call(LIB.dglhip_gspmm_chunked_device(
-            msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid), ptr(ufeat2),
+            msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(ufeat2),
             ptr(efeat2), elen, ptr(out), p["light"].numel(), ptr(p["light"]), p["num_chunks"],
             ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
             ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
     elif dev.type == "cuda":
         check_call(LIB.dglhip_gspmm_device(
-            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
+            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
             _stream_of(dev)))
     else:
         check_call(LIB.dglhip_gspmm_host(
-            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
+            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), 0))
     return out, arg
 

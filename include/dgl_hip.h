@@ -125,6 +125,8 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
  * feat_len (one value per edge and feature), or any H dividing feat_len (one
  * value per edge and head, broadcast over the D = feat_len / H consecutive
  * features of that head: GAT's (E, H, 1) attention x (N, H, D) features).
+ * eid may be NULL for the g-SpMM entry points: edge features are then
+ * indexed by CSR slot (efeat already permuted into slot order).
  * arg_out (int64[num_rows*feat_len], may be NULL): for MAX, the CSR slot that
  * won each element (-1 for empty rows); needed by the backward.
  * row_order (int32[num_rows], may be NULL): launch schedule (a permutation);

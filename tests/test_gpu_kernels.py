@@ -47,12 +47,14 @@ def test_gspmm_copy_u_sum_exact(cuda, F):
     assert np.array_equal(out.cpu().numpy().reshape(n, F), ref)
 
 
-@pytest.mark.parametrize("F", [1, 5, 128])
+@pytest.mark.parametrize("F", [1, 5, 100, 128, 200, 256, 602])
 @pytest.mark.parametrize("edge_len", ["scalar", "vector"])
 def test_gspmm_u_mul_e_sum(cuda, F, edge_len):
+    """F = 100 / 200 / 602 leave lanes idle in the last feature pass; skewed
+    rows run past the unroll depth many times."""
     rng = np.random.default_rng(7)
     n, m = 500, 20000  # many duplicate (row, col) pairs
-    row, col = rand_graph(rng, n, 60, m)
+    row, col = rand_graph(rng, n, 60, m, skew=True)
     H = rng.standard_normal((60, F)).astype(np.float32)
     W = rng.standard_normal((m, 1 if edge_len == "scalar" else F)).astype(np.float32)
     adj = kernel.from_coo(n, 60, row, col, kernel.ORDER_EID, cuda)
@@ -65,6 +67,41 @@ def test_gspmm_u_mul_e_sum(cuda, F, edge_len):
         for f in range(F):
             ref[:, f] = O.spmm_coo(n, row, col, H[:, f:f + 1], W[:, f])[:, 0]
         assert np.array_equal(out, ref)
+
+
+@pytest.mark.parametrize("F", [64, 128, 602])
+def test_gspmm_slot_ordered_edge_values(cuda, F):
+    """eid = NULL: edge values already in CSR slot order give the same bits as
+    the eid-indexed call (copy_e and u_mul_e, sum and mean)."""
+    rng = np.random.default_rng(F + 1)
+    n = 400
+    row, col = rand_graph(rng, n, n, 30000, skew=True)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    csr = adj.fwd
+    H = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(cuda)
+    W = torch.from_numpy(rng.standard_normal((len(row), 1)).astype(np.float32)).to(cuda)
+    Ws = W.index_select(0, csr.eid).contiguous()
+    stream = torch.cuda.current_stream(cuda).cuda_stream
+    for msg in (1, 2):
+        for red in (0, 2):
+            outs = []
+            for eid, w in ((csr.eid, W), (None, Ws)):
+                o = torch.empty(n, F, device=cuda)
+                _ffi.check_call(_ffi.LIB.dglhip_gspmm_device(
+                    msg, red, n, F, _ffi.ptr(csr.indptr), _ffi.ptr(csr.indices),
+                    None if eid is None else _ffi.ptr(eid), _ffi.ptr(H), _ffi.ptr(w), 1,
+                    _ffi.ptr(o), None, None, stream))
+                outs.append(o)
+            torch.cuda.synchronize()
+            assert torch.equal(outs[0], outs[1]), (msg, red)
+    ref = O.spmm_coo(n, row, col, H.cpu().numpy(), W.cpu().numpy()[:, 0])
+    o = torch.empty(n, F, device=cuda)
+    _ffi.check_call(_ffi.LIB.dglhip_gspmm_device(1, 0, n, F, _ffi.ptr(csr.indptr),
+                                                 _ffi.ptr(csr.indices), None, _ffi.ptr(H),
+                                                 _ffi.ptr(Ws), 1, _ffi.ptr(o), None, None,
+                                                 stream))
+    torch.cuda.synchronize()
+    assert np.array_equal(o.cpu().numpy(), ref)
 
 
 def test_gspmm_max_and_mean(cuda):
