@@ -189,7 +189,7 @@ def main():
     log("rank %d: graph %d nodes %d edges generated in %.1fs" % (rank, n, num_edges_total,
                                                                   time.time() - t0))
 
-    if world == 1 and args.workload == "rmat":
+    if world == 1 and args.workload == "rmat" and args.emulate_world <= 1:
         # 1.07B edges: build the device CSR directly (no host copy of the edge list)
         adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
         del src, dst
@@ -202,9 +202,10 @@ def main():
         parallelism = "single GPU (kernel API; heavy rows chunked)"
     elif world == 1 and args.emulate_world > 1:
         from dgl.distributed import balanced_bounds
-        del src, dst
         W = args.emulate_world
-        src, dst, n = data.reddit_like(scale=W, seed=0, device=dev)
+        if args.workload == "reddit":  # weak scaling: the x W graph
+            del src, dst
+            src, dst, n = data.reddit_like(scale=W, seed=0, device=dev)
         num_edges_total = int(src.numel())
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), W)
         lo, hi = int(bounds[0]), int(bounds[1])

@@ -222,8 +222,9 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
 }
 
 // Combine the chunk partials of each heavy row in chunk order:
-// out[row] = ((p0 + p1) + p2) + ... (deterministic), then MEAN scaling.
-template <bool MEAN>
+// out[row] = ((p0 + p1) + p2) + ... (deterministic), then MEAN scaling; with
+// ACCUM the row's running value comes first: out[row] = ((out[row] + p0) + p1) ...
+template <bool MEAN, bool ACCUM>
 __global__ __launch_bounds__(256) void gspmm_combine_kernel(
     int64_t num_heavy, int64_t F, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ heavy_rows, const int64_t* __restrict__ heavy_chunk_ptr,
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
   const int64_t c0 = heavy_chunk_ptr[wave], c1 = heavy_chunk_ptr[wave + 1];
   const float deg = static_cast<float>(indptr[row + 1] - indptr[row]);
   for (int64_t f = lane; f < F; f += 64) {
-    float acc = partial[c0 * F + f];
+    float acc = ACCUM ? out[row * F + f] + partial[c0 * F + f] : partial[c0 * F + f];
     for (int64_t c = c0 + 1; c < c1; ++c) acc += partial[c * F + f];
     if (MEAN && deg > 1.0f) acc = acc / deg;
     out[row * F + f] = acc;
@@ -469,7 +470,7 @@ struct SumLaunch {
   const int32_t* row_order;
   const int64_t* chunk_beg;  // non-null: chunked launch (partials to `out`)
   const int64_t* chunk_end;
-  bool accumulate;           // chunked launch continuing the chain in `out`
+  bool accumulate;           // continue each item's chain from the value in `out`
 };
 
 // Tuning override for the copy_u + sum shape (dglhip_set_spmm_variant);
@@ -492,6 +493,11 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
+    else if (!a.chunk_beg && a.accumulate && !MEAN)
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, false, true>),
+                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else if (a.chunk_beg)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
@@ -507,7 +513,7 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
 
 template <int MSG, int EM, bool MEAN>
 static bool dispatch_variant(const SumLaunch& a, hipStream_t stream) {
-  if (MSG != DGLHIP_MSG_COPY_U || MEAN || g_var_vec == 0) return false;
+  if (MSG != DGLHIP_MSG_COPY_U || MEAN || g_var_vec == 0 || a.accumulate) return false;
   const int v = g_var_vec, gr = g_var_group, u = g_var_unroll, pp = g_var_pipe;
   if (int64_t(v) * gr < a.F && (a.F % (int64_t(v) * gr)) != 0) return false;
   if (a.F % v != 0) return false;
@@ -641,7 +647,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
-  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 2, "unknown reduce op " << reduce_op);
+  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;  // empty tensors may carry null pointers
   DGLHIP_CHECK(indptr != nullptr && out != nullptr, "null indptr/out");
@@ -660,7 +666,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   SumLaunch a{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, row_order,
-              nullptr, nullptr, false};
+              nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM};
   dispatch_sum(msg_op, mean, a, stream);
   API_END();
 }
@@ -678,7 +684,8 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
-  DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN,
+  DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
+                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
                "chunked rows support sum/mean only");
   DGLHIP_CHECK(num_light >= 0 && num_chunks >= 0 && num_heavy >= 0, "negative size");
   if (feat_len == 0) return 0;
@@ -691,6 +698,7 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   DGLHIP_CHECK(num_chunks == 0 || (partial && chunk_beg && chunk_end), "null chunk plan");
   const int64_t elen = use_e ? efeat_len : 1;
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
+  const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM;
   if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
     SumLaunch c{num_chunks, feat_len, elen, indptr, indices, eid, ufeat, efeat, partial,
                 nullptr, chunk_beg, chunk_end, false};
@@ -698,20 +706,27 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   }
   if (num_light > 0) {
     SumLaunch l{num_light, feat_len, elen, indptr, indices, eid, ufeat, efeat, out,
-                light_rows, nullptr, nullptr, false};
+                light_rows, nullptr, nullptr, accum};
     dispatch_sum(msg_op, mean, l, stream);
   }
   if (num_heavy > 0) {
     const int64_t blocks = (num_heavy + 3) / 4;
     timed_launch(stream, [&] {
       if (mean)
-        hipLaunchKernelGGL(gspmm_combine_kernel<true>, dim3(static_cast<unsigned>(blocks)),
-                           dim3(256), 0, stream, num_heavy, feat_len, indptr, heavy_rows,
-                           heavy_chunk_ptr, partial, out);
+        hipLaunchKernelGGL((gspmm_combine_kernel<true, false>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
+                           out);
+      else if (accum)
+        hipLaunchKernelGGL((gspmm_combine_kernel<false, true>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
+                           out);
       else
-        hipLaunchKernelGGL(gspmm_combine_kernel<false>, dim3(static_cast<unsigned>(blocks)),
-                           dim3(256), 0, stream, num_heavy, feat_len, indptr, heavy_rows,
-                           heavy_chunk_ptr, partial, out);
+        hipLaunchKernelGGL((gspmm_combine_kernel<false, false>),
+                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
+                           out);
     });
   }
   API_END();

@@ -176,7 +176,7 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int num_threads) {
   API_BEGIN();
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
-  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 2, "unknown reduce op " << reduce_op);
+  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
@@ -208,7 +208,8 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
         }
         continue;
       }
-      for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
+      if (reduce_op != DGLHIP_REDUCE_SUM_ACCUM)
+        for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
       for (int64_t k = s; k < t; ++k) {
         const float* ur = use_u ? ufeat + int64_t(indices[k]) * F : nullptr;
         const float* er = use_e ? efeat + (eid ? eid[k] : k) * efeat_len : nullptr;

@@ -30,10 +30,13 @@ each row's slots are grouped into segments — sources this rank owns first,
 then the remote sources of halo chunk 1..C — so the own segment is reduced
 while the halo is still in flight, and each remote segment as soon as its
 chunk's all-gather (on a separate HIP stream) lands. The row's fma chain is
-continued segment by segment (dglhip_gspmm_ranges_device, accumulate), so
-the result is one sequential chain in (segment, edge-id) order: deterministic
-and within fp32 tolerance of the edge-id-order chain (bit-identical when edge
-ids already run in source order, as in bench.py's graphs).
+continued segment by segment: each segment is a CSR of its own, reduced with
+DGLHIP_REDUCE_SUM_ACCUM (out += ..., the chain continuing from out), so it
+keeps the degree-descending schedule and heavy-row chunking of a plain
+g-SpMM. The result is one sequential chain in (segment, edge-id) order:
+deterministic and within fp32 tolerance of the edge-id-order chain
+(bit-identical when edge ids already run in source order, as in bench.py's
+graphs, and no row is chunked).
 """
 from __future__ import absolute_import
 
@@ -215,14 +218,16 @@ class PartitionedGraph(object):
         # own sources index h_local directly; remote ones the chunked halo buffer
         cols = torch.where(own, j, c * (P * cr) + owner * cr + (j - c * cr))
         seg = torch.where(own, torch.zeros_like(c), c + 1)
-        S = C + 1
-        vrow = (dst - self.lo) * S + seg
-        csr = kernel.build_csr(R * S, max(P * cr * C, R), vrow, cols, kernel.ORDER_EID,
-                               self.device, schedule=False)
-        ip = csr.indptr
-        self.seg_ranges = [(ip[s:R * S:S].contiguous(), ip[s + 1:R * S + 1:S].contiguous())
-                           for s in range(S)]
-        self.pipe_csr = csr
+        # one CSR per segment (standard rows: degree-descending schedule and,
+        # under kernel.set_row_split, heavy rows chunked), edge order kept
+        lrow = dst - self.lo
+        self.seg_csrs = []
+        for sidx in range(C + 1):
+            m = seg == sidx
+            ncols = R if sidx == 0 else P * cr * C  # h_local / the halo buffer
+            self.seg_csrs.append(kernel.build_csr(R, ncols, lrow[m], cols[m], kernel.ORDER_EID,
+                                                  self.device))
+            del m
         self.halo = None
         # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
         overlap = (not self._emulated and self.device.type == "cuda"
@@ -257,8 +262,6 @@ class PartitionedGraph(object):
             self.hpad = torch.zeros(C * cr, F, device=dev)
         self.hpad[:self.num_local].copy_(h_local)
         out = torch.empty(self.num_local, F, device=dev)
-        ind = self.pipe_csr.indices
-        beg, end = self.seg_ranges[0]
         events = []
         if self.comm_stream is not None:
             ready = torch.cuda.Event()
@@ -273,15 +276,14 @@ class PartitionedGraph(object):
                     ev.record(self.comm_stream)
                     events.append(ev)
         # own sources while the halo is in flight
-        kernel.gspmm_ranges("copy_u", beg, end, False, ind, out, ufeat=h_local.contiguous())
+        kernel.gspmm_into(self.seg_csrs[0], out, h_local, accumulate=False)
         for c in range(C):
             if self.comm_stream is not None:
                 torch.cuda.current_stream(dev).wait_event(events[c])
             elif not self._emulated:
                 dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
                                             self.hpad[c * cr:(c + 1) * cr], group=self.group)
-            beg, end = self.seg_ranges[c + 1]
-            kernel.gspmm_ranges("copy_u", beg, end, True, ind, out, ufeat=self.halo)
+            kernel.gspmm_into(self.seg_csrs[c + 1], out, self.halo, accumulate=True)
         if self.comm_stream is not None:
             self.halo.record_stream(torch.cuda.current_stream(dev))
         return out

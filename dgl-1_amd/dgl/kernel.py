@@ -36,6 +36,7 @@ __all__ = ["CSR", "SparseAdj", "build_csr", "gspmm", "gsddmm_dot",
 
 MSG_COPY_U, MSG_U_MUL_E, MSG_COPY_E = 0, 1, 2
 RED_SUM, RED_MAX, RED_MEAN = 0, 1, 2
+RED_SUM_ACCUM = 3  # out += sum, each row's chain continued from out (include/dgl_hip.h)
 ORDER_EID, ORDER_COL = 0, 1
 
 _MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_U_MUL_E,
@@ -88,6 +89,7 @@ class CSR(object):
         self._host_indptr = host_indptr
         self._plans = {}
         self._max_degree = None
+        self._num_nonempty = None
         self._slot_eid = False  # not computed yet
 
     @property
@@ -123,16 +125,29 @@ class CSR(object):
             self._slot_eid = None if ident else self.eid
         return self._slot_eid
 
-    def split_plan(self, threshold):
+    @property
+    def num_nonempty(self):
+        """Rows holding at least one slot (a prefix of the degree-descending
+        row_order)."""
+        if self._num_nonempty is None:
+            ip = self.host_indptr
+            self._num_nonempty = int((ip[1:] > ip[:-1]).sum()) if self.num_rows else 0
+        return self._num_nonempty
+
+    def split_plan(self, threshold, skip_empty=False):
         """Launch plan cutting rows longer than ``threshold`` slots into chunks
         (cached per threshold): dict of device tensors for
-        dglhip_gspmm_chunked_device."""
-        if threshold in self._plans:
-            return self._plans[threshold]
+        dglhip_gspmm_chunked_device. ``skip_empty`` leaves rows without slots
+        out of the light list (accumulating launches need not touch them)."""
+        key = (threshold, bool(skip_empty))
+        if key in self._plans:
+            return self._plans[key]
         ip = self.host_indptr.numpy()
         deg = ip[1:] - ip[:-1]
         order = (self.row_order.cpu().numpy().astype(np.int64) if self.row_order is not None
                  else np.argsort(-deg, kind="stable"))
+        if skip_empty:
+            order = order[deg[order] > 0]
         heavy_mask = deg[order] > threshold
         light = order[~heavy_mask].astype(np.int32)
         heavy = order[heavy_mask]
@@ -149,7 +164,7 @@ class CSR(object):
                 "beg": torch.from_numpy(beg.astype(np.int64)).to(dev),
                 "end": torch.from_numpy(end.astype(np.int64)).to(dev),
                 "num_chunks": int(ptr[-1])}
-        self._plans[threshold] = plan
+        self._plans[key] = plan
         return plan
 
     @property
@@ -303,19 +318,22 @@ def _edge_len(eshape, fshape):
                    % (eshape, fshape))
 
 
-def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
-    """ufeat2: (num_cols, F) or None; efeat2: (E, elen) or None. Returns (out, arg)."""
+def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None):
+    """ufeat2: (num_cols, F) or None; efeat2: (E, elen) or None. Returns (out, arg).
+    ``out`` (optional) receives the result; RED_SUM_ACCUM adds into it."""
     dev = (ufeat2 if ufeat2 is not None else efeat2).device
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
-    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
+    if out is None:
+        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
     eid = csr.slot_eid if msg != MSG_COPY_U else None
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
+    skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
     if split:
-        p = csr.split_plan(split)
+        p = csr.split_plan(split, skip_empty=skip)
         partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
         check_call(LIB.dglhip_gspmm_chunked_device(
             msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(ufeat2),
@@ -324,7 +342,7 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg):
             ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
     elif dev.type == "cuda":
         check_call(LIB.dglhip_gspmm_device(
-            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
+            msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
             _stream_of(dev)))
     else:
@@ -483,6 +501,27 @@ def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
     adj = adj.to(dev)
     return _run_sddmm_dot(adj.fwd, _f32c(lhs.reshape(lhs.shape[0], -1)),
                           _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges, heads)
+
+
+def gspmm_into(csr, out, ufeat, accumulate=False):
+    """Raw copy_u + sum over ``csr`` into ``out`` (num_rows, F), no autograd:
+    out = A·ufeat, or with ``accumulate`` out += A·ufeat with every row's chain
+    continued from the value already in ``out`` (one product evaluated segment
+    by segment: dgl.distributed's pipelined forward). Degree-descending
+    schedule and, under set_row_split, heavy rows cut into chunks whose
+    partials are added in order (deterministic)."""
+    if out.dtype != torch.float32 or not out.is_contiguous():
+        raise DGLError("out must be a contiguous float32 tensor")
+    if out.shape[0] != csr.num_rows or out.device != csr.device:
+        raise DGLError("out does not match the adjacency")
+    if ufeat.shape[0] < csr.num_cols:
+        raise DGLError("ufeat has %d rows, the adjacency %d columns"
+                       % (ufeat.shape[0], csr.num_cols))
+    F = out.shape[1]
+    u2 = _f32c(ufeat.reshape(ufeat.shape[0], F))
+    _run_gspmm(csr, MSG_COPY_U, RED_SUM_ACCUM if accumulate else RED_SUM, u2, None, 0, F,
+               False, out=out)
+    return out
 
 
 def gspmm_ranges(msg, beg, end, accumulate, indices, out, ufeat=None, efeat=None, eid=None):

@@ -119,6 +119,9 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
 #define DGLHIP_REDUCE_SUM  0  /* sum(msg, out)                      reducer.py:52-73   */
 #define DGLHIP_REDUCE_MAX  1  /* max(msg, out)                      reducer.py:75-97   */
 #define DGLHIP_REDUCE_MEAN 2  /* mean: sum / max(deg, 1) (north-star extension) */
+#define DGLHIP_REDUCE_SUM_ACCUM 3  /* out += sum: each row's chain continues from the
+                                    * value already in out (segment-by-segment
+                                    * evaluation of one product; new design) */
 
 /* efeat_len: 0 (no edge feature), 1 (one scalar per edge, broadcast over the
  * feature row; the only case the reference specialises, message.py:37-44),
@@ -129,8 +132,11 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
  * indexed by CSR slot (efeat already permuted into slot order).
  * arg_out (int64[num_rows*feat_len], may be NULL): for MAX, the CSR slot that
  * won each element (-1 for empty rows); needed by the backward.
- * row_order (int32[num_rows], may be NULL): launch schedule (a permutation);
- * results never depend on it.
+ * row_order (int32[num_rows], may be NULL): launch schedule; rows are launched
+ * in this order and results never depend on it. It may list a subset of the
+ * CSR's rows (num_rows then counts the listed rows, indptr still spans the
+ * CSR): rows not listed are not written, which SUM_ACCUM uses to skip rows
+ * without slots.
  * Numerics: SUM/MEAN accumulate per output element in CSR slot order with
  * one fused multiply-add per slot (acc = fma(w, x, acc); copy: acc += x),
  * starting from +0.0 — the arithmetic of torch's CPU sparse x dense product

@@ -42,11 +42,12 @@ for s in $STEPS; do
         > gpurun_out/examples.log 2>&1
       rc=$?; tail -4 gpurun_out/examples.log; [ $rc -eq 0 ] || exit $rc ;;
     emul)
-      for w in 2 8; do for c in 0 4; do
-        timeout -k 10 600 python bench.py --emulate-world $w --pipeline-chunks $c --steps 10 \
-          --warmup 3 --no-traffic > gpurun_out/emul_${w}_$c.json 2> gpurun_out/emul_${w}_$c.err
-        rc=$?; tail -1 gpurun_out/emul_${w}_$c.err; [ $rc -eq 0 ] || exit $rc
-        python -c "import json; d=json.load(open('gpurun_out/emul_${w}_$c.json')); print('W=$w C=$c', d['ms_per_step'], d['roofline']['kernel_ms'])"
+      wl=${WORKLOAD:-reddit}
+      for w in ${EMUL_WORLDS:-2 8}; do for c in ${CHUNKS:-0 4}; do
+        timeout -k 10 600 python bench.py --workload $wl --emulate-world $w --pipeline-chunks $c \
+          --steps 10 --warmup 3 --no-traffic > gpurun_out/emul_${wl}_${w}_$c.json 2> gpurun_out/emul_${wl}_${w}_$c.err
+        rc=$?; tail -1 gpurun_out/emul_${wl}_${w}_$c.err; [ $rc -eq 0 ] || exit $rc
+        python -c "import json; d=json.load(open('gpurun_out/emul_${wl}_${w}_$c.json')); print('$wl W=$w C=$c', d['ms_per_step'], d['roofline']['kernel_ms'])"
       done; done ;;
     gcnprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gcnprof -o run \
