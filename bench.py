@@ -261,8 +261,9 @@ def main():
 
         def step():
             pg.update_all(h_local)
-        parallelism = "%d-way 1-D dst-row partition, RCCL all-gather halo%s" % (
-            world, " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
+        parallelism = "%d-way 1-D dst-row partition, %s all-gather halo%s" % (
+            world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend,
+            " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
             if args.pipeline_chunks > 0 else "")
     del src, dst
     torch.cuda.synchronize()

@@ -259,9 +259,22 @@ class PartitionedGraph(object):
         dev = self.device
         if self.halo is None or self.halo.shape[1] != F:
             self.halo = torch.empty(C * P * cr, F, device=dev)
-            self.hpad = torch.zeros(C * cr, F, device=dev)
-        self.hpad[:self.num_local].copy_(h_local)
-        out = torch.empty(self.num_local, F, device=dev)
+            self.hpads = {}
+        h_local = h_local.contiguous()
+        R = self.num_local
+        sends = []
+        for c in range(C):
+            lo, hi = c * cr, min((c + 1) * cr, R)
+            if hi - lo == cr:  # a full chunk: rows of h_local as they are
+                sends.append(h_local[lo:hi])
+                continue
+            pad = self.hpads.get(c)  # partial / empty chunk: zero-padded copy
+            if pad is None:
+                pad = self.hpads[c] = torch.zeros(cr, F, device=dev)
+            if hi > lo:
+                pad[:hi - lo].copy_(h_local[lo:hi])
+            sends.append(pad)
+        out = torch.empty(R, F, device=dev)
         events = []
         if self.comm_stream is not None:
             ready = torch.cuda.Event()
@@ -270,8 +283,7 @@ class PartitionedGraph(object):
                 self.comm_stream.wait_event(ready)
                 for c in range(C):
                     dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
-                                                self.hpad[c * cr:(c + 1) * cr],
-                                                group=self.group)
+                                                sends[c], group=self.group)
                     ev = torch.cuda.Event()
                     ev.record(self.comm_stream)
                     events.append(ev)
@@ -282,7 +294,7 @@ class PartitionedGraph(object):
                 torch.cuda.current_stream(dev).wait_event(events[c])
             elif not self._emulated:
                 dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
-                                            self.hpad[c * cr:(c + 1) * cr], group=self.group)
+                                            sends[c], group=self.group)
             kernel.gspmm_into(self.seg_csrs[c + 1], out, self.halo, accumulate=True)
         if self.comm_stream is not None:
             self.halo.record_stream(torch.cuda.current_stream(dev))
