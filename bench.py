@@ -22,6 +22,15 @@ cpu_baseline: the reference's own CPU arithmetic (torch.sparse.mm on the
 uncoalesced COO, python/dgl/backend/pytorch/tensor.py:145-146) on a bounded
 sample of the same graph, rank 0 at N = 1 only.
 
+rmat26 (secondary block of the same JSON line, keyed rmat<scale>;
+--no-rmat-leg skips it): the
+north star also asks for absolute edges/s on RMAT-26 at 1/2/4/8 GPUs next to
+the CPU baseline. After the headline timing (and with its memory released)
+the same ranks time one fixed Graph500 R-MAT graph (scale --rmat-scale, edge
+factor 16, 1.07B edges at 26): strong scaling, dst rows partitioned as above,
+heavy rows chunked. Its CPU baseline is the reference product on a compacted
+sample of that graph.
+
 Run: python bench.py [--gpus N --steps K --warmup W]
 """
 from __future__ import absolute_import
@@ -59,18 +68,25 @@ def algorithmic_bytes(num_edges, num_rows, feat):
 
 def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
     """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on the
-    in-edges of the first rows of the graph (bounded sample)."""
+    in-edges of the first rows of the graph (bounded sample). ``h_cpu`` None:
+    the sample's source columns are compacted and get random features (graphs
+    whose full feature matrix does not fit host memory)."""
     threads = torch.get_num_threads()
     torch.set_num_threads(1)  # torch's uncoalesced-COO CPU product is single-threaded
     try:
         deg = torch.bincount(dst, minlength=n)
         cum = torch.cumsum(deg, 0)
-        rows = int(torch.searchsorted(cum, torch.tensor(target_edges))) + 1
+        rows = int(torch.searchsorted(cum, torch.tensor(target_edges, device=cum.device))) + 1
         rows = min(rows, n)
         sel = dst < rows
-        s, d = src[sel], dst[sel]
+        s, d = src[sel].cpu(), dst[sel].cpu()
         e = int(s.numel())
-        A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, n))
+        ncols = n
+        if h_cpu is None:
+            uniq, s = torch.unique(s, return_inverse=True)
+            ncols = int(uniq.numel())
+            h_cpu = torch.rand(ncols, FEAT) * 2 - 1
+        A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, ncols))
         reps, t_total = 0, 0.0
         while reps < 2 and t_total < seconds_budget:
             t0 = time.perf_counter()
@@ -81,9 +97,10 @@ def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
         return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "reference",
                 "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
                           "edge-id order) over the in-edges of the first %d rows: %d edges x "
-                          "F=%d, %d call(s), torch %s, 1 thread (host has %d cpus)"
-                          % (rows, e, h_cpu.shape[1], reps, torch.__version__,
-                             os.cpu_count() or 0)}
+                          "F=%d%s, %d call(s), torch %s, 1 thread (host has %d cpus)"
+                          % (rows, e, h_cpu.shape[1],
+                             "" if ncols == n else " (%d source columns compacted)" % ncols,
+                             reps, torch.__version__, os.cpu_count() or 0)}
     finally:
         torch.set_num_threads(threads)
 
@@ -107,7 +124,7 @@ def pmc_traffic():
         d = os.path.join(out, counter)
         cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
                sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-               "--no-cpu-baseline", "--no-traffic"]
+               "--no-cpu-baseline", "--no-traffic", "--no-rmat-leg"]
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, timeout=300, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -122,6 +139,84 @@ def pmc_traffic():
         return None
     finally:
         shutil.rmtree(out, ignore_errors=True)
+
+
+def timed_steps(step, steps, warmup, world, dev):
+    """W warm-up steps, then K steps bracketed by barrier + synchronize; returns
+    (max-over-ranks seconds, this rank's g-SpMM kernel ms per step)."""
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    kernel.timing_enable(True)
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    kms, _ = kernel.timing_read()
+    kernel.timing_enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, kms / steps
+
+
+def rmat_leg(args, world, rank, dev):
+    """RMAT strong scaling on the same ranks: one fixed graph, 1-D dst-row
+    partition, heavy rows chunked (kernel.set_row_split("auto"))."""
+    from dgl.distributed import PartitionedGraph, balanced_bounds
+    old = kernel.set_row_split("auto")
+    try:
+        t0 = time.time()
+        src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
+        E = int(src.numel())
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(1)
+        cpu = None
+        if world == 1:
+            if rank == 0 and not args.no_cpu_baseline:
+                cpu = cpu_baseline(src, dst, n, None, 2_000_000, seconds_budget=10.0)
+            adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+            del src, dst
+            h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+
+            def step():
+                kernel.gspmm(adj, "copy_u", "sum", h)
+            par = "single GPU"
+        else:
+            bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+            lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+            sel = (dst >= lo) & (dst < hi)
+            pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
+                                  pipeline_chunks=args.pipeline_chunks)
+            del src, dst, sel
+            h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
+
+            def step():
+                pg.update_all(h_local)
+            par = "%d-way 1-D dst-row partition, %s all-gather halo%s" % (
+                world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend,
+                " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
+                if args.pipeline_chunks > 0 else "")
+        torch.cuda.synchronize()
+        log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
+        steps = min(args.steps, 5)
+        elapsed, kms = timed_steps(step, steps, 2, world, dev)
+        return {"value": E * steps / elapsed, "unit": "edges/s", "n_gpus": world,
+                "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
+                "scaling": "strong",
+                "config": "rmat-%d (Graph500 0.57/0.19/0.19/0.05, ids permuted, seed 0): "
+                          "%d nodes, %d edges, feat=%d, heavy rows chunked"
+                          % (args.rmat_scale, n, E, FEAT),
+                "parallelism": par, "kernel_ms_rank0": kms, "cpu_baseline": cpu}
+    finally:
+        kernel.set_row_split(old)
 
 
 def main():
@@ -147,6 +242,8 @@ def main():
     ap.add_argument("--pipeline-chunks", type=int, default=4,
                     help="N>1: halo all-gather chunks overlapped with the local g-SpMM "
                          "(0 = one all-gather, then the kernel; bit-exact rows)")
+    ap.add_argument("--no-rmat-leg", action="store_true",
+                    help="skip the secondary RMAT strong-scaling block (rmat26)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
                          "to rehearse the multi-rank path")
@@ -270,29 +367,8 @@ def main():
     log("setup done in %.1fs; peak HBM %.1f GB" % (time.time() - t0,
                                                     torch.cuda.max_memory_allocated(dev) / 1e9))
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    kernel.timing_enable(True)
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    kms, launches = kernel.timing_read()
-    kernel.timing_enable(False)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
+    elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
     value = num_edges_total * args.steps / elapsed
-    kernel_ms = kms / args.steps  # g-SpMM device time per step (all its launches)
     bytes_per_launch = algorithmic_bytes(num_local_edges, num_rows, FEAT)
     achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
     result = {
@@ -342,6 +418,20 @@ def main():
         result["cpu_baseline"] = cpu_baseline(gsrc, gdst, n, g.ndata["h"].cpu(),
                                               args.cpu_sample_edges)
         log("cpu baseline took %.1fs" % (time.time() - t2))
+    if not args.no_rmat_leg and args.workload == "reddit" and args.emulate_world <= 1:
+        # release the headline leg before the 1.07B-edge graph
+        step = g = h = adj = pg = h_local = None  # noqa: F841
+        import gc
+        gc.collect()
+        torch.cuda.empty_cache()
+        key = "rmat%d" % args.rmat_scale
+        if world == 1:
+            try:
+                result[key] = rmat_leg(args, world, rank, dev)
+            except (RuntimeError, MemoryError, dgl.DGLError) as err:
+                result[key] = {"error": repr(err)}
+        else:  # collectives: a failing rank must end the job, not leave peers waiting
+            result[key] = rmat_leg(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

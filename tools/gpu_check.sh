@@ -20,13 +20,13 @@ for s in $STEPS; do
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic \
+        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-rmat-leg \
         > gpurun_out/prof.log 2>&1
       rc=$?; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
     dist)
       # rehearse the multi-rank bench path: 2 ranks sharing the one GPU over gloo
       timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-        --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 1 \
+        --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 1 --rmat-scale 18 \
         --graph-scale 0.05 --dist-backend gloo > gpurun_out/dist.json 2> gpurun_out/dist.err
       rc=$?; tail -3 gpurun_out/dist.err; cat gpurun_out/dist.json; [ $rc -eq 0 ] || exit $rc ;;
     examples)
@@ -68,7 +68,7 @@ for s in $STEPS; do
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
-          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic > gpurun_out/pmc_$c.log 2>&1
+          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-rmat-leg > gpurun_out/pmc_$c.log 2>&1
         rc=$?; tail -2 gpurun_out/pmc_$c.log; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac
