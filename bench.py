@@ -141,6 +141,19 @@ def pmc_traffic():
         shutil.rmtree(out, ignore_errors=True)
 
 
+def describe_partition(pg, world, args):
+    backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
+    if pg.halo_mode == "alltoall":
+        halo = "%s all-to-allv halo (%d referenced remote rows on this rank)%s" % (
+            backend, pg.num_halo, ", own-source segment overlapped with the exchange"
+            if args.pipeline_chunks > 0 else "")
+    else:
+        halo = "%s all-gather halo%s" % (
+            backend, " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
+            if args.pipeline_chunks > 0 else "")
+    return "%d-way 1-D dst-row partition, %s" % (world, halo)
+
+
 def timed_steps(step, steps, warmup, world, dev):
     """W warm-up steps, then K steps bracketed by barrier + synchronize; returns
     (max-over-ranks seconds, this rank's g-SpMM kernel ms per step)."""
@@ -200,10 +213,7 @@ def rmat_leg(args, world, rank, dev):
 
             def step():
                 pg.update_all(h_local)
-            par = "%d-way 1-D dst-row partition, %s all-gather halo%s" % (
-                world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend,
-                " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
-                if args.pipeline_chunks > 0 else "")
+            par = describe_partition(pg, world, args)
         torch.cuda.synchronize()
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
@@ -358,10 +368,7 @@ def main():
 
         def step():
             pg.update_all(h_local)
-        parallelism = "%d-way 1-D dst-row partition, %s all-gather halo%s" % (
-            world, "RCCL" if args.dist_backend == "nccl" else args.dist_backend,
-            " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
-            if args.pipeline_chunks > 0 else "")
+        parallelism = describe_partition(pg, world, args)
     del src, dst
     torch.cuda.synchronize()
     log("setup done in %.1fs; peak HBM %.1f GB" % (time.time() - t0,

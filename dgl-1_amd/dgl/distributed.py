@@ -17,15 +17,21 @@ contiguous ranges balanced by in-edge count, one process per GPU
   one all-to-allv (``all_to_all_single`` with split sizes) per layer; the
   backward is the reverse all-to-allv with sum-on-receive. The request lists
   are exchanged once, at partition time. ``halo="auto"`` takes the
-  all-to-allv when the largest rank halo is below N/2 (one all-reduce MAX,
-  so every rank decides alike).
+  all-to-allv when it at least halves what a rank receives: the largest rank
+  halo against the (P-1) padded blocks of an all-gather (one all-reduce MAX,
+  so every rank decides alike). RMAT graphs land here: half their vertices
+  have no out-edges, and a rank's halo is about 0.2 N at P = 2..8, against
+  (P-1)/P N for the all-gather; Reddit-like graphs reference almost every node
+  and keep the all-gather.
 
 Column ids of the local CSR are remapped once (at partition time) from global
 node ids to positions in the padded all-gather buffer, so the kernel runs
 unchanged. Row results are bit-identical to the single-GPU product: each
 local row accumulates exactly the same edges in the same edge-id order.
 
-Pipelined forward (``pipeline_chunks = C > 0``, inference / benchmarking):
+Pipelined forward (``pipeline_chunks = C > 0``, inference / benchmarking).
+With the all-to-allv halo there are two segments: the own sources, reduced
+while the exchange is in flight, then the received rows. With the all-gather:
 each row's slots are grouped into segments — sources this rank owns first,
 then the remote sources of halo chunk 1..C — so the own segment is reduced
 while the halo is still in flight, and each remote segment as soon as its
@@ -155,31 +161,40 @@ class PartitionedGraph(object):
         dst = torch.as_tensor(dst, dtype=torch.int64).to(device)
         b = self.bounds.to(device)
         owner = torch.searchsorted(b, src, right=True) - 1
-        cols = owner * self.max_rows + (src - b[owner])
         self.num_edges = int(src.numel())
         self.device = device
         self.chunks = int(pipeline_chunks)
+        self.adj = None
         if halo not in ("auto", "allgather", "alltoall"):
             raise ValueError("halo must be auto, allgather or alltoall")
-        if halo != "allgather" and (self.chunks > 0 or self._emulated):
-            halo = "allgather"  # the pipelined / emulated studies model the all-gather
+        if halo != "allgather" and self._emulated:
+            halo = "allgather"  # emulated single-rank studies model the all-gather
         own = owner == self.rank
         if halo != "allgather":
             need = torch.unique(src[~own])       # sorted global ids = owner order
             if halo == "auto":
-                # largest halo over the ranks (one all-reduce: every rank decides alike)
+                # the all-to-allv when it at least halves what a rank receives:
+                # largest halo vs the (P-1) padded blocks of an all-gather (one
+                # all-reduce MAX, so every rank decides alike)
                 top = torch.tensor([need.numel()], dtype=torch.int64, device=self._coll_dev())
                 dist.all_reduce(top, op=dist.ReduceOp.MAX, group=group)
-                halo = "alltoall" if 2 * int(top) < self.num_nodes else "allgather"
+                gather_rows = (self.world - 1) * self.max_rows
+                halo = "alltoall" if 2 * int(top) <= gather_rows else "allgather"
         self.halo_mode = halo
+        self.comm_stream = None
         if halo == "alltoall":
             self._build_alltoall(src, dst, b, owner, own, need)
         elif self.chunks > 0:
             self._build_pipeline(src, dst, b, owner)
-            self.adj = None
         else:
+            cols = owner * self.max_rows + (src - b[owner])
             self.adj = kernel.from_coo(self.num_local, self.world * self.max_rows,
                                        dst - self.lo, cols, kernel.ORDER_EID, device)
+        if self.chunks > 0:
+            # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
+            overlap = (not self._emulated and self.device.type == "cuda"
+                       and dist.get_backend(self.group) == "nccl")
+            self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
 
     def _coll_dev(self):
         """Device the process group's collectives take tensors on."""
@@ -202,11 +217,22 @@ class PartitionedGraph(object):
         self.send_splits = send_splits.tolist()
         self.recv_splits = recv_splits.tolist()
         self.num_halo = int(need.numel())
-        # columns: own sources -> [0, R), remote -> R + position in `need`
         pos = torch.searchsorted(need, src)
-        cols = torch.where(own, src - self.lo, R + pos)
-        self.adj = kernel.from_coo(R, R + self.num_halo, dst - self.lo, cols,
-                                   kernel.ORDER_EID, self.device)
+        if self.chunks > 0:
+            # pipelined forward: own sources (columns of h_local) reduced while the
+            # exchange is in flight, then the received rows (columns of the receive
+            # buffer) continue each row's chain
+            lrow = dst - self.lo
+            self.seg_csrs = [
+                kernel.build_csr(R, R, lrow[own], (src - self.lo)[own], kernel.ORDER_EID,
+                                 self.device),
+                kernel.build_csr(R, max(self.num_halo, 1), lrow[~own], pos[~own],
+                                 kernel.ORDER_EID, self.device)]
+        else:
+            # columns: own sources -> [0, R), remote -> R + position in `need`
+            cols = torch.where(own, src - self.lo, R + pos)
+            self.adj = kernel.from_coo(R, R + self.num_halo, dst - self.lo, cols,
+                                       kernel.ORDER_EID, self.device)
 
     def _build_pipeline(self, src, dst, b, owner):
         C, P, R = self.chunks, self.world, self.num_local
@@ -229,10 +255,6 @@ class PartitionedGraph(object):
                                                   self.device))
             del m
         self.halo = None
-        # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
-        overlap = (not self._emulated and self.device.type == "cuda"
-                   and dist.get_backend(self.group) == "nccl")
-        self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
 
     def gather_halo(self, h_local):
         """Source rows the local CSR's columns index: all-gather of the padded
@@ -249,6 +271,8 @@ class PartitionedGraph(object):
         if self.chunks > 0:
             if msg != "copy_u" or reduce != "sum" or h_local.requires_grad:
                 raise ValueError("the pipelined forward covers copy_u + sum without autograd")
+            if self.halo_mode == "alltoall":
+                return self._pipelined_alltoall_sum(h_local)
             return self._pipelined_copy_sum(h_local)
         full = self.gather_halo(h_local)
         return kernel.gspmm(self.adj, msg, reduce, full, efeat)
@@ -298,4 +322,34 @@ class PartitionedGraph(object):
             kernel.gspmm_into(self.seg_csrs[c + 1], out, self.halo, accumulate=True)
         if self.comm_stream is not None:
             self.halo.record_stream(torch.cuda.current_stream(dev))
+        return out
+
+    def _pipelined_alltoall_sum(self, h_local):
+        dev = self.device
+        h_local = h_local.contiguous()
+        F = h_local.shape[1]
+        send = h_local.index_select(0, self.send_idx)
+        recv = h_local.new_empty((sum(self.recv_splits), F))
+        out = torch.empty(self.num_local, F, device=dev)
+        done = None
+        if self.comm_stream is not None:
+            ready = torch.cuda.Event()
+            ready.record()
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ready)
+                dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits,
+                                       group=self.group)
+                done = torch.cuda.Event()
+                done.record(self.comm_stream)
+        else:
+            dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits,
+                                   group=self.group)
+        # own sources while the exchange is in flight
+        kernel.gspmm_into(self.seg_csrs[0], out, h_local, accumulate=False)
+        if done is not None:
+            torch.cuda.current_stream(dev).wait_event(done)
+            recv.record_stream(torch.cuda.current_stream(dev))
+            send.record_stream(self.comm_stream)
+        if recv.shape[0]:
+            kernel.gspmm_into(self.seg_csrs[1], out, recv, accumulate=True)
         return out

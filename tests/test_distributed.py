@@ -125,7 +125,7 @@ def test_graphsage_distributed_matches_single():
         np.testing.assert_allclose(multi[k], v.numpy(), rtol=1e-4, atol=1e-5, err_msg=k)
 
 
-def _pipe_worker(rank, world, port):
+def _pipe_worker(rank, world, port, graph="chung_lu"):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
@@ -137,7 +137,10 @@ def _pipe_worker(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         n, F = 2500, 8
-        src, dst, n = data.chung_lu(n, 30 * n, 30.0, seed=5)  # edge ids in (src, dst) order
+        if graph == "banded":  # halo well under an all-gather: auto takes the all-to-allv
+            src, dst, n = _banded(n, 60, seed=5)
+        else:
+            src, dst, n = data.chung_lu(n, 30 * n, 30.0, seed=5)  # edge ids in (src, dst) order
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         sel = (dst >= lo) & (dst < hi)
@@ -145,14 +148,22 @@ def _pipe_worker(rank, world, port):
         ref = O.spmm_coo(n, dst.numpy(), src.numpy(), H.numpy())[lo:hi]
         for chunks in (1, 3):
             pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu", pipeline_chunks=chunks)
+            assert pg.halo_mode == ("alltoall" if graph == "banded" else "allgather")
             out = pg.update_all(H[lo:hi].contiguous()).numpy()
             np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
+            if graph == "banded":
+                # exactly the chain over (own source first, then received rows; edge id)
+                s, d = src[sel], dst[sel]
+                remote = ((s < lo) | (s >= hi)).numpy()
+                order = np.lexsort((np.arange(len(s)), remote))
+                exact = O.spmm_coo(n, d.numpy()[order], s.numpy()[order], H.numpy())[lo:hi]
+                assert np.array_equal(out, exact)
             # deterministic
             assert np.array_equal(out, pg.update_all(H[lo:hi].contiguous()).numpy())
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_pipelined_forward(world):
-    mp.spawn(_pipe_worker, args=(world, _free_port()), nprocs=world, join=True)
+@pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (3, "banded")])
+def test_pipelined_forward(world, graph):
+    mp.spawn(_pipe_worker, args=(world, _free_port(), graph), nprocs=world, join=True)
