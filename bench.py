@@ -329,7 +329,9 @@ def main():
 
             def step():
                 pg.update_all(h_local)
-            mode = "pipelined segments (own + %d halo chunks)" % args.pipeline_chunks
+            mode = ("pipelined segments (own + all-to-allv halo of %d rows)" % pg.num_halo
+                    if pg.halo_mode == "alltoall" else
+                    "pipelined segments (own + %d halo chunks)" % args.pipeline_chunks)
         else:
             adj = kernel.from_coo(hi - lo, n, dst[sel] - lo, src[sel], kernel.ORDER_EID, dev)
             h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1

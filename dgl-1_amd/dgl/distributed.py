@@ -165,14 +165,16 @@ class PartitionedGraph(object):
         self.device = device
         self.chunks = int(pipeline_chunks)
         self.adj = None
+        self.halo = None
         if halo not in ("auto", "allgather", "alltoall"):
             raise ValueError("halo must be auto, allgather or alltoall")
-        if halo != "allgather" and self._emulated:
-            halo = "allgather"  # emulated single-rank studies model the all-gather
         own = owner == self.rank
         if halo != "allgather":
             need = torch.unique(src[~own])       # sorted global ids = owner order
-            if halo == "auto":
+            if halo == "auto" and self._emulated:  # single-rank study: this rank's halo
+                gather_rows = (self.world - 1) * self.max_rows
+                halo = "alltoall" if 2 * need.numel() <= gather_rows else "allgather"
+            elif halo == "auto":
                 # the all-to-allv when it at least halves what a rank receives:
                 # largest halo vs the (P-1) padded blocks of an all-gather (one
                 # all-reduce MAX, so every rank decides alike)
@@ -202,10 +204,16 @@ class PartitionedGraph(object):
 
     def _build_alltoall(self, src, dst, b, owner, own, need):
         P, R = self.world, self.num_local
-        cdev = self._coll_dev()
         bd = b.to(need.device)
         need_owner = torch.searchsorted(bd, need, right=True) - 1
         recv_splits = torch.bincount(need_owner, minlength=P).cpu()
+        if self._emulated:  # no peers to ask: only this rank's receive side
+            self.send_idx, self.send_splits = None, None
+            self.recv_splits = recv_splits.tolist()
+            self.num_halo = int(need.numel())
+            self._build_alltoall_csrs(src, dst, own, need)
+            return
+        cdev = self._coll_dev()
         # tell every owner how many of its rows this rank needs, then which
         send_splits = torch.empty(P, dtype=torch.int64, device=cdev)
         dist.all_to_all_single(send_splits, recv_splits.to(cdev), group=self.group)
@@ -217,6 +225,10 @@ class PartitionedGraph(object):
         self.send_splits = send_splits.tolist()
         self.recv_splits = recv_splits.tolist()
         self.num_halo = int(need.numel())
+        self._build_alltoall_csrs(src, dst, own, need)
+
+    def _build_alltoall_csrs(self, src, dst, own, need):
+        R = self.num_local
         pos = torch.searchsorted(need, src)
         if self.chunks > 0:
             # pipelined forward: own sources (columns of h_local) reduced while the
@@ -328,11 +340,18 @@ class PartitionedGraph(object):
         dev = self.device
         h_local = h_local.contiguous()
         F = h_local.shape[1]
-        send = h_local.index_select(0, self.send_idx)
-        recv = h_local.new_empty((sum(self.recv_splits), F))
         out = torch.empty(self.num_local, F, device=dev)
         done = None
-        if self.comm_stream is not None:
+        if self._emulated:  # compute-only study: a resident random receive buffer
+            if self.halo is None or self.halo.shape[1] != F:
+                self.halo = torch.rand(self.num_halo, F, device=dev) * 2 - 1
+            recv = self.halo
+        else:
+            send = h_local.index_select(0, self.send_idx)
+            recv = h_local.new_empty((sum(self.recv_splits), F))
+        if self._emulated:
+            pass
+        elif self.comm_stream is not None:
             ready = torch.cuda.Event()
             ready.record()
             with torch.cuda.stream(self.comm_stream):
