@@ -83,3 +83,17 @@ def test_gcn_hip_graph_replay_matches_eager():
     graph = gcn_spmv.run(gcn_spmv.parser().parse_args(base + ["--hip-graph"]))
     assert graph["hip_graph"]
     assert abs(graph["loss"] - eager["loss"]) < 1e-4
+
+
+@pytest.mark.gpu
+def test_gat_hip_graph_replay_matches_eager():
+    """GAT (fused attention g-SDDMM, head-broadcast u_mul_e and copy_edge
+    g-SpMMs, their backward) captured in one HIP graph trains like eager."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    base = ["--dataset", "pubmed", "--epochs", "10", "--gpu", "0", "--in-drop", "0",
+            "--attn-drop", "0"]
+    eager = gat_train.run(gat_train.parser().parse_args(base))
+    graph = gat_train.run(gat_train.parser().parse_args(base + ["--hip-graph"]))
+    assert graph["hip_graph"]
+    assert abs(graph["loss"] - eager["loss"]) < 1e-4 * max(1.0, abs(eager["loss"]))

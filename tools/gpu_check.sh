@@ -36,6 +36,7 @@ for s in $STEPS; do
         timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 --n-hidden 128 --n-epochs 20 --hip-graph &&
         timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 &&
         timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 --udf &&
+        timeout -k 10 300 python examples/gat/train.py --dataset pubmed --gpu 0 --epochs 30 --hip-graph &&
         timeout -k 10 300 python examples/graphsage/train.py --dataset reddit --gpu 0 --n-epochs 10 &&
         timeout -k 10 300 python examples/rgcn/link_predict.py --gpu 0 --n-epochs 20 &&
         timeout -k 10 300 python examples/rgcn/link_predict.py --gpu 0 --n-epochs 20 --udf ) \
