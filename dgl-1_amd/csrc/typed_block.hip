@@ -32,46 +32,88 @@ namespace dglhip {
 
 namespace {
 
-constexpr int kMaxPass = 16;  // output features per lane: 64 * 16 = 1024 max
+constexpr int kEdgesInFlight = 4;
 
-template <int PASS>
+// One wave per (destination row, 64-wide slice of the output features): the
+// slices of a row run in parallel waves (8 for R-GCN's 500 features) instead
+// of one wave looping over them per edge, and each wave keeps
+// kEdgesInFlight edges' loads outstanding. For every output element the
+// arithmetic is unchanged:  m_e = fma chain over i of h[u, b*si+i] *
+// W[r, b, i, j];  acc = fma(norm_e, m_e, acc) in CSR-slot order.
+// SI > 0: the block width as a compile-time constant (all loads of an edge
+// group issued before its fma chains); SI == 0: runtime width.
+template <int SI>
 __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
-    int64_t num_rows, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ indptr,
-    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
-    const int64_t* __restrict__ etype, const float* __restrict__ ufeat,
-    const float* __restrict__ weight, const float* __restrict__ enorm,
-    float* __restrict__ out) {
-  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) +
-                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+    int64_t num_rows, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const int64_t* __restrict__ eid, const int64_t* __restrict__ etype,
+    const float* __restrict__ ufeat, const float* __restrict__ weight,
+    const float* __restrict__ enorm, float* __restrict__ out) {
+  const int64_t si = SI > 0 ? SI : si_rt;
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t row = wave / npass, pass = wave - (wave / npass) * npass;
   if (row >= num_rows) return;
   const int lane = threadIdx.x & 63;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
-  float acc[PASS];
+  const int64_t jg = pass * 64 + lane;
+  const bool active = jg < Fo;
+  // idle lanes of the last slice read block 0 (valid addresses) and never store
+  const int64_t b = active ? jg / so : 0, j = active ? jg - b * so : 0;
+  const int64_t hoff = b * si, woff = b * si * so + j;
+  float acc = 0.0f;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  int64_t k = beg;
+  for (; k + kEdgesInFlight <= end; k += kEdgesInFlight) {
+    const float* hb[kEdgesInFlight];
+    const float* wb[kEdgesInFlight];
+    float nrm[kEdgesInFlight];
 #pragma unroll
-  for (int t = 0; t < PASS; ++t) acc[t] = 0.0f;
-  for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
-    const int64_t e = eid[k];
-    const float* h = ufeat + int64_t(indices[k]) * Fi;
-    const float* w = weight + etype[e] * wr;
-    const float nrm = enorm ? enorm[e] : 1.0f;
+    for (int q = 0; q < kEdgesInFlight; ++q) {
+      const int64_t e = eid[k + q];
+      hb[q] = ufeat + int64_t(indices[k + q]) * Fi + hoff;
+      wb[q] = weight + etype[e] * wr + woff;
+      nrm[q] = enorm ? enorm[e] : 1.0f;
+    }
+    if (SI > 0) {
+      float hv[kEdgesInFlight][SI > 0 ? SI : 1], wv[kEdgesInFlight][SI > 0 ? SI : 1];
 #pragma unroll
-    for (int t = 0; t < PASS; ++t) {
-      const int64_t jg = lane + 64 * t;
-      if (jg < Fo) {
-        const int64_t b = jg / so, j = jg - b * so;
-        const float* hb = h + b * si;
-        const float* wb = w + b * si * so + j;
-        float m = 0.0f;
-        for (int64_t i = 0; i < si; ++i) m = __builtin_fmaf(hb[i], wb[i * so], m);
-        acc[t] = __builtin_fmaf(nrm, m, acc[t]);
+      for (int q = 0; q < kEdgesInFlight; ++q) {
+#pragma unroll
+        for (int i = 0; i < SI; ++i) {
+          hv[q][i] = hb[q][i];
+          wv[q][i] = wb[q][i * so];
+        }
       }
+#pragma unroll
+      for (int q = 0; q < kEdgesInFlight; ++q) {
+        float m = 0.0f;
+#pragma unroll
+        for (int i = 0; i < SI; ++i) m = __builtin_fmaf(hv[q][i], wv[q][i], m);
+        acc = __builtin_fmaf(nrm[q], m, acc);
+      }
+    } else {
+      float m[kEdgesInFlight];
+#pragma unroll
+      for (int q = 0; q < kEdgesInFlight; ++q) m[q] = 0.0f;
+      for (int64_t i = 0; i < si; ++i) {
+#pragma unroll
+        for (int q = 0; q < kEdgesInFlight; ++q)
+          m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
+      }
+#pragma unroll
+      for (int q = 0; q < kEdgesInFlight; ++q) acc = __builtin_fmaf(nrm[q], m[q], acc);
     }
   }
-#pragma unroll
-  for (int t = 0; t < PASS; ++t) {
-    const int64_t jg = lane + 64 * t;
-    if (jg < Fo) out[row * Fo + jg] = acc[t];
+  for (; k < end; ++k) {
+    const int64_t e = eid[k];
+    const float* h = ufeat + int64_t(indices[k]) * Fi + hoff;
+    const float* w = weight + etype[e] * wr + woff;
+    float m = 0.0f;
+    for (int64_t i = 0; i < si; ++i) m = __builtin_fmaf(h[i], w[i * so], m);
+    acc = __builtin_fmaf(enorm ? enorm[e] : 1.0f, m, acc);
   }
+  if (active) out[row * Fo + jg] = acc;
 }
 
 // dW[r, b, i, j] = sum over edges e of relation r (edge-id order) of
@@ -115,23 +157,28 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t
   DGLHIP_CHECK(num_rows >= 0 && num_blocks > 0 && in_block > 0 && out_block > 0,
                "bad sizes");
   const int64_t Fo = num_blocks * out_block;
-  DGLHIP_CHECK(Fo <= 64 * kMaxPass, "output width " << Fo << " exceeds " << 64 * kMaxPass);
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(indptr && indices && eid && etype && ufeat && weight && out,
                "null pointer argument");
-  DGLHIP_CHECK((num_rows + 3) / 4 <= 0x7fffffff, "grid too large");
-  const int64_t pass = (Fo + 63) / 64;
-  const dim3 grid(static_cast<unsigned>((num_rows + 3) / 4)), block(256);
-#define DGLHIP_TB(P)                                                                    \
-  if (pass <= P) {                                                                     \
-    hipLaunchKernelGGL(typed_block_spmm_kernel<P>, grid, block, 0, stream, num_rows,   \
-                       num_blocks, in_block, out_block, indptr, indices, eid, etype,   \
-                       ufeat, weight, enorm, out);                                     \
-    HIP_CALL(hipGetLastError());                                                       \
-    return 0;                                                                          \
+  const int64_t npass = (Fo + 63) / 64;
+  const int64_t waves = num_rows * npass;
+  DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
+  const dim3 grid(static_cast<unsigned>((waves + 3) / 4)), block(256);
+#define DGLHIP_TB(S)                                                                   \
+  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_rows, npass, \
+                     num_blocks, in_block, out_block, indptr, indices, eid, etype, ufeat, \
+                     weight, enorm, out)
+  switch (in_block) {
+    case 1: DGLHIP_TB(1); break;
+    case 2: DGLHIP_TB(2); break;
+    case 4: DGLHIP_TB(4); break;
+    case 5: DGLHIP_TB(5); break;
+    case 8: DGLHIP_TB(8); break;
+    case 16: DGLHIP_TB(16); break;
+    default: DGLHIP_TB(0); break;
   }
-  DGLHIP_TB(1) DGLHIP_TB(2) DGLHIP_TB(4) DGLHIP_TB(8) DGLHIP_TB(16)
 #undef DGLHIP_TB
+  HIP_CALL(hipGetLastError());
   API_END();
 }
 
