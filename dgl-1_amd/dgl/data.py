@@ -16,12 +16,32 @@ fetched here, so benchmarks use seeded synthetic graphs of the same shape
 Generation runs on whatever device is given (torch RNG seeded per call), so a
 1-GPU box builds the 115M-edge graph in seconds. Edge ids are assigned in
 (src, dst) order.
+
+On-disk formats, read with loaders that execute nothing
+from the file (numpy / scipy with pickling disabled, plain text):
+
+* ``CoraTextDataset``: the pygcn text release (``cora/cora.content``,
+  ``cora/cora.cites``) as the reference's CoraDataset._load parses it
+  (python/dgl/data/citation_graph.py:349-380).
+* ``RedditDataset``: DGL's Reddit release (``reddit/reddit_graph.npz``, a
+  scipy sparse matrix, and ``reddit/reddit_data.npz`` with feature / label /
+  node_types).
+* ``load_edge_list``: a plain edge list (text "src dst" lines, an (E, 2)
+  ``.npy`` or an ``.npz`` with src / dst arrays).
+
+``load_data(name, root=...)`` (or ``$DGL_DATA_DIR``) uses these files when
+they are present and falls back to the synthetic stand-ins otherwise.
 """
 from __future__ import absolute_import
 
 import torch
 
-__all__ = ["reddit_like", "chung_lu", "rmat", "REDDIT_NODES", "REDDIT_EDGES"]
+import os
+
+import numpy as np
+
+__all__ = ["reddit_like", "chung_lu", "rmat", "REDDIT_NODES", "REDDIT_EDGES", "load_data",
+           "load_edge_list", "CoraTextDataset", "RedditDataset", "SyntheticNodeDataset"]
 
 REDDIT_NODES = 232965
 REDDIT_EDGES = 114615892
@@ -178,6 +198,129 @@ class SyntheticNodeDataset(object):
         self.test_mask[perm[-min(1000, n // 5):]] = True
 
 
-def load_data(name, seed=0, device="cpu"):
-    """dgl.data.load_data counterpart (python/dgl/data/__init__.py:15-25), offline."""
-    return SyntheticNodeDataset(name, seed, device)
+def load_edge_list(path, num_nodes=None):
+    """(src, dst, num_nodes) int64 tensors from an edge-list file: text lines
+    "src dst" (whitespace or comma separated, '#' comments), an (E, 2) integer
+    ``.npy``, or an ``.npz`` holding ``src`` and ``dst``. Edge ids follow the
+    file order; num_nodes defaults to max id + 1."""
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            src, dst = np.asarray(z["src"]), np.asarray(z["dst"])
+    elif path.endswith(".npy"):
+        e = np.load(path, allow_pickle=False)
+        if e.ndim != 2 or e.shape[1] != 2:
+            raise ValueError("%s: expected an (E, 2) array, got %s" % (path, e.shape))
+        src, dst = e[:, 0], e[:, 1]
+    else:
+        e = np.loadtxt(path, dtype=np.int64, comments="#",
+                       delimiter="," if path.endswith(".csv") else None, ndmin=2)
+        if e.size and e.shape[1] != 2:
+            raise ValueError("%s: expected 2 columns, got %d" % (path, e.shape[1]))
+        src, dst = (e[:, 0], e[:, 1]) if e.size else (np.zeros(0), np.zeros(0))
+    src = torch.from_numpy(np.ascontiguousarray(src, dtype=np.int64))
+    dst = torch.from_numpy(np.ascontiguousarray(dst, dtype=np.int64))
+    if src.numel() and min(int(src.min()), int(dst.min())) < 0:
+        raise ValueError("%s: negative node id" % path)
+    top = int(max(int(src.max()), int(dst.max()))) + 1 if src.numel() else 0
+    n = top if num_nodes is None else int(num_nodes)
+    if n < top:
+        raise ValueError("%s: node id %d >= num_nodes %d" % (path, top - 1, n))
+    return src, dst, n
+
+
+def _masks(n, train, val, test, device):
+    out = []
+    for idx in (train, val, test):
+        m = torch.zeros(n, dtype=torch.bool)
+        m[torch.as_tensor(np.asarray(idx, dtype=np.int64))] = True
+        out.append(m.to(device))
+    return out
+
+
+class CoraTextDataset(object):
+    """The pygcn text release of Cora, parsed as the reference's
+    CoraDataset._load does (citation_graph.py:349-380): one line per paper
+    "id word_0 .. word_k label" in cora.content, "cited citing" pairs in
+    cora.cites; the adjacency is symmetrised (max of A and A^T); features are
+    row-normalised; train / val / test = ids 0-139 / 200-499 / 500-1499.
+    Deterministic where the reference is not: class ids follow the sorted
+    label names (the reference's set() order varies with the hash seed), and
+    the edges of the symmetric adjacency come in (src, dst) order, as
+    networkx yields them from the CSR matrix. ``graph`` = (src, dst)."""
+
+    def __init__(self, root, device="cpu"):
+        base = os.path.join(root, "cora")
+        rows = np.genfromtxt(os.path.join(base, "cora.content"), dtype=np.dtype(str), ndmin=2)
+        ids = rows[:, 0].astype(np.int64)
+        feats = rows[:, 1:-1].astype(np.float32)
+        names = rows[:, -1]
+        classes = sorted(set(names.tolist()))
+        self.labels = torch.as_tensor(np.searchsorted(np.asarray(classes), names),
+                                      dtype=torch.int64, device=device)
+        self.num_labels = len(classes)
+        n = len(ids)
+        pos = {int(j): i for i, j in enumerate(ids)}
+        cites = np.genfromtxt(os.path.join(base, "cora.cites"), dtype=np.int64, ndmin=2)
+        u = np.array([pos[int(a)] for a in cites[:, 0]], dtype=np.int64)
+        v = np.array([pos[int(b)] for b in cites[:, 1]], dtype=np.int64)
+        # symmetric pattern of max(A, A^T): every (u, v) and (v, u), once each
+        key = np.unique(np.concatenate([u * n + v, v * n + u]))
+        self.graph = (torch.from_numpy(key // n), torch.from_numpy(key % n))
+        rowsum = feats.sum(1, keepdims=True)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            feats = feats * np.power(rowsum, -1)  # inf rows stay inf, as _normalize
+        self.features = torch.from_numpy(feats).to(device)
+        self.num_nodes = n
+        self.train_mask, self.val_mask, self.test_mask = _masks(
+            n, range(min(140, n)), range(min(200, n), min(500, n)),
+            range(min(500, n), min(1500, n)), device)
+
+
+class RedditDataset(object):
+    """DGL's Reddit release: ``reddit_graph.npz`` (scipy sparse adjacency,
+    read with pickling disabled) and ``reddit_data.npz`` (feature, label,
+    node_types with 1 / 2 / 3 = train / val / test). Edges in the stored
+    COO order. ``graph`` = (src, dst)."""
+
+    def __init__(self, root, device="cpu"):
+        import scipy.sparse as sp
+        base = os.path.join(root, "reddit")
+        adj = sp.load_npz(os.path.join(base, "reddit_graph.npz")).tocoo()
+        with np.load(os.path.join(base, "reddit_data.npz"), allow_pickle=False) as z:
+            feat, label, types = z["feature"], z["label"], z["node_types"]
+        n = adj.shape[0]
+        self.graph = (torch.from_numpy(adj.row.astype(np.int64)),
+                      torch.from_numpy(adj.col.astype(np.int64)))
+        self.features = torch.from_numpy(np.asarray(feat, dtype=np.float32)).to(device)
+        self.labels = torch.from_numpy(np.asarray(label, dtype=np.int64)).to(device)
+        self.num_labels = int(self.labels.max()) + 1 if n else 0
+        self.num_nodes = n
+        t = torch.from_numpy(np.asarray(types))
+        self.train_mask, self.val_mask, self.test_mask = (
+            (t == k).to(device) for k in (1, 2, 3))
+
+
+def _on_disk(name, root):
+    if not root:
+        return None
+    if name == "cora" and os.path.exists(os.path.join(root, "cora", "cora.content")):
+        return CoraTextDataset
+    if name == "reddit" and os.path.exists(os.path.join(root, "reddit", "reddit_graph.npz")):
+        return RedditDataset
+    return None
+
+
+def load_data(name, seed=0, device="cpu", root=None):
+    """dgl.data.load_data counterpart (python/dgl/data/__init__.py:15-25):
+    the on-disk release under ``root`` (default ``$DGL_DATA_DIR``) when its
+    files are there, else the seeded synthetic stand-in (nothing is ever
+    downloaded)."""
+    root = root if root is not None else os.environ.get("DGL_DATA_DIR")
+    cls = _on_disk(name, root)
+    if cls is not None:
+        ds = cls(root, device)
+        ds.name, ds.source = name, "files under %s" % root
+        return ds
+    ds = SyntheticNodeDataset(name, seed, device)
+    ds.source = "synthetic (seed %d)" % seed
+    return ds
