@@ -18,11 +18,12 @@ for s in $STEPS; do
       timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json; [ $rc -eq 0 ] || exit $rc ;;
     prof)
+      # the bench line and the kernel statistics of the SAME process (headline leg only)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-traffic --no-rmat-leg \
-        > gpurun_out/prof.log 2>&1
-      rc=$?; tail -3 gpurun_out/prof.log; [ $rc -eq 0 ] || exit $rc ;;
+        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-cpu-baseline \
+        > gpurun_out/prof.json 2> gpurun_out/prof.log
+      rc=$?; tail -1 gpurun_out/prof.log; cat gpurun_out/prof.json; [ $rc -eq 0 ] || exit $rc ;;
     dist)
       # rehearse the multi-rank bench path: 2 ranks sharing the one GPU over gloo
       timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
