@@ -127,13 +127,25 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
       else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
     }
   }
-  for (; k < end; ++k) {
-    SlotLoad<VEC, MSG, EM> s;
-    s.load(ufeat, efeat, F, f0, elen, eoff, indices[k],
-           MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k] : k));
-    if (MSG == DGLHIP_MSG_COPY_U) acc += s.u;
-    else if (MSG == DGLHIP_MSG_COPY_E) acc += s.e;
-    else acc = Vec<VEC>::fma(s.e, s.u, acc);
+  // the last rem < UNROLL slots as one predicated batch: all their gathers in
+  // flight together (a slot-by-slot tail would serialise up to UNROLL - 1
+  // load latencies per row, which dominates rows shorter than UNROLL)
+  const int64_t rem = end - k;
+  if (rem > 0) {
+    SlotLoad<VEC, MSG, EM> s[UNROLL];
+#pragma unroll
+    for (int j = 0; j < UNROLL - 1; ++j)
+      if (j < rem)
+        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
+                  MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k + j] : k + j));
+#pragma unroll
+    for (int j = 0; j < UNROLL - 1; ++j) {
+      if (j < rem) {
+        if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
+        else if (MSG == DGLHIP_MSG_COPY_E) acc += s[j].e;
+        else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
+      }
+    }
   }
   return acc;
 }
@@ -297,15 +309,23 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
         }
       }
     }
-    for (; k < end; ++k) {
-      SlotLoad<VEC, MSG, EM> s;
-      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k], edge(k));
-      const V x = message(s);
+    const int64_t rem = end - k;  // the last < UNROLL slots: one predicated batch
+    if (rem > 0) {
+      SlotLoad<VEC, MSG, EM> s[UNROLL];
 #pragma unroll
-      for (int i = 0; i < VEC; ++i) {
-        const float xi = reinterpret_cast<const float*>(&x)[i];
-        float& bi = reinterpret_cast<float*>(&best)[i];
-        if (xi > bi) { bi = xi; arg[i] = k; }
+      for (int j = 0; j < UNROLL - 1; ++j)
+        if (j < rem) s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j], edge(k + j));
+#pragma unroll
+      for (int j = 0; j < UNROLL - 1; ++j) {
+        if (j < rem) {
+          const V x = message(s[j]);
+#pragma unroll
+          for (int i = 0; i < VEC; ++i) {
+            const float xi = reinterpret_cast<const float*>(&x)[i];
+            float& bi = reinterpret_cast<float*>(&best)[i];
+            if (xi > bi) { bi = xi; arg[i] = k + j; }
+          }
+        }
       }
     }
     stv<VEC>(out + row * F + f0, best);

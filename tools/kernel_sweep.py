@@ -1,7 +1,10 @@
 """Interleaved A/B sweep of g-SpMM copy_u+sum kernel variants on the bench graph
 (cdna_hip_programming.md §5.4 rule 24: variants x rounds in one process).
 
-  python tools/kernel_sweep.py [--rounds 5] [--workload reddit|rmat]
+  python tools/kernel_sweep.py [--rounds 5] [--workload reddit|rmat] [--rmat-scale 26]
+
+RMAT runs with the heavy-row split on (kernel.set_row_split("auto")), as
+bench.py's RMAT line does.
 """
 import argparse
 import json
@@ -16,6 +19,7 @@ from dgl import _ffi, data, kernel  # noqa: E402
 
 VARIANTS = [(0, 0, 0, 0), (2, 64, 8, 0), (2, 64, 16, 0), (2, 64, 32, 0), (4, 32, 16, 0),
             (4, 32, 32, 0), (2, 64, 8, 1), (2, 64, 16, 1), (4, 32, 8, 1), (4, 32, 16, 1)]
+# (vec, lanes per row, gathers per batch, software-pipelined batches); (0,0,0,0) = default
 
 
 def main():
@@ -28,6 +32,7 @@ def main():
     dev = torch.device("cuda", 0)
     if args.workload == "rmat":
         src, dst, n = data.rmat(args.rmat_scale, 16, device=dev)
+        kernel.set_row_split("auto")  # as bench.py's RMAT line
     else:
         src, dst, n = data.reddit_like(device=dev)
     adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
@@ -43,9 +48,9 @@ def main():
             kernel.timing_enable(True)
             for _ in range(args.iters):
                 kernel.gspmm(adj, "copy_u", "sum", h)
-            ms, cnt = kernel.timing_read()
+            ms, _ = kernel.timing_read()
             kernel.timing_enable(False)
-            times[v].append(ms / cnt)
+            times[v].append(ms / args.iters)  # per g-SpMM call (all its launches)
     _ffi.check_call(_ffi.LIB.dglhip_set_spmm_variant(0, 0, 0, 0))
     res = {"%d,%d,%d,%d" % v: {"median_ms": sorted(t)[len(t) // 2], "min_ms": min(t)}
            for v, t in times.items()}
