@@ -387,9 +387,23 @@ class DGLGraph(object):
         scheduler.schedule_update_all(self, mf, rf, af)
 
     # -- sparse views ----------------------------------------------------------
+    def _cached_view(self, key, build):
+        # per (view, arguments, ctx); cleared by mutation and clear_cache(),
+        # as the reference's adjacency / incidence caches (graph_index.py:537-662)
+        cache = self._graph._cache
+        if key not in cache:
+            cache[key] = build()
+        return cache[key]
+
     def adjacency_matrix(self, transpose=False, ctx=torch.device("cpu")):
         """Adjacency as a torch sparse COO tensor (rows = dst unless transpose)
-        in the reference's nnz order (graph.py:2721-2742)."""
+        in the reference's nnz order (graph.py:2721-2742); cached per
+        (transpose, ctx) until the graph changes."""
+        ctx = torch.device(ctx)
+        return self._cached_view(("adjmat", bool(transpose), str(ctx)),
+                                 lambda: self._adjacency_matrix(transpose, ctx))
+
+    def _adjacency_matrix(self, transpose, ctx):
         src, dst = self._graph.src(), self._graph.dst()
         row, col = (src, dst) if transpose else (dst, src)
         n = self.number_of_nodes()
@@ -397,7 +411,15 @@ class DGLGraph(object):
         return torch.sparse_coo_tensor(idx, torch.ones(len(row)), (n, n)).to(ctx)
 
     def incidence_matrix(self, typestr, ctx=torch.device("cpu")):
-        """'in' / 'out' / 'both' incidence matrix (graph_index.py:587-662)."""
+        """'in' / 'out' / 'both' incidence matrix (graph_index.py:587-662);
+        cached per (type, ctx) until the graph changes."""
+        if typestr not in ("in", "out", "both"):
+            raise DGLError("Invalid incidence matrix type: %s" % typestr)
+        ctx = torch.device(ctx)
+        return self._cached_view(("incmat", typestr, str(ctx)),
+                                 lambda: self._incidence_matrix(typestr, ctx))
+
+    def _incidence_matrix(self, typestr, ctx):
         src, dst = self._graph.src(), self._graph.dst()
         n, m = self.number_of_nodes(), self.number_of_edges()
         eid = torch.arange(m)
