@@ -168,6 +168,28 @@ class DGLGraph(object):
     def out_degrees(self, v=ALL):
         return self._graph.out_degrees(None if is_all(v) else v)
 
+    def to_networkx(self, node_attrs=None, edge_attrs=None):
+        """networkx (Multi)DiGraph of the structure (graph.py:1094-1135): every
+        edge carries its id as the 'id' attribute; node_attrs / edge_attrs
+        name feature columns copied as per-node / per-edge tensor rows."""
+        import networkx as nx
+        nxg = nx.MultiDiGraph() if self.is_multigraph else nx.DiGraph()
+        n = self.number_of_nodes()
+        nxg.add_nodes_from(range(n))
+        src, dst = self._graph.src().tolist(), self._graph.dst().tolist()
+        for e, (u, v) in enumerate(zip(src, dst)):
+            nxg.add_edge(u, v, id=e)
+        for attr in node_attrs or ():
+            col = self._node_frame[attr]
+            for i in range(n):
+                nxg.nodes[i][attr] = col[i]
+        if edge_attrs:
+            cols = {attr: self._edge_frame[attr] for attr in edge_attrs}
+            for _, _, d in nxg.edges(data=True):
+                for attr, col in cols.items():
+                    d[attr] = col[d["id"]]
+        return nxg
+
     def from_networkx(self, nx_graph, node_attrs=None, edge_attrs=None):
         """Replace the structure by a networkx graph (graph.py:1136-1232)."""
         self.clear()
