@@ -394,6 +394,82 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   }
 }
 
+// SDDMM dot for rows of NB x 32 floats (F = 32 * NB), one wave per row: the
+// wave takes 8 slots at a time, 8 lanes per slot; lane j of a slot reads the
+// 16 B at 32 i + 4 j of every 32-float column block i (one instruction = 8
+// whole 128-B lines), UNROLL groups of 8 slots in flight. Per lane and block
+// the partial is an fma chain over its 4 features (x, y, z, w); a head's
+// total is the sum of its lanes' partials in block order, then an xor
+// butterfly over the lanes sharing the head (both lanes of a pair add the
+// same two values, so every lane ends with identical bits: deterministic).
+//   D >= 32 (D % 32 == 0): a head spans D / 32 whole blocks, 8-lane butterfly;
+//   D <  32 (D in 4, 8, 16): D / 4 lanes per head, butterfly within them.
+template <int NB, int UNROLL>
+__global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
+    int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out) {
+  constexpr int F = NB * 32;
+  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) +
+                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (row >= num_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int s = lane >> 3, j = lane & 7;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  if (beg == end) return;
+  f32x4 a[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) a[i] = ldv<4>(lhs + row * F + 32 * i + 4 * j);
+  const int lph = D >= 32 ? 8 : static_cast<int>(D >> 2);   // lanes sharing a head
+  const int64_t dblk = D >= 32 ? D / 32 : 1;                 // blocks per head (D >= 32)
+  for (int64_t k0 = beg; k0 < end; k0 += 8 * UNROLL) {
+    f32x4 c[UNROLL][NB];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      int64_t k = k0 + 8 * u + s;
+      k = k < end ? k : end - 1;  // idle slot lanes re-read the row's last slot
+      const float* r = rhs + int64_t(indices[k]) * F + 4 * j;
+#pragma unroll
+      for (int i = 0; i < NB; ++i) c[u][i] = ldv<4>(r + 32 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t k = k0 + 8 * u + s;
+      float p[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        float t = a[i].x * c[u][i].x;
+        t = __builtin_fmaf(a[i].y, c[u][i].y, t);
+        t = __builtin_fmaf(a[i].z, c[u][i].z, t);
+        p[i] = __builtin_fmaf(a[i].w, c[u][i].w, t);
+      }
+      if (D >= 32) {
+        float t = 0.0f;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {  // blocks in order; a head closes every dblk blocks
+          t = (i % dblk == 0) ? p[i] : t + p[i];
+          if ((i + 1) % dblk == 0) {
+            float r = t;
+            r += __shfl_xor(r, 4, 64);
+            r += __shfl_xor(r, 2, 64);
+            r += __shfl_xor(r, 1, 64);
+            if (j == 0 && k < end) out[eid[k] * H + i / dblk] = r;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          float t = p[i];
+          if (lph >= 4) t += __shfl_xor(t, 2, 64);
+          if (lph >= 2) t += __shfl_xor(t, 1, 64);
+          const int64_t h = (32 * i + 4 * j) / D;
+          if ((j % lph) == 0 && k < end) out[eid[k] * H + h] = t;
+        }
+      }
+    }
+  }
+}
+
 // GAT edge attention, one wave per destination row v (gat/train.py:90-96):
 //   out[eid[k], h] = clamp(exp(leaky_relu(lhs[u, h] + rhs[v, h], alpha)), lo, hi)
 // with u = indices[k]; lanes run over the row's (slot, head) pairs.
@@ -789,10 +865,29 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
   const int64_t blocks = (num_rows + 3) / 4;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
+  const int64_t D = feat_len / num_heads;
+  const bool aligned = (reinterpret_cast<uintptr_t>(lhs) % 16) == 0 &&
+                       (reinterpret_cast<uintptr_t>(rhs) % 16) == 0;
+  const bool head_ok = D >= 32 ? (D % 32 == 0) : (D == 4 || D == 8 || D == 16);
+  const int64_t nb = feat_len % 32 == 0 ? feat_len / 32 : 0;
+  const bool sliced = aligned && head_ok && (nb == 1 || nb == 2 || nb == 4 || nb == 8 ||
+                                             nb == 16);
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL(gsddmm_dot_kernel, dim3(static_cast<unsigned>(blocks)),
-                       dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
-                       indices, eid, lhs, rhs, out);
+#define DGLHIP_SDDMM(NB)                                                                   \
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, (NB >= 8 ? 1 : 2)>),                    \
+                     dim3(static_cast<unsigned>(blocks)),                                  \
+                     dim3(256), 0, stream, num_rows, num_heads, D, indptr, indices, eid, lhs, \
+                     rhs, out)
+    if (sliced && nb == 1) DGLHIP_SDDMM(1);
+    else if (sliced && nb == 2) DGLHIP_SDDMM(2);
+    else if (sliced && nb == 4) DGLHIP_SDDMM(4);
+    else if (sliced && nb == 8) DGLHIP_SDDMM(8);
+    else if (sliced && nb == 16) DGLHIP_SDDMM(16);
+    else
+      hipLaunchKernelGGL(gsddmm_dot_kernel, dim3(static_cast<unsigned>(blocks)),
+                         dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
+                         indices, eid, lhs, rhs, out);
+#undef DGLHIP_SDDMM
   });
   API_END();
 }

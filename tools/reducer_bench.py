@@ -52,6 +52,22 @@ def main():
                     "edges_per_s": E / (t * 1e-3),
                     "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
                     "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
+    # g-SDDMM dot (u_mul_e weight gradient; GAT per-head dots): per slot one
+    # lhs row (the destination's, reused along the row) and one gathered rhs row
+    for heads in (1, 8):
+        kernel.gsddmm_dot(adj, h, h, E, heads)
+        torch.cuda.synchronize()
+        kernel.timing_enable(True)
+        for _ in range(args.iters):
+            kernel.gsddmm_dot(adj, h, h, E, heads)
+        ms, cnt = kernel.timing_read()
+        kernel.timing_enable(False)
+        t = ms / max(cnt, 1)
+        byts = E * (4 * F + 4 + 8 + 4 * heads) + n * (4 * F + 8)
+        res.append({"msg": "sddmm_dot", "reduce": "heads=%d" % heads, "kernel_ms": round(t, 3),
+                    "edges_per_s": E / (t * 1e-3),
+                    "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
+                    "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
     print(json.dumps({"graph": "reddit_like", "nodes": n, "edges": E, "feat": F,
                       "note": "max also writes the (N, F) int64 argmax only under autograd; "
                               "timed here without it", "cases": res}, indent=1))
