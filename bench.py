@@ -92,11 +92,13 @@ def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
         reps, t_total = 0, 0.0
         while reps < 2 and t_total < seconds_budget:
             t0 = time.perf_counter()
-            torch.sparse.mm(A, h_cpu)
+            ref = torch.sparse.mm(A, h_cpu)
             t_total += time.perf_counter() - t0
             reps += 1
         eps = e * reps / t_total
+        build = build_cpu_baseline(rows, ncols, d, s, h_cpu, ref)
         return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "reference",
+                "build_kernel": build,
                 "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
                           "edge-id order) over the in-edges of the first %d rows: %d edges x "
                           "F=%d%s, %d call(s), torch %s, 1 thread (host has %d cpus)"
@@ -105,6 +107,27 @@ def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
                              reps, torch.__version__, os.cpu_count() or 0)}
     finally:
         torch.set_num_threads(threads)
+
+
+def build_cpu_baseline(rows, ncols, d, s, h_cpu, ref):
+    """the build's own host g-SpMM (libdgl_hip's
+    dglhip_gspmm_host over a CSR, std::thread-parallel) on the same sample, at
+    the host-core share the job has ($OMP_NUM_THREADS / $DGL_NUM_THREADS, else
+    every hardware thread), and whether it reproduces (i) bit for bit."""
+    adj = kernel.from_coo(rows, ncols, d, s, kernel.ORDER_EID, "cpu")
+    out = kernel.gspmm(adj, "copy_u", "sum", h_cpu)  # warm: builds the host CSR once
+    reps, t_total = 0, 0.0
+    while reps < 3:
+        t0 = time.perf_counter()
+        out = kernel.gspmm(adj, "copy_u", "sum", h_cpu)
+        t_total += time.perf_counter() - t0
+        reps += 1
+    threads = int(os.environ.get("DGL_NUM_THREADS") or os.environ.get("OMP_NUM_THREADS")
+                  or (os.cpu_count() or 1))
+    return {"value": int(s.numel()) * reps / t_total, "unit": "edges/s",
+            "cores": min(threads, 64), "kind": "build",
+            "bit_identical_to_reference": bool(torch.equal(out, ref.to_dense()
+                                                           if ref.is_sparse else ref))}
 
 
 def pmc_traffic():
