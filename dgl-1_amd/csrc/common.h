@@ -6,7 +6,9 @@
 // src/runtime/c_runtime_api.cc:130-145).
 #pragma once
 
+#include <algorithm>
 #include <cstdint>
+#include <functional>
 #include <sstream>
 #include <stdexcept>
 #include <string>
@@ -45,24 +47,32 @@ class Error : public std::runtime_error {
 // hardware concurrency, capped at 64.
 int default_num_threads();
 
-// Static partition of [0, n) over `nthreads` std::threads; fn(begin, end, tid).
+// Persistent worker pool (threadpool.cc). pool_run executes task(tid) for tid
+// in [0, min(nparts, pool size)) and returns the number of parts it used; the
+// first exception from any part is rethrown here.
+bool in_parallel_region();
+int pool_run(int nparts, const std::function<void(int)>& task);
+
+// Static partition of [0, n) over up to `nthreads` pool workers; fn(begin, end,
+// tid). Ranges shorter than `min_n` items (each item being cheap), single-thread
+// requests and calls made from inside a running parallel_for execute inline;
+// pass min_n = 2 when every item is a large task.
 template <typename Fn>
-void parallel_for(int64_t n, int nthreads, Fn&& fn) {
-  if (nthreads <= 1 || n < 4096) {
+void parallel_for(int64_t n, int nthreads, Fn&& fn, int64_t min_n = 256) {
+  if (nthreads <= 1 || n < min_n || in_parallel_region()) {
     fn(int64_t(0), n, 0);
     return;
   }
   if (nthreads > n) nthreads = static_cast<int>(n);
-  std::vector<std::thread> pool;
-  pool.reserve(nthreads - 1);
   const int64_t chunk = (n + nthreads - 1) / nthreads;
-  for (int t = 1; t < nthreads; ++t) {
+  const std::function<void(int)> task = [&](int t) {
     const int64_t b = t * chunk, e = std::min<int64_t>(n, b + chunk);
-    if (b >= e) break;
-    pool.emplace_back([&fn, b, e, t] { fn(b, e, t); });
+    if (b < e) fn(b, e, t);
+  };
+  const int used = pool_run(nthreads, task);
+  if (used < nthreads) {  // pool smaller than asked: finish the remaining chunks here
+    for (int t = used; t < nthreads; ++t) task(t);
   }
-  fn(int64_t(0), std::min<int64_t>(n, chunk), 0);
-  for (auto& th : pool) th.join();
 }
 
 }  // namespace dglhip

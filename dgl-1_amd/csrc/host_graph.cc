@@ -69,7 +69,7 @@ static void csr_by_eid(int64_t num_rows, int64_t nnz, const int64_t* row,
           eid[p] = i;
         }
       }
-    });
+    }, 2);  // one item = one thread's whole row range
   } else {
     std::vector<int64_t> cursor(indptr, indptr + num_rows);
     for (int64_t i = 0; i < nnz; ++i) {
