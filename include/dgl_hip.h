@@ -35,6 +35,7 @@
 #ifndef DGL_HIP_H_
 #define DGL_HIP_H_
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -292,8 +293,15 @@ int dglhip_timing_read(double* total_ms, int64_t* launches);
 #define DGLHIP_TC_FLOAT 2
 #define DGLHIP_TC_HANDLE 3
 #define DGLHIP_TC_NULL 4
+#define DGLHIP_TC_DGL_TYPE 5
+#define DGLHIP_TC_DGL_CONTEXT 6
 #define DGLHIP_TC_ARRAY_HANDLE 7
+#define DGLHIP_TC_NODE_HANDLE 8
+#define DGLHIP_TC_MODULE_HANDLE 9
+#define DGLHIP_TC_FUNC_HANDLE 10
 #define DGLHIP_TC_STR 11
+#define DGLHIP_TC_BYTES 12
+#define DGLHIP_TC_NDARRAY_CONTAINER 13
 
 /* DLPack-compatible tensor (same layout as DLTensor with DLContext, which is
  * what include/dgl/runtime/ndarray.h:114 passes). device_type: 1 = CPU,
@@ -318,16 +326,75 @@ typedef union {
   const char* v_str;
 } DGLHipValue;
 
-typedef void* DGLHipFunctionHandle;
+/* DLManagedTensor (dlpack.h; the reference's include/dgl/runtime/ndarray.h
+ * exchanges these with torch through DGLArrayFromDLPack / DGLArrayToDLPack). */
+typedef struct DGLHipManagedTensor {
+  DGLHipTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(struct DGLHipManagedTensor* self);
+} DGLHipManagedTensor;
 
+typedef void* DGLHipFunctionHandle;
+typedef void* DGLHipModuleHandle;
+typedef void* DGLHipStreamHandle;
+/* A DGLArrayHandle points at a DGLHipTensor that is the first member of the
+ * library's ref-counted array container. */
+typedef DGLHipTensor* DGLHipArrayHandle;
+typedef void* DGLHipRetValueHandle;
+/* C callback types (c_runtime_api.h:300-314). */
+typedef int (*DGLHipPackedCFunc)(DGLHipValue* args, int* type_codes, int num_args,
+                                 DGLHipRetValueHandle ret, void* resource_handle);
+typedef void (*DGLHipPackedCFuncFinalizer)(void* resource_handle);
+
+/* Function registry and calls (c_runtime_api.h:233-375). */
 int DGLFuncGetGlobal(const char* name, DGLHipFunctionHandle* out);
 int DGLFuncListGlobalNames(int* out_size, const char*** out_array);
 int DGLFuncCall(DGLHipFunctionHandle func, DGLHipValue* arg_values,
                 int* type_codes, int num_args, DGLHipValue* ret_val,
                 int* ret_type_code);
 int DGLFuncFree(DGLHipFunctionHandle func);
+int DGLFuncRegisterGlobal(const char* name, DGLHipFunctionHandle f, int override_);
+int DGLFuncCreateFromCFunc(DGLHipPackedCFunc func, void* resource_handle,
+                           DGLHipPackedCFuncFinalizer fin, DGLHipFunctionHandle* out);
+int DGLCFuncSetReturn(DGLHipRetValueHandle ret, DGLHipValue* value, int* type_code,
+                      int num_ret);
+int DGLCbArgToReturn(DGLHipValue* value, int code);
 
-/* Registered names (argument lists are documented in csrc/registry.cc):
+/* NDArray (c_runtime_api.h:388-461). Host arrays are 64-B aligned host
+ * memory; device_type 10 (ROCm) arrays are hipMalloc'ed on device_id. */
+int DGLArrayAlloc(const int64_t* shape, int ndim, int dtype_code, int dtype_bits,
+                  int dtype_lanes, int device_type, int device_id,
+                  DGLHipArrayHandle* out);
+int DGLArrayFree(DGLHipArrayHandle handle);
+int DGLArrayCopyFromBytes(DGLHipArrayHandle handle, void* data, size_t nbytes);
+int DGLArrayCopyToBytes(DGLHipArrayHandle handle, void* data, size_t nbytes);
+int DGLArrayCopyFromTo(DGLHipArrayHandle from, DGLHipArrayHandle to,
+                       DGLHipStreamHandle stream);
+int DGLArrayFromDLPack(DGLHipManagedTensor* from, DGLHipArrayHandle* out);
+int DGLArrayToDLPack(DGLHipArrayHandle from, DGLHipManagedTensor** out);
+void DGLDLManagedTensorCallDeleter(DGLHipManagedTensor* dltensor);
+
+/* Streams (c_runtime_api.h:471-520); HIP streams on ROCm, no-ops on CPU. */
+int DGLStreamCreate(int device_type, int device_id, DGLHipStreamHandle* out);
+int DGLStreamFree(int device_type, int device_id, DGLHipStreamHandle stream);
+int DGLSetStream(int device_type, int device_id, DGLHipStreamHandle handle);
+int DGLSynchronize(int device_type, int device_id, DGLHipStreamHandle stream);
+int DGLStreamStreamSynchronize(int device_type, int device_id,
+                               DGLHipStreamHandle src, DGLHipStreamHandle dst);
+
+/* Modules / extension types (c_runtime_api.h:179-226). DGL never creates
+ * runtime modules or extension types; kernels are built into this library.
+ * These fail with a message (freeing NULL succeeds). */
+int DGLModLoadFromFile(const char* file_name, const char* format,
+                       DGLHipModuleHandle* out);
+int DGLModImport(DGLHipModuleHandle mod, DGLHipModuleHandle dep);
+int DGLModGetFunction(DGLHipModuleHandle mod, const char* func_name,
+                      int query_imports, DGLHipFunctionHandle* out);
+int DGLModFree(DGLHipModuleHandle mod);
+int DGLExtTypeFree(void* handle, int type_code);
+
+/* Registered names (argument lists are documented in csrc/registry.cc,
+ * csrc/graph_index.cc and csrc/scheduler.cc):
  *   "dglhip._CAPI_GSpMM"        (msg, reduce, indptr, indices, eid, ufeat,
  *                                efeat|null, out, arg_out|null,
  *                                row_order|null, stream)
@@ -336,7 +403,15 @@ int DGLFuncFree(DGLHipFunctionHandle func);
  *   "dglhip._CAPI_COOToCSR"     (num_rows, row, col, order, indptr, indices,
  *                                eid)
  *   "dglhip._CAPI_RowsByDegree" (indptr, row_order)
- * Tensors are DGLHipTensor* (type code 7); device is taken from the tensor. */
+ *   "graph_index._CAPI_*"       the 45 graph-index functions of
+ *                                src/graph/graph_apis.cc, same arguments and
+ *                                returns (graphs as HANDLEs, id arrays as
+ *                                int64 host NDArrays, edge/subgraph/adjacency
+ *                                results as indexable FUNC_HANDLEs)
+ *   "runtime.degree_bucketing._CAPI_*"  the 4 scheduler functions of
+ *                                src/scheduler/scheduler_apis.cc:16-60
+ * Tensors are DGLHipTensor* (type code 7 or 13); device is taken from the
+ * tensor. A NULL stream argument means the stream set by DGLSetStream. */
 
 #ifdef __cplusplus
 }  /* extern "C" */
