@@ -185,7 +185,7 @@ def timed_steps(step, steps, warmup, world, dev):
     for _ in range(warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     kernel.timing_enable(True)
     torch.cuda.synchronize()
@@ -193,12 +193,12 @@ def timed_steps(step, steps, warmup, world, dev):
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     kms, _ = kernel.timing_read()
     kernel.timing_enable(False)
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -217,7 +217,7 @@ def rmat_leg(args, world, rank, dev):
         gen = torch.Generator(device=dev)
         gen.manual_seed(1)
         cpu = None
-        if world == 1:
+        if not dist.is_initialized():
             if rank == 0 and not args.no_cpu_baseline:
                 cpu = cpu_baseline(src, dst, n, None, 2_000_000, seconds_budget=10.0)
             adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
@@ -279,6 +279,9 @@ def main():
                          "(0 = one all-gather, then the kernel; bit-exact rows)")
     ap.add_argument("--no-rmat-leg", action="store_true",
                     help="skip the secondary RMAT strong-scaling block (rmat26)")
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="run the multi-rank code path (RCCL group, partition, collectives) "
+                         "on a world of one rank (single-GPU rehearsal; not a driver line)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
                          "to rehearse the multi-rank path")
@@ -287,7 +290,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     pmc = None
-    if world == 1 and not args.no_traffic and args.workload == "reddit":
+    if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
         t0 = time.time()
         pmc = pmc_traffic()  # before this process initialises the GPU
         log("pmc traffic passes took %.1fs" % (time.time() - t0))
@@ -297,8 +300,12 @@ def main():
     dev_index = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
-    if world > 1:
+    if world > 1 or args.dist_rehearsal:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29631")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -310,7 +317,7 @@ def main():
         src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
         kernel.set_row_split("auto")
         args.no_cpu_baseline = True
-    elif (world == 1 and args.graph_scale == 1.0 and args.emulate_world <= 1
+    elif (not dist.is_initialized() and args.graph_scale == 1.0 and args.emulate_world <= 1
           and data._on_disk("reddit", os.environ.get("DGL_DATA_DIR"))):
         # the real graph when its release files are on the box
         root = os.environ["DGL_DATA_DIR"]
@@ -334,7 +341,7 @@ def main():
     log("rank %d: graph %d nodes %d edges generated in %.1fs" % (rank, n, num_edges_total,
                                                                   time.time() - t0))
 
-    if world == 1 and args.workload == "rmat" and args.emulate_world <= 1:
+    if not dist.is_initialized() and args.workload == "rmat" and args.emulate_world <= 1:
         # 1.07B edges: build the device CSR directly (no host copy of the edge list)
         adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
         del src, dst
@@ -345,7 +352,7 @@ def main():
         def step():
             kernel.gspmm(adj, "copy_u", "sum", h)
         parallelism = "single GPU (kernel API; heavy rows chunked)"
-    elif world == 1 and args.emulate_world > 1:
+    elif not dist.is_initialized() and args.emulate_world > 1:
         from dgl.distributed import balanced_bounds
         W = args.emulate_world
         if args.workload == "reddit":  # weak scaling: the x W graph
@@ -381,7 +388,7 @@ def main():
         parallelism = "emulated rank 0 of %d, %s, no communication (H = %.0f MB)" % (
             W, mode, n * FEAT * 4 / 1e6)
         args.no_cpu_baseline = True
-    elif world == 1:
+    elif not dist.is_initialized():
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))
         h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         g.ndata["h"] = h
@@ -461,7 +468,7 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not dist.is_initialized() and not args.no_cpu_baseline:
         t2 = time.time()
         gsrc, gdst = g._graph.src(), g._graph.dst()
         result["cpu_baseline"] = cpu_baseline(gsrc, gdst, n, g.ndata["h"].cpu(),
@@ -474,7 +481,7 @@ def main():
         gc.collect()
         torch.cuda.empty_cache()
         key = "rmat%d" % args.rmat_scale
-        if world == 1:
+        if not dist.is_initialized():
             try:
                 result[key] = rmat_leg(args, world, rank, dev)
             except (RuntimeError, MemoryError, dgl.DGLError) as err:
@@ -483,7 +490,7 @@ def main():
             result[key] = rmat_leg(args, world, rank, dev)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 

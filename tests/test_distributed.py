@@ -167,3 +167,52 @@ def _pipe_worker(rank, world, port, graph="chung_lu"):
 @pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (3, "banded")])
 def test_pipelined_forward(world, graph):
     mp.spawn(_pipe_worker, args=(world, _free_port(), graph), nprocs=world, join=True)
+
+
+@pytest.mark.gpu
+def test_single_rank_rccl_group_all_modes():
+    """The RCCL code path of PartitionedGraph on the one GPU this pool gives:
+    a world-size-1 nccl (RCCL) group, every halo mode and the pipelined
+    forward with its comm stream, forward rows bit-exact and backward against
+    the oracle. Multi-rank RCCL runs only in the driver's 8-GPU bench; this
+    pins the collective calls' device placement, split lists and stream use."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
+    from dgl import data
+    from dgl.distributed import PartitionedGraph
+    from oracle import oracle as O
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0,
+                            world_size=1, device_id=dev)
+    try:
+        assert dist.get_backend() == "nccl"
+        src, dst, n = data.chung_lu(4000, 40 * 4000, 30.0, seed=3)
+        bounds = torch.tensor([0, n])
+        gen = torch.Generator().manual_seed(7)
+        H = torch.rand(n, 16, generator=gen) * 2 - 1
+        G = torch.randn(n, 16, generator=gen)
+        ref = O.spmm_coo(n, dst.numpy(), src.numpy(), H.numpy())
+        gref = O.spmm_coo(n, src.numpy(), dst.numpy(), G.numpy())
+        for halo, chunks in (("auto", 0), ("allgather", 0), ("alltoall", 0),
+                             ("allgather", 2), ("alltoall", 2)):
+            pg = PartitionedGraph(n, src, dst, bounds, dev, halo=halo, pipeline_chunks=chunks)
+            h = H.to(dev).requires_grad_(chunks == 0)  # the pipelined forward is inference-only
+            out = pg.update_all(h)
+            torch.cuda.synchronize()
+            if chunks == 0:
+                assert np.array_equal(out.detach().cpu().numpy(), ref), (halo, chunks)
+                out.backward(G.to(dev))
+                torch.cuda.synchronize()
+                np.testing.assert_allclose(h.grad.cpu().numpy(), gref, rtol=1e-5, atol=1e-5)
+            else:
+                np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-5,
+                                           atol=1e-5)
+        t = torch.ones(1, device=dev)
+        dist.all_reduce(t)
+        dist.barrier()
+        assert t.item() == 1.0
+    finally:
+        dist.destroy_process_group()

@@ -30,6 +30,11 @@ for s in $STEPS; do
         --master-addr 127.0.0.1 --master-port 29611 bench.py --gpus 2 --steps 3 --warmup 1 --rmat-scale 18 \
         --graph-scale 0.05 --dist-backend gloo > gpurun_out/dist.json 2> gpurun_out/dist.err
       rc=$?; tail -3 gpurun_out/dist.err; cat gpurun_out/dist.json; [ $rc -eq 0 ] || exit $rc ;;
+    rehearsal)
+      # the N>1 bench path (RCCL group, partition, collectives, max-over-ranks timing) on one rank
+      timeout -k 10 600 python bench.py --dist-rehearsal --no-traffic --steps 5 --warmup 2 \
+        > gpurun_out/rehearsal.json 2> gpurun_out/rehearsal.err
+      rc=$?; tail -4 gpurun_out/rehearsal.err; cat gpurun_out/rehearsal.json; [ $rc -eq 0 ] || exit $rc ;;
     examples)
       ( timeout -k 10 600 python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 --n-hidden 128 --n-epochs 20 &&
         timeout -k 10 300 python examples/gcn/gcn_spmv.py --dataset cora --gpu 0 --n-epochs 50 &&
