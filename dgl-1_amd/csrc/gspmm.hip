@@ -77,6 +77,40 @@ __device__ __forceinline__ void stv(float* p, typename Vec<VEC>::T v) {
   *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
 }
 
+// Cache policy of the source-row gathers and output stores (POL template
+// parameter; copy_u + sum at VEC 2 x 64 lanes, selected by dglhip_set_cache_policy):
+//  POL_DEFAULT : default policy everywhere.
+//  POL_NT      : every gather and the output store non-temporal.
+//  POL_HOT     : column ids carry a "hot source" flag in bit 31 (set by the host on
+//                the sources with the most out-edges); hot rows load with the
+//                default policy, all other rows and the output non-temporal, so
+//                once-read traffic does not evict the rows that are read again.
+//  POL_NT_OUT  : only the output store non-temporal.
+enum { POL_DEFAULT = 0, POL_NT = 1, POL_HOT = 2, POL_NT_OUT = 3 };
+
+template <int VEC, int POL>
+__device__ __forceinline__ typename Vec<VEC>::T gather_row(const float* __restrict__ ufeat,
+                                                           int32_t col, int64_t F, int64_t f0) {
+  typedef typename Vec<VEC>::T V;
+  if (POL == POL_NT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const V*>(ufeat + int64_t(col) * F + f0));
+  } else if (POL == POL_HOT) {
+    const V* p = reinterpret_cast<const V*>(ufeat + int64_t(col & 0x7fffffff) * F + f0);
+    if (col < 0) return *p;  // wave-uniform: col comes from the scalar slot stream
+    return __builtin_nontemporal_load(p);
+  }
+  return ldv<VEC>(ufeat + int64_t(col) * F + f0);
+}
+
+// Output rows: non-temporal under every policy but the default. The policy is
+// a template parameter, not a runtime flag: the compiler merges a branch
+// between a plain and a non-temporal store into one plain store.
+template <int VEC, int POL>
+__device__ __forceinline__ void store_row(float* p, typename Vec<VEC>::T v) {
+  if (POL == POL_DEFAULT) stv<VEC>(p, v);
+  else __builtin_nontemporal_store(v, reinterpret_cast<typename Vec<VEC>::T*>(p));
+}
+
 // Edge-feature layouts (EM template parameter):
 //  EM_FULL   : one value per edge and feature, efeat[e, f]
 //  EM_SCALAR : one scalar per edge broadcast over the row, efeat[e]
@@ -88,7 +122,7 @@ enum { EM_FULL = 0, EM_SCALAR = 1, EM_HEAD = 2 };
 //  COPY_U : u                     U_MUL_E: w * u (fused into the reducer)
 //  COPY_E : e
 // `eoff` is the edge-feature column of f0 (f0, 0 or f0 / D by EM).
-template <int VEC, int MSG, int EM>
+template <int VEC, int MSG, int EM, int POL = POL_DEFAULT>
 struct SlotLoad {
   typedef typename Vec<VEC>::T V;
   V u;
@@ -97,7 +131,7 @@ struct SlotLoad {
                                        const float* __restrict__ efeat,
                                        int64_t F, int64_t f0, int64_t elen, int64_t eoff,
                                        int32_t src, int64_t edge) {
-    if (MSG != DGLHIP_MSG_COPY_E) u = ldv<VEC>(ufeat + int64_t(src) * F + f0);
+    if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, F, f0);
     if (MSG != DGLHIP_MSG_COPY_U) {
       if (EM == EM_FULL) e = ldv<VEC>(efeat + edge * F + f0);
       else e = Vec<VEC>::splat(efeat[edge * elen + eoff]);
@@ -107,7 +141,7 @@ struct SlotLoad {
 
 // Sequential reduction of slots [beg, end) of one row for the VEC features at
 // f0: the fma chain the reference's product runs (see the file header).
-template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID>
+template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID, int POL = POL_DEFAULT>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen,
     int64_t eoff, const int32_t* __restrict__ indices,
@@ -115,7 +149,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     const float* __restrict__ efeat) {
   int64_t k = beg;
   for (; k + UNROLL <= end; k += UNROLL) {
-    SlotLoad<VEC, MSG, EM> s[UNROLL];
+    SlotLoad<VEC, MSG, EM, POL> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
       s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
@@ -132,7 +166,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
   // load latencies per row, which dominates rows shorter than UNROLL)
   const int64_t rem = end - k;
   if (rem > 0) {
-    SlotLoad<VEC, MSG, EM> s[UNROLL];
+    SlotLoad<VEC, MSG, EM, POL> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL - 1; ++j)
       if (j < rem)
@@ -188,7 +222,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 // (CHUNKED = true). With ACCUM the chain continues from the value already in
 // out[i, :] (segment-by-segment evaluation of one sequential chain).
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
-          bool ACCUM, bool PIPE = false>
+          bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     int64_t num_items, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
@@ -222,14 +256,14 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, F, f0, indices, ufeat);
     else if (MSG == DGLHIP_MSG_COPY_U || eid != nullptr)  // uniform branch
-      acc = reduce_range<VEC, UNROLL, MSG, EM, true>(acc, beg, end, F, f0, elen, eoff, indices,
-                                                     eid, ufeat, efeat);
+      acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL>(acc, beg, end, F, f0, elen, eoff,
+                                                          indices, eid, ufeat, efeat);
     else
       acc = reduce_range<VEC, UNROLL, MSG, EM, false>(acc, beg, end, F, f0, elen, eoff, indices,
                                                       eid, ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
-    stv<VEC>(out + row * F + f0, acc);
+    store_row<VEC, POL>(out + row * F + f0, acc);
   }
 }
 
@@ -567,11 +601,23 @@ struct SumLaunch {
   const int64_t* chunk_beg;  // non-null: chunked launch (partials to `out`)
   const int64_t* chunk_end;
   bool accumulate;           // continue each item's chain from the value in `out`
+  bool nt_out = false;       // non-temporal output stores (see stream_output)
 };
+
+// Outputs past twice the 256 MiB Infinity Cache are stored non-temporally
+// (POL_NT_OUT): streamed out, they would evict the feature rows that are
+// gathered again (RMAT-26, 34 GB out: 94.1 -> 89.5 ms,
+// tools/cache_policy_study.py). Covers copy_u + sum at VEC 2 x 64 lanes.
+static bool stream_output(int64_t rows, int64_t feat_len) {
+  return rows * feat_len * int64_t(sizeof(float)) > (int64_t(512) << 20);
+}
 
 // Tuning override for the copy_u + sum shape (dglhip_set_spmm_variant);
 // 0 = automatic choice.
 static int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
+// Cache policy for copy_u + sum at VEC 2 x 64 lanes (dglhip_set_cache_policy).
+// -1: automatic (non-temporal output past 512 MiB, default otherwise).
+static int g_cache_policy = -1;
 
 template <int VEC, int GROUP, int MSG, int EM, bool MEAN, int UNROLL_OVERRIDE = 0,
           bool PIPE = false>
@@ -583,8 +629,23 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
   const int64_t blocks = (a.num_items + ITEMS_PER_BLOCK - 1) / ITEMS_PER_BLOCK;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
   if (blocks == 0) return;
+  constexpr bool POL_OK = MSG == DGLHIP_MSG_COPY_U && VEC == 2 && GROUP == 64 && !MEAN &&
+                         !PIPE && UNROLL_OVERRIDE == 0;
+  const int pol = !POL_OK ? POL_DEFAULT
+                  : g_cache_policy >= 0 ? g_cache_policy
+                  : a.nt_out ? POL_NT_OUT : POL_DEFAULT;
   timed_launch(stream, [&] {
-    if (a.chunk_beg && a.accumulate)
+#define DGLHIP_POL_LAUNCH(CH, P)                                                           \
+  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P>), \
+                     dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, a.num_items,   \
+                     a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
+                     a.row_order, a.chunk_beg, a.chunk_end)
+    if (POL_OK && pol != POL_DEFAULT && !a.accumulate) {
+      const bool ch = a.chunk_beg != nullptr;
+      if (pol == POL_NT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT); else DGLHIP_POL_LAUNCH(false, POL_NT); }
+      else if (pol == POL_HOT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_HOT); else DGLHIP_POL_LAUNCH(false, POL_HOT); }
+      else { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT_OUT); else DGLHIP_POL_LAUNCH(false, POL_NT_OUT); }
+    } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
@@ -604,6 +665,7 @@ static void launch_sum(const SumLaunch& a, hipStream_t stream) {
                          dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
+#undef DGLHIP_POL_LAUNCH
   });
 }
 
@@ -762,7 +824,8 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   }
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   SumLaunch a{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, row_order,
-              nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM};
+              nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+              stream_output(num_rows, feat_len)};
   dispatch_sum(msg_op, mean, a, stream);
   API_END();
 }
@@ -802,7 +865,8 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   }
   if (num_light > 0) {
     SumLaunch l{num_light, feat_len, elen, indptr, indices, eid, ufeat, efeat, out,
-                light_rows, nullptr, nullptr, accum};
+                light_rows, nullptr, nullptr, accum,
+                stream_output(num_light + num_heavy, feat_len)};
     dispatch_sum(msg_op, mean, l, stream);
   }
   if (num_heavy > 0) {
@@ -846,7 +910,8 @@ int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   SumLaunch a{num_items, feat_len, use_e ? efeat_len : 1, nullptr, indices, eid, ufeat, efeat,
-              out, nullptr, item_beg, item_end, accumulate != 0};
+              out, nullptr, item_beg, item_end, accumulate != 0,
+              stream_output(num_items, feat_len)};
   dispatch_sum(msg_op, false, a, stream);
   API_END();
 }
@@ -902,6 +967,13 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {
   g_var_group = group;
   g_var_unroll = unroll;
   g_var_pipe = pipelined ? 1 : 0;
+  API_END();
+}
+
+int dglhip_set_cache_policy(int policy) {
+  API_BEGIN();
+  DGLHIP_CHECK(policy >= -1 && policy <= POL_NT_OUT, "unknown cache policy " << policy);
+  g_cache_policy = policy;
   API_END();
 }
 

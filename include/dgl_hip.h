@@ -276,6 +276,14 @@ int dglhip_timing_enable(int enable);
  * restores the automatic choice. Results are identical for every variant
  * (same per-element chain). */
 int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined);
+/* Cache policy of copy_u + sum's source-row gathers and output stores (VEC 2 x
+ * 64-lane shape; results are identical under every policy):
+ *  -1 automatic (the default): non-temporal output stores when the output
+ *     exceeds 512 MiB (twice the Infinity Cache), default policy otherwise;
+ *   0 default policy; 1 all non-temporal; 2 "hot" rows (column id with bit 31
+ *   set by the caller, on a CSR copy no other kernel reads) default and the
+ *   rest non-temporal; 3 non-temporal output stores only. */
+int dglhip_set_cache_policy(int policy);
 /* Synchronises on the recorded events and returns the summed kernel time
  * (ms) and launch count since the last enable/reset. */
 int dglhip_timing_read(double* total_ms, int64_t* launches);
