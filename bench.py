@@ -170,7 +170,8 @@ def describe_partition(pg, world, args):
     backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
     if pg.halo_mode == "alltoall":
         halo = "%s all-to-allv halo (%d referenced remote rows on this rank)%s" % (
-            backend, pg.num_halo, ", own-source segment overlapped with the exchange"
+            backend, pg.num_halo, " in %d chunks, the own-source segment and each landed "
+            "chunk overlapped with the rest of the exchange" % args.pipeline_chunks
             if args.pipeline_chunks > 0 else "")
     else:
         halo = "%s all-gather halo%s" % (
@@ -370,11 +371,13 @@ def main():
                                   pipeline_chunks=args.pipeline_chunks, rank=0, world=W)
             h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
             pg.update_all(h_local)  # allocates the halo buffer
-            pg.halo.uniform_(-1, 1)
+            for buf in (pg.halo if isinstance(pg.halo, list) else [pg.halo]):
+                buf.uniform_(-1, 1)
 
             def step():
                 pg.update_all(h_local)
-            mode = ("pipelined segments (own + all-to-allv halo of %d rows)" % pg.num_halo
+            mode = ("pipelined segments (own + all-to-allv halo of %d rows in %d chunks)"
+                    % (pg.num_halo, args.pipeline_chunks)
                     if pg.halo_mode == "alltoall" else
                     "pipelined segments (own + %d halo chunks)" % args.pipeline_chunks)
         else:

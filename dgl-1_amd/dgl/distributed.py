@@ -30,8 +30,11 @@ unchanged. Row results are bit-identical to the single-GPU product: each
 local row accumulates exactly the same edges in the same edge-id order.
 
 Pipelined forward (``pipeline_chunks = C > 0``, inference / benchmarking).
-With the all-to-allv halo there are two segments: the own sources, reduced
-while the exchange is in flight, then the received rows. With the all-gather:
+With the all-to-allv halo, every peer's request list is cut into C parts and
+the exchange runs as C all-to-allv calls on a side stream: the own sources are
+reduced while chunk 1 is in flight, and the received rows of chunk c as soon
+as it lands, so only the last chunk's rows are reduced after the exchange
+ends (with one exchange, the whole halo segment ran after it). With the all-gather:
 each row's slots are grouped into segments — sources this rank owns first,
 then the remote sources of halo chunk 1..C — so the own segment is reduced
 while the halo is still in flight, and each remote segment as soon as its
@@ -52,6 +55,15 @@ import torch.distributed as dist
 from . import kernel
 
 __all__ = ["balanced_bounds", "PartitionedGraph"]
+
+
+def _chunk_parts(lengths, C):
+    """Split each of P lists (lengths int64[P]) into C consecutive parts of
+    near-equal size: int64[C+1, P] start offsets inside each list. Both ends
+    of an all-to-allv compute the same split from the same length."""
+    lengths = torch.as_tensor(lengths, dtype=torch.int64).cpu()
+    c = torch.arange(C + 1, dtype=torch.int64).unsqueeze(1)
+    return (lengths.unsqueeze(0) * c) // C
 
 
 def balanced_bounds(in_degrees, num_parts):
@@ -211,7 +223,7 @@ class PartitionedGraph(object):
             self.send_idx, self.send_splits = None, None
             self.recv_splits = recv_splits.tolist()
             self.num_halo = int(need.numel())
-            self._build_alltoall_csrs(src, dst, own, need)
+            self._build_alltoall_csrs(src, dst, own, need, need_owner)
             return
         cdev = self._coll_dev()
         # tell every owner how many of its rows this rank needs, then which
@@ -225,21 +237,50 @@ class PartitionedGraph(object):
         self.send_splits = send_splits.tolist()
         self.recv_splits = recv_splits.tolist()
         self.num_halo = int(need.numel())
-        self._build_alltoall_csrs(src, dst, own, need)
+        if self.chunks > 0:
+            # chunk c of the rows sent to peer q: part c of q's request list
+            parts = _chunk_parts(send_splits, self.chunks)
+            starts = torch.cumsum(send_splits, 0) - send_splits
+            idx = []
+            for c in range(self.chunks):
+                sel = [self.send_idx[int(starts[q] + parts[c, q]):int(starts[q] + parts[c + 1, q])]
+                       for q in range(P)]
+                idx.append(torch.cat(sel).contiguous())
+            self.chunk_send_idx = idx
+            self.chunk_send_splits = (parts[1:] - parts[:-1]).tolist()
+        self._build_alltoall_csrs(src, dst, own, need, need_owner)
 
-    def _build_alltoall_csrs(self, src, dst, own, need):
+    def _build_alltoall_csrs(self, src, dst, own, need, need_owner):
         R = self.num_local
         pos = torch.searchsorted(need, src)
         if self.chunks > 0:
             # pipelined forward: own sources (columns of h_local) reduced while the
-            # exchange is in flight, then the received rows (columns of the receive
-            # buffer) continue each row's chain
+            # exchange is in flight, then the rows of halo chunk 1..C (columns of
+            # that chunk's receive buffer) continue each row's chain
+            C, P = self.chunks, self.world
+            lens = torch.as_tensor(self.recv_splits, dtype=torch.int64)
+            parts = _chunk_parts(lens, C)                       # [C+1, P]
+            self.chunk_recv_splits = (parts[1:] - parts[:-1]).tolist()
+            # need entry i: owner p, offset j in p's list -> chunk, slot in chunk buffer
+            first = (torch.cumsum(lens, 0) - lens).to(need.device)
+            j = torch.arange(need.numel(), device=need.device) - first[need_owner]
+            pd = parts.to(need.device)
+            chunk = (j.unsqueeze(0) >= pd[1:-1, need_owner]).sum(0) if C > 1 else \
+                torch.zeros_like(j)
+            sizes = parts[1:] - parts[:-1]                      # [C, P]
+            base = (torch.cumsum(sizes, 1) - sizes).to(need.device)  # chunk buffer offsets
+            slot = base[chunk, need_owner] + (j - pd[chunk, need_owner])
             lrow = dst - self.lo
-            self.seg_csrs = [
-                kernel.build_csr(R, R, lrow[own], (src - self.lo)[own], kernel.ORDER_EID,
-                                 self.device),
-                kernel.build_csr(R, max(self.num_halo, 1), lrow[~own], pos[~own],
-                                 kernel.ORDER_EID, self.device)]
+            rem = ~own
+            seg_of = chunk[pos[rem]]
+            cols = slot[pos[rem]]
+            self.seg_csrs = [kernel.build_csr(R, R, lrow[own], (src - self.lo)[own],
+                                              kernel.ORDER_EID, self.device)]
+            for c in range(C):
+                m = seg_of == c
+                self.seg_csrs.append(kernel.build_csr(
+                    R, max(int(sizes[c].sum()), 1), lrow[rem][m], cols[m], kernel.ORDER_EID,
+                    self.device))
         else:
             # columns: own sources -> [0, R), remote -> R + position in `need`
             cols = torch.where(own, src - self.lo, R + pos)
@@ -338,37 +379,48 @@ class PartitionedGraph(object):
 
     def _pipelined_alltoall_sum(self, h_local):
         dev = self.device
+        C = self.chunks
         h_local = h_local.contiguous()
         F = h_local.shape[1]
         out = torch.empty(self.num_local, F, device=dev)
-        done = None
-        if self._emulated:  # compute-only study: a resident random receive buffer
-            if self.halo is None or self.halo.shape[1] != F:
-                self.halo = torch.rand(self.num_halo, F, device=dev) * 2 - 1
-            recv = self.halo
+        nrecv = [sum(x) for x in self.chunk_recv_splits]
+        if self._emulated:  # compute-only study: resident random receive buffers
+            if self.halo is None or self.halo[0].shape[1] != F:
+                self.halo = [torch.rand(n, F, device=dev) * 2 - 1 for n in nrecv]
+            recvs = self.halo
         else:
-            send = h_local.index_select(0, self.send_idx)
-            recv = h_local.new_empty((sum(self.recv_splits), F))
-        if self._emulated:
-            pass
-        elif self.comm_stream is not None:
+            recvs = [h_local.new_empty((n, F)) for n in nrecv]
+        main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
+        events, sends = [], []
+
+        def exchange(c):
+            send = h_local.index_select(0, self.chunk_send_idx[c])
+            dist.all_to_all_single(recvs[c], send, self.chunk_recv_splits[c],
+                                   self.chunk_send_splits[c], group=self.group)
+            sends.append(send)
+
+        if not self._emulated and self.comm_stream is not None:
             ready = torch.cuda.Event()
             ready.record()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ready)
-                dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits,
-                                       group=self.group)
-                done = torch.cuda.Event()
-                done.record(self.comm_stream)
-        else:
-            dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits,
-                                   group=self.group)
+                for c in range(C):
+                    exchange(c)
+                    ev = torch.cuda.Event()
+                    ev.record(self.comm_stream)
+                    events.append(ev)
         # own sources while the exchange is in flight
         kernel.gspmm_into(self.seg_csrs[0], out, h_local, accumulate=False)
-        if done is not None:
-            torch.cuda.current_stream(dev).wait_event(done)
-            recv.record_stream(torch.cuda.current_stream(dev))
-            send.record_stream(self.comm_stream)
-        if recv.shape[0]:
-            kernel.gspmm_into(self.seg_csrs[1], out, recv, accumulate=True)
+        for c in range(C):
+            if events:
+                main.wait_event(events[c])
+                recvs[c].record_stream(main)
+            elif not self._emulated:
+                exchange(c)
+            if nrecv[c]:
+                kernel.gspmm_into(self.seg_csrs[c + 1], out, recvs[c], accumulate=True)
+        if events:
+            h_local.record_stream(self.comm_stream)
+            for t in sends:
+                t.record_stream(self.comm_stream)
         return out

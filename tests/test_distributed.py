@@ -152,10 +152,22 @@ def _pipe_worker(rank, world, port, graph="chung_lu"):
             out = pg.update_all(H[lo:hi].contiguous()).numpy()
             np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-5)
             if graph == "banded":
-                # exactly the chain over (own source first, then received rows; edge id)
+                # exactly the chain over (own sources first, then the received rows
+                # chunk by chunk; edge id): chunk c holds part c of every owner's
+                # request list, cut at (len * c) // C
                 s, d = src[sel], dst[sel]
                 remote = ((s < lo) | (s >= hi)).numpy()
-                order = np.lexsort((np.arange(len(s)), remote))
+                need = np.unique(s.numpy()[remote])
+                owner = np.searchsorted(bounds.numpy(), need, side="right") - 1
+                chunk_of = {}
+                for p in range(world):
+                    ids = need[owner == p]
+                    for jj, v in enumerate(ids):
+                        chunk_of[int(v)] = sum(jj >= (len(ids) * c) // chunks
+                                               for c in range(1, chunks))
+                seg = np.array([1 + chunk_of[int(v)] if r else 0
+                                for v, r in zip(s.numpy(), remote)])
+                order = np.lexsort((np.arange(len(s)), seg))
                 exact = O.spmm_coo(n, d.numpy()[order], s.numpy()[order], H.numpy())[lo:hi]
                 assert np.array_equal(out, exact)
             # deterministic
