@@ -80,3 +80,24 @@ def test_registry_call_host_csr_and_spmm():
     with pytest.raises(DGLError):  # wrong dtype is rejected, not reinterpreted
         _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, indptr, indices.long(), eid, h, None,
                          out, None, None, None)
+
+
+def test_plain_c_client(tmp_path):
+    """A plain-C program (tests/c_client/capi_demo.c) links libdgl_hip.so and
+    drives the graph index through the registry, the host g-SpMM and the
+    error convention."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    libdir = os.path.dirname(_ffi.lib_path())
+    exe = str(tmp_path / "capi_demo")
+    subprocess.check_call([cc, "-std=c99", "-O1", "-Wall", "-Werror",
+                           "-I", os.path.join(root, "include"),
+                           os.path.join(root, "tests", "c_client", "capi_demo.c"),
+                           "-o", exe, "-L", libdir, "-ldgl_hip", "-Wl,-rpath," + libdir])
+    res = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, (res.returncode, res.stdout, res.stderr)
+    assert "capi_demo ok" in res.stdout
