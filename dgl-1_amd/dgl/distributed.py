@@ -57,6 +57,21 @@ from . import kernel
 __all__ = ["balanced_bounds", "PartitionedGraph"]
 
 
+def _pack(x, halo_dtype):
+    """Feature rows as sent over the wire: fp32 as they are, or rounded to
+    bf16 and carried as a float16 view (the collectives only move these bytes;
+    every backend takes float16, not all take bfloat16)."""
+    if halo_dtype is None:
+        return x
+    return x.to(halo_dtype).view(torch.float16)
+
+
+def _unpack(x, halo_dtype):
+    if halo_dtype is None:
+        return x
+    return x.view(halo_dtype).float()
+
+
 def _chunk_parts(lengths, C):
     """Split each of P lists (lengths int64[P]) into C consecutive parts of
     near-equal size: int64[C+1, P] start offsets inside each list. Both ends
@@ -83,25 +98,27 @@ def balanced_bounds(in_degrees, num_parts):
 
 
 class _AllGatherRows(torch.autograd.Function):
-    """Padded row blocks of every rank -> one (P * max_rows, F) tensor."""
+    """Padded row blocks of every rank -> one (P * max_rows, F) tensor. The
+    gradients go back in fp32 (a reduce-scatter sums them)."""
 
     @staticmethod
-    def forward(ctx, h_local, max_rows, group):
+    def forward(ctx, h_local, max_rows, group, halo_dtype=None):
         ctx.group = group
         ctx.n_local = h_local.shape[0]
         ctx.max_rows = max_rows
         world = dist.get_world_size(group)
         pad = h_local.new_zeros((max_rows,) + tuple(h_local.shape[1:]))
         pad[:h_local.shape[0]] = h_local
-        full = h_local.new_empty((world * max_rows,) + tuple(h_local.shape[1:]))
-        dist.all_gather_into_tensor(full, pad.contiguous(), group=group)
-        return full
+        pad = _pack(pad, halo_dtype).contiguous()
+        full = pad.new_empty((world * max_rows,) + tuple(pad.shape[1:]))
+        dist.all_gather_into_tensor(full, pad, group=group)
+        return _unpack(full, halo_dtype)
 
     @staticmethod
     def backward(ctx, dfull):
         out = dfull.new_empty((ctx.max_rows,) + tuple(dfull.shape[1:]))
         dist.reduce_scatter_tensor(out, dfull.contiguous(), op=dist.ReduceOp.SUM, group=ctx.group)
-        return out[:ctx.n_local], None, None
+        return out[:ctx.n_local], None, None, None
 
 
 class _AllToAllRows(torch.autograd.Function):
@@ -111,32 +128,34 @@ class _AllToAllRows(torch.autograd.Function):
     at a time (indices are unique within a peer, so the adds are ordered)."""
 
     @staticmethod
-    def forward(ctx, h_local, send_idx, send_splits, recv_splits, group):
+    def forward(ctx, h_local, send_idx, send_splits, recv_splits, group, halo_dtype=None):
         ctx.save_for_backward(send_idx)
         ctx.splits = (send_splits, recv_splits)
         ctx.group = group
         ctx.n_local = h_local.shape[0]
+        ctx.halo_dtype = halo_dtype
         tail = tuple(h_local.shape[1:])
-        send = h_local.index_select(0, send_idx)
-        recv = h_local.new_empty((sum(recv_splits),) + tail)
+        send = _pack(h_local.index_select(0, send_idx), halo_dtype).contiguous()
+        recv = send.new_empty((sum(recv_splits),) + tail)
         dist.all_to_all_single(recv, send, recv_splits, send_splits, group=group)
-        return recv
+        return _unpack(recv, halo_dtype)
 
     @staticmethod
     def backward(ctx, drecv):
         send_idx, = ctx.saved_tensors
         send_splits, recv_splits = ctx.splits
         tail = tuple(drecv.shape[1:])
-        dsend = drecv.new_empty((sum(send_splits),) + tail)
-        dist.all_to_all_single(dsend, drecv.contiguous(), send_splits, recv_splits,
-                               group=ctx.group)
+        wire = _pack(drecv, ctx.halo_dtype).contiguous()
+        dsend = wire.new_empty((sum(send_splits),) + tail)
+        dist.all_to_all_single(dsend, wire, send_splits, recv_splits, group=ctx.group)
+        dsend = _unpack(dsend, ctx.halo_dtype)
         dh = drecv.new_zeros((ctx.n_local,) + tail)
         off = 0
         for n in send_splits:
             if n:
                 dh.index_add_(0, send_idx[off:off + n], dsend[off:off + n])
             off += n
-        return dh, None, None, None, None
+        return dh, None, None, None, None, None
 
 
 class PartitionedGraph(object):
@@ -153,10 +172,17 @@ class PartitionedGraph(object):
     halo      : "allgather" (padded row blocks of every rank), "alltoall"
                 (only the referenced remote rows) or "auto" (alltoall when
                 the ranks' halos total less than half of N)
+    halo_dtype: None (fp32 rows, bit-exact results) or torch.bfloat16: remote
+                rows travel rounded to bf16, half the exchange volume
+                (SURVEY.md §8e); the local reduction stays fp32. Opt-in: the
+                rows' results then carry bf16 rounding of the remote inputs.
     """
 
     def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0,
-                 rank=None, world=None, halo="auto"):
+                 rank=None, world=None, halo="auto", halo_dtype=None):
+        if halo_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError("halo_dtype must be None, torch.float32 or torch.bfloat16")
+        self.halo_dtype = None if halo_dtype == torch.float32 else halo_dtype
         self.group = group
         # explicit rank/world: single-process studies of one rank's share (no collectives)
         self.rank = dist.get_rank(group) if rank is None else int(rank)
@@ -315,9 +341,14 @@ class PartitionedGraph(object):
         rows] through one all-to-allv."""
         if self.halo_mode == "alltoall":
             recv = _AllToAllRows.apply(h_local, self.send_idx, self.send_splits,
-                                       self.recv_splits, self.group)
+                                       self.recv_splits, self.group, self.halo_dtype)
             return torch.cat([h_local, recv], 0)
-        return _AllGatherRows.apply(h_local, self.max_rows, self.group)
+        full = _AllGatherRows.apply(h_local, self.max_rows, self.group, self.halo_dtype)
+        if self.halo_dtype is not None:
+            # the own block stays exact: splice the local rows back in
+            lo = self.rank * self.max_rows
+            full = torch.cat([full[:lo], h_local, full[lo + self.num_local:]], 0)
+        return full
 
     def update_all(self, h_local, msg="copy_u", reduce="sum", efeat=None):
         """Local rows of update_all(msg, reduce) given this rank's node features."""
@@ -334,9 +365,13 @@ class PartitionedGraph(object):
         C, P, cr = self.chunks, self.world, self.chunk_rows
         F = h_local.shape[1]
         dev = self.device
+        hd = self.halo_dtype
         if self.halo is None or self.halo.shape[1] != F:
             self.halo = torch.empty(C * P * cr, F, device=dev)
             self.hpads = {}
+            # bf16 rows as they arrive (float16 view), upcast chunk by chunk
+            self.halo_wire = None if hd is None else \
+                torch.empty(C * P * cr, F, dtype=torch.float16, device=dev)
         h_local = h_local.contiguous()
         R = self.num_local
         sends = []
@@ -352,15 +387,22 @@ class PartitionedGraph(object):
                 pad[:hi - lo].copy_(h_local[lo:hi])
             sends.append(pad)
         out = torch.empty(R, F, device=dev)
-        events = []
+        events, wires = [], []
+        land = self.halo if hd is None else self.halo_wire
+
+        def gather(c):
+            wire = _pack(sends[c], hd).contiguous()
+            dist.all_gather_into_tensor(land[c * P * cr:(c + 1) * P * cr], wire,
+                                        group=self.group)
+            wires.append(wire)
+
         if self.comm_stream is not None:
             ready = torch.cuda.Event()
             ready.record()
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ready)
                 for c in range(C):
-                    dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
-                                                sends[c], group=self.group)
+                    gather(c)
                     ev = torch.cuda.Event()
                     ev.record(self.comm_stream)
                     events.append(ev)
@@ -370,11 +412,18 @@ class PartitionedGraph(object):
             if self.comm_stream is not None:
                 torch.cuda.current_stream(dev).wait_event(events[c])
             elif not self._emulated:
-                dist.all_gather_into_tensor(self.halo[c * P * cr:(c + 1) * P * cr],
-                                            sends[c], group=self.group)
+                gather(c)
+            if hd is not None:
+                blk = slice(c * P * cr, (c + 1) * P * cr)
+                self.halo[blk].copy_(_unpack(self.halo_wire[blk], hd))
             kernel.gspmm_into(self.seg_csrs[c + 1], out, self.halo, accumulate=True)
         if self.comm_stream is not None:
             self.halo.record_stream(torch.cuda.current_stream(dev))
+            if hd is not None:
+                self.halo_wire.record_stream(torch.cuda.current_stream(dev))
+            for t in wires:
+                t.record_stream(self.comm_stream)
+            h_local.record_stream(self.comm_stream)
         return out
 
     def _pipelined_alltoall_sum(self, h_local):
@@ -383,18 +432,20 @@ class PartitionedGraph(object):
         h_local = h_local.contiguous()
         F = h_local.shape[1]
         out = torch.empty(self.num_local, F, device=dev)
+        hd = self.halo_dtype
         nrecv = [sum(x) for x in self.chunk_recv_splits]
+        wire_dtype = torch.float32 if hd is None else torch.float16
         if self._emulated:  # compute-only study: resident random receive buffers
             if self.halo is None or self.halo[0].shape[1] != F:
-                self.halo = [torch.rand(n, F, device=dev) * 2 - 1 for n in nrecv]
+                self.halo = [_pack(torch.rand(n, F, device=dev) * 2 - 1, hd) for n in nrecv]
             recvs = self.halo
         else:
-            recvs = [h_local.new_empty((n, F)) for n in nrecv]
+            recvs = [torch.empty((n, F), dtype=wire_dtype, device=dev) for n in nrecv]
         main = torch.cuda.current_stream(dev) if dev.type == "cuda" else None
         events, sends = [], []
 
         def exchange(c):
-            send = h_local.index_select(0, self.chunk_send_idx[c])
+            send = _pack(h_local.index_select(0, self.chunk_send_idx[c]), hd).contiguous()
             dist.all_to_all_single(recvs[c], send, self.chunk_recv_splits[c],
                                    self.chunk_send_splits[c], group=self.group)
             sends.append(send)
@@ -418,7 +469,8 @@ class PartitionedGraph(object):
             elif not self._emulated:
                 exchange(c)
             if nrecv[c]:
-                kernel.gspmm_into(self.seg_csrs[c + 1], out, recvs[c], accumulate=True)
+                kernel.gspmm_into(self.seg_csrs[c + 1], out, _unpack(recvs[c], hd),
+                                  accumulate=True)
         if events:
             h_local.record_stream(self.comm_stream)
             for t in sends:
