@@ -166,6 +166,9 @@ def pmc_traffic():
         shutil.rmtree(out, ignore_errors=True)
 
 
+HALO_DTYPE = {"fp32": None, "bf16": torch.bfloat16}
+
+
 def describe_partition(pg, world, args):
     backend = "RCCL" if args.dist_backend == "nccl" else args.dist_backend
     if pg.halo_mode == "alltoall":
@@ -177,6 +180,8 @@ def describe_partition(pg, world, args):
         halo = "%s all-gather halo%s" % (
             backend, " in %d chunks overlapped with the local g-SpMM" % args.pipeline_chunks
             if args.pipeline_chunks > 0 else "")
+    if pg.halo_dtype is not None:
+        halo += ", remote rows on the wire as bf16 (fp32 reduction)"
     return "%d-way 1-D dst-row partition, %s" % (world, halo)
 
 
@@ -233,7 +238,8 @@ def rmat_leg(args, world, rank, dev):
             lo, hi = int(bounds[rank]), int(bounds[rank + 1])
             sel = (dst >= lo) & (dst < hi)
             pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
-                                  pipeline_chunks=args.pipeline_chunks)
+                                  pipeline_chunks=args.pipeline_chunks,
+                                  halo_dtype=HALO_DTYPE[args.halo_dtype])
             del src, dst, sel
             h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
 
@@ -278,6 +284,9 @@ def main():
     ap.add_argument("--pipeline-chunks", type=int, default=4,
                     help="N>1: halo all-gather chunks overlapped with the local g-SpMM "
                          "(0 = one all-gather, then the kernel; bit-exact rows)")
+    ap.add_argument("--halo-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="N>1: wire type of the exchanged remote rows (bf16 halves the "
+                         "exchange; rows then carry bf16 rounding of remote inputs)")
     ap.add_argument("--no-rmat-leg", action="store_true",
                     help="skip the secondary RMAT strong-scaling block (rmat26)")
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -368,10 +377,16 @@ def main():
         if args.pipeline_chunks > 0:
             from dgl.distributed import PartitionedGraph
             pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
-                                  pipeline_chunks=args.pipeline_chunks, rank=0, world=W)
+                                  pipeline_chunks=args.pipeline_chunks,
+                                  halo_dtype=HALO_DTYPE[args.halo_dtype], rank=0, world=W)
             h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
             pg.update_all(h_local)  # allocates the halo buffer
-            for buf in (pg.halo if isinstance(pg.halo, list) else [pg.halo]):
+            bufs = pg.halo if isinstance(pg.halo, list) else [pg.halo]
+            if getattr(pg, "halo_wire", None) is not None:  # bf16 all-gather landing rows
+                bufs = bufs + [pg.halo_wire.view(torch.bfloat16)]
+            for buf in bufs:
+                if buf.dtype == torch.float16:  # bf16 rows in their wire view
+                    buf = buf.view(torch.bfloat16)
                 buf.uniform_(-1, 1)
 
             def step():
@@ -410,7 +425,8 @@ def main():
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         sel = (dst >= lo) & (dst < hi)
         pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev,
-                              pipeline_chunks=args.pipeline_chunks)
+                              pipeline_chunks=args.pipeline_chunks,
+                              halo_dtype=HALO_DTYPE[args.halo_dtype])
         h_full = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         h_local = h_full[lo:hi].contiguous()
         del h_full, sel

@@ -208,9 +208,16 @@ def test_single_rank_rccl_group_all_modes():
         G = torch.randn(n, 16, generator=gen)
         ref = O.spmm_coo(n, dst.numpy(), src.numpy(), H.numpy())
         gref = O.spmm_coo(n, src.numpy(), dst.numpy(), G.numpy())
-        for halo, chunks in (("auto", 0), ("allgather", 0), ("alltoall", 0),
-                             ("allgather", 2), ("alltoall", 2)):
-            pg = PartitionedGraph(n, src, dst, bounds, dev, halo=halo, pipeline_chunks=chunks)
+        # bf16 halo: at world size 1 every source is an own row, so the results stay
+        # exact; the runs pin the float16-view wire buffers through RCCL
+        for halo, chunks, hd in (("auto", 0, None), ("allgather", 0, None),
+                                 ("alltoall", 0, None), ("allgather", 2, None),
+                                 ("alltoall", 2, None), ("allgather", 0, torch.bfloat16),
+                                 ("alltoall", 0, torch.bfloat16),
+                                 ("allgather", 2, torch.bfloat16),
+                                 ("alltoall", 2, torch.bfloat16)):
+            pg = PartitionedGraph(n, src, dst, bounds, dev, halo=halo, pipeline_chunks=chunks,
+                                  halo_dtype=hd)
             h = H.to(dev).requires_grad_(chunks == 0)  # the pipelined forward is inference-only
             out = pg.update_all(h)
             torch.cuda.synchronize()

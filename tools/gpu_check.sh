@@ -65,6 +65,13 @@ for s in $STEPS; do
       timeout -k 10 600 python tools/kernel_sweep.py > gpurun_out/sweep_reddit.json 2> gpurun_out/sweep.err &&
       timeout -k 10 600 python tools/kernel_sweep.py --workload rmat --rmat-scale 25 > gpurun_out/sweep_rmat.json 2>> gpurun_out/sweep.err
       rc=$?; cat gpurun_out/sweep_reddit.json gpurun_out/sweep_rmat.json; [ $rc -eq 0 ] || exit $rc ;;
+    featsweep)
+      timeout -k 10 600 python tools/feat_sweep.py ${FEATS:+--feats $FEATS} > gpurun_out/feat_sweep.json 2> gpurun_out/feat_sweep.err
+      rc=$?; tail -12 gpurun_out/feat_sweep.err; [ $rc -eq 0 ] || exit $rc ;;
+    disttest)
+      timeout -k 10 300 python -u -m pytest tests/test_distributed.py -m gpu -x -v --timeout 240 \
+        --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_dist.log 2>&1
+      rc=$?; tail -3 gpurun_out/pytest_dist.log; ok $rc || exit $rc ;;
     reducers)
       timeout -k 10 600 python tools/reducer_bench.py > gpurun_out/reducers.json 2> gpurun_out/reducers.err
       rc=$?; cat gpurun_out/reducers.json; tail -3 gpurun_out/reducers.err; [ $rc -eq 0 ] || exit $rc ;;
