@@ -382,8 +382,6 @@ def main():
             h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
             pg.update_all(h_local)  # allocates the halo buffer
             bufs = pg.halo if isinstance(pg.halo, list) else [pg.halo]
-            if getattr(pg, "halo_wire", None) is not None:  # bf16 all-gather landing rows
-                bufs = bufs + [pg.halo_wire.view(torch.bfloat16)]
             for buf in bufs:
                 if buf.dtype == torch.float16:  # bf16 rows in their wire view
                     buf = buf.view(torch.bfloat16)

@@ -161,7 +161,9 @@ int g_cache_policy = -1;
 
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
   const int em = edge_mode(a.elen, a.F);
-  if (msg_op == DGLHIP_MSG_COPY_U) {
+  if (msg_op == DGLHIP_MSG_COPY_U_BF16) {
+    dispatch_sum_me<DGLHIP_MSG_COPY_U_BF16, EM_SCALAR>(mean, a, stream);
+  } else if (msg_op == DGLHIP_MSG_COPY_U) {
     dispatch_sum_me<DGLHIP_MSG_COPY_U, EM_SCALAR>(mean, a, stream);
   } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
     if (em == EM_FULL) dispatch_sum_me<DGLHIP_MSG_U_MUL_E, EM_FULL>(mean, a, stream);
@@ -176,7 +178,9 @@ static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t 
 
 static void dispatch_max(int msg_op, const MaxLaunch& a, hipStream_t stream) {
   const int em = edge_mode(a.elen, a.F);
-  if (msg_op == DGLHIP_MSG_COPY_U) {
+  if (msg_op == DGLHIP_MSG_COPY_U_BF16) {
+    dispatch_max_me<DGLHIP_MSG_COPY_U_BF16, EM_SCALAR>(a, stream);
+  } else if (msg_op == DGLHIP_MSG_COPY_U) {
     dispatch_max_me<DGLHIP_MSG_COPY_U, EM_SCALAR>(a, stream);
   } else if (msg_op == DGLHIP_MSG_U_MUL_E) {
     if (em == EM_FULL) dispatch_max_me<DGLHIP_MSG_U_MUL_E, EM_FULL>(a, stream);
@@ -203,13 +207,13 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
                         const int32_t* row_order, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;  // empty tensors may carry null pointers
   DGLHIP_CHECK(indptr != nullptr && out != nullptr, "null indptr/out");
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
-  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  const bool use_e = !copies_u(msg_op);
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || efeat, "efeat is null");
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
@@ -241,14 +245,14 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
                    reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
                "chunked rows support sum/mean only");
   DGLHIP_CHECK(num_light >= 0 && num_chunks >= 0 && num_heavy >= 0, "negative size");
   if (feat_len == 0) return 0;
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
-  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  const bool use_e = !copies_u(msg_op);
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || efeat, "efeat is null");
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
@@ -298,11 +302,11 @@ int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
                                float* out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   DGLHIP_CHECK(num_items >= 0 && feat_len >= 0, "negative size");
   if (num_items == 0 || feat_len == 0) return 0;
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
-  const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
+  const bool use_e = !copies_u(msg_op);
   DGLHIP_CHECK(item_beg && item_end && out, "null ranges/out");
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
   DGLHIP_CHECK(!use_e || efeat, "efeat is null");

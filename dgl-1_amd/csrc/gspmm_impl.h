@@ -63,6 +63,40 @@ __device__ __forceinline__ void stv(float* p, typename Vec<VEC>::T v) {
   *reinterpret_cast<typename Vec<VEC>::T*>(p) = v;
 }
 
+// DGLHIP_MSG_COPY_U_BF16: copy_u over source rows held as bf16 bits. Each
+// value widens exactly to fp32 (bits << 16) before it enters the fp32 chain,
+// so results equal the fp32 kernel on the widened rows, bit for bit.
+__host__ __device__ constexpr bool copies_u(int msg) {
+  return msg == DGLHIP_MSG_COPY_U || msg == DGLHIP_MSG_COPY_U_BF16;
+}
+
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T gather_bf16(const float* ufeat, int32_t col,
+                                                            int64_t F, int64_t f0);
+template <>
+__device__ __forceinline__ float gather_bf16<1>(const float* ufeat, int32_t col, int64_t F,
+                                                int64_t f0) {
+  const uint16_t b = reinterpret_cast<const uint16_t*>(ufeat)[int64_t(col) * F + f0];
+  return __uint_as_float(uint32_t(b) << 16);
+}
+template <>
+__device__ __forceinline__ f32x2 gather_bf16<2>(const float* ufeat, int32_t col, int64_t F,
+                                                int64_t f0) {
+  // two consecutive bf16 values, element f0 in the low half (little endian)
+  const uint32_t w = *reinterpret_cast<const uint32_t*>(
+      reinterpret_cast<const uint16_t*>(ufeat) + int64_t(col) * F + f0);
+  return f32x2{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+template <>
+__device__ __forceinline__ f32x4 gather_bf16<4>(const float* ufeat, int32_t col, int64_t F,
+                                                int64_t f0) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 w = *reinterpret_cast<const u32x2*>(
+      reinterpret_cast<const uint16_t*>(ufeat) + int64_t(col) * F + f0);
+  return f32x4{__uint_as_float(w.x << 16), __uint_as_float(w.x & 0xffff0000u),
+               __uint_as_float(w.y << 16), __uint_as_float(w.y & 0xffff0000u)};
+}
+
 // Cache policy of the source-row gathers and output stores (POL template
 // parameter; copy_u + sum at VEC 2 x 64 lanes, selected by dglhip_set_cache_policy):
 //  POL_DEFAULT : default policy everywhere.
@@ -117,8 +151,9 @@ struct SlotLoad {
                                        const float* __restrict__ efeat,
                                        int64_t F, int64_t f0, int64_t elen, int64_t eoff,
                                        int32_t src, int64_t edge) {
-    if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, F, f0);
-    if (MSG != DGLHIP_MSG_COPY_U) {
+    if (MSG == DGLHIP_MSG_COPY_U_BF16) u = gather_bf16<VEC>(ufeat, src, F, f0);
+    else if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, F, f0);
+    if (!copies_u(MSG)) {
       if (EM == EM_FULL) e = ldv<VEC>(efeat + edge * F + f0);
       else e = Vec<VEC>::splat(efeat[edge * elen + eoff]);
     }
@@ -139,10 +174,10 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
       s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
-                MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k + j] : k + j));
+                copies_u(MSG) ? 0 : (USE_EID ? eid[k + j] : k + j));
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
-      if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
+      if (copies_u(MSG)) acc += s[j].u;
       else if (MSG == DGLHIP_MSG_COPY_E) acc += s[j].e;
       else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
     }
@@ -157,11 +192,11 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     for (int j = 0; j < UNROLL - 1; ++j)
       if (j < rem)
         s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
-                  MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k + j] : k + j));
+                  copies_u(MSG) ? 0 : (USE_EID ? eid[k + j] : k + j));
 #pragma unroll
     for (int j = 0; j < UNROLL - 1; ++j) {
       if (j < rem) {
-        if (MSG == DGLHIP_MSG_COPY_U) acc += s[j].u;
+        if (copies_u(MSG)) acc += s[j].u;
         else if (MSG == DGLHIP_MSG_COPY_E) acc += s[j].e;
         else acc = Vec<VEC>::fma(s[j].e, s[j].u, acc);
       }
@@ -241,7 +276,7 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, F, f0, indices, ufeat);
-    else if (MSG == DGLHIP_MSG_COPY_U || eid != nullptr)  // uniform branch
+    else if (copies_u(MSG) || eid != nullptr)  // uniform branch
       acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL>(acc, beg, end, F, f0, elen, eoff,
                                                           indices, eid, ufeat, efeat);
     else
@@ -291,12 +326,12 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
                                         float* __restrict__ out, int64_t* __restrict__ arg_out) {
   typedef typename Vec<VEC>::T V;
   auto message = [](const SlotLoad<VEC, MSG, EM>& s) -> V {
-    if (MSG == DGLHIP_MSG_COPY_U) return s.u;
+    if (copies_u(MSG)) return s.u;
     if (MSG == DGLHIP_MSG_COPY_E) return s.e;
     return s.u * s.e;
   };
   auto edge = [&](int64_t k) -> int64_t {
-    return MSG == DGLHIP_MSG_COPY_U ? 0 : (USE_EID ? eid[k] : k);
+    return copies_u(MSG) ? 0 : (USE_EID ? eid[k] : k);
   };
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(group) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
@@ -374,7 +409,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
   int64_t row = row_order ? row_order[it] : it;
   if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
   const int64_t beg = indptr[row], end = indptr[row + 1];
-  if (MSG == DGLHIP_MSG_COPY_U || eid != nullptr)  // uniform branch
+  if (copies_u(MSG) || eid != nullptr)  // uniform branch
     max_row<VEC, UNROLL, MSG, EM, true>(row, gl, GROUP, beg, end, F, elen, indices, eid, ufeat,
                                         efeat, out, arg_out);
   else

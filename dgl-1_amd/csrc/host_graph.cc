@@ -168,6 +168,41 @@ int dglhip_rows_by_degree_host(int64_t num_rows, const int64_t* indptr,
 // CPU device: g-SpMM / g-SDDMM on host memory.
 // ---------------------------------------------------------------------------
 
+}  // extern "C"
+
+// bf16 source rows (DGLHIP_MSG_COPY_U_BF16) on the host: the rows the slots
+// reference are widened to fp32 (exact: bits << 16) and the fp32 kernel runs
+// on them, so host and device agree bit for bit.
+static std::vector<float> widen_bf16(const float* bits, int64_t n) {
+  const uint16_t* b = reinterpret_cast<const uint16_t*>(bits);
+  std::vector<float> w(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) {
+    const uint32_t x = uint32_t(b[i]) << 16;
+    std::memcpy(&w[i], &x, sizeof(float));
+  }
+  return w;
+}
+
+static int64_t max_index_plus_one(const int64_t* beg, const int64_t* end, int64_t n,
+                                  const int32_t* indices) {
+  int64_t m = 0;
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t k = beg[i]; k < end[i]; ++k) m = std::max<int64_t>(m, int64_t(indices[k]) + 1);
+  return m;
+}
+
+static int gspmm_host_bf16(int reduce_op, int64_t num_rows, int64_t feat_len,
+                           const int64_t* indptr, const int32_t* indices, const float* ufeat,
+                           float* out, int64_t* arg_out, int num_threads) {
+  DGLHIP_CHECK(ufeat && indptr && indices, "null indptr/indices/ufeat");
+  const int64_t cols = max_index_plus_one(indptr, indptr + 1, num_rows, indices);
+  std::vector<float> wide = widen_bf16(ufeat, cols * feat_len);
+  return dglhip_gspmm_host(DGLHIP_MSG_COPY_U, reduce_op, num_rows, feat_len, indptr, indices,
+                           nullptr, wide.data(), nullptr, 0, out, arg_out, num_threads);
+}
+
+extern "C" {
+
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,
                       const int32_t* indices, const int64_t* eid,
@@ -175,10 +210,14 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t efeat_len, float* out, int64_t* arg_out,
                       int num_threads) {
   API_BEGIN();
-  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;
+  if (msg_op == DGLHIP_MSG_COPY_U_BF16) {  // widen the rows once, then the fp32 path
+    return gspmm_host_bf16(reduce_op, num_rows, feat_len, indptr, indices, ufeat, out,
+                           arg_out, num_threads);
+  }
   const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
@@ -239,8 +278,16 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
                              const float* ufeat, const float* efeat, int64_t efeat_len,
                              float* out, int num_threads) {
   API_BEGIN();
-  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 2, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   if (num_items == 0 || feat_len == 0) return 0;
+  if (msg_op == DGLHIP_MSG_COPY_U_BF16) {
+    DGLHIP_CHECK(ufeat && indices, "ufeat is null");
+    const int64_t cols = max_index_plus_one(item_beg, item_end, num_items, indices);
+    std::vector<float> wide = widen_bf16(ufeat, cols * feat_len);
+    return dglhip_gspmm_ranges_host(DGLHIP_MSG_COPY_U, num_items, feat_len, item_beg, item_end,
+                                    accumulate, indices, eid, wide.data(), efeat, efeat_len,
+                                    out, num_threads);
+  }
   const bool use_e = msg_op != DGLHIP_MSG_COPY_U;
   DGLHIP_CHECK(!use_e || (efeat && efeat_len >= 1 && feat_len % efeat_len == 0),
                "bad edge feature");

@@ -367,11 +367,11 @@ class PartitionedGraph(object):
         dev = self.device
         hd = self.halo_dtype
         if self.halo is None or self.halo.shape[1] != F:
-            self.halo = torch.empty(C * P * cr, F, device=dev)
+            # the landing rows: fp32, or bf16 bits in a float16 view that the
+            # kernel reads as bf16 (no fp32 copy of the halo)
+            self.halo = torch.empty(C * P * cr, F, device=dev,
+                                    dtype=torch.float32 if hd is None else torch.float16)
             self.hpads = {}
-            # bf16 rows as they arrive (float16 view), upcast chunk by chunk
-            self.halo_wire = None if hd is None else \
-                torch.empty(C * P * cr, F, dtype=torch.float16, device=dev)
         h_local = h_local.contiguous()
         R = self.num_local
         sends = []
@@ -388,7 +388,8 @@ class PartitionedGraph(object):
             sends.append(pad)
         out = torch.empty(R, F, device=dev)
         events, wires = [], []
-        land = self.halo if hd is None else self.halo_wire
+        land = self.halo
+        rows = self.halo if hd is None else self.halo.view(hd)
 
         def gather(c):
             wire = _pack(sends[c], hd).contiguous()
@@ -413,14 +414,9 @@ class PartitionedGraph(object):
                 torch.cuda.current_stream(dev).wait_event(events[c])
             elif not self._emulated:
                 gather(c)
-            if hd is not None:
-                blk = slice(c * P * cr, (c + 1) * P * cr)
-                self.halo[blk].copy_(_unpack(self.halo_wire[blk], hd))
-            kernel.gspmm_into(self.seg_csrs[c + 1], out, self.halo, accumulate=True)
+            kernel.gspmm_into(self.seg_csrs[c + 1], out, rows, accumulate=True)
         if self.comm_stream is not None:
             self.halo.record_stream(torch.cuda.current_stream(dev))
-            if hd is not None:
-                self.halo_wire.record_stream(torch.cuda.current_stream(dev))
             for t in wires:
                 t.record_stream(self.comm_stream)
             h_local.record_stream(self.comm_stream)
@@ -469,7 +465,8 @@ class PartitionedGraph(object):
             elif not self._emulated:
                 exchange(c)
             if nrecv[c]:
-                kernel.gspmm_into(self.seg_csrs[c + 1], out, _unpack(recvs[c], hd),
+                kernel.gspmm_into(self.seg_csrs[c + 1], out,
+                                  recvs[c] if hd is None else recvs[c].view(hd),
                                   accumulate=True)
         if events:
             h_local.record_stream(self.comm_stream)

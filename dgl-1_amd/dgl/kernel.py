@@ -35,6 +35,7 @@ __all__ = ["CSR", "SparseAdj", "build_csr", "gspmm", "gsddmm_dot",
            "MSG_COPY_U", "MSG_U_MUL_E", "MSG_COPY_E", "RED_SUM", "RED_MAX", "RED_MEAN"]
 
 MSG_COPY_U, MSG_U_MUL_E, MSG_COPY_E = 0, 1, 2
+MSG_COPY_U_BF16 = 3  # copy_u over bf16 source rows, widened exactly to fp32 (dgl_hip.h)
 RED_SUM, RED_MAX, RED_MEAN = 0, 1, 2
 RED_SUM_ACCUM = 3  # out += sum, each row's chain continued from out (include/dgl_hip.h)
 ORDER_EID, ORDER_COL = 0, 1
@@ -329,7 +330,7 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
-    eid = csr.slot_eid if msg != MSG_COPY_U else None
+    eid = csr.slot_eid if msg not in (MSG_COPY_U, MSG_COPY_U_BF16) else None
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
     if split:
@@ -505,7 +506,8 @@ def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
 
 def gspmm_into(csr, out, ufeat, accumulate=False):
     """Raw copy_u + sum over ``csr`` into ``out`` (num_rows, F), no autograd:
-    out = A·ufeat, or with ``accumulate`` out += A·ufeat with every row's chain
+    out = A·ufeat (ufeat float32, or bfloat16 rows widened exactly to fp32 in
+    the kernel), or with ``accumulate`` out += A·ufeat with every row's chain
     continued from the value already in ``out`` (one product evaluated segment
     by segment: dgl.distributed's pipelined forward). Degree-descending
     schedule and, under set_row_split, heavy rows cut into chunks whose
@@ -518,8 +520,11 @@ def gspmm_into(csr, out, ufeat, accumulate=False):
         raise DGLError("ufeat has %d rows, the adjacency %d columns"
                        % (ufeat.shape[0], csr.num_cols))
     F = out.shape[1]
-    u2 = _f32c(ufeat.reshape(ufeat.shape[0], F))
-    _run_gspmm(csr, MSG_COPY_U, RED_SUM_ACCUM if accumulate else RED_SUM, u2, None, 0, F,
+    if ufeat.dtype == torch.bfloat16:  # rows read as bf16, summed in fp32 (exact widening)
+        u2, msg = ufeat.reshape(ufeat.shape[0], F).contiguous(), MSG_COPY_U_BF16
+    else:
+        u2, msg = _f32c(ufeat.reshape(ufeat.shape[0], F)), MSG_COPY_U
+    _run_gspmm(csr, msg, RED_SUM_ACCUM if accumulate else RED_SUM, u2, None, 0, F,
                False, out=out)
     return out
 

@@ -116,6 +116,13 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
 #define DGLHIP_MSG_COPY_U  0  /* copy_src(src, out)                 message.py:215-235 */
 #define DGLHIP_MSG_U_MUL_E 1  /* src_mul_edge(src, edge, out)       message.py:190-213 */
 #define DGLHIP_MSG_COPY_E  2  /* copy_edge(edge, out)               message.py:237-257 */
+#define DGLHIP_MSG_COPY_U_BF16 3  /* copy_src over source rows held as bf16: ufeat
+                                   * points to uint16 bf16 bits (cast to const float*);
+                                   * each value widens exactly to fp32 before the fp32
+                                   * chain, so the result equals COPY_U on the widened
+                                   * rows bit for bit. New design: a halved exchange of
+                                   * remote rows (dgl.distributed halo_dtype=bf16) is
+                                   * reduced where it lands, with no fp32 copy. */
 
 #define DGLHIP_REDUCE_SUM  0  /* sum(msg, out)                      reducer.py:52-73   */
 #define DGLHIP_REDUCE_MAX  1  /* max(msg, out)                      reducer.py:75-97   */

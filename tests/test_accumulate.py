@@ -90,3 +90,51 @@ def test_gspmm_into_checks_shapes():
         kernel.gspmm_into(csr, torch.empty(n - 1, 8), torch.from_numpy(H))
     with pytest.raises(Exception):
         kernel.gspmm_into(csr, torch.empty(n, 8), torch.from_numpy(H[:10]))
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("F", [1, 2, 41, 128, 256])
+def test_bf16_rows_equal_widened_fp32(device, F):
+    """DGLHIP_MSG_COPY_U_BF16 (gspmm_into on bfloat16 rows, the bf16 halo's
+    segments): segment 0 reads fp32 rows, the others bf16 rows; the result is
+    the oracle's chain in (segment, edge id) order over the bf16 rows widened
+    to fp32, bit for bit. F = 1 / 41 take the scalar lanes, 2 / 128 / 256 the
+    two-value loads."""
+    dev = _dev(device)
+    n, row, col, seg, H = _case(11 + F, F=F)
+    Hd = torch.from_numpy(H).to(dev)
+    Hb = Hd.to(torch.bfloat16)
+    Hw = Hb.float().cpu().numpy()  # the widened rows the bf16 segments see
+    out = torch.full((n, F), float("nan"), device=dev)
+    for s in range(seg.max() + 1):
+        m = seg == s
+        csr = kernel.build_csr(n, n, row[m], col[m], kernel.ORDER_EID, dev)
+        kernel.gspmm_into(csr, out, Hd if s == 0 else Hb, accumulate=s > 0)
+    order = np.lexsort((np.arange(len(row)), seg))
+    # the chain over rows that are fp32 in segment 0 and widened bf16 after
+    X = np.concatenate([H, Hw], 0)
+    src = np.where(seg[order] == 0, col[order], col[order] + n)
+    ref = O.spmm_coo(n, row[order], src, X)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    # one bf16 product on its own equals the fp32 product on the widened rows
+    csr = kernel.build_csr(n, n, row, col, kernel.ORDER_EID, dev)
+    one = kernel.gspmm_into(csr, torch.empty(n, F, device=dev), Hb)
+    assert np.array_equal(one.cpu().numpy(), O.spmm_coo(n, row, col, Hw))
+
+
+@pytest.mark.gpu
+def test_bf16_rows_heavy_row_chunks():
+    """bf16 rows through the heavy-row split (chunk partials + combine)."""
+    dev = _dev("cuda")
+    n, row, col, seg, H = _case(6, nnz=200000, F=128)
+    Hb = torch.from_numpy(H).to(dev).to(torch.bfloat16)
+    Hw = torch.from_numpy(H).to(dev).to(torch.bfloat16).float()
+    csr = kernel.build_csr(n, n, row, col, kernel.ORDER_EID, dev)
+    old = kernel.set_row_split(256)
+    try:
+        assert csr.max_degree > 4 * 256
+        a = kernel.gspmm_into(csr, torch.empty(n, 128, device=dev), Hb)
+        b = kernel.gspmm_into(csr, torch.empty(n, 128, device=dev), Hw)
+    finally:
+        kernel.set_row_split(old)
+    assert torch.equal(a, b)

@@ -51,10 +51,12 @@ for s in $STEPS; do
     emul)
       wl=${WORKLOAD:-reddit}
       for w in ${EMUL_WORLDS:-2 8}; do for c in ${CHUNKS:-0 4}; do
+        tag=${wl}_${w}_$c${HALO_DTYPE:+_$HALO_DTYPE}
         timeout -k 10 600 python bench.py --workload $wl --emulate-world $w --pipeline-chunks $c \
-          --steps 10 --warmup 3 --no-traffic > gpurun_out/emul_${wl}_${w}_$c.json 2> gpurun_out/emul_${wl}_${w}_$c.err
-        rc=$?; tail -1 gpurun_out/emul_${wl}_${w}_$c.err; [ $rc -eq 0 ] || exit $rc
-        python -c "import json; d=json.load(open('gpurun_out/emul_${wl}_${w}_$c.json')); print('$wl W=$w C=$c', d['ms_per_step'], d['roofline']['kernel_ms'])"
+          --steps 10 --warmup 3 --no-traffic ${HALO_DTYPE:+--halo-dtype $HALO_DTYPE} \
+          > gpurun_out/emul_$tag.json 2> gpurun_out/emul_$tag.err
+        rc=$?; tail -1 gpurun_out/emul_$tag.err; [ $rc -eq 0 ] || exit $rc
+        python -c "import json; d=json.load(open('gpurun_out/emul_$tag.json')); print('$tag', d['ms_per_step'], d['roofline']['kernel_ms'])"
       done; done ;;
     gcnprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gcnprof -o run \
