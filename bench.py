@@ -287,6 +287,8 @@ def main():
     ap.add_argument("--halo-dtype", default="fp32", choices=["fp32", "bf16"],
                     help="N>1: wire type of the exchanged remote rows (bf16 halves the "
                          "exchange; rows then carry bf16 rounding of remote inputs)")
+    ap.add_argument("--no-bf16-leg", action="store_true",
+                    help="N>1: skip the secondary timing of the same step with the bf16 halo")
     ap.add_argument("--no-rmat-leg", action="store_true",
                     help="skip the secondary RMAT strong-scaling block (rmat26)")
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -485,6 +487,18 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if dist.is_initialized() and args.halo_dtype == "fp32" and not args.no_bf16_leg:
+        # the opt-in bf16 halo on the same partition (not the headline: remote
+        # rows are rounded to bf16, so rows are no longer bit-exact)
+        pg.set_halo_dtype(torch.bfloat16)
+        el16, k16 = timed_steps(step, args.steps, args.warmup, world, dev)
+        pg.set_halo_dtype(None)
+        result["halo_bf16"] = {
+            "value": num_edges_total * args.steps / el16, "unit": "edges/s",
+            "ms_per_step": el16 / args.steps * 1e3, "kernel_ms_rank0": k16,
+            "note": "same partition and step with halo_dtype=bf16: remote rows travel and "
+                    "are read as bf16, summed in fp32; own rows exact. Opt-in, not the "
+                    "headline (results carry bf16 rounding of remote inputs)"}
     if rank == 0 and not dist.is_initialized() and not args.no_cpu_baseline:
         t2 = time.time()
         gsrc, gdst = g._graph.src(), g._graph.dst()

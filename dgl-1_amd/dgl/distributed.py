@@ -350,6 +350,16 @@ class PartitionedGraph(object):
             full = torch.cat([full[:lo], h_local, full[lo + self.num_local:]], 0)
         return full
 
+    def set_halo_dtype(self, halo_dtype):
+        """Switch the wire type of remote rows (None / torch.float32 or
+        torch.bfloat16); landing buffers are reallocated on the next call."""
+        if halo_dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError("halo_dtype must be None, torch.float32 or torch.bfloat16")
+        if self._emulated:
+            raise ValueError("an emulated rank keeps the halo_dtype it was built with")
+        self.halo_dtype = None if halo_dtype == torch.float32 else halo_dtype
+        self.halo = None
+
     def update_all(self, h_local, msg="copy_u", reduce="sum", efeat=None):
         """Local rows of update_all(msg, reduce) given this rank's node features."""
         if self.chunks > 0:

@@ -290,3 +290,37 @@ def test_bf16_halo(halo, chunks):
     those inputs bit for bit (pipelined: within 1e-5), the backward and the
     result stay within bf16 accuracy of the fp32 product."""
     mp.spawn(_bf16_worker, args=(2, _free_port(), halo, chunks), nprocs=2, join=True)
+
+
+def _switch_worker(rank, world, port):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
+    from dgl import data
+    from dgl.distributed import PartitionedGraph, balanced_bounds
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        src, dst, n = data.chung_lu(1500, 20 * 1500, 20.0, seed=5)
+        bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        sel = (dst >= lo) & (dst < hi)
+        H = torch.rand(n, 8, generator=torch.Generator().manual_seed(2)) * 2 - 1
+        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu", pipeline_chunks=2)
+        a = pg.update_all(H[lo:hi].contiguous())
+        pg.set_halo_dtype(torch.bfloat16)  # bench.py's secondary leg
+        b = pg.update_all(H[lo:hi].contiguous())
+        pg.set_halo_dtype(None)
+        c = pg.update_all(H[lo:hi].contiguous())
+        assert torch.equal(a, c)
+        assert not torch.equal(a, b)
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-2)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_switch_halo_dtype():
+    """set_halo_dtype: bf16 then back to fp32 on one partition gives the fp32
+    rows again, bit for bit (buffers reallocated for each wire type)."""
+    mp.spawn(_switch_worker, args=(2, _free_port()), nprocs=2, join=True)
