@@ -92,6 +92,7 @@ class CSR(object):
         self._max_degree = None
         self._num_nonempty = None
         self._slot_eid = False  # not computed yet
+        self._eid_loc = None
 
     @property
     def host_indptr(self):
@@ -125,6 +126,20 @@ class CSR(object):
                     break
             self._slot_eid = None if ident else self.eid
         return self._slot_eid
+
+    @property
+    def eid_locality(self):
+        """Fraction of consecutive slots whose edge ids are consecutive (1.0
+        when the slots walk edge-id order); how sequential per-edge stores at
+        out[eid] are along this CSR. Computed once, in bounded chunks."""
+        if self._eid_loc is None:
+            n = self.eid.numel()
+            runs, step = 0, 1 << 26
+            for b in range(0, n - 1, step):
+                e = min(n - 1, b + step)
+                runs += int((self.eid[b + 1:e + 1] == self.eid[b:e] + 1).sum().item())
+            self._eid_loc = 1.0 if n < 2 else runs / float(n - 1)
+        return self._eid_loc
 
     @property
     def num_nonempty(self):
@@ -369,6 +384,24 @@ def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1):
     return out
 
 
+def _eid_major(adj):
+    """(csr, transposed): the CSR of ``adj`` whose slots walk the edge ids most
+    nearly in order, for kernels that store one value per edge at out[eid]
+    (g-SDDMM): the stores are then sequential instead of a scatter. The
+    forward CSR unless the transpose's edge ids run clearly more in order
+    (edges added source-major, as the (src, dst)-sorted loaders add them).
+    Every per-edge value is symmetric in its two endpoint operands (a*b ==
+    b*a, fma(a, b, c) == fma(b, a, c), a + b == b + a, all exact), so both
+    walks give the same bits."""
+    fwd = adj.fwd
+    if fwd.slot_eid is None:
+        return fwd, False
+    bwd = adj.bwd
+    if bwd.eid_locality > max(0.5, 2.0 * fwd.eid_locality):
+        return bwd, True
+    return fwd, False
+
+
 def _f32c(t):
     if t is None:
         return None
@@ -424,8 +457,10 @@ class _GSpMM(torch.autograd.Function):
                     if efeat2.shape[1] == 1:
                         g = g.sum(1, keepdim=True)
                 elif efeat2.shape[1] < F:  # scalar or per-head weights: g-SDDMM dot
-                    de = _run_sddmm_dot(fwd, dout, ufeat2.contiguous(), ctx.num_edges,
-                                        efeat2.shape[1])
+                    csr, tr = _eid_major(adj)
+                    u2 = ufeat2.contiguous()
+                    de = _run_sddmm_dot(csr, u2 if tr else dout, dout if tr else u2,
+                                        ctx.num_edges, efeat2.shape[1])
                     g = None
                 else:
                     g = dout.index_select(0, rows) * ufeat2.index_select(0, fwd.indices.long())
@@ -500,8 +535,10 @@ def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
     (rows of lhs are the adjacency's rows, of rhs its columns; no autograd)."""
     dev = lhs.device
     adj = adj.to(dev)
-    return _run_sddmm_dot(adj.fwd, _f32c(lhs.reshape(lhs.shape[0], -1)),
-                          _f32c(rhs.reshape(rhs.shape[0], -1)), num_edges, heads)
+    lhs2 = _f32c(lhs.reshape(lhs.shape[0], -1))
+    rhs2 = _f32c(rhs.reshape(rhs.shape[0], -1))
+    csr, tr = _eid_major(adj)
+    return _run_sddmm_dot(csr, rhs2 if tr else lhs2, lhs2 if tr else rhs2, num_edges, heads)
 
 
 def gspmm_into(csr, out, ufeat, accumulate=False):
@@ -648,11 +685,14 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
 class _EdgeAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, adj, num_edges, alpha, lo, hi, apply_exp, a_src, a_dst):
-        fwd = adj.fwd
+        # lhs is gathered by column, rhs read per row: over the transpose the
+        # roles swap (a_dst[v] + a_src[u] == a_src[u] + a_dst[v] exactly)
+        csr, tr = _eid_major(adj)
         H = a_src.shape[1]
+        lhs, rhs = (a_dst, a_src) if tr else (a_src, a_dst)
         out = torch.empty(num_edges, H, dtype=torch.float32, device=a_src.device)
-        args = (fwd.num_rows, H, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.eid), ptr(a_src),
-                ptr(a_dst), float(alpha), float(lo), float(hi), 1 if apply_exp else 0, ptr(out))
+        args = (csr.num_rows, H, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid), ptr(lhs),
+                ptr(rhs), float(alpha), float(lo), float(hi), 1 if apply_exp else 0, ptr(out))
         if a_src.is_cuda:
             check_call(LIB.dglhip_gsddmm_attention_device(*(args + (_stream_of(a_src.device),))))
         else:
