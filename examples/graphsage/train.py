@@ -34,13 +34,16 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph, data  # noqa: E402
 from dgl.distributed import PartitionedGraph, balanced_bounds  # noqa: E402
+from dgl.nn.pytorch import NodeLinear  # noqa: E402
 
 
 class SAGELayer(nn.Module):
     def __init__(self, in_feats, out_feats, activation):
         super(SAGELayer, self).__init__()
-        self.fc_self = nn.Linear(in_feats, out_feats)
-        self.fc_neigh = nn.Linear(in_feats, out_feats, bias=False)
+        # NodeLinear: nn.Linear with MFMA-shaped backward reductions over the
+        # node dimension (dgl/nn/pytorch/linear.py)
+        self.fc_self = NodeLinear(in_feats, out_feats)
+        self.fc_neigh = NodeLinear(in_feats, out_feats, bias=False)
         self.activation = activation
 
     def forward(self, h, aggregate):

@@ -85,3 +85,35 @@ def test_relgraphconv(device):
     msg = torch.bmm(x[src].view(-1, 1, 4), W[et].reshape(-1, 4, 3)).view(400, 6)
     ref = torch.zeros(60, 6, device=dev).index_add(0, dst, msg) + x @ conv.loop_weight + conv.bias
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_node_linear_matches_linear():
+    """NodeLinear == nn.Linear: same forward bits, gradients within fp32
+    summation tolerance (split-K weight gradient, GEMV bias gradient), on a
+    row count that exercises several chunks plus a remainder."""
+    import torch.nn as nn
+    from dgl.nn.pytorch import NodeLinear
+    from dgl.nn.pytorch import linear as L
+    old = L._ROWS_PER_CHUNK
+    L._ROWS_PER_CHUNK = 1000
+    try:
+        torch.manual_seed(0)
+        ref = nn.Linear(24, 10)
+        mine = NodeLinear(24, 10)
+        mine.load_state_dict(ref.state_dict())
+        x = torch.randn(5321, 24)
+        g = torch.randn(5321, 10)
+        xa = x.clone().requires_grad_(True)
+        xb = x.clone().requires_grad_(True)
+        ya, yb = ref(xa), mine(xb)
+        assert torch.equal(ya, yb)
+        ya.backward(g)
+        yb.backward(g)
+        torch.testing.assert_close(xb.grad, xa.grad, rtol=1e-5, atol=1e-5)
+        torch.testing.assert_close(mine.weight.grad, ref.weight.grad, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(mine.bias.grad, ref.bias.grad, rtol=1e-4, atol=1e-3)
+        nb = NodeLinear(24, 10, bias=False)
+        nb(x.requires_grad_(True)).sum().backward()
+        assert nb.bias is None
+    finally:
+        L._ROWS_PER_CHUNK = old
