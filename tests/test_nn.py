@@ -89,7 +89,7 @@ def test_relgraphconv(device):
 
 def test_node_linear_matches_linear():
     """NodeLinear == nn.Linear: same forward bits, gradients within fp32
-    summation tolerance (split-K weight gradient, GEMV bias gradient), on a
+    summation tolerance (split-K weight gradient, chunked bias gradient), on a
     row count that exercises several chunks plus a remainder."""
     import torch.nn as nn
     from dgl.nn.pytorch import NodeLinear
