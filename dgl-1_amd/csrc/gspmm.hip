@@ -57,6 +57,16 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   }
 }
 
+// Quad butterflies through DPP (a VALU operand modifier) instead of
+// ds_bpermute: lane i reads lane i ^ 1 / i ^ 2 of its quad, the same pairing
+// as __shfl_xor(v, 1 / 2), so the sums keep their bits.
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+
 // SDDMM dot for rows of NB x 32 floats (F = 32 * NB), one wave per row: the
 // wave takes 8 slots at a time, 8 lanes per slot; lane j of a slot reads the
 // 16 B at 32 i + 4 j of every 32-float column block i (one instruction = 8
@@ -114,8 +124,8 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
           if ((i + 1) % dblk == 0) {
             float r = t;
             r += __shfl_xor(r, 4, 64);
-            r += __shfl_xor(r, 2, 64);
-            r += __shfl_xor(r, 1, 64);
+            r += quad_xor2(r);
+            r += quad_xor1(r);
             if (j == 0 && k < end) out[eid[k] * H + i / dblk] = r;
           }
         }
@@ -123,8 +133,8 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           float t = p[i];
-          if (lph >= 4) t += __shfl_xor(t, 2, 64);
-          if (lph >= 2) t += __shfl_xor(t, 1, 64);
+          if (lph >= 4) t += quad_xor2(t);
+          if (lph >= 2) t += quad_xor1(t);
           const int64_t h = (32 * i + 4 * j) / D;
           if ((j % lph) == 0 && k < end) out[eid[k] * H + h] = t;
         }
