@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from ... import function as fn
 from ... import kernel
 from ...base import DGLError
+from .linear import NodeLinear
 
 __all__ = ["GraphConv", "GATConv", "SAGEConv", "RelGraphConv"]
 
@@ -111,8 +112,10 @@ class SAGEConv(nn.Module):
 
     def __init__(self, in_feats, out_feats, bias=True, activation=None):
         super(SAGEConv, self).__init__()
-        self.fc_self = nn.Linear(in_feats, out_feats, bias=bias)
-        self.fc_neigh = nn.Linear(in_feats, out_feats, bias=False)
+        # NodeLinear: nn.Linear whose backward reductions over the node
+        # dimension are chunked (split-K weight gradient, chunked bias sum)
+        self.fc_self = NodeLinear(in_feats, out_feats, bias=bias)
+        self.fc_neigh = NodeLinear(in_feats, out_feats, bias=False)
         self.activation = activation
 
     def forward(self, g, feat):
