@@ -351,13 +351,17 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   const bool sliced = aligned && head_ok && (nb == 1 || nb == 2 || nb == 4 || nb == 8 ||
                                              nb == 16);
   timed_launch(stream, [&] {
-#define DGLHIP_SDDMM(NB)                                                                   \
-  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, (NB >= 8 ? 1 : 2)>),                    \
-                     dim3(static_cast<unsigned>(blocks)),                                  \
+#define DGLHIP_SDDMM_U(NB, U)                                                              \
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U>), dim3(static_cast<unsigned>(blocks)), \
                      dim3(256), 0, stream, num_rows, num_heads, D, indptr, indices, eid, lhs, \
                      rhs, out)
+#define DGLHIP_SDDMM(NB) DGLHIP_SDDMM_U(NB, (NB >= 8 ? 1 : 2))
+    // F=128 with heads of >= 32 features: 32 slots in flight (8.84 -> 8.51 ms at
+    // one head on the Reddit-shaped graph); narrower heads keep 16 (8 heads:
+    // 11.9 ms at 16, 12.4 ms at 32), reducers_reddit.json
     if (sliced && nb == 1) DGLHIP_SDDMM(1);
     else if (sliced && nb == 2) DGLHIP_SDDMM(2);
+    else if (sliced && nb == 4 && D >= 32) DGLHIP_SDDMM_U(4, 4);
     else if (sliced && nb == 4) DGLHIP_SDDMM(4);
     else if (sliced && nb == 8) DGLHIP_SDDMM(8);
     else if (sliced && nb == 16) DGLHIP_SDDMM(16);
@@ -366,6 +370,7 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                          dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
                          indices, eid, lhs, rhs, out);
 #undef DGLHIP_SDDMM
+#undef DGLHIP_SDDMM_U
   });
   API_END();
 }
