@@ -70,43 +70,52 @@ def algorithmic_bytes(num_edges, num_rows, feat):
 
 def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
     """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on the
-    in-edges of the first rows of the graph (bounded sample). ``h_cpu`` None:
-    the sample's source columns are compacted and get random features (graphs
+    in-edges of the first rows of the graph (bounded sample), timed at one
+    thread and at torch's default thread count (the setting the reference
+    runs with); ``value`` is the faster of the two. ``h_cpu`` None: the
+    sample's source columns are compacted and get random features (graphs
     whose full feature matrix does not fit host memory)."""
     threads = torch.get_num_threads()
-    torch.set_num_threads(1)  # torch's uncoalesced-COO CPU product is single-threaded
+    deg = torch.bincount(dst, minlength=n)
+    cum = torch.cumsum(deg, 0)
+    rows = int(torch.searchsorted(cum, torch.tensor(target_edges, device=cum.device))) + 1
+    rows = min(rows, n)
+    sel = dst < rows
+    s, d = src[sel].cpu(), dst[sel].cpu()
+    e = int(s.numel())
+    ncols = n
+    if h_cpu is None:
+        uniq, s = torch.unique(s, return_inverse=True)
+        ncols = int(uniq.numel())
+        h_cpu = torch.rand(ncols, FEAT) * 2 - 1
+    A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, ncols))
+    runs = {}
     try:
-        deg = torch.bincount(dst, minlength=n)
-        cum = torch.cumsum(deg, 0)
-        rows = int(torch.searchsorted(cum, torch.tensor(target_edges, device=cum.device))) + 1
-        rows = min(rows, n)
-        sel = dst < rows
-        s, d = src[sel].cpu(), dst[sel].cpu()
-        e = int(s.numel())
-        ncols = n
-        if h_cpu is None:
-            uniq, s = torch.unique(s, return_inverse=True)
-            ncols = int(uniq.numel())
-            h_cpu = torch.rand(ncols, FEAT) * 2 - 1
-        A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, ncols))
-        reps, t_total = 0, 0.0
-        while reps < 2 and t_total < seconds_budget:
-            t0 = time.perf_counter()
-            ref = torch.sparse.mm(A, h_cpu)
-            t_total += time.perf_counter() - t0
-            reps += 1
-        eps = e * reps / t_total
-        build = build_cpu_baseline(rows, ncols, d, s, h_cpu, ref)
-        return {"value": eps, "unit": "edges/s", "cores": 1, "kind": "reference",
-                "build_kernel": build,
-                "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
-                          "edge-id order) over the in-edges of the first %d rows: %d edges x "
-                          "F=%d%s, %d call(s), torch %s, 1 thread (host has %d cpus)"
-                          % (rows, e, h_cpu.shape[1],
-                             "" if ncols == n else " (%d source columns compacted)" % ncols,
-                             reps, torch.__version__, os.cpu_count() or 0)}
+        for nt in sorted({1, threads}):
+            torch.set_num_threads(nt)
+            reps, t_total = 0, 0.0
+            while reps < 2 and t_total < seconds_budget / 2:
+                t0 = time.perf_counter()
+                ref = torch.sparse.mm(A, h_cpu)
+                t_total += time.perf_counter() - t0
+                reps += 1
+            runs[nt] = (e * reps / t_total, reps)
     finally:
         torch.set_num_threads(threads)
+    best = max(runs, key=lambda k: runs[k][0])
+    build = build_cpu_baseline(rows, ncols, d, s, h_cpu, ref)
+    return {"value": runs[best][0], "unit": "edges/s", "cores": best, "kind": "reference",
+            "by_threads": {str(k): v[0] for k, v in sorted(runs.items())},
+            "build_kernel": build,
+            "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
+                      "edge-id order) over the in-edges of the first %d rows: %d edges x "
+                      "F=%d%s, %s call(s), torch %s, timed at %s thread(s) (torch default %d; "
+                      "value = the faster, at %d); host has %d cpus"
+                      % (rows, e, h_cpu.shape[1],
+                         "" if ncols == n else " (%d source columns compacted)" % ncols,
+                         "/".join(str(v[1]) for _, v in sorted(runs.items())),
+                         torch.__version__, " and ".join(str(k) for k in sorted(runs)),
+                         threads, best, os.cpu_count() or 0)}
 
 
 def build_cpu_baseline(rows, ncols, d, s, h_cpu, ref):
@@ -130,15 +139,18 @@ def build_cpu_baseline(rows, ncols, d, s, h_cpu, ref):
                                                            if ref.is_sparse else ref))}
 
 
-def pmc_traffic():
-    """HBM bytes per g-SpMM launch from two rocprofv3 --pmc passes (FETCH_SIZE,
+def pmc_traffic(child_args, per_call_calls=None):
+    """HBM bytes of the g-SpMM from two rocprofv3 --pmc passes (FETCH_SIZE,
     WRITE_SIZE) of a short child run of this script, corrected as
-    MI355X_MICROARCH.md §HBM prescribes (tools/pmc_traffic.py). Runs before
-    this process touches the GPU; returns None if the profiler is unavailable."""
+    MI355X_MICROARCH.md §HBM prescribes (tools/pmc_traffic.py): mean per
+    gspmm_sum_kernel launch, or (``per_call_calls``) every g-SpMM kernel of a
+    call (light rows + chunks + combine) summed and divided by the number of
+    calls. Runs before this process touches the GPU; None if the profiler is
+    unavailable."""
     import shutil
     import subprocess
     import tempfile
-    from tools.pmc_traffic import traffic
+    from tools.pmc_traffic import traffic, traffic_per_call
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None
@@ -148,8 +160,7 @@ def pmc_traffic():
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(out, counter)
         cmd = [prof, "--pmc", counter, "-d", d, "-o", "run", "--output-format", "csv", "--",
-               sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1",
-               "--no-cpu-baseline", "--no-traffic", "--no-rmat-leg"]
+               sys.executable, os.path.abspath(__file__)] + child_args
         try:
             subprocess.run(cmd, cwd="/tmp", env=env, timeout=300, check=True,
                            stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
@@ -158,6 +169,8 @@ def pmc_traffic():
             return None
         csvs.append(os.path.join(d, "run_counter_collection.csv"))
     try:
+        if per_call_calls:
+            return traffic_per_call(csvs[0], csvs[1], per_call_calls)
         return traffic(csvs[0], csvs[1])
     except (OSError, ValueError, KeyError) as err:
         log("pmc parse failed: %s" % err)
@@ -211,7 +224,7 @@ def timed_steps(step, steps, warmup, world, dev):
     return elapsed, kms / steps
 
 
-def rmat_leg(args, world, rank, dev):
+def rmat_leg(args, world, rank, dev, pmc=None):
     """RMAT strong scaling on the same ranks: one fixed graph, 1-D dst-row
     partition, heavy rows chunked (kernel.set_row_split("auto"))."""
     from dgl.distributed import PartitionedGraph, balanced_bounds
@@ -250,13 +263,29 @@ def rmat_leg(args, world, rank, dev):
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
         elapsed, kms = timed_steps(step, steps, 2, world, dev)
+        roof = None
+        if not dist.is_initialized():
+            # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
+            b = algorithmic_bytes(E, n, FEAT)
+            ach = b / (kms * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": ach / HBM_PEAK_GBS, "traffic": None if pmc is None else pmc["bytes"],
+                    "kernel": "g-SpMM copy_u+sum, heavy rows chunked (light-row, chunk and "
+                              "combine kernels of one call)",
+                    "kernel_ms": kms, "bytes_per_launch": b,
+                    "traffic_source": None if pmc is None else
+                    "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes (bench.py --workload "
+                    "rmat), every g-SpMM kernel of a call summed, mean per call, read x2 (gfx950)",
+                    "regime": "HBM-bound random row gather (H = %.0f GB >> 256 MB Infinity Cache)"
+                              % (n * FEAT * 4 / 1e9)}
         return {"value": E * steps / elapsed, "unit": "edges/s", "n_gpus": world,
                 "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
                 "scaling": "strong",
                 "config": "rmat-%d (Graph500 0.57/0.19/0.19/0.05, ids permuted, seed 0): "
                           "%d nodes, %d edges, feat=%d, heavy rows chunked"
                           % (args.rmat_scale, n, E, FEAT),
-                "parallelism": par, "kernel_ms_rank0": kms, "cpu_baseline": cpu}
+                "parallelism": par, "kernel_ms_rank0": kms, "roofline": roof,
+                "cpu_baseline": cpu}
     finally:
         kernel.set_row_split(old)
 
@@ -302,9 +331,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     pmc = None
+    rmat_pmc = None
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
-        t0 = time.time()
-        pmc = pmc_traffic()  # before this process initialises the GPU
+        t0 = time.time()  # before this process initialises the GPU
+        pmc = pmc_traffic(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
+                           "--no-rmat-leg"])
+        if not args.no_rmat_leg and args.emulate_world <= 1:
+            # the rmat leg's kernels: every g-SpMM kernel of a call, per call
+            rmat_pmc = pmc_traffic(["--workload", "rmat", "--rmat-scale", str(args.rmat_scale),
+                                    "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
+                                    "--no-traffic"], per_call_calls=3)
         log("pmc traffic passes took %.1fs" % (time.time() - t0))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
@@ -484,6 +520,10 @@ def main():
             "bytes_per_launch": bytes_per_launch,
             "traffic_source": None if pmc is None else
             "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
+            "regime": ("L2/MALL-resident gather: H = %.0f MB fits the 256 MB Infinity Cache, "
+                       "whose hits FETCH_SIZE counts as fetches; the DRAM-bound figure is the "
+                       "rmat%d block's roofline" % (n * FEAT * 4 / 1e6, args.rmat_scale))
+            if n * FEAT * 4 < 256e6 else "HBM-bound gather (H exceeds the Infinity Cache)",
         },
         "cpu_baseline": None,
     }
@@ -514,7 +554,7 @@ def main():
         key = "rmat%d" % args.rmat_scale
         if not dist.is_initialized():
             try:
-                result[key] = rmat_leg(args, world, rank, dev)
+                result[key] = rmat_leg(args, world, rank, dev, rmat_pmc)
             except (RuntimeError, MemoryError, dgl.DGLError) as err:
                 result[key] = {"error": repr(err)}
         else:  # collectives: a failing rank must end the job, not leave peers waiting

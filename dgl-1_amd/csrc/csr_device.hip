@@ -27,24 +27,33 @@ namespace dglhip {
 
 namespace {
 
+// Key of edge e: its row (ORDER_EID) or (row, col) flattened (ORDER_COL);
+// the sort's values are the edge ids. K / V are 32-bit whenever the keys and
+// the edge count fit (the narrow path: half the workspace at 1B edges).
+template <typename K, typename V>
 __global__ void make_keys(int64_t nnz, const int64_t* __restrict__ row,
                           const int64_t* __restrict__ col, int64_t num_cols,
-                          int order, uint64_t* __restrict__ keys,
-                          int64_t* __restrict__ ids) {
+                          int order, K* __restrict__ keys, V* __restrict__ ids) {
   for (int64_t e = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; e < nnz;
        e += int64_t(gridDim.x) * blockDim.x) {
     const uint64_t r = static_cast<uint64_t>(row[e]);
-    keys[e] = order == DGLHIP_ORDER_COL ? r * uint64_t(num_cols) + uint64_t(col[e]) : r;
-    ids[e] = e;
+    keys[e] = static_cast<K>(order == DGLHIP_ORDER_COL
+                                 ? r * uint64_t(num_cols) + uint64_t(col[e]) : r);
+    ids[e] = static_cast<V>(e);
   }
 }
 
+// Slot k: its edge id (widened to int64) and that edge's column.
+template <typename V>
 __global__ void gather_cols(int64_t nnz, const int64_t* __restrict__ col,
-                            const int64_t* __restrict__ eid,
-                            int32_t* __restrict__ indices) {
+                            const V* __restrict__ sorted_ids,
+                            int64_t* __restrict__ eid, int32_t* __restrict__ indices) {
   for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nnz;
-       k += int64_t(gridDim.x) * blockDim.x)
-    indices[k] = static_cast<int32_t>(col[eid[k]]);
+       k += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t e = static_cast<int64_t>(sorted_ids[k]);
+    eid[k] = e;
+    indices[k] = static_cast<int32_t>(col[e]);
+  }
 }
 
 // indptr[r] = first slot whose row >= r. Slot k writes the entries for the
@@ -79,19 +88,55 @@ int key_bits(int64_t num_rows, int64_t num_cols, int order) {
   return bits;
 }
 
+// 32-bit keys and edge ids when both fit
+bool narrow(int64_t nnz, int bits) { return bits <= 32 && nnz < (int64_t(1) << 31); }
+
+template <typename K, typename V>
 size_t sort_temp_bytes(int64_t nnz, int bits) {
   size_t bytes = 0;
-  uint64_t* k = nullptr;
-  int64_t* v = nullptr;
-  HIP_CALL(rocprim::radix_sort_pairs(nullptr, bytes, k, k, v, v, size_t(nnz), 0,
-                                     unsigned(bits)));
+  rocprim::double_buffer<K> k(nullptr, nullptr);
+  rocprim::double_buffer<V> v(nullptr, nullptr);
+  HIP_CALL(rocprim::radix_sort_pairs(nullptr, bytes, k, v, size_t(nnz), 0, unsigned(bits)));
   return bytes;
 }
 
 int64_t align256(int64_t x) { return (x + 255) & ~int64_t(255); }
 
+// Workspace: key and value double buffers (the sort ping-pongs between them,
+// no internal copies) + rocPRIM's small temporary storage. 16 B per edge on
+// the narrow path (17 GB at RMAT-26's 1.07B edges), 32 B otherwise.
+int64_t workspace_bytes(int64_t nnz, int bits) {
+  if (narrow(nnz, bits))
+    return 4 * align256(nnz * 4) + align256(int64_t(sort_temp_bytes<uint32_t, int32_t>(nnz, bits)));
+  return 4 * align256(nnz * 8) + align256(int64_t(sort_temp_bytes<uint64_t, int64_t>(nnz, bits)));
+}
+
 unsigned grid_for(int64_t n) {
   return static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 65536));
+}
+
+template <typename K, typename V>
+void build(int64_t num_rows, int64_t num_cols, int64_t nnz, const int64_t* row,
+           const int64_t* col, int order, int bits, int64_t* indptr, int32_t* indices,
+           int64_t* eid, char* ws, hipStream_t stream) {
+  const int64_t kb = align256(nnz * int64_t(sizeof(K)));
+  const int64_t vb = align256(nnz * int64_t(sizeof(V)));
+  rocprim::double_buffer<K> keys(reinterpret_cast<K*>(ws), reinterpret_cast<K*>(ws + kb));
+  rocprim::double_buffer<V> ids(reinterpret_cast<V*>(ws + 2 * kb),
+                                reinterpret_cast<V*>(ws + 2 * kb + vb));
+  void* tmp = ws + 2 * kb + 2 * vb;
+  size_t temp = sort_temp_bytes<K, V>(nnz, bits);
+  hipLaunchKernelGGL((make_keys<K, V>), dim3(grid_for(nnz)), dim3(256), 0, stream, nnz, row,
+                     col, num_cols, order, keys.current(), ids.current());
+  HIP_CALL(hipGetLastError());
+  HIP_CALL(rocprim::radix_sort_pairs(tmp, temp, keys, ids, size_t(nnz), 0, unsigned(bits),
+                                     stream));
+  hipLaunchKernelGGL((gather_cols<V>), dim3(grid_for(nnz)), dim3(256), 0, stream, nnz, col,
+                     ids.current(), eid, indices);
+  HIP_CALL(hipGetLastError());
+  hipLaunchKernelGGL(fill_indptr, dim3(grid_for(nnz)), dim3(256), 0, stream, nnz, num_rows,
+                     row, eid, indptr);
+  HIP_CALL(hipGetLastError());
 }
 
 }  // namespace
@@ -104,8 +149,7 @@ extern "C" {
 int64_t dglhip_coo_to_csr_workspace_bytes(int64_t num_rows, int64_t num_cols,
                                           int64_t nnz, int order) {
   try {
-    const int bits = key_bits(num_rows, num_cols, order);
-    return 3 * align256(nnz * 8) + align256(int64_t(sort_temp_bytes(nnz, bits)));
+    return workspace_bytes(nnz, key_bits(num_rows, num_cols, order));
   } catch (const std::exception& e) {
     set_last_error(e.what());
     return -1;
@@ -115,7 +159,7 @@ int64_t dglhip_coo_to_csr_workspace_bytes(int64_t num_rows, int64_t num_cols,
 int dglhip_coo_to_csr_device(int64_t num_rows, int64_t num_cols, int64_t nnz,
                              const int64_t* row, const int64_t* col, int order,
                              int64_t* indptr, int32_t* indices, int64_t* eid,
-                             void* workspace, int64_t workspace_bytes,
+                             void* workspace, int64_t workspace_bytes_given,
                              void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
@@ -130,26 +174,16 @@ int dglhip_coo_to_csr_device(int64_t num_rows, int64_t num_cols, int64_t nnz,
     return 0;
   }
   const int bits = key_bits(num_rows, num_cols, order);
-  size_t temp = sort_temp_bytes(nnz, bits);
-  const int64_t need = 3 * align256(nnz * 8) + align256(int64_t(temp));
-  DGLHIP_CHECK(workspace && workspace_bytes >= need,
-               "workspace too small: " << workspace_bytes << " < " << need);
+  const int64_t need = workspace_bytes(nnz, bits);
+  DGLHIP_CHECK(workspace && workspace_bytes_given >= need,
+               "workspace too small: " << workspace_bytes_given << " < " << need);
   char* ws = static_cast<char*>(workspace);
-  uint64_t* keys_in = reinterpret_cast<uint64_t*>(ws);
-  uint64_t* keys_out = reinterpret_cast<uint64_t*>(ws + align256(nnz * 8));
-  int64_t* ids_in = reinterpret_cast<int64_t*>(ws + 2 * align256(nnz * 8));
-  void* tmp = ws + 3 * align256(nnz * 8);
-  hipLaunchKernelGGL(make_keys, dim3(grid_for(nnz)), dim3(256), 0, stream, nnz,
-                     row, col, num_cols, order, keys_in, ids_in);
-  HIP_CALL(hipGetLastError());
-  HIP_CALL(rocprim::radix_sort_pairs(tmp, temp, keys_in, keys_out, ids_in, eid,
-                                     size_t(nnz), 0, unsigned(bits), stream));
-  hipLaunchKernelGGL(gather_cols, dim3(grid_for(nnz)), dim3(256), 0, stream, nnz,
-                     col, eid, indices);
-  HIP_CALL(hipGetLastError());
-  hipLaunchKernelGGL(fill_indptr, dim3(grid_for(nnz)), dim3(256), 0, stream, nnz,
-                     num_rows, row, eid, indptr);
-  HIP_CALL(hipGetLastError());
+  if (narrow(nnz, bits))
+    build<uint32_t, int32_t>(num_rows, num_cols, nnz, row, col, order, bits, indptr, indices,
+                             eid, ws, stream);
+  else
+    build<uint64_t, int64_t>(num_rows, num_cols, nnz, row, col, order, bits, indptr, indices,
+                             eid, ws, stream);
   API_END();
 }
 

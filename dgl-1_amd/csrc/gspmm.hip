@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs,
     float* __restrict__ out) {
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wave = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wave >= num_rows) return;
   const int lane = threadIdx.x & 63;
   const float* a = lhs + wave * F;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out) {
   constexpr int F = NB * 32;
-  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) +
+  const int64_t row = block_linear() * (blockDim.x >> 6) +
                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   if (row >= num_rows) return;
   const int lane = threadIdx.x & 63;
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(256) void gsddmm_attention_kernel(
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs, float alpha, float lo,
     float hi, int apply_exp, float* __restrict__ out) {
-  const int64_t row = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t row = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (row >= num_rows) return;
   const int lane = threadIdx.x & 63;
   const int64_t beg = indptr[row], n = (indptr[row + 1] - beg) * H;
@@ -287,17 +287,17 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
     timed_launch(stream, [&] {
       if (mean)
         hipLaunchKernelGGL((gspmm_combine_kernel<true, false>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           grid_1d(blocks), dim3(256), 0, stream,
                            num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
                            out);
       else if (accum)
         hipLaunchKernelGGL((gspmm_combine_kernel<false, true>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           grid_1d(blocks), dim3(256), 0, stream,
                            num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
                            out);
       else
         hipLaunchKernelGGL((gspmm_combine_kernel<false, false>),
-                           dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                           grid_1d(blocks), dim3(256), 0, stream,
                            num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
                            out);
     });
@@ -352,7 +352,7 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                                              nb == 16);
   timed_launch(stream, [&] {
 #define DGLHIP_SDDMM_U(NB, U)                                                              \
-  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U>), dim3(static_cast<unsigned>(blocks)), \
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U>), grid_1d(blocks), \
                      dim3(256), 0, stream, num_rows, num_heads, D, indptr, indices, eid, lhs, \
                      rhs, out)
 #define DGLHIP_SDDMM(NB) DGLHIP_SDDMM_U(NB, (NB >= 8 ? 1 : 2))
@@ -366,7 +366,7 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
     else if (sliced && nb == 8) DGLHIP_SDDMM(8);
     else if (sliced && nb == 16) DGLHIP_SDDMM(16);
     else
-      hipLaunchKernelGGL(gsddmm_dot_kernel, dim3(static_cast<unsigned>(blocks)),
+      hipLaunchKernelGGL(gsddmm_dot_kernel, grid_1d(blocks),
                          dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
                          indices, eid, lhs, rhs, out);
 #undef DGLHIP_SDDMM
@@ -407,7 +407,7 @@ int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
   DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
   DGLHIP_CHECK((num_rows + 3) / 4 <= 0x7fffffff, "grid too large");
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL(gsddmm_attention_kernel, dim3(static_cast<unsigned>((num_rows + 3) / 4)),
+    hipLaunchKernelGGL(gsddmm_attention_kernel, grid_1d((num_rows + 3) / 4),
                        dim3(256), 0, stream, num_rows, num_heads, indptr, indices, eid, lhs,
                        rhs, alpha, clamp_lo, clamp_hi, apply_exp, out);
   });

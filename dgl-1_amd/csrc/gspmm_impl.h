@@ -16,6 +16,7 @@
 
 #include "../../include/dgl_hip.h"
 #include "common.h"
+#include "launch.h"
 
 namespace dglhip {
 
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   const int lane = threadIdx.x & 63;
   // wave index is uniform; make that explicit so slot data goes through SGPRs
   const int64_t wave =
-      int64_t(blockIdx.x) * (blockDim.x >> 6) +
+      block_linear() * (blockDim.x >> 6) +
       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
   if (it >= num_items) return;
@@ -296,7 +297,7 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
     int64_t num_heavy, int64_t F, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ heavy_rows, const int64_t* __restrict__ heavy_chunk_ptr,
     const float* __restrict__ partial, float* __restrict__ out) {
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wave = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wave >= num_heavy) return;
   const int lane = threadIdx.x & 63;
   const int64_t row = heavy_rows[wave];
@@ -401,7 +402,7 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
   constexpr int ITEMS_PER_WAVE = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   const int64_t wave =
-      int64_t(blockIdx.x) * (blockDim.x >> 6) +
+      block_linear() * (blockDim.x >> 6) +
       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t it = wave * ITEMS_PER_WAVE + (GROUP == 64 ? 0 : lane / GROUP);
   if (it >= num_rows) return;
@@ -544,7 +545,7 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
   timed_launch(stream, [&] {
 #define DGLHIP_POL_LAUNCH(CH, P)                                                           \
   hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P>), \
-                     dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream, a.num_items,   \
+                     grid_1d(blocks), dim3(256), 0, stream, a.num_items,   \
                      a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
                      a.row_order, a.chunk_beg, a.chunk_end)
     if (POL_OK && pol != POL_DEFAULT && !a.accumulate) {
@@ -554,22 +555,22 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
       else { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT_OUT); else DGLHIP_POL_LAUNCH(false, POL_NT_OUT); }
     } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
-                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else if (!a.chunk_beg && a.accumulate && !MEAN)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, false, true>),
-                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else if (a.chunk_beg)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false>),
-                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, false, PIPE>),
-                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,
+                         grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
 #undef DGLHIP_POL_LAUNCH
@@ -652,7 +653,7 @@ static inline void dispatch_max_shape(const MaxLaunch& a, hipStream_t stream) {
     DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);                \
     timed_launch(stream, [&] {                                                       \
       hipLaunchKernelGGL((gspmm_max_kernel<V, G, 8, MSG, EM>),                       \
-                         dim3(static_cast<unsigned>(blocks)), dim3(256), 0, stream,  \
+                         grid_1d(blocks), dim3(256), 0, stream,  \
                          a.num_rows, a.F, a.elen, a.indptr, a.indices, a.eid,        \
                          a.ufeat, a.efeat, a.out, a.arg_out, a.row_order);           \
     });                                                                              \

@@ -21,6 +21,7 @@
 
 #include "../../include/dgl_hip.h"
 #include "common.h"
+#include "launch.h"
 
 namespace dglhip {
 
@@ -50,7 +51,7 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
     const float* __restrict__ ufeat, const float* __restrict__ weight,
     const float* __restrict__ enorm, float* __restrict__ out) {
   const int64_t si = SI > 0 ? SI : si_rt;
-  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) +
+  const int64_t wave = block_linear() * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t row = wave / npass, pass = wave - (wave / npass) * npass;
   if (row >= num_rows) return;
@@ -124,7 +125,7 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
     const int64_t* __restrict__ edge_dst, const float* __restrict__ ufeat,
     const float* __restrict__ dout, const float* __restrict__ enorm, float* __restrict__ dw) {
   const int64_t wr = nb * si * so;
-  const int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
   if (idx >= num_rels * wr) return;
   const int64_t r = idx / wr, rem = idx - r * wr;
   const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
@@ -163,7 +164,7 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t
   const int64_t npass = (Fo + 63) / 64;
   const int64_t waves = num_rows * npass;
   DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
-  const dim3 grid(static_cast<unsigned>((waves + 3) / 4)), block(256);
+  const dim3 grid = grid_1d((waves + 3) / 4), block(256);
 #define DGLHIP_TB(S)                                                                   \
   hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_rows, npass, \
                      num_blocks, in_block, out_block, indptr, indices, eid, etype, ufeat, \
@@ -197,7 +198,7 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks, int64_
   DGLHIP_CHECK(rel_ptr && rel_src && rel_eid && edge_dst && ufeat && dout && dweight,
                "null pointer argument");
   DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
-  hipLaunchKernelGGL(typed_block_wgrad_kernel, dim3(static_cast<unsigned>((total + 255) / 256)),
+  hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256),
                      dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
                      rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);
   HIP_CALL(hipGetLastError());

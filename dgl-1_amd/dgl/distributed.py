@@ -124,8 +124,9 @@ class _AllGatherRows(torch.autograd.Function):
 class _AllToAllRows(torch.autograd.Function):
     """Sparse halo: rows h_local[send_idx] go to their requesting ranks
     (send_splits), the rows this rank requested come back in owner order
-    (recv_splits). Backward: reverse all-to-allv, then sum-on-receive one peer
-    at a time (indices are unique within a peer, so the adds are ordered)."""
+    (recv_splits). Backward: reverse all-to-allv of the fp32 gradients, then
+    sum-on-receive one peer at a time (indices are unique within a peer, so
+    the adds are ordered)."""
 
     @staticmethod
     def forward(ctx, h_local, send_idx, send_splits, recv_splits, group, halo_dtype=None):
@@ -145,10 +146,11 @@ class _AllToAllRows(torch.autograd.Function):
         send_idx, = ctx.saved_tensors
         send_splits, recv_splits = ctx.splits
         tail = tuple(drecv.shape[1:])
-        wire = _pack(drecv, ctx.halo_dtype).contiguous()
+        # gradients travel in fp32 whatever the forward's wire type, as in the
+        # all-gather mode's reduce-scatter (halo_dtype rounds features only)
+        wire = drecv.float().contiguous()
         dsend = wire.new_empty((sum(send_splits),) + tail)
         dist.all_to_all_single(dsend, wire, send_splits, recv_splits, group=ctx.group)
-        dsend = _unpack(dsend, ctx.halo_dtype)
         dh = drecv.new_zeros((ctx.n_local,) + tail)
         off = 0
         for n in send_splits:
@@ -170,12 +172,16 @@ class PartitionedGraph(object):
     device    : where the shard lives
     group     : torch.distributed process group (default world)
     halo      : "allgather" (padded row blocks of every rank), "alltoall"
-                (only the referenced remote rows) or "auto" (alltoall when
-                the ranks' halos total less than half of N)
+                (only the referenced remote rows) or "auto": alltoall when it
+                at least halves what a rank receives, i.e. when
+                2 * (largest rank halo) <= (P - 1) * max_rows (the rows of the
+                all-gather's P - 1 remote padded blocks), decided by one
+                all-reduce MAX so every rank picks the same collective
     halo_dtype: None (fp32 rows, bit-exact results) or torch.bfloat16: remote
                 rows travel rounded to bf16, half the exchange volume
                 (SURVEY.md §8e); the local reduction stays fp32. Opt-in: the
                 rows' results then carry bf16 rounding of the remote inputs.
+                Gradients travel in fp32 in every halo mode.
     """
 
     def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0,
@@ -381,6 +387,8 @@ class PartitionedGraph(object):
             # kernel reads as bf16 (no fp32 copy of the halo)
             self.halo = torch.empty(C * P * cr, F, device=dev,
                                     dtype=torch.float32 if hd is None else torch.float16)
+            if self._emulated:  # compute-only study: no gather ever lands, use finite rows
+                (self.halo if hd is None else self.halo.view(hd)).uniform_(-1, 1)
             self.hpads = {}
         h_local = h_local.contiguous()
         R = self.num_local

@@ -298,15 +298,36 @@ class SparseAdj(object):
         return self._dev[key]
 
 
+def coo_of(csr):
+    """(row, col) int64 in edge-id order, recovered from a CSR built by
+    build_csr (slot k holds edge eid[k] of row r): the inverse of the build."""
+    ip = csr.indptr
+    row = torch.repeat_interleave(torch.arange(csr.num_rows, device=ip.device),
+                                  ip[1:] - ip[:-1], output_size=csr.nnz)
+    r = torch.empty_like(row)
+    r[csr.eid] = row
+    del row
+    c = torch.empty(csr.nnz, dtype=torch.int64, device=ip.device)
+    c[csr.eid] = csr.indices.long()
+    return r, c
+
+
 def from_coo(num_rows, num_cols, row, col, order=ORDER_EID, device=None):
     """SparseAdj whose forward CSR groups (row, col) by row and whose backward
-    CSR groups the same edges by col, both in ``order``."""
+    CSR groups the same edges by col, both in ``order``.
+
+    The edge list is held only until the transposed CSR is first built (an
+    int64 pair per edge: 17 GB at a billion edges); later builds (another
+    device) recover it from the forward CSR."""
     row = torch.as_tensor(row, dtype=torch.int64)
     col = torch.as_tensor(col, dtype=torch.int64)
     fwd = build_csr(num_rows, num_cols, row, col, order, device)
+    coo = [row, col]
 
     def tb(dev):
-        return build_csr(num_cols, num_rows, col, row, order, dev)
+        r, c = coo if coo[0] is not None else coo_of(fwd)
+        coo[0] = coo[1] = None
+        return build_csr(num_cols, num_rows, c, r, order, dev)
 
     return SparseAdj(fwd, tb, (num_rows, num_cols))
 
@@ -425,7 +446,17 @@ class _GSpMM(torch.autograd.Function):
             (efeat2 is not None and efeat2.requires_grad))
         out, arg = _run_gspmm(adj.fwd, msg, red, ufeat2, efeat2, elen, feat_len, need_arg)
         ctx.adj, ctx.msg, ctx.red, ctx.num_edges = adj, msg, red, num_edges
-        ctx.save_for_backward(ufeat2, efeat2, arg)
+        # keep an operand alive only when the backward reads its values: the
+        # node rows for u_mul_e's edge gradient, the edge values for its node
+        # gradient. copy_u/copy_e + sum/mean save nothing (in a partitioned
+        # layer ufeat2 is the whole gathered halo, GBs per layer)
+        u_mul_e = msg == MSG_U_MUL_E
+        need_u = ufeat2 is not None and ufeat2.requires_grad
+        need_e = efeat2 is not None and efeat2.requires_grad
+        ctx.ushape = None if ufeat2 is None else tuple(ufeat2.shape)
+        ctx.eshape = None if efeat2 is None else tuple(efeat2.shape)
+        ctx.save_for_backward(ufeat2 if (u_mul_e and need_e) else None,
+                              efeat2 if (u_mul_e and need_u) else None, arg)
         return out
 
     @staticmethod
@@ -454,18 +485,18 @@ class _GSpMM(torch.autograd.Function):
                 rows = fwd.row_ids()
                 if msg == MSG_COPY_E:
                     g = dout.index_select(0, rows)
-                    if efeat2.shape[1] == 1:
+                    if ctx.eshape[1] == 1:
                         g = g.sum(1, keepdim=True)
-                elif efeat2.shape[1] < F:  # scalar or per-head weights: g-SDDMM dot
+                elif ctx.eshape[1] < F:  # scalar or per-head weights: g-SDDMM dot
                     csr, tr = _eid_major(adj)
                     u2 = ufeat2.contiguous()
                     de = _run_sddmm_dot(csr, u2 if tr else dout, dout if tr else u2,
-                                        ctx.num_edges, efeat2.shape[1])
+                                        ctx.num_edges, ctx.eshape[1])
                     g = None
                 else:
                     g = dout.index_select(0, rows) * ufeat2.index_select(0, fwd.indices.long())
                 if g is not None:
-                    de = torch.zeros_like(efeat2)
+                    de = dout.new_zeros(ctx.eshape)
                     de.index_copy_(0, fwd.eid, g)
         else:  # MAX: route each output element's gradient to its argmax slot
             valid = arg >= 0
@@ -474,21 +505,21 @@ class _GSpMM(torch.autograd.Function):
             sl = slots[rowsel]
             g = dout[rowsel]
             fidx = rowsel[1]
-            dpe = F // efeat2.shape[1] if efeat2 is not None else 1
+            dpe = F // ctx.eshape[1] if ctx.eshape is not None else 1
             if need_u:
                 src = fwd.indices.long()[sl]
                 gu = g
                 if msg == MSG_U_MUL_E:
                     e = fwd.eid[sl]
                     gu = g * efeat2[e, fidx // dpe]
-                du = torch.zeros_like(ufeat2)
+                du = dout.new_zeros(ctx.ushape)
                 du.index_put_((src, fidx), gu, accumulate=True)
             if need_e:
                 e = fwd.eid[sl]
                 ge = g
                 if msg == MSG_U_MUL_E:
                     ge = g * ufeat2[fwd.indices.long()[sl], fidx]
-                de = torch.zeros_like(efeat2)
+                de = dout.new_zeros(ctx.eshape)
                 de.index_put_((e, fidx // dpe), ge, accumulate=True)
         return None, None, None, None, None, du, de
 

@@ -32,7 +32,7 @@ import torch.nn.functional as F
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..",
                                 "dgl-1_amd"))
 import dgl.function as fn  # noqa: E402
-from dgl import DGLGraph, data  # noqa: E402
+from dgl import DGLGraph, data, kernel  # noqa: E402
 from dgl.distributed import PartitionedGraph, balanced_bounds  # noqa: E402
 from dgl.nn.pytorch import NodeLinear  # noqa: E402
 
@@ -124,6 +124,8 @@ def run(args):
             g.update_all(fn.copy_src("h", "m"), fn.mean("m", "neigh"))
             return g.ndata.pop("neigh")
     del src, dst
+    if args.row_split is not None:
+        kernel.set_row_split(args.row_split)
 
     torch.manual_seed(args.seed)
     model = SAGE(feats.shape[1], args.n_hidden, ncls, args.n_layers, args.dropout).to(device)
@@ -158,7 +160,7 @@ def run(args):
     state = {k: v.detach().cpu() for k, v in
              (model.module if distributed else model).state_dict().items()}
     return {"graph": args.graph if args.graph == "rmat" else args.dataset, "world": world,
-            "epoch_s": mean, "edges": num_edges,
+            "epoch_s": mean, "edges": num_edges, "row_split": kernel._ROW_SPLIT,
             "edges_per_s": num_edges * (args.n_layers + 1) / mean, "loss": losses[-1],
             "state": state}
 
@@ -179,6 +181,9 @@ def parser():
     p.add_argument("--lr", type=float, default=1e-2)
     p.add_argument("--n-epochs", type=int, default=10)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--row-split", default=None,
+                   help="heavy-row policy of the g-SpMM (off / auto / a chunk length; "
+                        "default: the library's, dgl.kernel.set_row_split)")
     return p
 
 

@@ -77,6 +77,28 @@ def random_graph(rng, n, m, self_loops=False, allow_dup=False):
     return src.astype(np.int64), dst.astype(np.int64)
 
 
+def reddit_rows_case():
+    import portable as P
+    src, dst, H, W, G = P.reddit_rows()
+    n = P.N
+    r_copy = coo_spmm(n, n, dst, src, H, None, G)
+    r_mul = coo_spmm(n, n, dst, src, H, W, G)
+    deg = np.bincount(dst, minlength=n)
+    rng = np.random.default_rng(5)
+    top = np.argsort(-deg, kind="stable")[:16]
+    rows = np.unique(np.concatenate([top, rng.choice(n, 112, replace=False),
+                                     np.nonzero(deg == 0)[0][:2]])).astype(np.int64)
+    case = dict(n=n, e=len(src), f=H.shape[1], rows=rows, max_in_degree=int(deg.max()),
+                torch_version=np.array(torch.__version__))
+    for k, a in (("src", src), ("dst", dst), ("h", H), ("w", W), ("g", G)):
+        case["sha_" + k] = np.array(P.digest(a))
+    for k, a in (("copy_out", r_copy["out"]), ("copy_grad_h", r_copy["grad_h"]),
+                 ("mul_out", r_mul["out"]), ("mul_grad_h", r_mul["grad_h"])):
+        case["sha_" + k] = np.array(P.digest(a))
+        case[k + "_rows"] = a[rows]
+    return case
+
+
 def main():
     rng = np.random.default_rng(20181205)
     cases = {}
@@ -141,6 +163,12 @@ def main():
     h = rng.standard_normal((n, 5, 5)).astype(np.float32)
     r = coo_spmm(n, n, dst, src, h.reshape(n, 25))
     cases["feat3d"] = dict(src=src, dst=dst, n=n, h=h, copy_out=r["out"].reshape(n, 5, 5))
+
+    # 7. Reddit row lengths (tests/golden/portable.py): 1.5M edges, F = 128,
+    #    rows of 13k-54k in-edges, heavy duplicates. The inputs are regenerated
+    #    from a portable integer hash; the fixture keeps their digests, the
+    #    digests of the whole outputs and the outputs of a row sample.
+    cases["reddit_rows"] = reddit_rows_case()
 
     for name, arrays in cases.items():
         np.savez_compressed(os.path.join(OUT, name + ".npz"),

@@ -74,6 +74,22 @@ def test_rgcn_fused_matches_udf(device):
 
 
 @pytest.mark.gpu
+def test_rgcn_fused_matches_udf_fb15k_shape():
+    """configs[4] at the example's defaults (FB15k-237 shape: 14,541 entities,
+    237 relations -> 474 typed, 30,000-edge samples, hidden 500, 100 bases of
+    5 x 5; rgcn/link_predict.py:168-184 vs the reference's
+    examples/pytorch/rgcn/link_predict.py defaults): fused and UDF training
+    reach the same loss."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    base = ["--n-epochs", "3", "--gpu", "0", "--dropout", "0"]
+    fused = rgcn.run(rgcn.parser().parse_args(base))
+    udf = rgcn.run(rgcn.parser().parse_args(base + ["--udf"]))
+    assert fused["graph_edges"] == 30000
+    assert abs(fused["loss"] - udf["loss"]) < 1e-4 * max(1.0, abs(udf["loss"]))
+
+
+@pytest.mark.gpu
 def test_gcn_hip_graph_replay_matches_eager():
     """The captured (HIP graph) training step computes the same losses as eager."""
     if not torch.cuda.is_available():

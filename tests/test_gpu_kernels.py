@@ -130,7 +130,9 @@ def test_empty_and_degenerate(cuda):
 @pytest.mark.parametrize("order", [kernel.ORDER_EID, kernel.ORDER_COL])
 def test_device_csr_builder_matches_host(cuda, order):
     rng = np.random.default_rng(5)
-    for n_rows, n_cols, nnz in ((1, 1, 0), (10, 7, 100), (5000, 3000, 200000)):
+    # the last shape's (row, col) keys need more than 32 bits: the 64-bit sort
+    for n_rows, n_cols, nnz in ((1, 1, 0), (10, 7, 100), (5000, 3000, 200000),
+                                (70000, 70000, 300000)):
         row, col = rand_graph(rng, n_rows, n_cols, nnz)
         h = kernel.build_csr(n_rows, n_cols, row, col, order, "cpu")
         d = kernel.build_csr(n_rows, n_cols, row, col, order, cuda)
@@ -249,7 +251,8 @@ def test_full_reddit_bench_graph_bit_exact(cuda):
     assert np.array_equal(out, ref)
 
 
-@pytest.mark.parametrize("F,H", [(32, 1), (64, 8), (128, 1), (128, 8), (128, 32), (64, 2),
+@pytest.mark.parametrize("F,H", [(32, 1), (64, 8), (128, 1), (128, 2), (128, 4), (128, 8),
+                                 (128, 32), (64, 2),
                                  (256, 2), (512, 4), (5, 1), (48, 3), (96, 3), (256, 64)])
 def test_gsddmm_dot_heads(cuda, F, H):
     """Per-head dot products out[eid, h] = <lhs[row, h], rhs[col, h]>: the
@@ -271,3 +274,25 @@ def test_gsddmm_dot_heads(cuda, F, H):
     ref = (A[row].astype(np.float64).reshape(-1, H, D) *
            B[col].astype(np.float64).reshape(-1, H, D)).sum(-1)
     np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-4)
+
+
+def test_rows_beyond_one_grid_dimension(cuda):
+    """2^26 + 5 rows of one in-edge each at F = 16 (one wave per row): the
+    launch folds into a 2-D grid (a 1-D grid of 2^26 waves is 2^32 lanes, past
+    the per-dimension limit; RMAT-26 without heavy-row chunking hit it). Every
+    row's result is checked: sum, mean, max (one slot each = the source row)
+    and the per-edge g-SDDMM dot."""
+    n = (1 << 26) + 5
+    g = torch.Generator(device=cuda).manual_seed(3)
+    col = torch.randperm(n, generator=g, device=cuda)
+    row = torch.arange(n, device=cuda)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    H = torch.rand(n, 16, generator=g, device=cuda)
+    expect = H.index_select(0, col)
+    for red in ("sum", "mean", "max"):
+        out = kernel.gspmm(adj, "copy_u", red, H)
+        assert torch.equal(out, expect), red
+        del out
+    dots = kernel.gsddmm_dot(adj, H, H, n, 1)
+    ref = (H * expect).sum(1, keepdim=True)
+    torch.testing.assert_close(dots, ref, rtol=1e-5, atol=1e-5)

@@ -75,3 +75,38 @@ def test_feat3d(golden):
     n = int(c["n"])
     out = O.spmm_coo(n, c["dst"], c["src"], c["h"].reshape(n, 25)).reshape(n, 5, 5)
     assert np.array_equal(out, c["copy_out"])
+
+
+def _reddit_rows_inputs(golden):
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import portable as P
+    c = golden("reddit_rows")
+    src, dst, H, W, G = P.reddit_rows()
+    for k, a in (("src", src), ("dst", dst), ("h", H), ("w", W), ("g", G)):
+        assert P.digest(a) == str(c["sha_" + k]), "portable generator drifted: " + k
+    return c, P, src, dst, H, W, G
+
+
+def test_reddit_rows_fixture(golden):
+    """Reddit row lengths (rows of 13k-54k in-edges, thousands of parallel
+    duplicates, 1.5M edges, F = 128): the oracle's chain equals
+    torch.sparse.mm on the reference's uncoalesced COO bit for bit, for
+    copy_u and u_mul_e, forward and dH, over the whole output (digest) and a
+    row sample (stored rows). The OpenMP CSR form (the multi-core CPU
+    baseline) gives the same bits."""
+    c, P, src, dst, H, W, G = _reddit_rows_inputs(golden)
+    n = int(c["n"])
+    assert int(c["max_in_degree"]) >= 20000
+    rows = c["rows"]
+    outs = {"copy_out": O.spmm_coo(n, dst, src, H),
+            "mul_out": O.spmm_coo(n, dst, src, H, W),
+            "copy_grad_h": O.spmm_coo(n, src, dst, G),
+            "mul_grad_h": O.spmm_coo(n, src, dst, G, W)}
+    for k, out in outs.items():
+        assert np.array_equal(out[rows], c[k + "_rows"]), k
+        assert P.digest(out) == str(c["sha_" + k]), k
+    ip, ix, pos = O.coo_to_csr(n, dst, src)
+    assert P.digest(O.spmm_csr(ip, ix, pos, H, num_threads=8)) == str(c["sha_copy_out"])
+    assert P.digest(O.spmm_csr(ip, ix, pos, H, W, num_threads=8)) == str(c["sha_mul_out"])

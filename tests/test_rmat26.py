@@ -1,0 +1,206 @@
+"""BASELINE.json configs[3] at its size on one MI355X: Graph500 R-MAT scale 26
+(67,108,864 nodes, 1,073,741,824 edges, F = 128), the graph the bench's
+``rmat26`` block reports.
+
+* copy_u + sum and copy_u + mean with heavy-row chunking on
+  (``kernel.set_row_split("auto")``, as the bench and the API default for
+  such graphs run them), checked on a row sample against the oracle: every
+  chunked heavy row plus 20,000 random rows. For each sampled row the slots
+  of the device CSR are checked against the generated edge list (integer
+  arrays bit-exact: same edges, edge-id order), then the oracle recomputes
+  the rows on the host from those slots (oracle.spmm_csr over the sub-CSR,
+  16 threads). Rows that are not chunked are one sequential chain and must
+  match bit for bit; chunked rows must lie within the north-star 1e-5 of the
+  oracle's chain, measured against the row's condition scale sum_k |H[col_k]|
+  (the summation error bound's own yardstick).
+* A 2-layer GraphSAGE-mean (in 128 -> hidden 128 -> 41 classes), forward +
+  backward through the mean g-SpMM and its transposed backward on the same
+  graph: finite loss and gradients; the step time is written to
+  gpurun_out/graphsage_rmat26_test.json.
+
+The reference path this replaces for mean is the degree-bucketing UDF
+(python/dgl/runtime/degree_bucketing.py:13-84, function/reducer.py:52-75).
+Scale: $DGLHIP_TEST_RMAT_SCALE (default 26).
+"""
+import json
+import os
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from dgl import data, kernel
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SCALE = int(os.environ.get("DGLHIP_TEST_RMAT_SCALE", "26"))
+FEAT = 128
+RANDOM_ROWS = 20000
+
+
+@pytest.fixture(scope="module")
+def rmat():
+    dev = torch.device(os.environ.get("DGLHIP_TEST_RMAT_DEVICE", "cuda:0"))
+    if dev.type == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    t0 = time.time()
+    src, dst, n = data.rmat(SCALE, 16, seed=0, device=dev)
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    adj.bwd  # the transposed CSR (GraphSAGE backward) while HBM is still free
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    print("rmat-%d: %d nodes, %d edges, setup %.1fs" % (SCALE, n, src.numel(), time.time() - t0),
+          flush=True)
+    yield {"adj": adj, "h": h, "n": n, "src": src, "dst": dst, "dev": dev}
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+
+
+def _sample(rmat, threshold):
+    """(sampled rows int64, is_heavy bool) on the host: all rows longer than
+    ``threshold`` plus RANDOM_ROWS uniform rows (empty rows included)."""
+    csr = rmat["adj"].fwd
+    deg = (csr.host_indptr[1:] - csr.host_indptr[:-1]).numpy()
+    heavy = np.nonzero(deg > threshold)[0]
+    rng = np.random.default_rng(7)
+    rand = rng.choice(rmat["n"], min(RANDOM_ROWS, rmat["n"] // 2), replace=False)
+    rows = np.unique(np.concatenate([heavy, rand]))
+    return rows, deg[rows] > threshold, deg
+
+
+def _sub_csr(rmat, rows):
+    """Slots of ``rows`` from the device CSR, checked against the edge list;
+    returns (sub_indptr, compacted cols, H rows of those cols) on the host."""
+    csr = rmat["adj"].fwd
+    dev = rmat["dev"]
+    r = torch.from_numpy(rows).to(dev)
+    beg, end = csr.indptr[r], csr.indptr[r + 1]
+    lens = end - beg
+    total = int(lens.sum())
+    starts = torch.cumsum(lens, 0) - lens
+    slot = torch.repeat_interleave(beg - starts, lens) + torch.arange(total, device=dev)
+    cols = csr.indices[slot].long()
+    eids = csr.eid[slot]
+    owner = torch.repeat_interleave(r, lens)
+    # integer arrays: every slot is an edge of its row with that source, in
+    # ascending edge-id order inside the row, and the row holds all its edges
+    assert torch.equal(rmat["dst"][eids], owner)
+    assert torch.equal(rmat["src"][eids], cols)
+    first = torch.zeros(total, dtype=torch.bool, device=dev)
+    first[starts[lens > 0]] = True
+    assert bool(((eids[1:] > eids[:-1]) | first[1:]).all())
+    uniq, inv = torch.unique(cols, return_inverse=True)
+    hsub = rmat["h"].index_select(0, uniq).cpu().numpy()
+    ip = np.concatenate([[0], np.cumsum(lens.cpu().numpy())]).astype(np.int64)
+    ix = inv.cpu().numpy().astype(np.int64)
+    return ip, ix, hsub
+
+
+def _check_rows(out_rows, ref, absref, heavy, label):
+    light = ~heavy
+    assert np.array_equal(out_rows[light], ref[light]), "%s: unchunked rows differ" % label
+    if heavy.any():
+        err = np.abs(out_rows[heavy] - ref[heavy])
+        bound = 1e-5 * absref[heavy] + 1e-30
+        worst = float((err / bound).max())
+        print("%s: %d chunked rows, worst error / (1e-5 * sum|x|) = %.3g"
+              % (label, int(heavy.sum()), worst), flush=True)
+        assert worst <= 1.0
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean"])
+def test_rmat26_heavy_rows_vs_oracle(rmat, reduce):
+    csr = rmat["adj"].fwd
+    old = kernel.set_row_split("auto")
+    try:
+        threshold = kernel._split_threshold(csr)
+        assert threshold > 0, "RMAT-%d must have rows above the split threshold" % SCALE
+        t0 = time.time()
+        out = kernel.gspmm(rmat["adj"], "copy_u", reduce, rmat["h"])
+        if out.is_cuda:
+            torch.cuda.synchronize()
+        print("gspmm %s: %.1f ms (first call, plan included)" % (reduce, (time.time() - t0) * 1e3))
+    finally:
+        kernel.set_row_split(old)
+    rows, heavy, deg = _sample(rmat, threshold)
+    out_rows = out.index_select(0, torch.from_numpy(rows).to(rmat["dev"])).cpu().numpy()
+    del out
+    ip, ix, hsub = _sub_csr(rmat, rows)
+    pos = np.arange(len(ix), dtype=np.int64)
+    ref = O.spmm_csr(ip, ix, pos, hsub, num_threads=16)
+    absref = O.spmm_csr(ip, ix, pos, np.abs(hsub), num_threads=16)
+    d = deg[rows].astype(np.float32)[:, None]
+    if reduce == "mean":
+        # mean = the sum's chain / degree (empty rows 0, the zero initializer)
+        nz = d[:, 0] > 0
+        assert np.array_equal(out_rows[~nz], np.zeros_like(out_rows[~nz]))
+        ref = np.where(d > 0, ref / np.maximum(d, 1), 0).astype(np.float32)
+        absref = absref / np.maximum(d, 1)
+        # 1e-5 on every row (the division's rounding is the kernel's own)
+        worst = float((np.abs(out_rows - ref) / (1e-5 * absref + 1e-30)).max())
+        print("mean: worst error / (1e-5 * sum|x| / deg) = %.3g" % worst)
+        assert worst <= 1.0
+    else:
+        _check_rows(out_rows, ref, absref, heavy, "sum")
+    print("checked %d rows (%d chunked, %d empty), %d slots"
+          % (len(rows), int(heavy.sum()), int((deg[rows] == 0).sum()), len(ix)))
+
+
+def test_rmat26_graphsage_mean_fwd_bwd(rmat):
+    """2-layer GraphSAGE-mean forward + backward at full size (configs[3] model
+    on one GPU); the step time goes to gpurun_out/."""
+    import torch.nn.functional as F
+    from conftest import load_example
+    sage = load_example("graphsage/train.py", "sage_rmat26")
+    dev, n = rmat["dev"], rmat["n"]
+    adj = rmat["adj"]
+    # the edge list is not needed any more: make room for activations
+    rmat.pop("src")
+    rmat.pop("dst")
+    rmat.pop("h")
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(2)
+    feats = 0.1 * torch.randn(n, FEAT, generator=gen, device=dev)
+    labels = torch.randint(0, 41, (n,), generator=gen, device=dev)
+    torch.manual_seed(0)
+    model = sage.SAGE(FEAT, 128, 41, 1, 0.0).to(dev)
+
+    def aggregate(x):
+        return kernel.gspmm(adj, "copy_u", "mean", x)
+
+    old = kernel.set_row_split("auto")
+    times = []
+    try:
+        for _ in range(2):
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            t0 = time.time()
+            logits = model(feats, aggregate)
+            loss = F.cross_entropy(logits, labels)
+            model.zero_grad(set_to_none=True)
+            loss.backward()
+            if dev.type == "cuda":
+                torch.cuda.synchronize()
+            times.append(time.time() - t0)
+            del logits
+    finally:
+        kernel.set_row_split(old)
+    assert torch.isfinite(loss).item()
+    for p in model.parameters():
+        assert p.grad is not None and torch.isfinite(p.grad).all().item()
+    rec = {"graph": "rmat-%d" % SCALE, "nodes": n, "edges": int(adj.fwd.nnz),
+           "model": "GraphSAGE-mean 128-128-41, 2 layers, fwd+bwd (no optimizer)",
+           "step_s": times, "loss": float(loss.item()),
+           "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda"
+           else None}
+    print(rec, flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open(os.path.join("gpurun_out", "graphsage_rmat26_test.json"), "w") as f:
+        json.dump(rec, f)

@@ -11,6 +11,18 @@ for s in $STEPS; do
     tests)
       timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; tail -5 gpurun_out/pytest_gpu.log; ok $rc || exit $rc ;;
+    seltests)
+      # a chosen subset, verbose, each test bounded: SEL="tests/x.py tests/y.py::z" [KEXPR=...]
+      timeout -k 10 1100 python -u -m pytest $SEL -m gpu -x -v -s --timeout ${TEST_TIMEOUT:-300} \
+        --timeout-method thread -p no:cacheprovider ${KEXPR:+-k "$KEXPR"} > gpurun_out/pytest_sel.log 2>&1
+      rc=$?; tail -5 gpurun_out/pytest_sel.log; ok $rc || exit $rc ;;
+    sage)
+      # GraphSAGE-mean full-graph epochs on RMAT-$RMAT_SCALE, one GPU, heavy-row policy both ways
+      for rs in ${ROW_SPLITS:-off auto}; do
+        timeout -k 10 600 python -u examples/graphsage/train.py --graph rmat --rmat-scale ${RMAT_SCALE:-26} \
+          --gpu 0 --n-epochs ${EPOCHS:-5} --row-split $rs > gpurun_out/sage_rmat_$rs.log 2>&1
+        rc=$?; tail -2 gpurun_out/sage_rmat_$rs.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;

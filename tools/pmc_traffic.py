@@ -24,6 +24,31 @@ def per_launch(csv_path, counter, kernel_sub):
     return sum(vals) / len(vals), len(vals)
 
 
+def per_call(csv_path, counter, kernel_sub, calls):
+    """Sum of ``counter`` over every dispatch whose name contains ``kernel_sub``,
+    divided by ``calls`` (API calls that each launch several kernels: the
+    heavy-row split runs the light rows, the chunks and the combine)."""
+    total, n = 0.0, 0
+    with open(csv_path) as f:
+        for r in csv.DictReader(f):
+            if kernel_sub in r["Kernel_Name"] and r["Counter_Name"] == counter:
+                total += float(r["Counter_Value"])
+                n += 1
+    if not n:
+        raise ValueError("no %s samples for kernel %r in %s" % (counter, kernel_sub, csv_path))
+    return total / calls, n
+
+
+def traffic_per_call(fetch_csv, write_csv, calls, kernel_sub="gspmm"):
+    fetch_kib, n1 = per_call(fetch_csv, "FETCH_SIZE", kernel_sub, calls)
+    write_kib, n2 = per_call(write_csv, "WRITE_SIZE", kernel_sub, calls)
+    read_b = 2.0 * fetch_kib * 1024
+    write_b = write_kib * 1024
+    return {"read_bytes": read_b, "write_bytes": write_b, "bytes": read_b + write_b,
+            "raw_fetch_kib": fetch_kib, "raw_write_kib": write_kib, "dispatches": [n1, n2],
+            "calls": calls}
+
+
 def traffic(fetch_csv, write_csv, kernel_sub="gspmm_sum_kernel"):
     fetch_kib, n1 = per_launch(fetch_csv, "FETCH_SIZE", kernel_sub)
     write_kib, n2 = per_launch(write_csv, "WRITE_SIZE", kernel_sub)
