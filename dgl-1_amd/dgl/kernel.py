@@ -46,14 +46,24 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 
 
 # Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device):
-#   "off"  : every row is one sequential chain — bit-exact with the reference (default)
-#   "auto" : rows longer than max(4096, nnz / 12000) slots are split into chunks
-#   <int>  : explicit chunk length
-_ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "off")
+#   "auto" : (default) rows are cut into chunks of max(4096, nnz / 12000) slots,
+#            but only when the longest row is the launch's critical path: a row
+#            is one wave's sequential chain, the launch spreads its slots over
+#            ~7168 resident waves (256 CUs x 4 SIMDs x 7), and rows start
+#            longest-first, so a row longer than twice a wave's share
+#            (nnz / 3584 slots) outlasts the rest of the launch. RMAT-26
+#            (max in-degree ~10x that share) is split: GraphSAGE-mean epoch
+#            0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
+#            Reddit (21,657 <= 32,000) is not, and stays bit-exact.
+#   "off"  : every row is one sequential chain — bit-exact with the reference
+#            on every graph (the documented bit-exact switch)
+#   <int>  : explicit chunk length, applied whenever some row is longer
+_ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
+_CRITICAL_SHARE = 3584  # half the resident waves of a full-chip launch
 
 
 def set_row_split(policy):
-    """Set the heavy-row policy ("off", "auto" or a chunk length); returns the old one."""
+    """Set the heavy-row policy ("auto", "off" or a chunk length); returns the old one."""
     global _ROW_SPLIT
     old = _ROW_SPLIT
     _ROW_SPLIT = str(policy)
@@ -64,7 +74,10 @@ def _split_threshold(csr):
     pol = _ROW_SPLIT
     if pol in ("off", "0", "", "none", "None"):
         return 0
-    t = max(4096, csr.nnz // 12000) if pol == "auto" else int(pol)
+    if pol == "auto":
+        t = max(4096, csr.nnz // 12000)
+        return t if csr.max_degree > max(t, csr.nnz // _CRITICAL_SHARE) else 0
+    t = int(pol)
     return t if csr.max_degree > t else 0
 
 

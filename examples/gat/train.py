@@ -166,7 +166,8 @@ def run_captured(args, model, opt, data, g):
     torch.cuda.current_stream().wait_stream(side)
     graph = torch.cuda.CUDAGraph()
     opt.zero_grad(set_to_none=True)
-    with torch.cuda.graph(graph):
+    # same stream as the warm-up (where the AccumulateGrad nodes were made)
+    with torch.cuda.graph(graph, stream=side):
         static_loss = step()
     dur = []
     for _ in range(3, args.epochs):  # the warm-up steps count as epochs 0-2

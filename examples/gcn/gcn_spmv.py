@@ -148,7 +148,9 @@ def run_captured(args, model, opt, loss_fcn, data, g, n_edges):
     torch.cuda.current_stream().wait_stream(side)
     graph = torch.cuda.CUDAGraph()
     opt.zero_grad(set_to_none=True)
-    with torch.cuda.graph(graph):
+    # capture on the warm-up stream: the parameters' AccumulateGrad nodes were
+    # created there, so the captured backward accumulates on the same stream
+    with torch.cuda.graph(graph, stream=side):
         static_loss = loss_fcn(model(feats).index_select(0, mask), labels_train)
         static_loss.backward()
         opt.step()

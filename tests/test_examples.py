@@ -1,6 +1,8 @@
 """The BASELINE config drivers run end to end (few epochs): GCN (configs 0/1)
 and GAT (config 2) on synthetic shape-matched data, on CPU and — under the
 `gpu` marker — on the MI355X."""
+import warnings
+
 import pytest
 import torch
 
@@ -96,9 +98,13 @@ def test_gcn_hip_graph_replay_matches_eager():
         pytest.skip("no ROCm device")
     base = ["--dataset", "cora", "--n-epochs", "20", "--gpu", "0", "--dropout", "0"]
     eager = gcn_spmv.run(gcn_spmv.parser().parse_args(base))
-    graph = gcn_spmv.run(gcn_spmv.parser().parse_args(base + ["--hip-graph"]))
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        graph = gcn_spmv.run(gcn_spmv.parser().parse_args(base + ["--hip-graph"]))
     assert graph["hip_graph"]
-    assert abs(graph["loss"] - eager["loss"]) < 1e-4
+    # warm-up and capture share a stream: no AccumulateGrad stream mismatch
+    assert not [w for w in caught if "AccumulateGrad" in str(w.message)]
+    assert abs(graph["loss"] - eager["loss"]) < 1e-6 * max(1.0, abs(eager["loss"]))
 
 
 @pytest.mark.gpu
@@ -110,6 +116,9 @@ def test_gat_hip_graph_replay_matches_eager():
     base = ["--dataset", "pubmed", "--epochs", "10", "--gpu", "0", "--in-drop", "0",
             "--attn-drop", "0"]
     eager = gat_train.run(gat_train.parser().parse_args(base))
-    graph = gat_train.run(gat_train.parser().parse_args(base + ["--hip-graph"]))
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        graph = gat_train.run(gat_train.parser().parse_args(base + ["--hip-graph"]))
     assert graph["hip_graph"]
-    assert abs(graph["loss"] - eager["loss"]) < 1e-4 * max(1.0, abs(eager["loss"]))
+    assert not [w for w in caught if "AccumulateGrad" in str(w.message)]
+    assert abs(graph["loss"] - eager["loss"]) < 1e-6 * max(1.0, abs(eager["loss"]))
