@@ -46,12 +46,12 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
       for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) out[eid[k]] = acc;
+      if (lane == 0) out[eid ? eid[k] : k] = acc;
     } else {
       for (int64_t h = lane; h < H; h += 64) {
         float acc = 0.0f;
         for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);
-        out[eid[k] * H + h] = acc;
+        out[(eid ? eid[k] : k) * H + h] = acc;
       }
     }
   }
@@ -67,22 +67,77 @@ __device__ __forceinline__ float quad_xor2(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
 }
 
-// SDDMM dot for rows of NB x 32 floats (F = 32 * NB), one wave per row: the
-// wave takes 8 slots at a time, 8 lanes per slot; lane j of a slot reads the
-// 16 B at 32 i + 4 j of every 32-float column block i (one instruction = 8
-// whole 128-B lines), UNROLL groups of 8 slots in flight. Per lane and block
-// the partial is an fma chain over its 4 features (x, y, z, w); a head's
-// total is the sum of its lanes' partials in block order, then an xor
-// butterfly over the lanes sharing the head (both lanes of a pair add the
-// same two values, so every lane ends with identical bits: deterministic).
-//   D >= 32 (D % 32 == 0): a head spans D / 32 whole blocks, 8-lane butterfly;
-//   D <  32 (D in 4, 8, 16): D / 4 lanes per head, butterfly within them.
-template <int NB, int UNROLL>
+// One xor-exchange across the lanes of a slot (M = 4: __shfl_xor; 2, 1: DPP).
+template <int M>
+__device__ __forceinline__ float slot_xchg(float v) {
+  if (M == 4) return __shfl_xor(v, 4, 64);
+  if (M == 2) return quad_xor2(v);
+  return quad_xor1(v);
+}
+
+// One reduce-scatter stage over lane pairs (j, j ^ M) on Q per-lane values:
+// the lane with bit M set keeps the upper half, its partner the lower half;
+// each sends the half it drops and adds what it receives to what it keeps
+// (own + partner, the butterfly's operand order, so both lanes that end up
+// holding a value hold the same bits). Q == 1 is a plain butterfly step.
+// The exchanges move only the half that is kept elsewhere: for Q values over
+// 8 lanes, Q/2 + Q/4 + Q/8 shuffles instead of the butterfly's 3 Q.
+template <int Q, int M>
+__device__ __forceinline__ void rs_step(float* q, int j) {
+  if (Q == 1) {
+    q[0] = q[0] + slot_xchg<M>(q[0]);
+    return;
+  }
+  const bool up = (j & M) != 0;
+#pragma unroll
+  for (int i = 0; i < Q / 2; ++i) {
+    const float keep = up ? q[i + Q / 2] : q[i];
+    const float send = up ? q[i] : q[i + Q / 2];
+    q[i] = keep + slot_xchg<M>(send);
+  }
+}
+
+// Reduce-scatter of Q values across L lanes (xor L/2, ..., 1: the pairing
+// order of the full butterfly, so every total carries the same bits). Lane r
+// of the group (r = j % L) ends with values r * Q/L .. (r+1) * Q/L - 1 of the
+// group's totals in q[0..Q/L) when Q >= L; else with value r / (L/Q) in q[0].
+template <int Q, int L>
+__device__ __forceinline__ void slot_reduce_scatter(float* q, int j) {
+  if (L >= 8) rs_step<Q, 4>(q, j);
+  constexpr int Q2 = (L >= 8 && Q > 1) ? Q / 2 : Q;
+  if (L >= 4) rs_step<Q2, 2>(q, j);
+  constexpr int Q3 = (L >= 4 && Q2 > 1) ? Q2 / 2 : Q2;
+  if (L >= 2) rs_step<Q3, 1>(q, j);
+}
+
+// SDDMM dot for rows of NB x 32 floats (F = 32 * NB) and H heads of
+// D = F / H features, one wave per row: the wave takes 8 slots at a time,
+// 8 lanes per slot; lane j of a slot reads the 16 B at 32 i + 4 j of every
+// 32-float column block i (one instruction = 8 whole 128-B lines), UNROLL
+// groups of 8 slots in flight. Per lane and block the partial is an fma chain
+// over its 4 features (x, y, z, w).
+//   D >= 32 (LPH = 8 lanes per head): a head's lane partial sums its D / 32
+//     blocks in block order; the H partials are reduce-scattered over the 8
+//     lanes, and lane j stores heads j * H/8 .. (H >= 8), or lane j with
+//     j % (8/H) == 0 stores head j / (8/H): one store instruction per slot,
+//     the slot's H values contiguous.
+//   D < 32 (LPH = D / 4 lanes per head, HPB = 8 / LPH heads per block): the
+//     NB block partials are reduce-scattered within each LPH-lane group g;
+//     lane (g, r) then holds blocks r * NB/LPH + t, i.e. heads
+//     (r * NB/LPH + t) * HPB + g: each t is one store instruction covering 8
+//     of the slot's heads (8 heads at D = 16: one 32-B run per slot).
+// The pairing of lanes is the full xor butterfly's (4, 2, 1 / 2, 1 / 1), so
+// results are deterministic and equal the butterfly's bits.
+template <int NB, int UNROLL, int H>
 __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
-    int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ indptr,
+    int64_t num_rows, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out) {
   constexpr int F = NB * 32;
+  constexpr int D = F / H;
+  constexpr int LPH = D >= 32 ? 8 : D / 4;  // lanes sharing a head
+  constexpr int DBLK = D >= 32 ? D / 32 : 1;  // blocks per head (D >= 32)
+  static_assert(D >= 32 ? D % 32 == 0 : (D == 4 || D == 8 || D == 16), "head width");
   const int64_t row = block_linear() * (blockDim.x >> 6) +
                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   if (row >= num_rows) return;
@@ -93,8 +148,6 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   f32x4 a[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) a[i] = ldv<4>(lhs + row * F + 32 * i + 4 * j);
-  const int lph = D >= 32 ? 8 : static_cast<int>(D >> 2);   // lanes sharing a head
-  const int64_t dblk = D >= 32 ? D / 32 : 1;                 // blocks per head (D >= 32)
   for (int64_t k0 = beg; k0 < end; k0 += 8 * UNROLL) {
     f32x4 c[UNROLL][NB];
 #pragma unroll
@@ -116,27 +169,35 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
         t = __builtin_fmaf(a[i].z, c[u][i].z, t);
         p[i] = __builtin_fmaf(a[i].w, c[u][i].w, t);
       }
-      if (D >= 32) {
-        float t = 0.0f;
+      const int64_t obase = (k < end ? (eid ? eid[k] : k) : 0) * H;
+      if (LPH == 8) {
+        float q[H];
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {  // blocks in order; a head closes every dblk blocks
-          t = (i % dblk == 0) ? p[i] : t + p[i];
-          if ((i + 1) % dblk == 0) {
-            float r = t;
-            r += __shfl_xor(r, 4, 64);
-            r += quad_xor2(r);
-            r += quad_xor1(r);
-            if (j == 0 && k < end) out[eid[k] * H + i / dblk] = r;
-          }
+        for (int h = 0; h < H; ++h) {  // a head's blocks in order
+          q[h] = p[h * DBLK];
+#pragma unroll
+          for (int b = 1; b < DBLK; ++b) q[h] = q[h] + p[h * DBLK + b];
+        }
+        slot_reduce_scatter<H, 8>(q, j);
+        if (H >= 8) {
+#pragma unroll
+          for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t)
+            if (k < end) out[obase + j * (H / 8) + t] = q[t];
+        } else {
+          constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
+          if (k < end && j % DUP == 0) out[obase + j / DUP] = q[0];
         }
       } else {
+        constexpr int HPB = 8 / LPH;
+        const int g = j / LPH, r = j % LPH;
+        slot_reduce_scatter<NB, LPH>(p, j);
+        if (NB >= LPH) {
 #pragma unroll
-        for (int i = 0; i < NB; ++i) {
-          float t = p[i];
-          if (lph >= 4) t += quad_xor2(t);
-          if (lph >= 2) t += quad_xor1(t);
-          const int64_t h = (32 * i + 4 * j) / D;
-          if ((j % lph) == 0 && k < end) out[eid[k] * H + h] = t;
+          for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t)
+            if (k < end) out[obase + (r * (NB / LPH) + t) * HPB + g] = p[t];
+        } else {
+          constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
+          if (k < end && r % DUP == 0) out[obase + (r / DUP) * HPB + g] = p[0];
         }
       }
     }
@@ -145,7 +206,8 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 
 // GAT edge attention, one wave per destination row v (gat/train.py:90-96):
 //   out[eid[k], h] = clamp(exp(leaky_relu(lhs[u, h] + rhs[v, h], alpha)), lo, hi)
-// with u = indices[k]; lanes run over the row's (slot, head) pairs.
+// with u = indices[k]; lanes run over the row's (slot, head) pairs. Generic
+// head count; the common ones take gsddmm_attention_vec_kernel.
 __global__ __launch_bounds__(256) void gsddmm_attention_kernel(
     int64_t num_rows, int64_t H, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
@@ -160,7 +222,58 @@ __global__ __launch_bounds__(256) void gsddmm_attention_kernel(
     float x = lhs[int64_t(indices[k]) * H + h] + rhs[row * H + h];
     x = x > 0.0f ? x : alpha * x;
     if (apply_exp) x = __expf(x);
-    out[eid[k] * H + h] = fminf(fmaxf(x, lo), hi);
+    out[(eid ? eid[k] : k) * H + h] = fminf(fmaxf(x, lo), hi);
+  }
+}
+
+template <int H> struct HeadVec { typedef float T; };
+template <> struct HeadVec<2> { typedef f32x2 T; };
+template <> struct HeadVec<4> { typedef f32x4 T; };
+template <> struct HeadVec<8> { typedef f32x4 T; };
+template <> struct HeadVec<16> { typedef f32x4 T; };
+
+// Same operation for H in {1, 2, 4, 8, 16}: lane = slot. Each lane gathers
+// its source's H values as whole vectors (H = 8: two 16-B loads of one 32-B
+// row) and stores the slot's H results the same way; the destination's H
+// values are wave-uniform (one row per wave). 64 slots per wave step instead
+// of 64 / H, and no per-lane division. Same per-element arithmetic as
+// gsddmm_attention_kernel (bit-identical).
+template <int H>
+__global__ __launch_bounds__(256) void gsddmm_attention_vec_kernel(
+    int64_t num_rows, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const float* __restrict__ lhs, const float* __restrict__ rhs, float alpha, float lo,
+    float hi, int apply_exp, float* __restrict__ out) {
+  typedef typename HeadVec<H>::T V;
+  constexpr int W = sizeof(V) / sizeof(float);  // floats per vector
+  constexpr int NV = H / W;                      // vectors per slot
+  const int64_t row = block_linear() * (blockDim.x >> 6) +
+                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (row >= num_rows) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  if (beg == end) return;
+  float r[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) r[h] = rhs[row * H + h];
+  for (int64_t k = beg + lane; k < end; k += 64) {
+    const V* src = reinterpret_cast<const V*>(lhs + int64_t(indices[k]) * H);
+    V* dst = reinterpret_cast<V*>(out + (eid ? eid[k] : k) * H);
+    V l[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) l[v] = src[v];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      V y;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float x = reinterpret_cast<const float*>(&l[v])[w] + r[v * W + w];
+        x = x > 0.0f ? x : alpha * x;
+        if (apply_exp) x = __expf(x);
+        reinterpret_cast<float*>(&y)[w] = fminf(fmaxf(x, lo), hi);
+      }
+      dst[v] = y;
+    }
   }
 }
 
@@ -168,6 +281,7 @@ __global__ __launch_bounds__(256) void gsddmm_attention_kernel(
 Timing g_timing;
 int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
 int g_cache_policy = -1;
+int g_sddmm_alt = 0;
 
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
   const int em = edge_mode(a.elen, a.F);
@@ -340,7 +454,7 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
                "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
+  DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
   const int64_t blocks = (num_rows + 3) / 4;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
   const int64_t D = feat_len / num_heads;
@@ -351,26 +465,41 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   const bool sliced = aligned && head_ok && (nb == 1 || nb == 2 || nb == 4 || nb == 8 ||
                                              nb == 16);
   timed_launch(stream, [&] {
-#define DGLHIP_SDDMM_U(NB, U)                                                              \
-  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U>), grid_1d(blocks), \
-                     dim3(256), 0, stream, num_rows, num_heads, D, indptr, indices, eid, lhs, \
-                     rhs, out)
-#define DGLHIP_SDDMM(NB) DGLHIP_SDDMM_U(NB, (NB >= 8 ? 1 : 2))
-    // F=128 with heads of >= 32 features: 32 slots in flight (8.84 -> 8.51 ms at
-    // one head on the Reddit-shaped graph); narrower heads keep 16 (8 heads:
-    // 11.9 ms at 16, 12.4 ms at 32), reducers_reddit.json
-    if (sliced && nb == 1) DGLHIP_SDDMM(1);
-    else if (sliced && nb == 2) DGLHIP_SDDMM(2);
-    else if (sliced && nb == 4 && D >= 32) DGLHIP_SDDMM_U(4, 4);
-    else if (sliced && nb == 4) DGLHIP_SDDMM(4);
-    else if (sliced && nb == 8) DGLHIP_SDDMM(8);
-    else if (sliced && nb == 16) DGLHIP_SDDMM(16);
-    else
-      hipLaunchKernelGGL(gsddmm_dot_kernel, grid_1d(blocks),
-                         dim3(256), 0, stream, num_rows, feat_len, num_heads, indptr,
-                         indices, eid, lhs, rhs, out);
-#undef DGLHIP_SDDMM
-#undef DGLHIP_SDDMM_U
+#define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH>), grid_1d(blocks), dim3(256), 0, \
+                     stream, num_rows, indptr, indices, eid, lhs, rhs, out)
+#define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
+  if (num_heads == HH) {                                                                   \
+    if (!g_sddmm_alt) DGLHIP_SDDMM_K(NB, U, HH);                                          \
+    else DGLHIP_SDDMM_K(NB, (U == 4 ? 2 : 2 * U), HH);                                     \
+    return;                                                                                \
+  }
+    // default slots in flight: 8 x U. F = 128: U = 4 for every head count
+    // (Reddit-shaped graph, profiles/r02/reducers_reddit.json, 16 -> 32 slots:
+    // H = 1 8.92 -> 8.36 ms, H = 8 9.38 -> 8.83, H = 16 9.73 -> 9.23,
+    // H = 32 10.77 -> 10.44); dglhip_set_sddmm_variant(1) takes the other depth
+    if (sliced && nb == 1) {
+      DGLHIP_SDDMM_H(1, 2, 1) DGLHIP_SDDMM_H(1, 2, 2) DGLHIP_SDDMM_H(1, 2, 4)
+      DGLHIP_SDDMM_H(1, 2, 8)
+    } else if (sliced && nb == 2) {
+      DGLHIP_SDDMM_H(2, 2, 1) DGLHIP_SDDMM_H(2, 2, 2) DGLHIP_SDDMM_H(2, 2, 4)
+      DGLHIP_SDDMM_H(2, 2, 8) DGLHIP_SDDMM_H(2, 2, 16)
+    } else if (sliced && nb == 4) {
+      DGLHIP_SDDMM_H(4, 4, 1) DGLHIP_SDDMM_H(4, 4, 2) DGLHIP_SDDMM_H(4, 4, 4)
+      DGLHIP_SDDMM_H(4, 4, 8) DGLHIP_SDDMM_H(4, 4, 16) DGLHIP_SDDMM_H(4, 4, 32)
+    } else if (sliced && nb == 8) {
+      DGLHIP_SDDMM_H(8, 1, 1) DGLHIP_SDDMM_H(8, 1, 2) DGLHIP_SDDMM_H(8, 1, 4)
+      DGLHIP_SDDMM_H(8, 1, 8) DGLHIP_SDDMM_H(8, 1, 16) DGLHIP_SDDMM_H(8, 1, 32)
+      DGLHIP_SDDMM_H(8, 1, 64)
+    } else if (sliced && nb == 16) {
+      DGLHIP_SDDMM_H(16, 1, 1) DGLHIP_SDDMM_H(16, 1, 2) DGLHIP_SDDMM_H(16, 1, 4)
+      DGLHIP_SDDMM_H(16, 1, 8) DGLHIP_SDDMM_H(16, 1, 16) DGLHIP_SDDMM_H(16, 1, 32)
+      DGLHIP_SDDMM_H(16, 1, 64) DGLHIP_SDDMM_H(16, 1, 128)
+    }
+    hipLaunchKernelGGL(gsddmm_dot_kernel, grid_1d(blocks), dim3(256), 0, stream, num_rows,
+                       feat_len, num_heads, indptr, indices, eid, lhs, rhs, out);
+#undef DGLHIP_SDDMM_K
+#undef DGLHIP_SDDMM_H
   });
   API_END();
 }
@@ -385,6 +514,13 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {
   g_var_group = group;
   g_var_unroll = unroll;
   g_var_pipe = pipelined ? 1 : 0;
+  API_END();
+}
+
+int dglhip_set_sddmm_variant(int alternate) {
+  API_BEGIN();
+  DGLHIP_CHECK(alternate == 0 || alternate == 1, "unsupported g-SDDMM variant " << alternate);
+  g_sddmm_alt = alternate;
   API_END();
 }
 
@@ -404,9 +540,22 @@ int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && num_heads >= 1, "bad sizes");
   if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && eid && lhs && rhs && out, "null pointer argument");
+  DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
   DGLHIP_CHECK((num_rows + 3) / 4 <= 0x7fffffff, "grid too large");
+  // vector rows need lhs / out rows aligned to the vector width
+  const int64_t vbytes = num_heads >= 4 ? 16 : 4 * num_heads;
+  const bool aligned = (reinterpret_cast<uintptr_t>(lhs) % vbytes) == 0 &&
+                       (reinterpret_cast<uintptr_t>(out) % vbytes) == 0;
   timed_launch(stream, [&] {
+#define DGLHIP_ATT(HH)                                                                     \
+  if (aligned && num_heads == HH) {                                                        \
+    hipLaunchKernelGGL((gsddmm_attention_vec_kernel<HH>), grid_1d((num_rows + 3) / 4),     \
+                       dim3(256), 0, stream, num_rows, indptr, indices, eid, lhs, rhs,      \
+                       alpha, clamp_lo, clamp_hi, apply_exp, out);                          \
+    return;                                                                                \
+  }
+    DGLHIP_ATT(1) DGLHIP_ATT(2) DGLHIP_ATT(4) DGLHIP_ATT(8) DGLHIP_ATT(16)
+#undef DGLHIP_ATT
     hipLaunchKernelGGL(gsddmm_attention_kernel, grid_1d((num_rows + 3) / 4),
                        dim3(256), 0, stream, num_rows, num_heads, indptr, indices, eid, lhs,
                        rhs, alpha, clamp_lo, clamp_hi, apply_exp, out);

@@ -386,7 +386,7 @@ int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads, const int6
           float x = lhs[int64_t(indices[k]) * H + h] + rhs[r * H + h];
           x = x > 0.0f ? x : alpha * x;
           if (apply_exp) x = std::exp(x);
-          out[eid[k] * H + h] = std::min(std::max(x, clamp_lo), clamp_hi);
+          out[(eid ? eid[k] : k) * H + h] = std::min(std::max(x, clamp_lo), clamp_hi);
         }
   });
   API_END();
@@ -459,7 +459,7 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len, int64_t num_h
         for (int64_t h = 0; h < H; ++h) {
           float acc = 0.0f;
           for (int64_t d = 0; d < D; ++d) acc = std::fma(a[h * D + d], c[h * D + d], acc);
-          out[eid[k] * H + h] = acc;
+          out[(eid ? eid[k] : k) * H + h] = acc;
         }
       }
     }

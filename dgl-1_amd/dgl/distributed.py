@@ -29,8 +29,8 @@ node ids to positions in the padded all-gather buffer, so the kernel runs
 unchanged. Row results are bit-identical to the single-GPU product: each
 local row accumulates exactly the same edges in the same edge-id order.
 
-Pipelined forward (``pipeline_chunks = C > 0``, inference / benchmarking).
-With the all-to-allv halo, every peer's request list is cut into C parts and
+Pipelined path (``pipeline_chunks = C > 0``, copy_u with sum or mean,
+differentiable: _PipelinedAggregate). With the all-to-allv halo, every peer's request list is cut into C parts and
 the exchange runs as C all-to-allv calls on a side stream: the own sources are
 reduced while chunk 1 is in flight, and the received rows of chunk c as soon
 as it lands, so only the last chunk's rows are reduced after the exchange
@@ -45,7 +45,12 @@ keeps the degree-descending schedule and heavy-row chunking of a plain
 g-SpMM. The result is one sequential chain in (segment, edge-id) order:
 deterministic and within fp32 tolerance of the edge-id-order chain
 (bit-identical when edge ids already run in source order, as in bench.py's
-graphs, and no row is chunked).
+graphs, and no row is chunked). The backward runs the segments' transposes:
+each halo chunk's gradient rows are computed and sent back to their owners
+(reduce-scatter of the chunk's landing rows / reverse all-to-allv) on the
+comm stream while the next chunk's transposed product runs, and the own
+segment's product overlaps the last exchange; the received gradients are
+then added in chunk (and peer) order, so the result is deterministic.
 """
 from __future__ import absolute_import
 
@@ -160,6 +165,37 @@ class _AllToAllRows(torch.autograd.Function):
         return dh, None, None, None, None, None
 
 
+class _PipelinedAggregate(torch.autograd.Function):
+    """update_all(copy_u, sum | mean) over a PartitionedGraph with the halo
+    exchange cut into chunks and overlapped with the local g-SpMM segments,
+    in both directions (full-graph training at N > 1, the layer of
+    examples/pytorch/gcn/gcn_spmv.py:45-62 sharded; its backward is
+    SURVEY.md §3.2's dH = Aᵀ·dC).
+
+    Forward: PartitionedGraph._pipelined_* (own segment while the exchange
+    is in flight, each chunk's segment as it lands), then the mean's divisor.
+    Backward: each halo chunk's transposed product, returned to the owners
+    (reduce-scatter / reverse all-to-allv on the comm stream) while the next
+    chunk's product runs; the own segment's transposed product overlaps the
+    last exchange; the received gradients are added in chunk order."""
+
+    @staticmethod
+    def forward(ctx, h_local, pg, mean):
+        out = pg._pipelined_sum(h_local.detach())
+        if mean:
+            out = out / pg._mean_divisor(out.dtype)
+        ctx.pg, ctx.mean = pg, mean
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pg = ctx.pg
+        dout = dout.contiguous()
+        if ctx.mean:
+            dout = (dout / pg._mean_divisor(dout.dtype)).contiguous()
+        return pg._pipelined_backward(dout), None, None
+
+
 class PartitionedGraph(object):
     """This rank's shard of a graph for full-graph message passing.
 
@@ -207,6 +243,10 @@ class PartitionedGraph(object):
         owner = torch.searchsorted(b, src, right=True) - 1
         self.num_edges = int(src.numel())
         self.device = device
+        # in-degree of each local row (all of a row's in-edges live on this
+        # rank): the mean reducer's divisor
+        self.in_deg = torch.bincount(dst - self.lo, minlength=self.num_local)
+        self._seg_t = None  # transposed segment CSRs, built by the first backward
         self.chunks = int(pipeline_chunks)
         self.adj = None
         self.halo = None
@@ -367,15 +407,125 @@ class PartitionedGraph(object):
         self.halo = None
 
     def update_all(self, h_local, msg="copy_u", reduce="sum", efeat=None):
-        """Local rows of update_all(msg, reduce) given this rank's node features."""
+        """Local rows of update_all(msg, reduce) given this rank's node features.
+
+        Pipelined (pipeline_chunks > 0): copy_u with sum or mean, differentiable
+        in h_local; the backward overlaps each chunk's reverse exchange with the
+        next chunk's transposed g-SpMM (_PipelinedAggregate)."""
         if self.chunks > 0:
-            if msg != "copy_u" or reduce != "sum" or h_local.requires_grad:
-                raise ValueError("the pipelined forward covers copy_u + sum without autograd")
-            if self.halo_mode == "alltoall":
-                return self._pipelined_alltoall_sum(h_local)
-            return self._pipelined_copy_sum(h_local)
+            if msg not in ("copy_u", "copy_src") or reduce not in ("sum", "mean"):
+                raise ValueError("the pipelined path covers copy_u with sum or mean")
+            if efeat is not None:
+                raise ValueError("copy_u takes no edge features")
+            return _PipelinedAggregate.apply(h_local, self, reduce == "mean")
         full = self.gather_halo(h_local)
         return kernel.gspmm(self.adj, msg, reduce, full, efeat)
+
+    def _pipelined_sum(self, h_local):
+        if self.halo_mode == "alltoall":
+            return self._pipelined_alltoall_sum(h_local)
+        return self._pipelined_copy_sum(h_local)
+
+    def _mean_divisor(self, dtype):
+        d = getattr(self, "_deg_f", None)
+        if d is None or d.dtype != dtype:
+            d = self._deg_f = self.in_deg.clamp(min=1).to(dtype).unsqueeze(1)
+        return d
+
+    def _transposed_segments(self):
+        """Per segment of the pipelined forward, the CSR of its transpose: rows
+        are the segment's source rows (h_local for the own segment; one
+        chunk's landing rows for a halo segment, rebased to the chunk), slots
+        in the forward's edge order (kernel.coo_of recovers it)."""
+        if self._seg_t is None:
+            R, C = self.num_local, self.chunks
+            segs = []
+            for i, csr in enumerate(self.seg_csrs):
+                row, col = kernel.coo_of(csr)
+                if i == 0:
+                    base, nrows = 0, R
+                elif self.halo_mode == "alltoall":
+                    base, nrows = 0, sum(self.chunk_recv_splits[i - 1])
+                else:
+                    cw = self.world * self.chunk_rows  # landing rows of one chunk
+                    base, nrows = (i - 1) * cw, cw
+                segs.append(kernel.build_csr(max(nrows, 1), R, col - base, row,
+                                             kernel.ORDER_EID, self.device))
+                del row, col
+            self._seg_t = segs
+        return self._seg_t
+
+    def _pipelined_backward(self, dout):
+        """dh_local for d(out) = dout: every segment's transposed product, the
+        halo chunks' gradients returned to their owners (reduce-scatter of the
+        chunk's landing rows, or the reverse all-to-allv then sum-on-receive
+        one peer at a time), the own segment reduced while they travel.
+        Gradients travel in fp32 whatever the forward's wire type."""
+        if self._emulated:
+            raise ValueError("an emulated rank has no peers to return gradients to")
+        R, C, P = self.num_local, self.chunks, self.world
+        F = dout.shape[1]
+        dev = self.device
+        segs = self._transposed_segments()
+        comm = self.comm_stream
+        main = torch.cuda.current_stream(dev) if comm is not None else None
+        landed, events, keep = [], [], []
+        for c in range(C):
+            t = segs[c + 1]
+            d_rows = torch.empty(t.num_rows, F, device=dev)
+            kernel.gspmm_into(t, d_rows, dout, accumulate=False)
+            if self.halo_mode == "alltoall":
+                nsend = sum(self.chunk_send_splits[c])
+                recv = torch.empty(nsend, F, device=dev)
+                n_in = sum(self.chunk_recv_splits[c])
+                src_rows = d_rows[:n_in]
+
+                def run(recv=recv, src_rows=src_rows, c=c):
+                    dist.all_to_all_single(recv, src_rows, self.chunk_send_splits[c],
+                                           self.chunk_recv_splits[c], group=self.group)
+            else:
+                recv = torch.empty(self.chunk_rows, F, device=dev)
+
+                def run(recv=recv, d_rows=d_rows):
+                    dist.reduce_scatter_tensor(recv, d_rows, op=dist.ReduceOp.SUM,
+                                               group=self.group)
+            if comm is not None:
+                ev = torch.cuda.Event()
+                ev.record(main)
+                with torch.cuda.stream(comm):
+                    comm.wait_event(ev)
+                    run()
+                    done = torch.cuda.Event()
+                    done.record(comm)
+                events.append(done)
+                keep.append(d_rows)
+            else:
+                run()
+            landed.append(recv)
+        # own sources while the last chunks travel
+        dh = torch.empty(R, F, device=dev)
+        kernel.gspmm_into(segs[0], dh, dout, accumulate=False)
+        cr = getattr(self, "chunk_rows", 0)
+        for c in range(C):
+            if comm is not None:
+                main.wait_event(events[c])
+                landed[c].record_stream(main)
+            if self.halo_mode == "alltoall":
+                off = 0
+                idx = self.chunk_send_idx[c]
+                for n in self.chunk_send_splits[c]:
+                    if n:  # row ids are unique within a peer: ordered adds
+                        dh.index_add_(0, idx[off:off + n], landed[c][off:off + n])
+                    off += n
+            else:
+                lo, hi = c * cr, min((c + 1) * cr, R)
+                if hi > lo:
+                    dh[lo:hi] += landed[c][:hi - lo]
+        if comm is not None:
+            for t in keep:
+                t.record_stream(comm)
+            dout.record_stream(comm)
+        return dh
 
     def _pipelined_copy_sum(self, h_local):
         C, P, cr = self.chunks, self.world, self.chunk_rows

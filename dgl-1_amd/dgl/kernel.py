@@ -39,6 +39,9 @@ MSG_COPY_U_BF16 = 3  # copy_u over bf16 source rows, widened exactly to fp32 (dg
 RED_SUM, RED_MAX, RED_MEAN = 0, 1, 2
 RED_SUM_ACCUM = 3  # out += sum, each row's chain continued from out (include/dgl_hip.h)
 ORDER_EID, ORDER_COL = 0, 1
+# edge values laid out in the forward CSR's slot order (edge_order="slot"):
+# kernels read / write slot k at row k, no eid indirection
+SLOT = "slot"
 
 _MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_U_MUL_E,
               "u_mul_e": MSG_U_MUL_E, "copy_edge": MSG_COPY_E, "copy_e": MSG_COPY_E}
@@ -51,15 +54,18 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 #            is one wave's sequential chain, the launch spreads its slots over
 #            ~7168 resident waves (256 CUs x 4 SIMDs x 7), and rows start
 #            longest-first, so a row longer than twice a wave's share
-#            (nnz / 3584 slots) outlasts the rest of the launch. RMAT-26
-#            (max in-degree ~10x that share) is split: GraphSAGE-mean epoch
-#            0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
-#            Reddit (21,657 <= 32,000) is not, and stays bit-exact.
+#            (nnz / 3584 slots) outlasts the rest of the launch — and it must
+#            also be longer than 65,536 slots (~4 ms of chained gathers), below
+#            which the loss is small and every row stays one exact chain.
+#            RMAT-26 (max in-degree ~855k, 2.9x the share) is split: GraphSAGE-
+#            mean epoch 0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
+#            Reddit (21,657) is not, and stays bit-exact.
 #   "off"  : every row is one sequential chain — bit-exact with the reference
 #            on every graph (the documented bit-exact switch)
 #   <int>  : explicit chunk length, applied whenever some row is longer
 _ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
 _CRITICAL_SHARE = 3584  # half the resident waves of a full-chip launch
+_CRITICAL_MIN = 65536   # rows up to this length are never split by "auto"
 
 
 def set_row_split(policy):
@@ -76,7 +82,7 @@ def _split_threshold(csr):
         return 0
     if pol == "auto":
         t = max(4096, csr.nnz // 12000)
-        return t if csr.max_degree > max(t, csr.nnz // _CRITICAL_SHARE) else 0
+        return t if csr.max_degree > max(_CRITICAL_MIN, csr.nnz // _CRITICAL_SHARE) else 0
     t = int(pol)
     return t if csr.max_degree > t else 0
 
@@ -354,7 +360,7 @@ def _edge_len(eshape, fshape):
     H (leading dims of fshape, broadcast over the rest: GAT's (H, 1) vs (H, D))."""
     eshape, fshape = tuple(eshape), tuple(fshape)
     F = int(np.prod(fshape)) if fshape else 1
-    if eshape in ((), (1,)):
+    if all(d == 1 for d in eshape):  # (), (1,), (1, 1): one scalar per edge
         return 1
     if eshape == fshape:
         return F
@@ -368,9 +374,12 @@ def _edge_len(eshape, fshape):
                    % (eshape, fshape))
 
 
-def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None):
+def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None, emap=None):
     """ufeat2: (num_cols, F) or None; efeat2: (E, elen) or None. Returns (out, arg).
-    ``out`` (optional) receives the result; RED_SUM_ACCUM adds into it."""
+    ``out`` (optional) receives the result; RED_SUM_ACCUM adds into it.
+    ``emap`` says where slot k's edge values are: None = row eid[k] (edge-id
+    order), SLOT = row k (efeat2 laid out in this CSR's slot order), or an
+    int64 tensor of rows per slot."""
     dev = (ufeat2 if ufeat2 is not None else efeat2).device
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
@@ -379,7 +388,10 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
-    eid = csr.slot_eid if msg not in (MSG_COPY_U, MSG_COPY_U_BF16) else None
+    if msg in (MSG_COPY_U, MSG_COPY_U_BF16) or emap is SLOT:
+        eid = None
+    else:
+        eid = csr.slot_eid if emap is None else emap
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
     if split:
@@ -402,20 +414,54 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     return out, arg
 
 
-def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1):
-    """out[eid, h] = <lhs[row, head h], rhs[col, head h]>; returns (num_edges, heads)."""
+def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1, slot=False):
+    """out[eid, h] = <lhs[row, head h], rhs[col, head h]>; returns (num_edges, heads).
+    ``slot``: out[k] for slot k of ``csr`` instead (values in its slot order)."""
     dev = lhs2.device
     out = torch.zeros(num_edges, heads, dtype=torch.float32, device=dev)
     F = lhs2.shape[1]
+    eid = None if slot else csr.eid
     if dev.type == "cuda":
         check_call(LIB.dglhip_gsddmm_device(0, csr.num_rows, F, heads, ptr(csr.indptr),
-                                            ptr(csr.indices), ptr(csr.eid), ptr(lhs2), ptr(rhs2),
+                                            ptr(csr.indices), ptr(eid), ptr(lhs2), ptr(rhs2),
                                             ptr(out), _stream_of(dev)))
     else:
         check_call(LIB.dglhip_gsddmm_host(0, csr.num_rows, F, heads, ptr(csr.indptr),
-                                          ptr(csr.indices), ptr(csr.eid), ptr(lhs2), ptr(rhs2),
+                                          ptr(csr.indices), ptr(eid), ptr(lhs2), ptr(rhs2),
                                           ptr(out), 0))
     return out
+
+
+def _fwd_slot_of_bwd(adj):
+    """For each slot of the transposed CSR, the forward-CSR slot holding the
+    same edge: how an edge tensor laid out in forward slot order is read along
+    the transpose (backward of slot-ordered edge values). Cached on ``adj``."""
+    m = getattr(adj, "_bwd_fslot", None)
+    if m is None:
+        fwd, bwd = adj.fwd, adj.bwd
+        if fwd.slot_eid is None:  # forward slots already run in edge-id order
+            m = bwd.eid
+        else:
+            inv = torch.empty_like(fwd.eid)
+            inv[fwd.eid] = torch.arange(fwd.nnz, dtype=fwd.eid.dtype, device=fwd.eid.device)
+            m = inv.index_select(0, bwd.eid)
+            del inv
+        adj._bwd_fslot = m
+    return m
+
+
+def edge_order_of(adj, edge_order):
+    """Validate an ``edge_order`` argument ("eid" or "slot")."""
+    if edge_order not in ("eid", "slot"):
+        raise DGLError("edge_order must be 'eid' or 'slot', got %r" % (edge_order,))
+    return edge_order == "slot"
+
+
+def slot_permutation(adj):
+    """int64[nnz]: the edge id held by each forward-CSR slot of ``adj``. An
+    edge tensor ``x`` in edge-id order is ``x[slot_permutation(adj)]`` in slot
+    order; a slot-ordered ``y`` goes back with ``out[perm] = y``."""
+    return adj.fwd.eid
 
 
 def _eid_major(adj):
@@ -449,16 +495,21 @@ class _GSpMM(torch.autograd.Function):
 
     Backward (SUM/MEAN): dU = the same product over the transposed CSR (the
     reference's autograd of torch.sparse.mm computes Aᵀ·dC the same way,
-    accumulating over out-edges in edge-id order); dE by g-SDDMM."""
+    accumulating over out-edges in edge-id order); dE by g-SDDMM.
+
+    ``slot``: efeat is laid out in the forward CSR's slot order (row k = slot
+    k), so the forward reads it without the eid indirection and dE comes back
+    in the same layout (the SDDMM walks the forward CSR, sequential stores)."""
 
     @staticmethod
-    def forward(ctx, adj, msg, red, feat_len, num_edges, ufeat2, efeat2):
+    def forward(ctx, adj, msg, red, feat_len, num_edges, ufeat2, efeat2, slot=False):
         elen = 0 if efeat2 is None else efeat2.shape[1]
         need_arg = red == RED_MAX and (
             (ufeat2 is not None and ufeat2.requires_grad) or
             (efeat2 is not None and efeat2.requires_grad))
-        out, arg = _run_gspmm(adj.fwd, msg, red, ufeat2, efeat2, elen, feat_len, need_arg)
-        ctx.adj, ctx.msg, ctx.red, ctx.num_edges = adj, msg, red, num_edges
+        out, arg = _run_gspmm(adj.fwd, msg, red, ufeat2, efeat2, elen, feat_len, need_arg,
+                              emap=SLOT if slot else None)
+        ctx.adj, ctx.msg, ctx.red, ctx.num_edges, ctx.slot = adj, msg, red, num_edges, slot
         # keep an operand alive only when the backward reads its values: the
         # node rows for u_mul_e's edge gradient, the edge values for its node
         # gradient. copy_u/copy_e + sum/mean save nothing (in a partitioned
@@ -475,7 +526,7 @@ class _GSpMM(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dout):
         ufeat2, efeat2, arg = ctx.saved_tensors
-        adj, msg, red = ctx.adj, ctx.msg, ctx.red
+        adj, msg, red, slot = ctx.adj, ctx.msg, ctx.red, ctx.slot
         dout = dout.contiguous()
         fwd = adj.fwd
         du = de = None
@@ -491,9 +542,11 @@ class _GSpMM(torch.autograd.Function):
         if red_b == RED_SUM:
             if need_u:
                 elen = 0 if efeat2 is None else efeat2.shape[1]
+                reads_e = msg == MSG_U_MUL_E
                 du, _ = _run_gspmm(adj.bwd, msg if msg != MSG_COPY_E else MSG_COPY_U, RED_SUM,
-                                   dout, efeat2 if msg == MSG_U_MUL_E else None,
-                                   elen if msg == MSG_U_MUL_E else 0, F, False)
+                                   dout, efeat2 if reads_e else None, elen if reads_e else 0, F,
+                                   False, emap=_fwd_slot_of_bwd(adj) if (slot and reads_e)
+                                   else None)
             if need_e:
                 rows = fwd.row_ids()
                 if msg == MSG_COPY_E:
@@ -501,16 +554,23 @@ class _GSpMM(torch.autograd.Function):
                     if ctx.eshape[1] == 1:
                         g = g.sum(1, keepdim=True)
                 elif ctx.eshape[1] < F:  # scalar or per-head weights: g-SDDMM dot
-                    csr, tr = _eid_major(adj)
                     u2 = ufeat2.contiguous()
-                    de = _run_sddmm_dot(csr, u2 if tr else dout, dout if tr else u2,
-                                        ctx.num_edges, ctx.eshape[1])
+                    if slot:  # forward walk, de[k] stored in slot order
+                        de = _run_sddmm_dot(fwd, dout, u2, ctx.num_edges, ctx.eshape[1],
+                                            slot=True)
+                    else:
+                        csr, tr = _eid_major(adj)
+                        de = _run_sddmm_dot(csr, u2 if tr else dout, dout if tr else u2,
+                                            ctx.num_edges, ctx.eshape[1])
                     g = None
                 else:
                     g = dout.index_select(0, rows) * ufeat2.index_select(0, fwd.indices.long())
                 if g is not None:
-                    de = dout.new_zeros(ctx.eshape)
-                    de.index_copy_(0, fwd.eid, g)
+                    if slot:
+                        de = g.reshape(ctx.eshape)
+                    else:
+                        de = dout.new_zeros(ctx.eshape)
+                        de.index_copy_(0, fwd.eid, g)
         else:  # MAX: route each output element's gradient to its argmax slot
             valid = arg >= 0
             slots = arg.clamp(min=0)
@@ -523,28 +583,32 @@ class _GSpMM(torch.autograd.Function):
                 src = fwd.indices.long()[sl]
                 gu = g
                 if msg == MSG_U_MUL_E:
-                    e = fwd.eid[sl]
+                    e = sl if slot else fwd.eid[sl]
                     gu = g * efeat2[e, fidx // dpe]
                 du = dout.new_zeros(ctx.ushape)
                 du.index_put_((src, fidx), gu, accumulate=True)
             if need_e:
-                e = fwd.eid[sl]
+                e = sl if slot else fwd.eid[sl]
                 ge = g
                 if msg == MSG_U_MUL_E:
                     ge = g * ufeat2[fwd.indices.long()[sl], fidx]
                 de = dout.new_zeros(ctx.eshape)
                 de.index_put_((e, fidx // dpe), ge, accumulate=True)
-        return None, None, None, None, None, du, de
+        return None, None, None, None, None, du, de, None
 
 
-def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None):
+def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None, edge_order="eid"):
     """Generalised SpMM over ``adj`` (a SparseAdj on the features' device).
 
     ufeat : (num_cols, *fshape) node features or None (copy_e)
     efeat : (num_edges,) / (num_edges, 1) scalar or (num_edges, *fshape) edge
             features indexed by the adjacency's eid, or None (copy_u)
+    edge_order : "eid" (efeat row e = edge id e, the frame's layout) or
+            "slot" (row k = the forward CSR's slot k, as edge_attention /
+            gsddmm_dot return with edge_order="slot": no eid indirection)
     returns (num_rows, *fshape) float32
     """
+    slot = edge_order_of(adj, edge_order)
     msg = _MSG_NAMES.get(msg, msg)
     red = _RED_NAMES.get(reduce, reduce)
     if msg != MSG_COPY_E and ufeat is None:
@@ -570,17 +634,21 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None):
         e2 = _f32c(efeat.reshape(ne, elen))
     if num_edges is None:
         num_edges = 0 if e2 is None else e2.shape[0]
-    out = _GSpMM.apply(adj, msg, red, F, num_edges, u2, e2)
+    out = _GSpMM.apply(adj, msg, red, F, num_edges, u2, e2, slot)
     return out.reshape((adj.shape[0],) + fshape) if fshape else out.reshape(adj.shape[0])
 
 
-def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1):
+def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1, edge_order="eid"):
     """out[eid, h] = <lhs[row, h], rhs[col, h]> for every slot of ``adj``
-    (rows of lhs are the adjacency's rows, of rhs its columns; no autograd)."""
+    (rows of lhs are the adjacency's rows, of rhs its columns; no autograd).
+    edge_order="slot" returns row k = forward CSR slot k instead."""
+    slot = edge_order_of(adj, edge_order)
     dev = lhs.device
     adj = adj.to(dev)
     lhs2 = _f32c(lhs.reshape(lhs.shape[0], -1))
     rhs2 = _f32c(rhs.reshape(rhs.shape[0], -1))
+    if slot:
+        return _run_sddmm_dot(adj.fwd, lhs2, rhs2, num_edges, heads, slot=True)
     csr, tr = _eid_major(adj)
     return _run_sddmm_dot(csr, rhs2 if tr else lhs2, lhs2 if tr else rhs2, num_edges, heads)
 
@@ -625,6 +693,12 @@ def gspmm_ranges(msg, beg, end, accumulate, indices, out, ufeat=None, efeat=None
     else:
         check_call(LIB.dglhip_gspmm_ranges_host(*(args + (0,))))
     return out
+
+
+def set_sddmm_variant(alternate):
+    """Study knob: run the sliced g-SDDMM dot at its alternative depth of
+    slots in flight (1) or the default (0)."""
+    check_call(LIB.dglhip_set_sddmm_variant(1 if alternate else 0))
 
 
 def timing_enable(flag=True):
@@ -728,20 +802,23 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
 # ---------------------------------------------------------------------------
 class _EdgeAttention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, adj, num_edges, alpha, lo, hi, apply_exp, a_src, a_dst):
+    def forward(ctx, adj, num_edges, alpha, lo, hi, apply_exp, a_src, a_dst, slot=False):
         # lhs is gathered by column, rhs read per row: over the transpose the
-        # roles swap (a_dst[v] + a_src[u] == a_src[u] + a_dst[v] exactly)
-        csr, tr = _eid_major(adj)
+        # roles swap (a_dst[v] + a_src[u] == a_src[u] + a_dst[v] exactly).
+        # slot: the forward CSR, out[k] per slot (no eid, sequential stores)
+        csr, tr = (adj.fwd, False) if slot else _eid_major(adj)
         H = a_src.shape[1]
         lhs, rhs = (a_dst, a_src) if tr else (a_src, a_dst)
         out = torch.empty(num_edges, H, dtype=torch.float32, device=a_src.device)
-        args = (csr.num_rows, H, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid), ptr(lhs),
-                ptr(rhs), float(alpha), float(lo), float(hi), 1 if apply_exp else 0, ptr(out))
+        args = (csr.num_rows, H, ptr(csr.indptr), ptr(csr.indices),
+                ptr(None if slot else csr.eid), ptr(lhs), ptr(rhs), float(alpha), float(lo),
+                float(hi), 1 if apply_exp else 0, ptr(out))
         if a_src.is_cuda:
             check_call(LIB.dglhip_gsddmm_attention_device(*(args + (_stream_of(a_src.device),))))
         else:
             check_call(LIB.dglhip_gsddmm_attention_host(*(args + (0,))))
         ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp = adj, alpha, lo, hi, apply_exp
+        ctx.slot = slot
         ctx.save_for_backward(out)
         return out
 
@@ -761,19 +838,24 @@ class _EdgeAttention(torch.autograd.Function):
         adj = ctx.adj
         # sum the per-edge gradient at the source (transposed CSR) and destination
         H = g.shape[1]
-        d_src, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False)
-        d_dst, _ = _run_gspmm(adj.fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False)
-        return None, None, None, None, None, None, d_src, d_dst
+        d_src, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
+                              emap=_fwd_slot_of_bwd(adj) if ctx.slot else None)
+        d_dst, _ = _run_gspmm(adj.fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
+                              emap=SLOT if ctx.slot else None)
+        return None, None, None, None, None, None, d_src, d_dst, None
 
 
 def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
-                   apply_exp=True):
+                   apply_exp=True, edge_order="eid"):
     """Per-edge, per-head GAT attention in one kernel:
     clamp(exp(leaky_relu(a_src[u] + a_dst[v], alpha))) for every edge u -> v,
-    returned as (num_edges, H) indexed by edge id. Differentiable in a_src/a_dst."""
+    returned as (num_edges, H) indexed by edge id (edge_order="slot": by
+    forward CSR slot, for gspmm(..., edge_order="slot")). Differentiable in
+    a_src/a_dst."""
+    slot = edge_order_of(adj, edge_order)
     dev = a_src.device
     adj = adj.to(dev)
     H = a_src.reshape(a_src.shape[0], -1).shape[1]
     return _EdgeAttention.apply(adj, int(num_edges), float(alpha), float(clamp[0]),
                                 float(clamp[1]), bool(apply_exp),
-                                _f32c(a_src.reshape(-1, H)), _f32c(a_dst.reshape(-1, H)))
+                                _f32c(a_src.reshape(-1, H)), _f32c(a_dst.reshape(-1, H)), slot)

@@ -8,7 +8,7 @@ the later-DGL module names and arguments) on top of:
 
 * GraphConv    : update_all(copy_src, sum) -> one g-SpMM (gcn_spmv.py:45-62)
 * GATConv      : fused attention g-SDDMM + per-head u_mul_e g-SpMM + copy_edge
-                 normaliser (gat/train.py:61-96)
+                 normaliser (gat/train.py:61-96), attention kept in CSR slot order
 * SAGEConv     : update_all(copy_src, mean) -> g-SpMM mean
 * RelGraphConv : typed-edge block-diagonal g-SpMM (rgcn/layers.py:121-132)
 """
@@ -89,19 +89,17 @@ class GATConv(nn.Module):
         ft = self.fc(h).view(-1, self.num_heads, self.out_feats)
         el = (ft * self.attn_l).sum(-1)  # N x H
         er = (ft * self.attn_r).sum(-1)
-        a = kernel.edge_attention(g.sparse_adjacency(feat.device), el, er, g.number_of_edges(),
-                                  self.negative_slope, clamp=(-float("inf"), float("inf")))
+        adj = g.sparse_adjacency(feat.device)
+        # attention in the forward CSR's slot order: the two g-SpMMs then read
+        # it by slot (no per-edge eid gather) and its gradient comes back in
+        # the same layout; the arithmetic per element is unchanged
+        a = kernel.edge_attention(adj, el, er, g.number_of_edges(), self.negative_slope,
+                                  clamp=(-float("inf"), float("inf")), edge_order="slot")
         a = a.unsqueeze(-1)  # E x H x 1
         a_drop = self.attn_drop(a) if self.attn_drop is not None else a
-        g.ndata["_gat_ft"] = ft
-        g.edata["_gat_a"] = a
-        g.edata["_gat_ad"] = a_drop
-        g.update_all([fn.src_mul_edge("_gat_ft", "_gat_ad", "_gat_m"),
-                      fn.copy_edge("_gat_a", "_gat_z")],
-                     [fn.sum("_gat_m", "_gat_ft"), fn.sum("_gat_z", "_gat_z")])
-        rst = g.ndata.pop("_gat_ft") / g.ndata.pop("_gat_z").clamp(min=1e-20)
-        g.edata.pop("_gat_a")
-        g.edata.pop("_gat_ad")
+        ft_sum = kernel.gspmm(adj, "u_mul_e", "sum", ft, a_drop, edge_order="slot")
+        z = kernel.gspmm(adj, "copy_e", "sum", None, a, edge_order="slot")
+        rst = ft_sum / z.clamp(min=1e-20)
         if self.res_fc is not None:
             rst = rst + self.res_fc(h).view(-1, self.num_heads, self.out_feats)
         return self.activation(rst) if self.activation else rst

@@ -208,6 +208,8 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
 /* edge attention (gat/train.py:74-96).                                      */
 /*   DOT : out[eid[k], h] = sum_{d<D} lhs[r, hD+d] * rhs[indices[k], hD+d]   */
 /*         (r = row of slot k, H = num_heads, D = feat_len / H)              */
+/* eid may be NULL: out is then indexed by slot k (edge values laid out in   */
+/* this CSR's slot order, as the g-SpMM reads them with a NULL eid).         */
 /* ------------------------------------------------------------------------ */
 #define DGLHIP_SDDMM_DOT 0
 int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
@@ -221,10 +223,15 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
                        const float* lhs, const float* rhs, float* out,
                        int num_threads);
 
+/* Study knob: 1 = the sliced g-SDDMM dot runs at its alternative depth of
+ * slots in flight (16 <-> 32, or 8 -> 16 for F >= 256), 0 = the default. */
+int dglhip_set_sddmm_variant(int alternate);
+
 /* GAT edge attention (gat/train.py:90-96), fused u_add_v SDDMM + activation:
  *   out[eid[k], h] = clamp(act(lhs[indices[k], h] + rhs[r, h]), lo, hi),
  *   act(x) = exp(leaky_relu(x, alpha)) if apply_exp else leaky_relu(x, alpha)
- * lhs: [num_src, H], rhs: [num_rows, H], out: [num_edges, H]. */
+ * lhs: [num_src, H], rhs: [num_rows, H], out: [num_edges, H]; a NULL eid
+ * indexes out by slot k (CSR slot order). */
 int dglhip_gsddmm_attention_device(int64_t num_rows, int64_t num_heads,
                                    const int64_t* indptr, const int32_t* indices,
                                    const int64_t* eid, const float* lhs,

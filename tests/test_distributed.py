@@ -17,6 +17,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _assert_chain_close(got, ref, scale):
+    """A reassociated fp32 chain (segments, chunks, reduce-scatter) against
+    the oracle's: within 1e-5 of the row's condition scale sum_k |x_k| (the
+    summation error bound's yardstick), elementwise."""
+    err = np.abs(np.asarray(got, dtype=np.float64) - ref)
+    assert np.all(err <= 1e-5 * scale + 1e-6), float((err - 1e-5 * scale).max())
+
+
 def _banded(n, width, seed):
     """Graph with locality: every source within `width` ids of its destination."""
     gen = torch.Generator().manual_seed(seed)
@@ -172,12 +180,35 @@ def _pipe_worker(rank, world, port, graph="chung_lu"):
                 assert np.array_equal(out, exact)
             # deterministic
             assert np.array_equal(out, pg.update_all(H[lo:hi].contiguous()).numpy())
+            # trainable: sum and mean, forward + backward (transposed segments,
+            # chunked reverse exchange) against the oracle, deterministic
+            G = torch.randn(n, F, generator=torch.Generator().manual_seed(3))
+            deg = torch.bincount(dst, minlength=n).clamp(min=1).float().unsqueeze(1)
+            fscale = O.spmm_coo(n, dst.numpy(), src.numpy(), np.abs(H.numpy()))[lo:hi]
+            for reduce in ("sum", "mean"):
+                h = H[lo:hi].clone().requires_grad_(True)
+                o = pg.update_all(h, "copy_u", reduce)
+                dv = 1.0 if reduce == "sum" else deg[lo:hi].numpy()
+                _assert_chain_close(o.detach().numpy(), ref / dv, fscale / dv)
+                o.backward(G[lo:hi])
+                Gs = G if reduce == "sum" else G / deg
+                gref = O.spmm_coo(n, src.numpy(), dst.numpy(), Gs.numpy())[lo:hi]
+                gscale = O.spmm_coo(n, src.numpy(), dst.numpy(), np.abs(Gs.numpy()))[lo:hi]
+                _assert_chain_close(h.grad.numpy(), gref, gscale)
+                h2 = H[lo:hi].clone().requires_grad_(True)
+                pg.update_all(h2, "copy_u", reduce).backward(G[lo:hi])
+                assert torch.equal(h.grad, h2.grad)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (3, "banded")])
+@pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (2, "banded"),
+                                         (3, "banded")])
 def test_pipelined_forward(world, graph):
+    """Pipelined halo (chunked exchange overlapped with the segments) in both
+    halo modes: forward within 1e-5 (exactly the (segment, eid) chain for the
+    all-to-allv), and trainable — sum and mean, backward within 1e-5 of the
+    oracle's transposed product, deterministic."""
     mp.spawn(_pipe_worker, args=(world, _free_port(), graph), nprocs=world, join=True)
 
 
@@ -218,17 +249,18 @@ def test_single_rank_rccl_group_all_modes():
                                  ("alltoall", 2, torch.bfloat16)):
             pg = PartitionedGraph(n, src, dst, bounds, dev, halo=halo, pipeline_chunks=chunks,
                                   halo_dtype=hd)
-            h = H.to(dev).requires_grad_(chunks == 0)  # the pipelined forward is inference-only
+            h = H.to(dev).requires_grad_(True)
             out = pg.update_all(h)
             torch.cuda.synchronize()
             if chunks == 0:
                 assert np.array_equal(out.detach().cpu().numpy(), ref), (halo, chunks)
-                out.backward(G.to(dev))
-                torch.cuda.synchronize()
-                np.testing.assert_allclose(h.grad.cpu().numpy(), gref, rtol=1e-5, atol=1e-5)
             else:
                 np.testing.assert_allclose(out.detach().cpu().numpy(), ref, rtol=1e-5,
                                            atol=1e-5)
+            # the pipelined backward: reverse exchanges on the comm stream
+            out.backward(G.to(dev))
+            torch.cuda.synchronize()
+            np.testing.assert_allclose(h.grad.cpu().numpy(), gref, rtol=1e-5, atol=1e-5)
         t = torch.ones(1, device=dev)
         dist.all_reduce(t)
         dist.barrier()
@@ -264,17 +296,18 @@ def _bf16_worker(rank, world, port, halo, chunks):
         pg = PartitionedGraph(n, src[sel], dst[sel], bounds, "cpu", halo=halo,
                               pipeline_chunks=chunks, halo_dtype=torch.bfloat16)
         assert pg.halo_mode == halo
-        h = H[lo:hi].clone().requires_grad_(chunks == 0)
+        h = H[lo:hi].clone().requires_grad_(True)
         out = pg.update_all(h)
         ref = O.spmm_coo(n, dst.numpy(), src.numpy(), Heff.numpy())[lo:hi]
         if chunks == 0:
             # same chain as the fp32 exchange, on the rounded remote rows: bit-exact
             assert np.array_equal(out.detach().numpy(), ref)
-            out.backward(G[lo:hi])
-            gref = O.spmm_coo(n, src.numpy(), dst.numpy(), G.numpy())[lo:hi]
-            np.testing.assert_allclose(h.grad.numpy(), gref, rtol=2e-2, atol=2e-2)
         else:
-            np.testing.assert_allclose(out.numpy(), ref, rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(out.detach().numpy(), ref, rtol=1e-5, atol=1e-5)
+        # gradients travel in fp32 in every mode: the fp32 transposed product
+        out.backward(G[lo:hi])
+        gref = O.spmm_coo(n, src.numpy(), dst.numpy(), G.numpy())[lo:hi]
+        np.testing.assert_allclose(h.grad.numpy(), gref, rtol=1e-5, atol=1e-5)
         # and the halving costs bf16 accuracy only: within 1 % of the fp32 product
         full = O.spmm_coo(n, dst.numpy(), src.numpy(), H.numpy())[lo:hi]
         np.testing.assert_allclose(out.detach().numpy(), full, rtol=2e-2, atol=2e-2)

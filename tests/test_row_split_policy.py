@@ -1,0 +1,51 @@
+"""The heavy-row policy (dgl.kernel._split_threshold): which graphs the
+default "auto" policy cuts into chunked rows. Host logic only: the chunked
+kernels themselves are tested in test_gpu_kernels.py / test_accumulate.py /
+test_rmat26.py."""
+import pytest
+
+from dgl import kernel
+
+
+class _FakeCSR(object):
+    def __init__(self, nnz, max_degree):
+        self.nnz, self.max_degree = nnz, max_degree
+
+
+@pytest.fixture
+def policy():
+    old = kernel.set_row_split("auto")
+    yield kernel.set_row_split
+    kernel.set_row_split(old)
+
+
+def test_default_is_auto():
+    assert kernel._ROW_SPLIT in ("auto",) or "DGLHIP_ROW_SPLIT" in __import__("os").environ
+
+
+@pytest.mark.parametrize("nnz,max_degree,expect", [
+    # Reddit-shaped bench graph: the longest row is 1.35x a wave's share and
+    # under the floor: one exact chain per row
+    (114_848_857, 21_657, 0),
+    # RMAT-26: max in-degree ~ E * 0.76^26 = 855k, 2.9x the share: chunks of
+    # nnz / 12000 slots
+    (1_073_741_824, 855_000, 1_073_741_824 // 12000),
+    # RMAT-22 (max 160,139 measured, 8.6x the share): chunks of 5592 slots
+    (67_108_864, 160_139, 67_108_864 // 12000),
+    # small skewed test graphs: never split by default (bit-exact)
+    (40_000, 9_000, 0),
+    (2_000_000, 65_536, 0),
+    (2_000_000, 65_537, 4096),
+    # a hub row that is long but not the critical path of a huge launch
+    (4_000_000_000, 1_000_000, 0),
+])
+def test_auto_gate(policy, nnz, max_degree, expect):
+    assert kernel._split_threshold(_FakeCSR(nnz, max_degree)) == expect
+
+
+def test_off_and_explicit(policy):
+    policy("off")
+    assert kernel._split_threshold(_FakeCSR(1 << 30, 1 << 20)) == 0
+    policy(1000)
+    assert kernel._split_threshold(_FakeCSR(50_000, 1001)) == 1000
+    assert kernel._split_threshold(_FakeCSR(50_000, 1000)) == 0

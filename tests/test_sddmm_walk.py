@@ -94,3 +94,24 @@ def test_u_mul_e_weight_grad_walk_bits(device):
     kernel.gspmm(adj, "u_mul_e", "sum", H, W).backward(G)
     ref = kernel._run_sddmm_dot(adj.fwd, G, H, m, 1).reshape(-1)
     assert torch.equal(W.grad.reshape(-1), ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H", [1, 2, 4, 8, 16])
+def test_edge_attention_vector_kernel_bits(H):
+    """The per-slot vector kernel (H in 1, 2, 4, 8, 16; aligned rows) gives the
+    bits of the generic (slot, head)-lane kernel, which runs when the rows are
+    not vector-aligned: same inputs at an odd float offset."""
+    dev = _dev("cuda")
+    n, m = 400, 30000
+    src, dst = _graph(H, n, m, "dst")
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    rng = np.random.default_rng(H)
+    a1 = torch.from_numpy(rng.standard_normal((n, H)).astype(np.float32)).to(dev)
+    a2 = torch.from_numpy(rng.standard_normal((n, H)).astype(np.float32)).to(dev)
+    vec = kernel.edge_attention(adj, a1, a2, m)
+    buf = torch.empty(n * H + 1, device=dev)
+    a1_odd = buf[1:].view(n, H)
+    a1_odd.copy_(a1)
+    gen = kernel.edge_attention(adj, a1_odd, a2, m)
+    assert torch.equal(vec, gen)

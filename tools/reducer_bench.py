@@ -33,39 +33,69 @@ def main():
     F = args.feat
     h = torch.rand(n, F, device=dev) * 2 - 1
     w = torch.rand(E, device=dev)
-    cases = [("copy_u", "sum", None), ("copy_u", "mean", None), ("copy_u", "max", None),
-             ("u_mul_e", "sum", w), ("u_mul_e", "max", w)]
+    cases = [("copy_u", "sum", None, "eid"), ("copy_u", "mean", None, "eid"),
+             ("copy_u", "max", None, "eid"), ("u_mul_e", "sum", w, "eid"),
+             ("u_mul_e", "max", w, "eid"),
+             # the weights laid out in forward-CSR slot order (GATConv's
+             # attention): no per-slot eid gather
+             ("u_mul_e", "sum", w, "slot")]
     res = []
-    for msg, red, e in cases:
-        kernel.gspmm(adj, msg, red, h, e)
+    for msg, red, e, order in cases:
+        kernel.gspmm(adj, msg, red, h, e, edge_order=order)
         torch.cuda.synchronize()
         kernel.timing_enable(True)
         for _ in range(args.iters):
-            kernel.gspmm(adj, msg, red, h, e)
+            kernel.gspmm(adj, msg, red, h, e, edge_order=order)
         ms, cnt = kernel.timing_read()
         kernel.timing_enable(False)
         t = ms / max(cnt, 1)
-        per_edge = 4 * F + 4 + (12 if e is not None else 0)
+        per_edge = 4 * F + 4 + ((12 if order == "eid" else 4) if e is not None else 0)
         per_row = 4 * F + 8
         byts = E * per_edge + n * per_row
-        res.append({"msg": msg, "reduce": red, "kernel_ms": round(t, 3),
+        res.append({"msg": msg, "reduce": red, "edge_order": order, "kernel_ms": round(t, 3),
                     "edges_per_s": E / (t * 1e-3),
                     "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
                     "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
     # g-SDDMM dot (u_mul_e weight gradient; GAT per-head dots): per slot one
     # lhs row (the destination's, reused along the row) and one gathered rhs row
-    for heads in (1, 8):
-        kernel.gsddmm_dot(adj, h, h, E, heads)
+    for heads in (1, 2, 4, 8, 16, 32):
+        for alt in (0, 1):
+            for order in ("eid", "slot"):
+                if order == "slot" and alt:
+                    continue
+                kernel.set_sddmm_variant(alt)
+                kernel.gsddmm_dot(adj, h, h, E, heads, edge_order=order)
+                torch.cuda.synchronize()
+                kernel.timing_enable(True)
+                for _ in range(args.iters):
+                    kernel.gsddmm_dot(adj, h, h, E, heads, edge_order=order)
+                ms, cnt = kernel.timing_read()
+                kernel.timing_enable(False)
+                kernel.set_sddmm_variant(0)
+                t = ms / max(cnt, 1)
+                byts = E * (4 * F + 4 + (8 if order == "eid" else 0) + 4 * heads) + \
+                    n * (4 * F + 8)
+                res.append({"msg": "sddmm_dot", "reduce": "heads=%d" % heads,
+                            "variant": "alternate depth" if alt else "default",
+                            "edge_order": order, "kernel_ms": round(t, 3),
+                            "edges_per_s": E / (t * 1e-3),
+                            "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
+                            "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
+    # GAT edge attention (fused u_add_v -> leaky_relu -> exp), 8 heads
+    a1 = torch.rand(n, 8, device=dev)
+    a2 = torch.rand(n, 8, device=dev)
+    for order in ("eid", "slot"):
+        kernel.edge_attention(adj, a1, a2, E, edge_order=order)
         torch.cuda.synchronize()
         kernel.timing_enable(True)
         for _ in range(args.iters):
-            kernel.gsddmm_dot(adj, h, h, E, heads)
+            kernel.edge_attention(adj, a1, a2, E, edge_order=order)
         ms, cnt = kernel.timing_read()
         kernel.timing_enable(False)
         t = ms / max(cnt, 1)
-        byts = E * (4 * F + 4 + 8 + 4 * heads) + n * (4 * F + 8)
-        res.append({"msg": "sddmm_dot", "reduce": "heads=%d" % heads, "kernel_ms": round(t, 3),
-                    "edges_per_s": E / (t * 1e-3),
+        byts = E * (4 + 32 + 32 + (8 if order == "eid" else 0)) + n * (32 + 8)
+        res.append({"msg": "edge_attention", "reduce": "heads=8", "edge_order": order,
+                    "kernel_ms": round(t, 3), "edges_per_s": E / (t * 1e-3),
                     "algorithmic_GBs": round(byts / (t * 1e-3) / 1e9, 1),
                     "frac": round(byts / (t * 1e-3) / 1e9 / PEAK_GBS, 3)})
     print(json.dumps({"graph": "reddit_like", "nodes": n, "edges": E, "feat": F,
