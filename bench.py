@@ -318,6 +318,8 @@ def main():
                          "exchange; rows then carry bf16 rounding of remote inputs)")
     ap.add_argument("--no-bf16-leg", action="store_true",
                     help="N>1: skip the secondary timing of the same step with the bf16 halo")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the secondary timing of a training step (forward + backward)")
     ap.add_argument("--no-rmat-leg", action="store_true",
                     help="skip the secondary RMAT strong-scaling block (rmat26)")
     ap.add_argument("--dist-rehearsal", action="store_true",
@@ -335,7 +337,7 @@ def main():
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
         t0 = time.time()  # before this process initialises the GPU
         pmc = pmc_traffic(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
-                           "--no-rmat-leg"])
+                           "--no-rmat-leg", "--no-train-leg"])
         if not args.no_rmat_leg and args.emulate_world <= 1:
             # the rmat leg's kernels: every g-SpMM kernel of a call, per call
             rmat_pmc = pmc_traffic(["--workload", "rmat", "--rmat-scale", str(args.rmat_scale),
@@ -539,6 +541,36 @@ def main():
             "note": "same partition and step with halo_dtype=bf16: remote rows travel and "
                     "are read as bf16, summed in fp32; own rows exact. Opt-in, not the "
                     "headline (results carry bf16 rounding of remote inputs)"}
+    if args.workload == "reddit" and args.emulate_world <= 1 and not args.no_train_leg:
+        # training step of the same layer: forward + backward (the transposed
+        # g-SpMM; at N > 1 the pipelined halo's reverse exchange overlapped with
+        # the transposed segments), inputs requiring grad, a fixed upstream grad
+        if dist.is_initialized():
+            h_tr = h_local.detach().clone().requires_grad_(True)
+            d_out = torch.rand(pg.num_local, FEAT, generator=gen, device=dev) * 2 - 1
+
+            def train_step():
+                pg.update_all(h_tr).backward(d_out)
+        else:
+            h_tr = h.detach().clone().requires_grad_(True)
+            d_out = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+
+            def train_step():
+                g.ndata["h"] = h_tr
+                g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
+                g.ndata["h_out"].backward(d_out)
+        el_tr, k_tr = timed_steps(train_step, args.steps, args.warmup, world, dev)
+        if not dist.is_initialized():
+            g.ndata["h"] = h
+        result["train_step"] = {
+            "value": num_edges_total * args.steps / el_tr, "unit": "edges/s (fwd+bwd)",
+            "ms_per_step": el_tr / args.steps * 1e3, "kernel_ms_rank0": k_tr,
+            "note": "update_all(copy_src, sum) forward + backward (dH = A^T dC through the "
+                    "transposed CSR%s) per step, same graph and partition"
+                    % ("; halo exchange and its reverse pipelined in %d chunks"
+                       % args.pipeline_chunks if dist.is_initialized() and
+                       args.pipeline_chunks > 0 else "")}
+        del h_tr, d_out
     if rank == 0 and not dist.is_initialized() and not args.no_cpu_baseline:
         t2 = time.time()
         gsrc, gdst = g._graph.src(), g._graph.dst()

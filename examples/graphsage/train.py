@@ -7,8 +7,11 @@ dgl.distributed:
 
 * single device: ``g.update_all(fn.copy_src('h','m'), fn.mean('m','neigh'))``;
 * ``--dist``: one process per GPU (torchrun), dst rows 1-D partitioned;
-  each layer all-gathers the feature halo over RCCL and runs the local g-SpMM
-  (bit-identical rows); dense-layer gradients are all-reduced by DDP.
+  each layer exchanges the feature halo over RCCL (all-gather or
+  all-to-allv, dgl.distributed) in ``--pipeline-chunks`` chunks overlapped
+  with the local g-SpMM segments, forward and backward (the reverse exchange
+  of each chunk's gradient rows runs while the next chunk's transposed
+  product does); dense-layer gradients are all-reduced by DDP.
 
 Layer: h' = act(fc_self(h) + fc_neigh(mean_{u->v} h_u)). fc_neigh has no bias,
 so it commutes with the mean: when it narrows the features (602 -> 128 on
@@ -109,7 +112,8 @@ def run(args):
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
         lo, hi = int(bounds[rank]), int(bounds[rank + 1])
         sel = (dst >= lo) & (dst < hi)
-        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, device)
+        pg = PartitionedGraph(n, src[sel], dst[sel], bounds, device,
+                              pipeline_chunks=args.pipeline_chunks)
         feats, labels, train = feats[lo:hi], labels[lo:hi], train[lo:hi]
 
         def aggregate(h):
@@ -175,6 +179,10 @@ def parser():
     p.add_argument("--gpu", type=int, default=0)
     p.add_argument("--dist", action="store_true")
     p.add_argument("--dist-backend", default=None)
+    p.add_argument("--pipeline-chunks", type=int, default=4,
+                   help="--dist: halo exchange cut into this many chunks, overlapped with "
+                        "the local g-SpMM segments in the forward and backward (0: one "
+                        "exchange, then the kernel; bit-identical rows)")
     p.add_argument("--n-hidden", type=int, default=128)
     p.add_argument("--n-layers", type=int, default=1)
     p.add_argument("--dropout", type=float, default=0.0)

@@ -23,6 +23,15 @@ for s in $STEPS; do
           --gpu 0 --n-epochs ${EPOCHS:-5} --row-split $rs > gpurun_out/sage_rmat_$rs.log 2>&1
         rc=$?; tail -2 gpurun_out/sage_rmat_$rs.log; [ $rc -eq 0 ] || exit $rc
       done ;;
+    sagedist)
+      # GraphSAGE-mean --dist on a world-1 RCCL group (pipelined halo fwd + bwd), RMAT-$RMAT_SCALE
+      for pc in ${PIPE_CHUNKS:-0 4}; do
+        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+          --master-addr 127.0.0.1 --master-port 29613 examples/graphsage/train.py --dist \
+          --graph rmat --rmat-scale ${RMAT_SCALE:-24} --gpu 0 --n-epochs ${EPOCHS:-5} \
+          --pipeline-chunks $pc > gpurun_out/sagedist_$pc.log 2>&1
+        rc=$?; tail -2 gpurun_out/sagedist_$pc.log; [ $rc -eq 0 ] || exit $rc
+      done ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
@@ -33,7 +42,7 @@ for s in $STEPS; do
       # the bench line and the kernel statistics of the SAME process (headline leg only)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-cpu-baseline \
+        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-train-leg --no-cpu-baseline \
         > gpurun_out/prof.json 2> gpurun_out/prof.log
       rc=$?; tail -1 gpurun_out/prof.log; cat gpurun_out/prof.json; [ $rc -eq 0 ] || exit $rc ;;
     dist)
@@ -96,7 +105,7 @@ for s in $STEPS; do
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
-          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-rmat-leg > gpurun_out/pmc_$c.log 2>&1
+          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-rmat-leg --no-train-leg > gpurun_out/pmc_$c.log 2>&1
         rc=$?; tail -2 gpurun_out/pmc_$c.log; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac
