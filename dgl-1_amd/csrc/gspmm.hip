@@ -357,6 +357,35 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   API_END();
 }
 
+int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
+                                int64_t feat_len, int64_t ufeat_ld, const int64_t* indptr,
+                                const int32_t* indices, const int64_t* eid,
+                                const float* ufeat, const float* efeat, int64_t efeat_len,
+                                float* out, const int32_t* row_order, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(msg_op == DGLHIP_MSG_COPY_U || msg_op == DGLHIP_MSG_U_MUL_E,
+               "strided source rows: copy_u or u_mul_e, got msg op " << msg_op);
+  DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
+                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+               "strided source rows: sum / mean reducers only");
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(ufeat_ld >= feat_len, "ufeat_ld " << ufeat_ld << " < feat_len " << feat_len);
+  if (num_rows == 0 || feat_len == 0) return 0;
+  DGLHIP_CHECK(indptr && out && ufeat, "null indptr/out/ufeat");
+  const bool use_e = msg_op == DGLHIP_MSG_U_MUL_E;
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
+  // a lane's vector of VEC features must not straddle padded rows: even strides only
+  DGLHIP_CHECK(ufeat_ld == feat_len || ufeat_ld % 2 == 0, "odd padded stride " << ufeat_ld);
+  SumLaunch a{num_rows, feat_len, use_e ? efeat_len : 1, indptr, indices, eid, ufeat, efeat, out,
+              row_order, nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+              stream_output(num_rows, feat_len), ufeat_ld};
+  dispatch_sum(msg_op, reduce_op == DGLHIP_REDUCE_MEAN, a, stream);
+  API_END();
+}
+
 int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 const int64_t* indptr, const int32_t* indices,
                                 const int64_t* eid, const float* ufeat,

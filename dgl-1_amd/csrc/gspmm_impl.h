@@ -149,11 +149,12 @@ struct SlotLoad {
   V u;
   V e;
   __device__ __forceinline__ void load(const float* __restrict__ ufeat,
-                                       const float* __restrict__ efeat,
+                                       const float* __restrict__ efeat, int64_t ldu,
                                        int64_t F, int64_t f0, int64_t elen, int64_t eoff,
                                        int32_t src, int64_t edge) {
-    if (MSG == DGLHIP_MSG_COPY_U_BF16) u = gather_bf16<VEC>(ufeat, src, F, f0);
-    else if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, F, f0);
+    // ldu: row stride of ufeat in elements (F, or a padded width)
+    if (MSG == DGLHIP_MSG_COPY_U_BF16) u = gather_bf16<VEC>(ufeat, src, ldu, f0);
+    else if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, ldu, f0);
     if (!copies_u(MSG)) {
       if (EM == EM_FULL) e = ldv<VEC>(efeat + edge * F + f0);
       else e = Vec<VEC>::splat(efeat[edge * elen + eoff]);
@@ -165,8 +166,8 @@ struct SlotLoad {
 // f0: the fma chain the reference's product runs (see the file header).
 template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID, int POL = POL_DEFAULT>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
-    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0, int64_t elen,
-    int64_t eoff, const int32_t* __restrict__ indices,
+    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t ldu, int64_t F, int64_t f0,
+    int64_t elen, int64_t eoff, const int32_t* __restrict__ indices,
     const int64_t* __restrict__ eid, const float* __restrict__ ufeat,
     const float* __restrict__ efeat) {
   int64_t k = beg;
@@ -174,7 +175,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     SlotLoad<VEC, MSG, EM, POL> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
-      s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
+      s[j].load(ufeat, efeat, ldu, F, f0, elen, eoff, indices[k + j],
                 copies_u(MSG) ? 0 : (USE_EID ? eid[k + j] : k + j));
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
@@ -192,7 +193,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 #pragma unroll
     for (int j = 0; j < UNROLL - 1; ++j)
       if (j < rem)
-        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j],
+        s[j].load(ufeat, efeat, ldu, F, f0, elen, eoff, indices[k + j],
                   copies_u(MSG) ? 0 : (USE_EID ? eid[k + j] : k + j));
 #pragma unroll
     for (int j = 0; j < UNROLL - 1; ++j) {
@@ -212,20 +213,20 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
 // Same per-element operation order (bit-identical results).
 template <int VEC, int UNROLL>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
-    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t F, int64_t f0,
+    typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t ldu, int64_t f0,
     const int32_t* __restrict__ indices, const float* __restrict__ ufeat) {
   typedef typename Vec<VEC>::T V;
   int64_t k = beg;
   if (k + UNROLL <= end) {
     V cur[UNROLL];
 #pragma unroll
-    for (int j = 0; j < UNROLL; ++j) cur[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * F + f0);
+    for (int j = 0; j < UNROLL; ++j) cur[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * ldu + f0);
     k += UNROLL;
     for (; k + UNROLL <= end; k += UNROLL) {
       V nxt[UNROLL];
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j)
-        nxt[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * F + f0);
+        nxt[j] = ldv<VEC>(ufeat + int64_t(indices[k + j]) * ldu + f0);
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j) acc += cur[j];
 #pragma unroll
@@ -234,7 +235,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) acc += cur[j];
   }
-  for (; k < end; ++k) acc += ldv<VEC>(ufeat + int64_t(indices[k]) * F + f0);
+  for (; k < end; ++k) acc += ldv<VEC>(ufeat + int64_t(indices[k]) * ldu + f0);
   return acc;
 }
 
@@ -246,7 +247,8 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
           bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
-    int64_t num_items, int64_t F, int64_t elen, const int64_t* __restrict__ indptr,
+    int64_t num_items, int64_t F, int64_t elen, int64_t ldu,
+    const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
     float* __restrict__ out, const int32_t* __restrict__ row_order,
@@ -276,12 +278,12 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
     V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
-      acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, F, f0, indices, ufeat);
+      acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, ldu, f0, indices, ufeat);
     else if (copies_u(MSG) || eid != nullptr)  // uniform branch
-      acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL>(acc, beg, end, F, f0, elen, eoff,
+      acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL>(acc, beg, end, ldu, F, f0, elen, eoff,
                                                           indices, eid, ufeat, efeat);
     else
-      acc = reduce_range<VEC, UNROLL, MSG, EM, false>(acc, beg, end, F, f0, elen, eoff, indices,
+      acc = reduce_range<VEC, UNROLL, MSG, EM, false>(acc, beg, end, ldu, F, f0, elen, eoff, indices,
                                                       eid, ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
@@ -343,7 +345,7 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
     int64_t k = beg;
     if (k < end) {
       SlotLoad<VEC, MSG, EM> s;
-      s.load(ufeat, efeat, F, f0, elen, eoff, indices[k], edge(k));
+      s.load(ufeat, efeat, F, F, f0, elen, eoff, indices[k], edge(k));
       best = message(s);
 #pragma unroll
       for (int i = 0; i < VEC; ++i) arg[i] = k;
@@ -353,7 +355,7 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
       SlotLoad<VEC, MSG, EM> s[UNROLL];
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j)
-        s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j], edge(k + j));
+        s[j].load(ufeat, efeat, F, F, f0, elen, eoff, indices[k + j], edge(k + j));
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j) {
         const V x = message(s[j]);
@@ -370,7 +372,7 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
       SlotLoad<VEC, MSG, EM> s[UNROLL];
 #pragma unroll
       for (int j = 0; j < UNROLL - 1; ++j)
-        if (j < rem) s[j].load(ufeat, efeat, F, f0, elen, eoff, indices[k + j], edge(k + j));
+        if (j < rem) s[j].load(ufeat, efeat, F, F, f0, elen, eoff, indices[k + j], edge(k + j));
 #pragma unroll
       for (int j = 0; j < UNROLL - 1; ++j) {
         if (j < rem) {
@@ -510,6 +512,7 @@ struct SumLaunch {
   const int64_t* chunk_end;
   bool accumulate;           // continue each item's chain from the value in `out`
   bool nt_out = false;       // non-temporal output stores (see stream_output)
+  int64_t ldu = 0;           // ufeat row stride in elements (0: F)
 };
 
 // Outputs past twice the 256 MiB Infinity Cache are stored non-temporally
@@ -546,7 +549,7 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
 #define DGLHIP_POL_LAUNCH(CH, P)                                                           \
   hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P>), \
                      grid_1d(blocks), dim3(256), 0, stream, a.num_items,   \
-                     a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
+                     a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
                      a.row_order, a.chunk_beg, a.chunk_end)
     if (POL_OK && pol != POL_DEFAULT && !a.accumulate) {
       const bool ch = a.chunk_beg != nullptr;
@@ -556,22 +559,22 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
     } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
                          grid_1d(blocks), dim3(256), 0, stream,
-                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else if (!a.chunk_beg && a.accumulate && !MEAN)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, false, true>),
                          grid_1d(blocks), dim3(256), 0, stream,
-                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else if (a.chunk_beg)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false>),
                          grid_1d(blocks), dim3(256), 0, stream,
-                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
     else
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, false, PIPE>),
                          grid_1d(blocks), dim3(256), 0, stream,
-                         a.num_items, a.F, a.elen, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
+                         a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
 #undef DGLHIP_POL_LAUNCH
   });

@@ -374,6 +374,38 @@ def _edge_len(eshape, fshape):
                    % (eshape, fshape))
 
 
+# tables past one XCD's 4 MiB L2 are gathered from the Infinity Cache / HBM in
+# whole 128-B lines (Reddit-shaped graph, tools/feat_sweep.py: F = 24 takes
+# 2.26 ms at 1.5 lines per row vs 1.75 ms for F = 32 at one line; F = 41 and
+# 50 padded both read 3.52 ms, F = 64 3.57)
+_PAD_MIN_BYTES = 4 << 20
+
+
+def _lines_per_row(F, ld):
+    """Mean number of 128-B lines one gathered row of F floats touches when
+    rows sit at a stride of ``ld`` floats (row starts cycle through the
+    offsets (u * ld * 4) mod 128)."""
+    tot = 0
+    for u in range(32):
+        off = (u * ld * 4) % 128
+        tot += (off + 4 * F + 127) // 128
+    return tot / 32.0
+
+
+def padded_width(F):
+    """Row stride (floats) for the source rows of a g-SpMM gather: F itself,
+    or F rounded up to 16 / 32 floats when that cuts the 128-B lines a row
+    touches by at least 5 % (F = 41: 2.28 -> 2.0 lines at a 48-float stride;
+    F = 24: 1.5 -> 1.0 at 32). Rows of 16, 32, 64, 128 floats already fit."""
+    best, best_lines = F, _lines_per_row(F, F)
+    for ld in (-(-F // 16) * 16, -(-F // 32) * 32):
+        if ld > F and ld % 2 == 0:
+            lines = _lines_per_row(F, ld)
+            if lines < best_lines * 0.95 and lines < _lines_per_row(F, best) - 1e-9:
+                best, best_lines = ld, lines
+    return best
+
+
 def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None, emap=None):
     """ufeat2: (num_cols, F) or None; efeat2: (E, elen) or None. Returns (out, arg).
     ``out`` (optional) receives the result; RED_SUM_ACCUM adds into it.
@@ -402,6 +434,17 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
             ptr(efeat2), elen, ptr(out), p["light"].numel(), ptr(p["light"]), p["num_chunks"],
             ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
             ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
+    elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
+        # source rows straddle cache lines: gather them from a padded copy
+        # (same values, same chains: identical results, fewer lines per row)
+        ld = padded_width(feat_len)
+        up = ufeat2.new_empty(ufeat2.shape[0], ld)
+        up[:, :feat_len] = ufeat2
+        check_call(LIB.dglhip_gspmm_strided_device(
+            msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ld,
+            ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(up), ptr(efeat2), elen, ptr(out),
+            ptr(csr.row_order), _stream_of(dev)))
+        del up
     elif dev.type == "cuda":
         check_call(LIB.dglhip_gspmm_device(
             msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
@@ -412,6 +455,25 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
             msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), 0))
     return out, arg
+
+
+_PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")
+
+
+def set_pad_rows(policy):
+    """Padded-stride gathers for line-straddling rows: "auto" (default) or
+    "off"; returns the old policy."""
+    global _PAD_ROWS
+    old = _PAD_ROWS
+    _PAD_ROWS = str(policy)
+    return old
+
+
+def _pad_rows(msg, red, ufeat2, feat_len):
+    return (_PAD_ROWS == "auto" and msg in (MSG_COPY_U, MSG_U_MUL_E) and
+            red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM) and ufeat2 is not None and
+            ufeat2.dtype == torch.float32 and
+            ufeat2.numel() * 4 >= _PAD_MIN_BYTES and padded_width(feat_len) != feat_len)
 
 
 def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1, slot=False):

@@ -1,33 +1,52 @@
-"""Scheduler: lowers message-passing API calls onto g-SpMM kernels.
+"""Scheduler: lowers message-passing API calls into IR programs.
 
 Counterpart of python/dgl/runtime/scheduler.py (schedule_update_all
 :158-198, schedule_snr :111-156, schedule_pull :309-361, schedule_push
 :279-307, schedule_recv :58-109, schedule_send :26-56, schedule_apply_nodes /
 apply_edges, _gen_send_reduce :470-570, _apply_with_accum :398-426).
 
+Every public schedule_* call issues executors (runtime/ir/executor.py) into a
+fresh program and runs it (runtime/runtime.py), as the reference does.
 Lowering rules (same decisions and result layout as the reference):
   * builtin (message, reduce) pairs with kernel-compatible operands ->
-    ``SPMV``: one g-SpMM over the (cached) destination-major adjacency;
+    ``SPMV`` / ``SPMV_WITH_DATA`` (copy_edge: ``SPMV_E2V`` over the
+    adjacency): one g-SpMM over the (cached) destination-major adjacency;
   * everything else -> messages are materialised on the triggered edges
-    (EDGE_UDF), then builtin reducers run as e2v g-SpMM (copy_e over the
-    incidence CSR) and UDF reducers through degree bucketing;
+    (``EDGE_UDF``), then builtin reducers run as e2v g-SpMM (``SPMV_E2V``,
+    copy_e over the incidence CSR) and UDF reducers through degree bucketing
+    (``DEGREE_BUCKETING``);
   * reduced rows are in sorted-unique receiver order; an apply function sees
-    the node data updated with the reduced values (_apply_with_accum);
-  * update_all replaces whole columns (WRITE_DICT_), the others write rows.
+    the node data updated with the reduced values (``NODE_UDF`` over
+    ``UPDATE_DICT(READ_ROW(nf, recv), reduced)``, _apply_with_accum);
+  * update_all replaces whole columns (``WRITE_DICT_``), the others write rows
+    (``WRITE_ROW_`` / ``WRITE_ROW_INPLACE_``).
 """
 from __future__ import absolute_import
 
+import functools
+
 import torch
 
-from .. import kernel
 from ..base import DGLError
 from ..function.base import BuiltinFunction, BundledFunction
 from ..udf import EdgeBatch, LazyDict, NodeBatch
 from ..utils import is_iterable
 from . import degree_bucketing, ir, spmv
+from .ir import var
+from .runtime import Runtime
 
 __all__ = ["schedule_update_all", "schedule_snr", "schedule_pull", "schedule_push",
            "schedule_recv", "schedule_send", "schedule_apply_nodes", "schedule_apply_edges"]
+
+
+def _program(fn):
+    """A public schedule_* entry: lower the call into a new program, run it."""
+    @functools.wraps(fn)
+    def wrapper(*args, **kw):
+        with ir.prog() as p:
+            fn(*args, **kw)
+            Runtime.run(p)
+    return wrapper
 
 
 def _standardize(func, what):
@@ -45,28 +64,23 @@ def _standardize(func, what):
     return func
 
 
-def _edge_batch(g, u, v, eid):
+def _edge_vars(g, u, v, eid):
+    """(src, edge, dst) feature-dict variables of the triggered edges: lazy
+    row gathers from the frames, taken when an executor reads them."""
     nf, ef = g._node_frame, g._edge_frame
     src = LazyDict(lambda k: nf[k].index_select(0, u.to(nf[k].device)), nf.keys())
     dst = LazyDict(lambda k: nf[k].index_select(0, v.to(nf[k].device)), nf.keys())
     edata = LazyDict(lambda k: ef[k].index_select(0, eid.to(ef[k].device)), ef.keys())
-    return EdgeBatch(g, (u, v, eid), src, edata, dst)
+    return var.FEAT_DICT(src, "src"), var.FEAT_DICT(edata, "edata"), var.FEAT_DICT(dst, "dst")
 
 
-def _materialize(g, mfunc, u, v, eid):
+def _edge_udf(g, func, u, v, eid):
     """EDGE_UDF over the triggered edges (scheduler.py:572-583)."""
-    ir.record("EDGE_UDF", num_edges=len(eid))
-    if is_iterable(mfunc):
-        mfunc = BundledFunction(mfunc)
-    return mfunc(_edge_batch(g, u, v, eid))
-
-
-def _msg_operands(g, mfn):
-    """(ufeat, efeat) for a kernel message on the graph's frames."""
-    nf, ef = g._node_frame, g._edge_frame
-    ufeat = nf[mfn.src_field] if mfn.kernel_msg != "copy_e" else None
-    efeat = ef[mfn.edge_field] if mfn.kernel_msg != "copy_u" else None
-    return ufeat, efeat
+    if is_iterable(func):
+        func = BundledFunction(func)
+    fn = var.FUNC(lambda src, edata, dst: func(EdgeBatch(g, (u, v, eid), src, edata, dst)),
+                  "edge_func")
+    return ir.EDGE_UDF(fn, *_edge_vars(g, u, v, eid))
 
 
 class _Edges(object):
@@ -83,12 +97,35 @@ class _Edges(object):
         return self._val
 
 
+def _bucket_fn(g, rfunc, recv_nodes, msg_dst):
+    return var.FUNC(lambda msgs: degree_bucketing.bucket_reduce(
+        g, rfunc, recv_nodes, msg_dst, msgs, g._node_frame), "reduce_func")
+
+
+def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out):
+    """A builtin reducer over materialised messages: SPMV_E2V (copy_e over the
+    incidence matrix), or degree bucketing when the messages are not float32."""
+    def check():
+        if rfn.msg_field not in msgs.data:
+            raise DGLError('Reduce function requires message field "%s", but no message '
+                           'function generates it.' % rfn.msg_field)
+    ir.CALL_(var.FUNC(check, "check_msg"))
+    m = ir.READ_COL(msgs, var.STR(rfn.msg_field))
+    fallback = var.FUNC(lambda mt: degree_bucketing.bucket_reduce(
+        g, rfn, recv_nodes, msg_dst, {rfn.msg_field: mt}, g._node_frame)[rfn.out_field],
+        "bucket_" + rfn.name)
+    r = ir.SPMV_E2V(inc, m, var.STR(rfn.kernel_reduce), fallback)
+    ir.WRITE_COL_(out, var.STR(rfn.out_field), r)
+
+
 def _send_reduce(g, mfunc, rfunc, edges, recv_nodes, whole_graph):
-    """Returns the reduced feature dict (rows = recv_nodes)."""
+    """Issue the send + reduce; returns the FEAT_DICT variable of the reduced
+    features (rows = recv_nodes)."""
     nf, ef = g._node_frame, g._edge_frame
+    nf_var, ef_var = var.FEAT_DICT(nf, "nf"), var.FEAT_DICT(ef, "ef")
     mfunc = _standardize(mfunc, "message")
     rfunc = _standardize(rfunc, "reduce")
-    out = {}
+    out = ir.NEW_DICT()
     adj_cache = {}
 
     def adjacency(dev):
@@ -104,110 +141,113 @@ def _send_reduce(g, mfunc, rfunc, edges, recv_nodes, whole_graph):
 
     if is_iterable(mfunc) and is_iterable(rfunc):
         pairs, mfunc, rfunc = spmv.analyze_v2v(mfunc, rfunc, nf, ef)
+        spmat = var.SPMAT(adjacency, "adj")
         for mfn, rfn in pairs:
-            ufeat, efeat = _msg_operands(g, mfn)
-            dev = (ufeat if ufeat is not None else efeat).device
-            ir.record("SPMV", msg=mfn.kernel_msg, reduce=rfn.kernel_reduce,
-                      src=mfn.src_field, edge=mfn.edge_field, out=rfn.out_field)
-            out[rfn.out_field] = kernel.gspmm(adjacency(dev), mfn.kernel_msg,
-                                              rfn.kernel_reduce, ufeat, efeat)
+            red = var.STR(rfn.kernel_reduce)
+            if mfn.kernel_msg == "copy_u":
+                r = ir.SPMV(spmat, ir.READ_COL(nf_var, var.STR(mfn.src_field)), red)
+            elif mfn.kernel_msg == "u_mul_e":
+                r = ir.SPMV_WITH_DATA(spmat, ir.READ_COL(ef_var, var.STR(mfn.edge_field)),
+                                      ir.READ_COL(nf_var, var.STR(mfn.src_field)), red)
+            else:  # copy_e over the adjacency: edge values by the slots' edge ids
+                r = ir.SPMV_E2V(spmat, ir.READ_COL(ef_var, var.STR(mfn.edge_field)), red)
+            ir.WRITE_COL_(out, var.STR(rfn.out_field), r)
         if not mfunc:
             return out
     u, v, eid = edges.get()
-    msgs = _materialize(g, mfunc, u, v, eid)
+    msgs = _edge_udf(g, mfunc, u, v, eid)
     if is_iterable(rfunc):
+        if whole_graph:
+            inc = var.SPMAT(lambda dev: g._graph.incidence_in(dev), "inc")
+        else:
+            inc = var.SPMAT(lambda dev: spmv.build_inc_dst(v, recv_nodes, dev), "inc")
         for rfn in rfunc:
-            if rfn.msg_field not in msgs:
-                raise DGLError('Reduce function requires message field "%s", but no message '
-                               'function generates it.' % rfn.msg_field)
-            m = msgs[rfn.msg_field]
-            if m.dtype == torch.float32:
-                ir.record("SPMV_E2V", reduce=rfn.kernel_reduce, msg=rfn.msg_field,
-                          out=rfn.out_field)
-                if whole_graph:
-                    inc = g._graph.incidence_in(m.device)
-                else:
-                    inc = spmv.build_inc_dst(v, recv_nodes, m.device)
-                out[rfn.out_field] = kernel.gspmm(inc, "copy_e", rfn.kernel_reduce, None, m)
-            else:  # non-float32 messages: builtin reducer as a UDF
-                ir.record("DEGREE_BUCKETING", reduce=rfn.name, num_msgs=len(v))
-                out.update(degree_bucketing.bucket_reduce(g, rfn, recv_nodes, v,
-                                                          {rfn.msg_field: m}, nf))
+            _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, v, out)
         return out
-    ir.record("DEGREE_BUCKETING", reduce="udf", num_msgs=len(v))
-    out.update(degree_bucketing.bucket_reduce(g, rfunc, recv_nodes, v, msgs, nf))
-    return out
+    return ir.UPDATE_DICT(out, ir.DEGREE_BUCKETING(_bucket_fn(g, rfunc, recv_nodes, v), msgs))
 
 
 def _apply_with_accum(g, nodes, reduced, apply_func):
     """Apply function over node data updated with the reduced values."""
     if not apply_func:
         return reduced
-    ir.record("NODE_UDF", num_nodes=g.number_of_nodes() if nodes is None else len(nodes))
-    nf = g._node_frame
-    data = nf.select_rows(None if nodes is None else nodes)
-    data.update(reduced)
     ids = torch.arange(g.number_of_nodes()) if nodes is None else nodes
-    applied = apply_func(NodeBatch(g, ids, data))
-    final = dict(reduced)
-    final.update(applied)
-    return final
+    data = ir.UPDATE_DICT(ir.READ_ROW(var.FEAT_DICT(g._node_frame, "nf"), var.IDX(nodes)),
+                          reduced)
+    fn = var.FUNC(lambda nd: apply_func(NodeBatch(g, ids, nd)), "apply_func")
+    return ir.UPDATE_DICT(reduced, ir.NODE_UDF(fn, data))
 
 
+def _write_rows(g, rows, final, inplace):
+    nf_var = var.FEAT_DICT(g._node_frame, "nf")
+    if inplace:
+        ir.WRITE_ROW_INPLACE_(nf_var, var.IDX(rows), final)
+    else:
+        ir.WRITE_ROW_(nf_var, var.IDX(rows), final)
+
+
+@_program
 def schedule_update_all(g, message_func, reduce_func, apply_func):
     """update_all: send on every edge, reduce at every node."""
     if g.number_of_edges() == 0:
         if apply_func is not None:
-            schedule_apply_nodes(g, None, apply_func, inplace=False)
+            _apply_nodes(g, None, apply_func, inplace=False)
         return
     edges = _Edges(g._graph.edges)
     recv = torch.arange(g.number_of_nodes(), dtype=torch.int64)
     reduced = _send_reduce(g, message_func, reduce_func, edges, recv, True)
     final = _apply_with_accum(g, None, reduced, apply_func)
-    ir.record("WRITE_DICT_", keys=sorted(final.keys()))
-    g._node_frame.update_rows(None, final)
+    ir.WRITE_DICT_(var.FEAT_DICT(g._node_frame, "nf"), final)
 
 
-def schedule_snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace):
-    """send_and_recv on the given edges."""
+def _snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace):
     recv = torch.unique(v, sorted=True)
     reduced = _send_reduce(g, message_func, reduce_func, _Edges(lambda: (u, v, eid)), recv,
                            False)
-    final = _apply_with_accum(g, recv, reduced, apply_func)
-    ir.record("WRITE_ROW_", num_rows=len(recv), inplace=inplace)
-    g._node_frame.update_rows(recv, final, inplace)
+    _write_rows(g, recv, _apply_with_accum(g, recv, reduced, apply_func), inplace)
 
 
+@_program
+def schedule_snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace):
+    """send_and_recv on the given edges."""
+    _snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace)
+
+
+@_program
 def schedule_pull(g, pull_nodes, message_func, reduce_func, apply_func, inplace):
     """pull: receivers are ``pull_nodes`` (including ones without in-edges)."""
     u, v, eid = g._graph.in_edges(pull_nodes)
     if len(eid) == 0:
         if apply_func is not None:
-            schedule_apply_nodes(g, pull_nodes, apply_func, inplace)
+            _apply_nodes(g, pull_nodes, apply_func, inplace)
         return
     recv = torch.unique(pull_nodes, sorted=True)
     reduced = _send_reduce(g, message_func, reduce_func, _Edges(lambda: (u, v, eid)), recv,
                            False)
-    final = _apply_with_accum(g, recv, reduced, apply_func)
-    ir.record("WRITE_ROW_", num_rows=len(recv), inplace=inplace)
-    g._node_frame.update_rows(recv, final, inplace)
+    _write_rows(g, recv, _apply_with_accum(g, recv, reduced, apply_func), inplace)
 
 
+@_program
 def schedule_push(g, push_nodes, message_func, reduce_func, apply_func, inplace):
     """push: send_and_recv along the out-edges of ``push_nodes``."""
     u, v, eid = g._graph.out_edges(push_nodes)
     if len(eid) == 0:
         return
-    schedule_snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace)
+    _snr(g, u, v, eid, message_func, reduce_func, apply_func, inplace)
 
 
+@_program
 def schedule_send(g, u, v, eid, message_func):
     """send: materialise messages into the message frame (scheduler.py:26-56)."""
-    msgs = _materialize(g, _standardize(message_func, "message"), u, v, eid)
-    g._msg_frame.update_rows(eid, msgs)
-    g._msg_pending[eid] = True
+    msgs = _edge_udf(g, _standardize(message_func, "message"), u, v, eid)
+    ir.WRITE_ROW_(var.FEAT_DICT(g._msg_frame, "mf"), var.IDX(eid), msgs)
+
+    def mark():
+        g._msg_pending[eid] = True
+    ir.CALL_(var.FUNC(mark, "mark_pending"))
 
 
+@_program
 def schedule_recv(g, recv_nodes, reduce_func, apply_func, inplace):
     """recv: reduce pending messages on the in-edges of ``recv_nodes``."""
     src, dst, eid = g._graph.in_edges(recv_nodes)
@@ -216,49 +256,51 @@ def schedule_recv(g, recv_nodes, reduce_func, apply_func, inplace):
         src, dst, eid = src[keep], dst[keep], eid[keep]
     if len(eid) == 0:
         if apply_func is not None:
-            schedule_apply_nodes(g, recv_nodes, apply_func, inplace)
+            _apply_nodes(g, recv_nodes, apply_func, inplace)
         return
     recv = torch.unique(recv_nodes, sorted=True)
     rfunc = _standardize(reduce_func, "reduce")
-    msgs = g._msg_frame.select_rows(eid)
-    out = {}
+    msgs = ir.READ_ROW(var.FEAT_DICT(g._msg_frame, "mf"), var.IDX(eid))
+    out = ir.NEW_DICT()
     if is_iterable(rfunc):
+        inc = var.SPMAT(lambda dev: spmv.build_inc_dst(dst, recv, dev), "inc")
         for rfn in rfunc:
-            m = msgs[rfn.msg_field]
-            if m.dtype == torch.float32:
-                ir.record("SPMV_E2V", reduce=rfn.kernel_reduce, msg=rfn.msg_field)
-                inc = spmv.build_inc_dst(dst, recv, m.device)
-                out[rfn.out_field] = kernel.gspmm(inc, "copy_e", rfn.kernel_reduce, None, m)
-            else:
-                out.update(degree_bucketing.bucket_reduce(g, rfn, recv, dst,
-                                                          {rfn.msg_field: m}, g._node_frame))
+            _builtin_over_messages(g, rfn, msgs, inc, recv, dst, out)
     else:
-        ir.record("DEGREE_BUCKETING", reduce="udf", num_msgs=len(dst))
-        out = degree_bucketing.bucket_reduce(g, rfunc, recv, dst, msgs, g._node_frame)
-    final = _apply_with_accum(g, recv, out, apply_func)
-    g._node_frame.update_rows(recv, final, inplace)
-    g._msg_pending[eid] = False
-    if not bool(g._msg_pending.any()):
-        g._msg_frame.clear()
+        out = ir.UPDATE_DICT(out, ir.DEGREE_BUCKETING(_bucket_fn(g, rfunc, recv, dst), msgs))
+    _write_rows(g, recv, _apply_with_accum(g, recv, out, apply_func), inplace)
+
+    def consume():
+        g._msg_pending[eid] = False
+        if not bool(g._msg_pending.any()):
+            g._msg_frame.clear()
+    ir.CALL_(var.FUNC(consume, "consume_pending"))
 
 
+def _apply_nodes(g, v, apply_func, inplace):
+    ids = torch.arange(g.number_of_nodes()) if v is None else v
+    fn = var.FUNC(lambda nd: apply_func(NodeBatch(g, ids, nd)), "apply_func")
+    out = ir.NODE_UDF(fn, ir.READ_ROW(var.FEAT_DICT(g._node_frame, "nf"), var.IDX(v)))
+    _write_rows(g, v, out, inplace)
+
+
+@_program
 def schedule_apply_nodes(g, v, apply_func, inplace):
     """apply_nodes over ``v`` (None = all nodes)."""
-    nf = g._node_frame
-    ids = torch.arange(g.number_of_nodes()) if v is None else v
-    ir.record("NODE_UDF", num_nodes=len(ids))
-    out = apply_func(NodeBatch(g, ids, nf.select_rows(v)))
-    nf.update_rows(v, out, inplace)
+    _apply_nodes(g, v, apply_func, inplace)
 
 
+@_program
 def schedule_apply_edges(g, u, v, eid, apply_func, inplace):
     """apply_edges over the given edges (``eid`` None = all edges)."""
-    ef = g._edge_frame
     if eid is None:
         u, v, eid = g._graph.edges()
         rows = None
     else:
         rows = eid
-    ir.record("EDGE_UDF", num_edges=len(eid))
-    out = apply_func(_edge_batch(g, u, v, eid))
-    ef.update_rows(rows, out, inplace)
+    out = _edge_udf(g, apply_func, u, v, eid)
+    ef_var = var.FEAT_DICT(g._edge_frame, "ef")
+    if inplace:
+        ir.WRITE_ROW_INPLACE_(ef_var, var.IDX(rows), out)
+    else:
+        ir.WRITE_ROW_(ef_var, var.IDX(rows), out)

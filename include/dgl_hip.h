@@ -195,6 +195,19 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
                              const float* efeat, int64_t efeat_len, float* out,
                              int num_threads);
 
+/* Device g-SpMM whose source rows have a row stride of ufeat_ld >= feat_len
+ * elements (feature f of row u at ufeat[u * ufeat_ld + f]): rows padded so
+ * that none straddles more cache lines than its width needs (F = 41: 164-B
+ * rows padded to 192 B touch 2 lines instead of 2.3 on average). Messages
+ * copy_u / u_mul_e, reducers sum / mean / sum_accum; the per-element chains
+ * are those of dglhip_gspmm_device (identical results). ufeat_ld must equal
+ * feat_len or be even. */
+int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
+                                int64_t feat_len, int64_t ufeat_ld, const int64_t* indptr,
+                                const int32_t* indices, const int64_t* eid,
+                                const float* ufeat, const float* efeat, int64_t efeat_len,
+                                float* out, const int32_t* row_order, void* stream);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,

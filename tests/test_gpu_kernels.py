@@ -314,3 +314,33 @@ def test_rows_beyond_one_grid_dimension(cuda):
     dots = kernel.gsddmm_dot(adj, H, H, n, 1)
     ref = (H * expect).sum(1, keepdim=True)
     torch.testing.assert_close(dots, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("F", [24, 41, 50])
+@pytest.mark.parametrize("case", ["copy_u-sum", "copy_u-mean", "u_mul_e-sum"])
+def test_padded_stride_gather(cuda, F, case):
+    """Source rows that straddle cache lines (F = 24, 41, 50) are gathered
+    from a padded copy (kernel.padded_width) once the table exceeds the L2s:
+    the same chains, so the result equals the in-place gather bit for bit
+    (and the oracle for sum)."""
+    msg, red = case.split("-")
+    rng = np.random.default_rng(F)
+    n = (kernel._PAD_MIN_BYTES // (4 * F)) + 1000
+    row, col = rand_graph(rng, n, n, 400_000, skew=True)  # hub row ~51k: one chain
+    H = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    W = rng.uniform(-1, 1, (400_000, 1)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    assert kernel._split_threshold(adj.fwd) == 0
+    Hd = torch.from_numpy(H).to(cuda)
+    Wd = torch.from_numpy(W).to(cuda) if msg == "u_mul_e" else None
+    assert kernel.padded_width(F) > F
+    assert kernel._pad_rows(kernel._MSG_NAMES[msg], kernel._RED_NAMES[red], Hd, F)
+    padded = kernel.gspmm(adj, msg, red, Hd, Wd)
+    old = kernel.set_pad_rows("off")
+    try:
+        plain = kernel.gspmm(adj, msg, red, Hd, Wd)
+    finally:
+        kernel.set_pad_rows(old)
+    assert torch.equal(padded, plain)
+    if case == "copy_u-sum":
+        assert np.array_equal(padded.cpu().numpy(), O.spmm_coo(n, row, col, H))

@@ -335,7 +335,7 @@ def test_gat_head_broadcast(device):
             else:
                 g.update_all(lambda e: {"m": e.src["ft"] * e.data["a"]},
                              lambda nd: {"o": nd.mailbox["m"].sum(1)})
-        assert ("SPMV" in p.opcodes()) == fused
+        assert ("SPMV_WITH_DATA" in p.opcodes()) == fused
         g.ndata["o"].backward(G)
         outs.append((g.ndata["o"].detach().cpu(), f1.grad.cpu(), a1.grad.cpu()))
     for x, y in zip(outs[0], outs[1]):

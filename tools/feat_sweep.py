@@ -52,7 +52,7 @@ def mean_lines(F):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--feats", default="16,32,41,64,100,128,256,602")
+    ap.add_argument("--feats", default="16,24,32,41,50,64,100,128,256,602")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=5)
     args = ap.parse_args()
@@ -80,6 +80,28 @@ def main():
                 kernel.timing_enable(False)
                 times[v].append(ms / args.iters)
         _ffi.check_call(_ffi.LIB.dglhip_set_spmm_variant(0, 0, 0, 0))
+        # padded-stride gathers (kernel.padded_width): the automatic choice with
+        # the source rows gathered from a padded copy vs in place; kernel time
+        # from the hooks, call time (copy included) from events around the call
+        pad = {}
+        for _ in range(args.rounds):
+            for pol in ("auto", "off"):
+                old = kernel.set_pad_rows(pol)
+                o = kernel.gspmm(adj, "copy_u", "sum", h)
+                assert torch.equal(o, ref), (F, pol)
+                torch.cuda.synchronize()
+                kernel.timing_enable(True)
+                t0 = torch.cuda.Event(enable_timing=True)
+                t1 = torch.cuda.Event(enable_timing=True)
+                t0.record()
+                for _ in range(args.iters):
+                    kernel.gspmm(adj, "copy_u", "sum", h)
+                t1.record()
+                torch.cuda.synchronize()
+                ms, _ = kernel.timing_read()
+                kernel.timing_enable(False)
+                kernel.set_pad_rows(old)
+                pad.setdefault(pol, []).append((ms / args.iters, t0.elapsed_time(t1) / args.iters))
         alg = E * (4 * F + 4) + n * (4 * F + 8)
         lines = E * (128 * mean_lines(F) + 4) + n * (4 * F + 8)
         row = {"feat": F, "algorithmic_GB": round(alg / 1e9, 2),
@@ -91,6 +113,15 @@ def main():
                 "alg_GBs": round(alg / (med * 1e-3) / 1e9, 1),
                 "frac": round(alg / (med * 1e-3) / 1e9 / PEAK_GBS, 3),
                 "line_GBs": round(lines / (med * 1e-3) / 1e9, 1)}
+        ld = kernel.padded_width(F)
+        for pol, t in pad.items():
+            t.sort()
+            km, cm = t[len(t) // 2]
+            row["padded" if pol == "auto" else "unpadded"] = {
+                "stride": ld if pol == "auto" else F, "kernel_ms": round(km, 3),
+                "call_ms": round(cm, 3), "lines_per_row": round(
+                    kernel._lines_per_row(F, ld if pol == "auto" else F), 3),
+                "alg_GBs": round(alg / (km * 1e-3) / 1e9, 1)}
         out.append(row)
         print("F=%d" % F, {k: x["ms"] for k, x in row["variants"].items()},
               file=sys.stderr, flush=True)
