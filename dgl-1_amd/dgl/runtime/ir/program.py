@@ -13,6 +13,8 @@ from __future__ import absolute_import
 import threading
 from contextlib import contextmanager
 
+from .registry import op_name
+
 __all__ = ["Prog", "get_current_prog", "set_current_prog", "prog"]
 
 
@@ -33,11 +35,9 @@ class Prog(object):
 
     def opcodes(self):
         """Names of the executors that ran (or were issued, before a run)."""
-        from .registry import op_name
         return [op_name(e.opcode()) for e in (self.trace or self.execs)]
 
     def pprint_exe(self, exe):
-        from .registry import op_name
         args = ", ".join(str(a) for a in exe.arg_vars() if a is not None)
         ret = exe.ret_var()
         if ret is None:

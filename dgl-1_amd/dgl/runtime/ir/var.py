@@ -6,6 +6,8 @@ tensor or feature dict that an executor fills in when the program runs.
 """
 from __future__ import absolute_import
 
+from .program import get_current_prog
+
 __all__ = ["VarType", "Var", "new", "FEAT", "FEAT_DICT", "SPMAT", "IDX", "STR", "FUNC"]
 
 
@@ -42,7 +44,6 @@ class Var(object):
 def new(typecode, data=None, name=None):
     """A fresh variable; unnamed ones are numbered per program (_z0, _z1, ...)."""
     if name is None:
-        from .program import get_current_prog
         p = get_current_prog()
         if p is None:
             name = "_z"
