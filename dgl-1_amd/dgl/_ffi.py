@@ -85,6 +85,8 @@ def _load():
         "dglhip_set_spmm_variant": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
         "dglhip_set_cache_policy": (_c_int, [_c_int]),
         "dglhip_set_sddmm_variant": (_c_int, [_c_int]),
+        "dglhip_gspmm_short_rows_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                                                    _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_gspmm_strided_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp,
                                                  _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp]),
         "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),

@@ -202,6 +202,42 @@ class CSR(object):
         self._plans[key] = plan
         return plan
 
+    def tiers(self, rows, key):
+        """Row-length tiers of a degree-descending row list ``rows`` (device
+        int32, cached under ``key``): (n_long, [(max_deg, items), ...]). Rows
+        [0, n_long) have more than 8 slots; each tier lists rows of at most
+        max_deg (8, 4, 0) slots as a compacted CSR of their own for
+        dglhip_gspmm_short_rows_device: ``items`` = (rows, slot_ptr, slot_cols)
+        device tensors (slot_ptr / slot_cols None for the empty tier)."""
+        ck = ("tiers", key)
+        if ck in self._plans:
+            return self._plans[ck]
+        ip = self.host_indptr.numpy()
+        rows_h = rows.cpu().numpy().astype(np.int64)
+        deg = (ip[1:] - ip[:-1])[rows_h]
+        neg = -deg  # ascending
+        cut = [int(np.searchsorted(neg, -t, side="left")) for t in (8, 4, 0)]
+        n = len(deg)
+        tiers = []
+        for maxd, lo, hi in ((8, cut[0], cut[1]), (4, cut[1], cut[2]), (0, cut[2], n)):
+            if hi <= lo:
+                continue
+            r = rows[lo:hi].contiguous()
+            if maxd == 0:
+                tiers.append((maxd, (r, None, None), hi - lo))
+                continue
+            d = torch.from_numpy(deg[lo:hi]).to(self.device)
+            sp = torch.zeros(hi - lo + 1, dtype=torch.int64, device=self.device)
+            torch.cumsum(d, 0, out=sp[1:])
+            total = int(deg[lo:hi].sum())
+            start = self.indptr.index_select(0, r.long())
+            pos = torch.repeat_interleave(start - sp[:-1], d, output_size=total) + \
+                torch.arange(total, device=self.device)
+            tiers.append((maxd, (r, sp, self.indices.index_select(0, pos)), hi - lo))
+        res = (cut[0], tiers)
+        self._plans[ck] = res
+        return res
+
     @property
     def nnz(self):
         return self.indices.numel()
@@ -426,14 +462,35 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         eid = csr.slot_eid if emap is None else emap
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
+    tiered = (dev.type == "cuda" and _TIERED and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and
+              red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM) and
+              not _pad_rows(msg, red, ufeat2, feat_len))
     if split:
         p = csr.split_plan(split, skip_empty=skip)
         partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
+        light = p["light"]
+        n_light, tail = light.numel(), []
+        if tiered:
+            n_long, tail = csr.tiers(light, ("split", split, skip))
+            if sum(t[2] for t in tail) >= _TIER_MIN_ROWS:
+                n_light = n_long
+            else:
+                tail = []
         check_call(LIB.dglhip_gspmm_chunked_device(
             msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(ufeat2),
-            ptr(efeat2), elen, ptr(out), p["light"].numel(), ptr(p["light"]), p["num_chunks"],
+            ptr(efeat2), elen, ptr(out), n_light, ptr(light), p["num_chunks"],
             ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
             ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
+        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail)
+    elif tiered and csr.row_order is not None and \
+            _tail_rows(csr, csr.num_nonempty if skip else csr.num_rows, skip):
+        nrows = csr.num_nonempty if skip else csr.num_rows
+        n_long, tail = csr.tiers(csr.row_order[:nrows], ("plain", skip))
+        check_call(LIB.dglhip_gspmm_device(
+            msg, red, n_long, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
+            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
+            _stream_of(dev)))
+        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail)
     elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
         # source rows straddle cache lines: gather them from a padded copy
         # (same values, same chains: identical results, fewer lines per row)
@@ -455,6 +512,39 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
             msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
             ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), 0))
     return out, arg
+
+
+# Short-row tiers (dglhip_gspmm_short_rows_device): rows of <= 8 slots, and
+# rows without slots, of a degree-descending schedule go to the batched
+# short-row kernel once there are at least _TIER_MIN_ROWS of them (RMAT-26:
+# 55M of its 67M rows; tools/rmat_tail_study.py). Same chains, same bits.
+_TIERED = os.environ.get("DGLHIP_SHORT_ROWS", "on") != "off"
+_TIER_MIN_ROWS = 1 << 16
+
+
+def set_short_rows(on):
+    """Route short / empty rows to the batched short-row kernel (default on);
+    returns the old setting."""
+    global _TIERED
+    old = _TIERED
+    _TIERED = bool(on)
+    return old
+
+
+def _tail_rows(csr, nrows, skip):
+    """Whether the schedule's short tail is long enough to tier."""
+    _, tail = csr.tiers(csr.row_order[:nrows], ("plain", skip))
+    return sum(t[2] for t in tail) >= _TIER_MIN_ROWS
+
+
+def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail):
+    dev = out.device
+    for maxd, (rows, sp, cols), n in tail:
+        if maxd == 0 and red == RED_SUM_ACCUM:
+            continue  # nothing to add
+        check_call(LIB.dglhip_gspmm_short_rows_device(
+            msg, red, n, feat_len, maxd, csr.num_rows, ptr(rows), ptr(sp), ptr(cols),
+            ptr(ufeat2), ptr(out), _stream_of(dev)))
 
 
 _PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")

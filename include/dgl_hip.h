@@ -208,6 +208,22 @@ int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
                                 const float* ufeat, const float* efeat, int64_t efeat_len,
                                 float* out, const int32_t* row_order, void* stream);
 
+/* copy_u g-SpMM (sum / mean / sum_accum) over SHORT rows given as a compacted
+ * CSR of their own: item i writes output row rows[i] from its column ids
+ * slot_cols[slot_ptr[i] .. slot_ptr[i+1]) in slot order, every item having
+ * at most max_deg slots (0 = rows without slots: stored as zeros, or left as
+ * they are for sum_accum; slot_ptr / slot_cols may then be NULL). Several
+ * items per wave with all their gathers in flight together, for the tail of a
+ * power-law graph's degree-descending schedule where one wave per row leaves
+ * the memory system idle. Longer items are still reduced correctly, in batches
+ * of the kernel's depth. Results equal dglhip_gspmm_device's on the same rows
+ * bit for bit. total_rows: rows of the whole output (non-temporal store rule). */
+int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t num_items,
+                                   int64_t feat_len, int64_t max_deg, int64_t total_rows,
+                                   const int32_t* rows, const int64_t* slot_ptr,
+                                   const int32_t* slot_cols, const float* ufeat, float* out,
+                                   void* stream);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,

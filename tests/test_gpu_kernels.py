@@ -344,3 +344,60 @@ def test_padded_stride_gather(cuda, F, case):
     assert torch.equal(padded, plain)
     if case == "copy_u-sum":
         assert np.array_equal(padded.cpu().numpy(), O.spmm_coo(n, row, col, H))
+
+
+@pytest.mark.parametrize("red", ["sum", "mean"])
+@pytest.mark.parametrize("F", [128, 41, 2])
+def test_short_row_tiers(cuda, red, F):
+    """Rows of <= 8 slots and rows without slots go to the batched short-row
+    kernel (kernel.CSR.tiers): the same chains, so the result equals the
+    one-wave-per-row kernel bit for bit (and the oracle for sum), with and
+    without the heavy-row split."""
+    rng = np.random.default_rng(F)
+    n = 300_000
+    row, col = rand_graph(rng, n, n, 900_000, skew=True)
+    H = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    Hd = torch.from_numpy(H).to(cuda)
+    n_long, tail = adj.fwd.tiers(adj.fwd.row_order, ("plain", False))
+    assert sum(t[2] for t in tail) >= kernel._TIER_MIN_ROWS
+    assert {t[0] for t in tail} == {0, 4, 8}
+    outs = {}
+    for split in ("off", 2000):
+        old_s = kernel.set_row_split(split)
+        try:
+            for tiered in (True, False):
+                old = kernel.set_short_rows(tiered)
+                try:
+                    outs[(split, tiered)] = kernel.gspmm(adj, "copy_u", red, Hd)
+                finally:
+                    kernel.set_short_rows(old)
+        finally:
+            kernel.set_row_split(old_s)
+    assert torch.equal(outs[("off", True)], outs[("off", False)])
+    assert torch.equal(outs[(2000, True)], outs[(2000, False)])
+    if red == "sum":
+        assert np.array_equal(outs[("off", True)].cpu().numpy().reshape(n, F),
+                              O.spmm_coo(n, row, col, H))
+
+
+def test_short_row_tiers_accumulate_and_bf16(cuda):
+    """SUM_ACCUM (empty rows skipped, the others continued from out) and bf16
+    source rows through the short-row tiers: bit-identical to the untiered path."""
+    rng = np.random.default_rng(3)
+    n, F = 250_000, 64
+    row, col = rand_graph(rng, n, n, 700_000, skew=True)
+    csr = kernel.build_csr(n, n, row, col, kernel.ORDER_EID, cuda)
+    H = torch.from_numpy(rng.uniform(-1, 1, (n, F)).astype(np.float32)).to(cuda)
+    base = torch.from_numpy(rng.uniform(-1, 1, (n, F)).astype(np.float32)).to(cuda)
+    for src in (H, H.to(torch.bfloat16)):
+        res = []
+        for tiered in (True, False):
+            old = kernel.set_short_rows(tiered)
+            try:
+                o = base.clone()
+                kernel.gspmm_into(csr, o, src, accumulate=True)
+                res.append(o)
+            finally:
+                kernel.set_short_rows(old)
+        assert torch.equal(res[0], res[1])

@@ -57,9 +57,30 @@ def main():
         res.append({"rows_with_deg_gt": cut, "rows": rows, "edges": edges,
                     "ms": round(ms / cnt, 3)})
         print(res[-1], file=sys.stderr, flush=True)
+    # the same tail through the batched short-row kernel, tier by tier
+    tiers = []
+    n_long, tail = csr.tiers(light, ("study",))
+    lo = n_long
+    for maxd, (rows_t, sp, cols), cnt_rows in tail:
+        hi = lo + cnt_rows
+        for _ in range(2):
+            kernel.timing_enable(True)
+            for _ in range(args.iters):
+                _ffi.check_call(_ffi.LIB.dglhip_gspmm_short_rows_device(
+                    0, 0, cnt_rows, F, maxd, n, _ffi.ptr(rows_t), _ffi.ptr(sp),
+                    _ffi.ptr(cols), _ffi.ptr(h), _ffi.ptr(out), stream))
+            ms, cnt = kernel.timing_read()
+            kernel.timing_enable(False)
+        edges = int(deg[lo:hi].sum())
+        byts = edges * (4 * F + 4) + (hi - lo) * (4 * F + 8)
+        tiers.append({"max_deg": maxd, "rows": hi - lo, "edges": edges, "ms": round(ms / cnt, 3),
+                      "GBs": round(byts / (ms / cnt * 1e-3) / 1e9, 1)})
+        print(tiers[-1], file=sys.stderr, flush=True)
+        lo = hi
     print(json.dumps({"graph": "rmat-%d" % args.rmat_scale, "nodes": n, "edges": E,
                       "heavy_split_threshold": t, "light_rows": int(light.numel()),
-                      "prefixes": res}, indent=1))
+                      "prefixes": res, "long_rows": n_long, "short_row_tiers": tiers},
+                     indent=1))
 
 
 if __name__ == "__main__":
