@@ -55,17 +55,21 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 #            ~7168 resident waves (256 CUs x 4 SIMDs x 7), and rows start
 #            longest-first, so a row longer than twice a wave's share
 #            (nnz / 3584 slots) outlasts the rest of the launch — and it must
-#            also be longer than 65,536 slots (~4 ms of chained gathers), below
-#            which the loss is small and every row stays one exact chain.
+#            also be longer than 16,384 slots (~1.5 ms of chained gathers), below
+#            which the loss is bounded and every row stays one exact chain (a
+#            floor of 65,536 left the 60k-slot hub rows of RMAT-26's pipelined
+#            segments at 1/8 unsplit: 13.2 -> 24.3 ms per step, bench.py
+#            --emulate-world 8 --workload rmat).
 #            RMAT-26 (max in-degree ~855k, 2.9x the share) is split: GraphSAGE-
 #            mean epoch 0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
-#            Reddit (21,657) is not, and stays bit-exact.
+#            Reddit (max 21,657 <= 114.8M / 3584 = 32,045) is not, and stays
+#            bit-exact.
 #   "off"  : every row is one sequential chain — bit-exact with the reference
 #            on every graph (the documented bit-exact switch)
 #   <int>  : explicit chunk length, applied whenever some row is longer
 _ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
 _CRITICAL_SHARE = 3584  # half the resident waves of a full-chip launch
-_CRITICAL_MIN = 65536   # rows up to this length are never split by "auto"
+_CRITICAL_MIN = 16384   # rows up to this length are never split by "auto"
 
 
 def set_row_split(policy):

@@ -202,8 +202,8 @@ def _pipe_worker(rank, world, port, graph="chung_lu"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (2, "banded"),
-                                         (3, "banded")])
+@pytest.mark.parametrize("world,graph", [(2, "chung_lu"), (3, "chung_lu"), (4, "chung_lu"),
+                                         (2, "banded"), (3, "banded"), (4, "banded")])
 def test_pipelined_forward(world, graph):
     """Pipelined halo (chunked exchange overlapped with the segments) in both
     halo modes: forward within 1e-5 (exactly the (segment, eid) chain for the

@@ -34,8 +34,10 @@ def test_default_is_auto():
     (67_108_864, 160_139, 67_108_864 // 12000),
     # small skewed test graphs: never split by default (bit-exact)
     (40_000, 9_000, 0),
-    (2_000_000, 65_536, 0),
-    (2_000_000, 65_537, 4096),
+    (2_000_000, 16_384, 0),
+    (2_000_000, 16_385, 4096),
+    # RMAT-26's pipelined segments at 1/8 (~30M edges, hub rows ~60k): split
+    (30_000_000, 60_000, 4096),
     # a hub row that is long but not the critical path of a huge launch
     (4_000_000_000, 1_000_000, 0),
 ])
