@@ -27,6 +27,7 @@ namespace {
 int num_threads() { return default_num_threads(); }
 
 NDArray to_nd(const id_vec& v) { return NDArray::FromVector(v); }
+NDArray to_nd(const edge_vec& v) { return NDArray::FromIds(v.data(), static_cast<int64_t>(v.size())); }
 
 Body edge_array_func(const EdgeArrays& ea) {
   // ConvertEdgeArrayToPackedFunc (graph_apis.cc:21-36): 0 src, 1 dst, 2 id.
@@ -74,24 +75,64 @@ void sample_positions(int64_t n, int64_t k, std::mt19937_64* rng, id_vec* out) {
 }  // namespace
 
 // ------------------------------------------------------------------ CSR
+// First entry i in [0, n) with !ok(i), or -1 (parallel scan; the reported
+// entry is the lowest failing one, so the message does not depend on threads).
+template <typename Ok>
+static int64_t first_invalid(int64_t n, Ok&& ok) {
+  std::atomic<int64_t> bad{n};
+  parallel_for(n, num_threads(), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e && i < bad.load(std::memory_order_relaxed); ++i)
+      if (!ok(i)) {
+        int64_t cur = bad.load();
+        while (i < cur && !bad.compare_exchange_weak(cur, i)) {}
+        break;
+      }
+  }, int64_t(1) << 16);
+  return bad.load() == n ? -1 : bad.load();
+}
+
 CSR build_csr(int64_t nrows, int64_t ncols, const int64_t* row, const int64_t* col,
               const int64_t* id, int64_t n, bool sort_cols) {
+  // Stable counting sort by row. Degrees are counted with relaxed atomic adds;
+  // placement splits the rows into nnz-balanced ranges and every thread scans
+  // the entries in input order, placing only its own rows', so a row's slots
+  // keep input order whatever the thread count.
   CSR c;
+  const int64_t bad = first_invalid(n, [&](int64_t i) {
+    return row[i] >= 0 && row[i] < nrows && col[i] >= 0 && col[i] < ncols;
+  });
+  DGLHIP_CHECK(bad < 0, "Invalid vertices: " << row[bad] << ", " << col[bad]);
   c.indptr.assign(static_cast<size_t>(nrows) + 1, 0);
-  for (int64_t i = 0; i < n; ++i) {
-    DGLHIP_CHECK(row[i] >= 0 && row[i] < nrows && col[i] >= 0 && col[i] < ncols,
-                 "Invalid vertices: " << row[i] << ", " << col[i]);
-    ++c.indptr[row[i] + 1];
-  }
+  int64_t* cnt = c.indptr.data() + 1;
+  const int nt = num_threads();
+  parallel_for(n, nt, [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) __atomic_fetch_add(&cnt[row[i]], 1, __ATOMIC_RELAXED);
+  }, int64_t(1) << 16);
   for (int64_t r = 0; r < nrows; ++r) c.indptr[r + 1] += c.indptr[r];
   c.indices.resize(n);
   c.eid.resize(n);
-  id_vec pos(c.indptr.begin(), c.indptr.end() - 1);
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t k = pos[row[i]]++;
-    c.indices[k] = col[i];
-    c.eid[k] = id ? id[i] : i;
+  const int parts = (n >= (int64_t(1) << 20)) ? nt : 1;
+  std::vector<int64_t> bounds(parts + 1, nrows);
+  bounds[0] = 0;
+  for (int t = 1; t < parts; ++t) {
+    bounds[t] = std::upper_bound(c.indptr.begin(), c.indptr.end(), n * t / parts) -
+                c.indptr.begin() - 1;
+    bounds[t] = std::max(bounds[t], bounds[t - 1]);
   }
+  parallel_for(parts, parts, [&](int64_t b, int64_t e, int) {
+    for (int64_t t = b; t < e; ++t) {
+      const int64_t r0 = bounds[t], r1 = bounds[t + 1];
+      if (r0 >= r1) continue;
+      id_vec pos(c.indptr.begin() + r0, c.indptr.begin() + r1);
+      for (int64_t i = 0; i < n; ++i) {
+        const int64_t r = row[i];
+        if (r < r0 || r >= r1) continue;
+        const int64_t k = pos[r - r0]++;
+        c.indices[k] = col[i];
+        c.eid[k] = id ? id[i] : i;
+      }
+    }
+  }, 2);
   if (sort_cols) {
     parallel_for(nrows, num_threads(), [&](int64_t b, int64_t e, int) {
       std::vector<std::pair<int64_t, int64_t>> tmp;
@@ -170,23 +211,19 @@ id_vec Graph::has_edges_between(Ids u, Ids v) const {
   return out;
 }
 
-id_vec Graph::in_degrees(Ids v) const {
+static id_vec degrees_of(const Graph& g, const CSR& c, Ids v) {
+  const int64_t bad = first_invalid(v.n, [&](int64_t i) { return g.has_vertex(v[i]); });
+  DGLHIP_CHECK(bad < 0, "Invalid vertex: " << v[bad]);
   id_vec out(v.n);
-  for (int64_t i = 0; i < v.n; ++i) {
-    DGLHIP_CHECK(has_vertex(v[i]), "Invalid vertex: " << v[i]);
-    out[i] = in_degree(v[i]);
-  }
+  parallel_for(v.n, num_threads(), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) out[i] = c.degree(v[i]);
+  }, int64_t(1) << 16);
   return out;
 }
 
-id_vec Graph::out_degrees(Ids v) const {
-  id_vec out(v.n);
-  for (int64_t i = 0; i < v.n; ++i) {
-    DGLHIP_CHECK(has_vertex(v[i]), "Invalid vertex: " << v[i]);
-    out[i] = out_degree(v[i]);
-  }
-  return out;
-}
+id_vec Graph::in_degrees(Ids v) const { return degrees_of(*this, *in_csr(), v); }
+
+id_vec Graph::out_degrees(Ids v) const { return degrees_of(*this, *out_csr(), v); }
 
 // ------------------------------------------------------------------ MutableGraph
 MutableGraph::MutableGraph(Ids src, Ids dst, Ids eid, int64_t num_nodes, bool multigraph)
@@ -195,9 +232,10 @@ MutableGraph::MutableGraph(Ids src, Ids dst, Ids eid, int64_t num_nodes, bool mu
   DGLHIP_CHECK(src.n == dst.n && src.n == eid.n, "vectors in COO must have the same length");
   DGLHIP_CHECK(num_nodes >= 0, "invalid number of nodes " << num_nodes);
   n_ = num_nodes;
-  for (int64_t i = 0; i < src.n; ++i)
-    DGLHIP_CHECK(has_vertex(src[i]) && has_vertex(dst[i]),
-                 "Invalid vertices: src=" << src[i] << " dst=" << dst[i]);
+  const int64_t bad = first_invalid(src.n, [&](int64_t i) {
+    return has_vertex(src[i]) && has_vertex(dst[i]);
+  });
+  DGLHIP_CHECK(bad < 0, "Invalid vertices: src=" << src[bad] << " dst=" << dst[bad]);
   src_.assign(src.p, src.p + src.n);
   dst_.assign(dst.p, dst.p + dst.n);
   eid_.assign(eid.p, eid.p + eid.n);
@@ -218,6 +256,39 @@ void MutableGraph::invalidate() {
   std::lock_guard<std::mutex> lk(mu_);
   in_.reset();
   out_.reset();
+  in_deg_.reset();
+  out_deg_.reset();
+}
+
+std::shared_ptr<const id_vec> MutableGraph::degree_table(bool in) const {
+  std::lock_guard<std::mutex> lk(mu_);
+  auto& slot = in ? in_deg_ : out_deg_;
+  if (!slot) {
+    auto deg = std::make_shared<id_vec>(static_cast<size_t>(n_), 0);
+    const edge_vec& end = in ? dst_ : src_;
+    int64_t* d = deg->data();
+    parallel_for(num_edges(), num_threads(), [&](int64_t b, int64_t e, int) {
+      for (int64_t i = b; i < e; ++i) __atomic_fetch_add(&d[end[i]], 1, __ATOMIC_RELAXED);
+    }, int64_t(1) << 16);
+    slot = deg;
+  }
+  return slot;
+}
+
+static id_vec lookup_degrees(const Graph& g, const id_vec& deg, Ids v) {
+  const int64_t bad = first_invalid(v.n, [&](int64_t i) { return g.has_vertex(v[i]); });
+  DGLHIP_CHECK(bad < 0, "Invalid vertex: " << v[bad]);
+  id_vec out(v.n);
+  parallel_for(v.n, num_threads(), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) out[i] = deg[v[i]];
+  }, int64_t(1) << 16);
+  return out;
+}
+
+id_vec MutableGraph::in_degrees(Ids v) const { return lookup_degrees(*this, *degree_table(true), v); }
+
+id_vec MutableGraph::out_degrees(Ids v) const {
+  return lookup_degrees(*this, *degree_table(false), v);
 }
 
 CSRPtr MutableGraph::in_csr() const {
@@ -264,15 +335,31 @@ void MutableGraph::add_edges(Ids u, Ids v) {
     m = u.n;
   }
   const int64_t us = u.n == 1 ? 0 : 1, vs = (v.n == 1 && u.n != 1) ? 0 : 1;
-  for (int64_t i = 0; i < m; ++i)
-    DGLHIP_CHECK(has_vertex(u[i * us]) && has_vertex(v[i * vs]),
-                 "Invalid vertices: src=" << u[i * us] << " dst=" << v[i * vs]);
+  const int64_t bad = first_invalid(m, [&](int64_t i) {
+    return has_vertex(u[i * us]) && has_vertex(v[i * vs]);
+  });
+  DGLHIP_CHECK(bad < 0, "Invalid vertices: src=" << u[bad * us] << " dst=" << v[bad * vs]);
   const int64_t e0 = num_edges();
-  for (int64_t i = 0; i < m; ++i) {
-    src_.push_back(u[i * us]);
-    dst_.push_back(v[i * vs]);
-    eid_.push_back(e0 + i);
+  // geometric growth even for one bulk append (a graph of 10^9 edges is built
+  // by one call; growing to the exact size would make repeated small appends
+  // quadratic)
+  const size_t need = static_cast<size_t>(e0 + m);
+  if (src_.capacity() < need) {
+    const size_t cap = std::max(need, 2 * src_.capacity());
+    src_.reserve(cap);
+    dst_.reserve(cap);
+    eid_.reserve(cap);
   }
+  src_.resize(need);
+  dst_.resize(need);
+  eid_.resize(need);
+  parallel_for(m, num_threads(), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) {
+      src_[e0 + i] = u[i * us];
+      dst_[e0 + i] = v[i * vs];
+      eid_[e0 + i] = e0 + i;
+    }
+  }, int64_t(1) << 16);
   invalidate();
 }
 
@@ -383,12 +470,12 @@ EdgeArrays MutableGraph::edges(const std::string& order) const {
 
 int64_t MutableGraph::in_degree(int64_t v) const {
   check_vertex(v);
-  return in_csr()->degree(v);
+  return (*degree_table(true))[v];
 }
 
 int64_t MutableGraph::out_degree(int64_t v) const {
   check_vertex(v);
-  return out_csr()->degree(v);
+  return (*degree_table(false))[v];
 }
 
 Subgraph MutableGraph::vertex_subgraph(Ids v) const {
@@ -447,8 +534,8 @@ std::vector<NDArray> MutableGraph::get_adj(bool transpose, const std::string& fm
   if (fmt == "coo") {
     NDArray idx = NDArray::Ids(2 * m), eid = NDArray::Ids(m);
     int64_t* p = idx.data<int64_t>();
-    const id_vec& first = transpose ? src_ : dst_;
-    const id_vec& second = transpose ? dst_ : src_;
+    const edge_vec& first = transpose ? src_ : dst_;
+    const edge_vec& second = transpose ? dst_ : src_;
     std::copy(first.begin(), first.end(), p);
     std::copy(second.begin(), second.end(), p + m);
     std::iota(eid.data<int64_t>(), eid.data<int64_t>() + m, int64_t(0));
@@ -641,8 +728,8 @@ EdgeArrays ImmutableGraph::edges(const std::string& order) const {
   EdgeArrays out;
   const int64_t m = c->nnz();
   out.src.resize(m);
-  out.dst = c->indices;
-  out.id = c->eid;
+  out.dst.assign(c->indices.begin(), c->indices.end());
+  out.id.assign(c->eid.begin(), c->eid.end());
   for (int64_t r = 0; r < c->rows(); ++r)
     std::fill(out.src.begin() + c->indptr[r], out.src.begin() + c->indptr[r + 1], r);
   if (order == "eid") {
@@ -1037,7 +1124,18 @@ void register_graph_index_functions() {
     rv->set_func(edge_array_func(graph_arg(a, 0)->out_edges(id_arg(a, 1))));
   });
   register_global(ns + "DGLGraphEdges", [](const Args& a, RetValue* rv) {
-    rv->set_func(edge_array_func(graph_arg(a, 0)->edges(a.str(1))));
+    Graph* g = graph_arg(a, 0);
+    const std::string order = a.str(1);
+    auto* mg = dynamic_cast<MutableGraph*>(g);
+    if (mg && order != "srcdst") {
+      // id order is the storage order: one copy per array straight into the
+      // returned NDArrays (no permutation, no intermediate vectors), which is
+      // what the engine reads to build its device CSRs of 10^9-edge graphs
+      rv->set_func(rt::ndarray_vector_func(
+          {to_nd(mg->src()), to_nd(mg->dst()), to_nd(mg->eid())}));
+      return;
+    }
+    rv->set_func(edge_array_func(g->edges(order)));
   });
   register_global(ns + "DGLGraphInDegree", [](const Args& a, RetValue* rv) {
     rv->set_int(graph_arg(a, 0)->in_degree(a.i64(1)));

@@ -20,6 +20,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "runtime.h"
@@ -29,12 +30,27 @@ namespace gi {
 
 using id_vec = std::vector<int64_t>;
 
+// Allocator whose resize() leaves new elements uninitialised: the edge arrays
+// of a 10^9-edge graph are filled in parallel right after they grow, so a
+// serial zero-fill (and its page faults) would double the cost of AddEdges.
+template <typename T>
+struct uninit_allocator : std::allocator<T> {
+  template <typename U> struct rebind { using other = uninit_allocator<U>; };
+  uninit_allocator() = default;
+  template <typename U> uninit_allocator(const uninit_allocator<U>&) noexcept {}
+  template <typename U> void construct(U* p) noexcept { ::new (static_cast<void*>(p)) U; }
+  template <typename U, typename... A> void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
+  }
+};
+using edge_vec = std::vector<int64_t, uninit_allocator<int64_t>>;
+
 // Compressed adjacency: row r owns slots [indptr[r], indptr[r+1]); indices[k]
 // is the neighbour and eid[k] the edge id of slot k.
 struct CSR {
   id_vec indptr{0};
-  id_vec indices;
-  id_vec eid;
+  edge_vec indices;
+  edge_vec eid;
   int64_t rows() const { return static_cast<int64_t>(indptr.size()) - 1; }
   int64_t nnz() const { return static_cast<int64_t>(indices.size()); }
   int64_t degree(int64_t r) const { return indptr[r + 1] - indptr[r]; }
@@ -99,8 +115,11 @@ class Graph {
   virtual EdgeArrays edges(const std::string& order) const = 0;
   virtual int64_t in_degree(int64_t v) const = 0;
   virtual int64_t out_degree(int64_t v) const = 0;
-  id_vec in_degrees(Ids v) const;
-  id_vec out_degrees(Ids v) const;
+  // in-adjacency (rows = dst) and out-adjacency (rows = src), built on demand
+  virtual CSRPtr in_csr() const = 0;
+  virtual CSRPtr out_csr() const = 0;
+  virtual id_vec in_degrees(Ids v) const;
+  virtual id_vec out_degrees(Ids v) const;
   virtual Subgraph vertex_subgraph(Ids v) const = 0;
   virtual Subgraph edge_subgraph(Ids e) const;
   // [idx(2E), eid(E)] for "coo", [indptr, indices, eid] for "csr"
@@ -137,6 +156,8 @@ class MutableGraph : public Graph {
   EdgeArrays edges(const std::string& order) const override;
   int64_t in_degree(int64_t v) const override;
   int64_t out_degree(int64_t v) const override;
+  id_vec in_degrees(Ids v) const override;
+  id_vec out_degrees(Ids v) const override;
   Subgraph vertex_subgraph(Ids v) const override;
   Subgraph edge_subgraph(Ids e) const override;
   std::vector<rt::NDArray> get_adj(bool transpose, const std::string& fmt) const override;
@@ -146,18 +167,22 @@ class MutableGraph : public Graph {
   static MutableGraph disjoint_union(const std::vector<const MutableGraph*>& graphs);
   std::vector<MutableGraph> partition_by_sizes(const id_vec& sizes) const;
 
-  const id_vec& src() const { return src_; }
-  const id_vec& dst() const { return dst_; }
-  const id_vec& eid() const { return eid_; }
-  CSRPtr in_csr() const;   // rows = dst, slots in edge-insertion order
-  CSRPtr out_csr() const;  // rows = src
+  const edge_vec& src() const { return src_; }
+  const edge_vec& dst() const { return dst_; }
+  const edge_vec& eid() const { return eid_; }
+  CSRPtr in_csr() const override;   // rows = dst, slots in edge-insertion order
+  CSRPtr out_csr() const override;  // rows = src
 
  private:
   void invalidate();
+  // per-vertex in/out degree, counted from the edge arrays on demand (no CSR
+  // needed: the reference's adjacency vectors know their sizes)
+  std::shared_ptr<const id_vec> degree_table(bool in) const;
   int64_t n_ = 0;
-  id_vec src_, dst_, eid_;  // per edge position; eid_ = id kept in the adjacency
+  edge_vec src_, dst_, eid_;  // per edge position; eid_ = id kept in the adjacency
   mutable std::mutex mu_;
   mutable CSRPtr in_, out_;
+  mutable std::shared_ptr<const id_vec> in_deg_, out_deg_;
 };
 
 class ImmutableGraph : public Graph {
@@ -183,8 +208,8 @@ class ImmutableGraph : public Graph {
   Subgraph vertex_subgraph(Ids v) const override;
   std::vector<rt::NDArray> get_adj(bool transpose, const std::string& fmt) const override;
 
-  CSRPtr in_csr() const;   // rows = dst, indices = src, sorted per row
-  CSRPtr out_csr() const;  // rows = src, indices = dst, sorted per row
+  CSRPtr in_csr() const override;   // rows = dst, indices = src, sorted per row
+  CSRPtr out_csr() const override;  // rows = src, indices = dst, sorted per row
 
  private:
   mutable std::mutex mu_;

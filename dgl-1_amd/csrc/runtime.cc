@@ -131,9 +131,14 @@ NDArray NDArray::Empty(const std::vector<int64_t>& shape, int code, int bits,
   return out;
 }
 
-NDArray NDArray::FromVector(const std::vector<int64_t>& v) {
-  NDArray a = Ids(static_cast<int64_t>(v.size()));
-  if (!v.empty()) std::memcpy(a.data<int64_t>(), v.data(), v.size() * sizeof(int64_t));
+NDArray NDArray::FromIds(const int64_t* p, int64_t n) {
+  NDArray a = Ids(n);
+  int64_t* dst = a.data<int64_t>();
+  // threads share the first-touch page faults of the new buffer (10^9-id
+  // exports of the graph index)
+  parallel_for(n, default_num_threads(), [&](int64_t b, int64_t e, int) {
+    std::memcpy(dst + b, p + b, static_cast<size_t>(e - b) * sizeof(int64_t));
+  }, int64_t(1) << 18);
   return a;
 }
 

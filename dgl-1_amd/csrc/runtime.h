@@ -56,7 +56,11 @@ class NDArray {
                        int device_type = kDLCPU, int device_id = 0);
   // 1-D host int64 array.
   static NDArray Ids(int64_t n) { return Empty({n}, 0, 64); }
-  static NDArray FromVector(const std::vector<int64_t>& v);
+  static NDArray FromVector(const std::vector<int64_t>& v) {
+    return FromIds(v.data(), static_cast<int64_t>(v.size()));
+  }
+  // 1-D host int64 copy of p[0, n) (parallel copy for large n).
+  static NDArray FromIds(const int64_t* p, int64_t n);
 
   bool defined() const { return c_ != nullptr; }
   NDContainer* get() const { return c_; }

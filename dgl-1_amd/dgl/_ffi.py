@@ -18,7 +18,8 @@ import torch  # noqa: F401  (loads the HIP runtime torch links against first)
 
 from .base import DGLError
 
-__all__ = ["LIB", "check_call", "lib_path", "tensor_arg", "call_packed", "list_global_names"]
+__all__ = ["LIB", "check_call", "lib_path", "tensor_arg", "call_packed", "list_global_names",
+           "PackedFunction", "get_global_func", "CAPINamespace"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIBNAME = "libdgl_hip.so"
@@ -95,6 +96,9 @@ def _load():
                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))]),
         "DGLFuncCall": (_c_int, [_vp, _vp, ctypes.POINTER(_c_int), _c_int, _vp, ctypes.POINTER(_c_int)]),
         "DGLFuncFree": (_c_int, [_vp]),
+        "DGLArrayFree": (_c_int, [_vp]),
+        "DGLArrayToDLPack": (_c_int, [_vp, ctypes.POINTER(_vp)]),
+        "DGLDLManagedTensorCallDeleter": (None, [_vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -194,30 +198,138 @@ def list_global_names():
 
 def call_packed(name, *args):
     """Call a registered function by name with ints, tensors, None or
-    ``("handle", int)`` stream handles — the DGLFuncCall convention."""
-    h = _vp()
-    check_call(LIB.DGLFuncGetGlobal(name.encode(), ctypes.byref(h)))
-    if not h.value:
-        raise DGLError("global function %s is not registered" % name)
-    n = len(args)
-    vals = (_DGLHipValue * max(n, 1))()
-    codes = (_c_int * max(n, 1))()
-    keep = []
-    for i, a in enumerate(args):
-        if a is None:
-            codes[i] = _TC_NULL
-        elif isinstance(a, torch.Tensor):
-            st = tensor_arg(a)
-            keep.append(st)
-            vals[i].v_handle = ctypes.cast(ctypes.pointer(st), _vp)
-            codes[i] = _TC_ARRAY
-        elif isinstance(a, tuple) and a[0] == "handle":
-            vals[i].v_handle = a[1]
-            codes[i] = _TC_HANDLE
-        else:
-            vals[i].v_int64 = int(a)
-            codes[i] = _TC_INT
-    ret = _DGLHipValue()
-    rc = _c_int()
-    check_call(LIB.DGLFuncCall(h, ctypes.cast(vals, _vp), codes, n,
-                               ctypes.cast(ctypes.pointer(ret), _vp), ctypes.byref(rc)))
+    ``("handle", int)`` stream handles — the DGLFuncCall convention; returns
+    the decoded result (see :class:`PackedFunction`)."""
+    return get_global_func(name)(*args)
+
+
+_TC_FLOAT, _TC_FUNC, _TC_STR, _TC_NDARRAY = 2, 10, 11, 13
+
+ctypes.pythonapi.PyCapsule_New.restype = ctypes.py_object
+ctypes.pythonapi.PyCapsule_New.argtypes = [_vp, ctypes.c_char_p, _vp]
+ctypes.pythonapi.PyCapsule_GetPointer.restype = _vp
+ctypes.pythonapi.PyCapsule_GetPointer.argtypes = [ctypes.py_object, ctypes.c_char_p]
+ctypes.pythonapi.PyCapsule_IsValid.argtypes = [ctypes.py_object, ctypes.c_char_p]
+
+
+@ctypes.CFUNCTYPE(None, _vp)
+def _dltensor_capsule_deleter(capsule):
+    # a capsule torch never consumed still owns its DGLHipManagedTensor
+    cap = ctypes.cast(capsule, ctypes.py_object)
+    if ctypes.pythonapi.PyCapsule_IsValid(cap, b"dltensor"):
+        LIB.DGLDLManagedTensorCallDeleter(ctypes.pythonapi.PyCapsule_GetPointer(cap, b"dltensor"))
+
+
+def _ndarray_to_torch(handle):
+    """Library-owned NDArray container -> torch tensor without a copy
+    (zerocopy_from_dgl_ndarray: DGLArrayToDLPack, then the container's own
+    reference is dropped; the DLPack manager keeps the storage alive)."""
+    import torch.utils.dlpack
+    mt = _vp()
+    try:
+        check_call(LIB.DGLArrayToDLPack(handle, ctypes.byref(mt)))
+    finally:
+        check_call(LIB.DGLArrayFree(handle))
+    cap = ctypes.pythonapi.PyCapsule_New(mt, b"dltensor",
+                                         ctypes.cast(_dltensor_capsule_deleter, _vp))
+    return torch.utils.dlpack.from_dlpack(cap)
+
+
+class PackedFunction(object):
+    """A function of the library's PackedFunc table, or one it returned
+    (python/dgl/_ffi/_ctypes/function.py:150-190). Calls take ints, bools,
+    floats, strings, torch tensors (passed as non-owning arrays), None and
+    ``("handle", int)``; results come back decoded by type code: ints,
+    floats, strings, handles (ints), torch tensors for returned arrays
+    (zero-copy) and PackedFunction for returned functions (freed with
+    DGLFuncFree when collected)."""
+
+    __slots__ = ("handle", "_owned")
+
+    def __init__(self, handle, owned):
+        self.handle = handle
+        self._owned = owned
+
+    def __del__(self):
+        if self._owned and self.handle:
+            try:
+                LIB.DGLFuncFree(self.handle)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
+    def __call__(self, *args):
+        n = len(args)
+        vals = (_DGLHipValue * max(n, 1))()
+        codes = (_c_int * max(n, 1))()
+        keep = []
+        for i, a in enumerate(args):
+            if a is None:
+                codes[i] = _TC_NULL
+            elif isinstance(a, torch.Tensor):
+                st = tensor_arg(a)
+                keep.append(st)
+                vals[i].v_handle = ctypes.cast(ctypes.pointer(st), _vp)
+                codes[i] = _TC_ARRAY
+            elif isinstance(a, tuple) and a[0] == "handle":
+                vals[i].v_handle = a[1]
+                codes[i] = _TC_HANDLE
+            elif isinstance(a, str):
+                b = a.encode()
+                keep.append(b)
+                vals[i].v_str = b
+                codes[i] = _TC_STR
+            elif isinstance(a, float):
+                vals[i].v_float64 = a
+                codes[i] = _TC_FLOAT
+            else:
+                vals[i].v_int64 = int(a)
+                codes[i] = _TC_INT
+        ret = _DGLHipValue()
+        rc = _c_int()
+        check_call(LIB.DGLFuncCall(self.handle, ctypes.cast(vals, _vp), codes, n,
+                                   ctypes.cast(ctypes.pointer(ret), _vp), ctypes.byref(rc)))
+        del keep
+        code = rc.value
+        if code == _TC_INT:
+            return ret.v_int64
+        if code == _TC_FLOAT:
+            return ret.v_float64
+        if code == _TC_NULL:
+            return None
+        if code == _TC_HANDLE:
+            return ret.v_handle
+        if code == _TC_STR:
+            return ret.v_str.decode()
+        if code == _TC_NDARRAY:
+            return _ndarray_to_torch(ret.v_handle)
+        if code == _TC_FUNC:
+            return PackedFunction(ret.v_handle, True)
+        raise DGLError("unsupported return type code %d" % code)
+
+
+_GLOBALS = {}
+
+
+def get_global_func(name):
+    """The registered function ``name`` (cached; DGLFuncGetGlobal)."""
+    f = _GLOBALS.get(name)
+    if f is None:
+        h = _vp()
+        check_call(LIB.DGLFuncGetGlobal(name.encode(), ctypes.byref(h)))
+        if not h.value:
+            raise DGLError("global function %s is not registered" % name)
+        f = _GLOBALS[name] = PackedFunction(h.value, False)
+    return f
+
+
+class CAPINamespace(object):
+    """``ns._CAPI_<name>`` attribute access to the registry, as the reference's
+    _init_api binds a module's functions (python/dgl/_ffi/function.py:267-306)."""
+
+    def __init__(self, namespace):
+        self._ns = namespace
+
+    def __getattr__(self, name):
+        f = get_global_func("%s.%s" % (self._ns, name))
+        setattr(self, name, f)
+        return f

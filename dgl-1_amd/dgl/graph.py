@@ -426,11 +426,11 @@ class DGLGraph(object):
                                  lambda: self._adjacency_matrix(transpose, ctx))
 
     def _adjacency_matrix(self, transpose, ctx):
-        src, dst = self._graph.src(), self._graph.dst()
-        row, col = (src, dst) if transpose else (dst, src)
-        n = self.number_of_nodes()
-        idx = torch.stack([row, col])
-        return torch.sparse_coo_tensor(idx, torch.ones(len(row)), (n, n)).to(ctx)
+        # the index's COO (graph_index.py:565-583 -> _CAPI_DGLGraphGetAdj):
+        # edge-id order for a mutable graph, in-CSR order for an immutable one
+        idx = self._graph.get_adj(transpose, "coo")[0]
+        n, m = self.number_of_nodes(), self.number_of_edges()
+        return torch.sparse_coo_tensor(idx.reshape(2, m), torch.ones(m), (n, n)).to(ctx)
 
     def incidence_matrix(self, typestr, ctx=torch.device("cpu")):
         """'in' / 'out' / 'both' incidence matrix (graph_index.py:587-662);
@@ -442,9 +442,8 @@ class DGLGraph(object):
                                  lambda: self._incidence_matrix(typestr, ctx))
 
     def _incidence_matrix(self, typestr, ctx):
-        src, dst = self._graph.src(), self._graph.dst()
+        src, dst, eid = self._graph.edges()
         n, m = self.number_of_nodes(), self.number_of_edges()
-        eid = torch.arange(m)
         if typestr == "in":
             idx, val = torch.stack([dst, eid]), torch.ones(m)
         elif typestr == "out":

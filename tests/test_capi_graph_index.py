@@ -250,8 +250,10 @@ def test_edge_subgraph_known_answer():
 
 
 def test_against_engine_graph_index():
-    """Differential: the native index answers what dgl.graph_index.GraphIndex
-    (the engine's product index) answers, on a random multigraph."""
+    """The engine's DGLGraph index (dgl.graph_index.GraphIndex, a handle on
+    the native index since r02) answers what a second native index built
+    through the raw C-ABI client answers, on a random multigraph; and the
+    engine's own CSR builder (the g-SpMM path) reproduces the index's CSR."""
     rng = np.random.default_rng(0)
     n, m = 300, 4000
     src = rng.integers(0, n, m)
