@@ -395,7 +395,7 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 const int64_t* chunk_end, int64_t num_heavy,
                                 const int32_t* heavy_rows,
                                 const int64_t* heavy_chunk_ptr, float* partial,
-                                void* stream_) {
+                                int64_t ufeat_ld, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
@@ -411,18 +411,23 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
                "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
   DGLHIP_CHECK(num_chunks == 0 || (partial && chunk_beg && chunk_end), "null chunk plan");
+  DGLHIP_CHECK(ufeat_ld == 0 || ufeat_ld == feat_len || (ufeat_ld > feat_len && ufeat_ld % 2 == 0),
+               "ufeat_ld " << ufeat_ld << ": 0, feat_len, or an even width > feat_len");
+  DGLHIP_CHECK(ufeat_ld == 0 || ufeat_ld == feat_len || msg_op == DGLHIP_MSG_COPY_U ||
+                   msg_op == DGLHIP_MSG_U_MUL_E,
+               "strided source rows: copy_u or u_mul_e, got msg op " << msg_op);
   const int64_t elen = use_e ? efeat_len : 1;
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM;
   if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
     SumLaunch c{num_chunks, feat_len, elen, indptr, indices, eid, ufeat, efeat, partial,
-                nullptr, chunk_beg, chunk_end, false};
+                nullptr, chunk_beg, chunk_end, false, false, ufeat_ld};
     dispatch_sum(msg_op, false, c, stream);
   }
   if (num_light > 0) {
     SumLaunch l{num_light, feat_len, elen, indptr, indices, eid, ufeat, efeat, out,
                 light_rows, nullptr, nullptr, accum,
-                stream_output(num_light + num_heavy, feat_len)};
+                stream_output(num_light + num_heavy, feat_len), ufeat_ld};
     dispatch_sum(msg_op, mean, l, stream);
   }
   if (num_heavy > 0) {

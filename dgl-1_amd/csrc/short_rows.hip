@@ -28,7 +28,7 @@ template <int VEC, int MAXD, int R, int MSG, int POL>
 __global__ __launch_bounds__(256) void gspmm_short_rows_kernel(
     int64_t num_items, int64_t F, const int32_t* __restrict__ rows,
     const int64_t* __restrict__ slot_ptr, const int32_t* __restrict__ slot_cols,
-    const float* __restrict__ ufeat, float* __restrict__ out, int mean, int accum) {
+    const float* __restrict__ ufeat, float* __restrict__ out, int mean, int accum, int64_t ldu) {
   typedef typename Vec<VEC>::T V;
   const int64_t wave = block_linear() * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -66,8 +66,8 @@ __global__ __launch_bounds__(256) void gspmm_short_rows_kernel(
           for (int j = 0; j < MAXD; ++j)
             if (b + j < deg[r]) {
               const int32_t c = slot_cols[beg[r] + b + j];
-              if (MSG == DGLHIP_MSG_COPY_U_BF16) v[r][j] = gather_bf16<VEC>(ufeat, c, F, f0);
-              else v[r][j] = gather_row<VEC, POL_DEFAULT>(ufeat, c, F, f0);
+              if (MSG == DGLHIP_MSG_COPY_U_BF16) v[r][j] = gather_bf16<VEC>(ufeat, c, ldu, f0);
+              else v[r][j] = gather_row<VEC, POL_DEFAULT>(ufeat, c, ldu, f0);
             }
 #pragma unroll
         for (int r = 0; r < R; ++r)
@@ -87,37 +87,37 @@ __global__ __launch_bounds__(256) void gspmm_short_rows_kernel(
 }
 
 template <int VEC, int MAXD, int R, int MSG>
-static void launch_short(int64_t n, int64_t F, const int32_t* rows, const int64_t* slot_ptr,
-                         const int32_t* slot_cols, const float* ufeat, float* out, bool mean,
-                         bool accum, bool nt, hipStream_t stream) {
+static void launch_short(int64_t n, int64_t F, int64_t ldu, const int32_t* rows,
+                         const int64_t* slot_ptr, const int32_t* slot_cols, const float* ufeat,
+                         float* out, bool mean, bool accum, bool nt, hipStream_t stream) {
   const int64_t waves = (n + R - 1) / R;
   const int64_t blocks = (waves + 3) / 4;
   timed_launch(stream, [&] {
     if (nt)
       hipLaunchKernelGGL((gspmm_short_rows_kernel<VEC, MAXD, R, MSG, POL_NT_OUT>),
                          grid_1d(blocks), dim3(256), 0, stream, n, F, rows, slot_ptr,
-                         slot_cols, ufeat, out, mean ? 1 : 0, accum ? 1 : 0);
+                         slot_cols, ufeat, out, mean ? 1 : 0, accum ? 1 : 0, ldu);
     else
       hipLaunchKernelGGL((gspmm_short_rows_kernel<VEC, MAXD, R, MSG, POL_DEFAULT>),
                          grid_1d(blocks), dim3(256), 0, stream, n, F, rows, slot_ptr,
-                         slot_cols, ufeat, out, mean ? 1 : 0, accum ? 1 : 0);
+                         slot_cols, ufeat, out, mean ? 1 : 0, accum ? 1 : 0, ldu);
   });
 }
 
 template <int VEC, int MSG>
-static void dispatch_short(int64_t max_deg, int64_t n, int64_t F, const int32_t* rows,
+static void dispatch_short(int64_t max_deg, int64_t n, int64_t F, int64_t ldu, const int32_t* rows,
                            const int64_t* slot_ptr, const int32_t* slot_cols,
                            const float* ufeat, float* out, bool mean, bool accum, bool nt,
                            hipStream_t stream) {
   // R * MAXD = 32 gathers in flight per wave (the main kernel keeps 16)
   if (max_deg == 0)
-    launch_short<VEC, 0, 16, MSG>(n, F, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
+    launch_short<VEC, 0, 16, MSG>(n, F, ldu, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
                                   nt, stream);
   else if (max_deg <= 4)
-    launch_short<VEC, 4, 8, MSG>(n, F, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
+    launch_short<VEC, 4, 8, MSG>(n, F, ldu, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
                                  nt, stream);
   else
-    launch_short<VEC, 8, 4, MSG>(n, F, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
+    launch_short<VEC, 8, 4, MSG>(n, F, ldu, rows, slot_ptr, slot_cols, ufeat, out, mean, accum,
                                  nt, stream);
 }
 
@@ -130,7 +130,7 @@ extern "C" int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t
                                               int64_t total_rows, const int32_t* rows,
                                               const int64_t* slot_ptr,
                                               const int32_t* slot_cols, const float* ufeat,
-                                              float* out, void* stream_) {
+                                              float* out, int64_t ufeat_ld, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(copies_u(msg_op), "short-row g-SpMM: copy_u messages only, got " << msg_op);
@@ -141,6 +141,9 @@ extern "C" int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t
   if (num_items == 0 || feat_len == 0) return 0;
   DGLHIP_CHECK(out && rows && (max_deg == 0 || (slot_ptr && slot_cols && ufeat)),
                "null pointer argument");
+  DGLHIP_CHECK(ufeat_ld == 0 || ufeat_ld == feat_len || (ufeat_ld > feat_len && ufeat_ld % 2 == 0),
+               "ufeat_ld " << ufeat_ld << ": 0, feat_len, or an even width > feat_len");
+  const int64_t ldu = ufeat_ld ? ufeat_ld : feat_len;
   const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
   const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM;
   // non-temporal output once the whole launch's output is past twice the
@@ -150,7 +153,7 @@ extern "C" int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t
                   reinterpret_cast<uintptr_t>(out) % 8 == 0 &&
                   (max_deg == 0 || reinterpret_cast<uintptr_t>(ufeat) % 8 == 0);
 #define DGLHIP_SHORT(V, M)                                                                  \
-  dispatch_short<V, M>(max_deg, num_items, feat_len, rows, slot_ptr, slot_cols, ufeat, out, \
+  dispatch_short<V, M>(max_deg, num_items, feat_len, ldu, rows, slot_ptr, slot_cols, ufeat, out, \
                        mean, accum, nt, stream)
   if (msg_op == DGLHIP_MSG_COPY_U_BF16) {
     if (v2) DGLHIP_SHORT(2, DGLHIP_MSG_COPY_U_BF16);

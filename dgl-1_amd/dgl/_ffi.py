@@ -60,7 +60,7 @@ def _load():
                                          _c_i64, _vp, _vp, _vp, _vp]),
         "dglhip_gspmm_chunked_device": (_c_int, [_c_int, _c_int, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                  _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp,
-                                                 _c_i64, _vp, _vp, _vp, _vp]),
+                                                 _c_i64, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_gspmm_ranges_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
                                                 _vp, _vp, _c_i64, _vp, _vp]),
         "dglhip_gspmm_ranges_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
@@ -87,7 +87,7 @@ def _load():
         "dglhip_set_cache_policy": (_c_int, [_c_int]),
         "dglhip_set_sddmm_variant": (_c_int, [_c_int]),
         "dglhip_gspmm_short_rows_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64,
-                                                    _c_i64, _vp, _vp, _vp, _vp, _vp, _vp]),
+                                                    _c_i64, _vp, _vp, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_gspmm_strided_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp,
                                                  _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp]),
         "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),

@@ -466,9 +466,17 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         eid = csr.slot_eid if emap is None else emap
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
+    ld = 0
+    if dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
+        # source rows straddle cache lines: every schedule below gathers them
+        # from a padded copy (same values, same chains: identical results,
+        # fewer lines per row)
+        ld = padded_width(feat_len)
+        up = ufeat2.new_empty(ufeat2.shape[0], ld)
+        up[:, :feat_len] = ufeat2
+        ufeat2 = up
     tiered = (dev.type == "cuda" and _TIERED and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and
-              red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM) and
-              not _pad_rows(msg, red, ufeat2, feat_len))
+              red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM))
     if split:
         p = csr.split_plan(split, skip_empty=skip)
         partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
@@ -484,33 +492,17 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
             msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(ufeat2),
             ptr(efeat2), elen, ptr(out), n_light, ptr(light), p["num_chunks"],
             ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
-            ptr(p["chunk_ptr"]), ptr(partial), _stream_of(dev)))
-        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail)
+            ptr(p["chunk_ptr"]), ptr(partial), ld, _stream_of(dev)))
+        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld)
     elif tiered and csr.row_order is not None and \
             _tail_rows(csr, csr.num_nonempty if skip else csr.num_rows, skip):
         nrows = csr.num_nonempty if skip else csr.num_rows
         n_long, tail = csr.tiers(csr.row_order[:nrows], ("plain", skip))
-        check_call(LIB.dglhip_gspmm_device(
-            msg, red, n_long, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
-            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
-            _stream_of(dev)))
-        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail)
-    elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
-        # source rows straddle cache lines: gather them from a padded copy
-        # (same values, same chains: identical results, fewer lines per row)
-        ld = padded_width(feat_len)
-        up = ufeat2.new_empty(ufeat2.shape[0], ld)
-        up[:, :feat_len] = ufeat2
-        check_call(LIB.dglhip_gspmm_strided_device(
-            msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ld,
-            ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(up), ptr(efeat2), elen, ptr(out),
-            ptr(csr.row_order), _stream_of(dev)))
-        del up
+        _run_rows(csr, msg, red, n_long, feat_len, ld, eid, ufeat2, efeat2, elen, out, arg)
+        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld)
     elif dev.type == "cuda":
-        check_call(LIB.dglhip_gspmm_device(
-            msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
-            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
-            _stream_of(dev)))
+        _run_rows(csr, msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ld,
+                  eid, ufeat2, efeat2, elen, out, arg)
     else:
         check_call(LIB.dglhip_gspmm_host(
             msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
@@ -541,14 +533,28 @@ def _tail_rows(csr, nrows, skip):
     return sum(t[2] for t in tail) >= _TIER_MIN_ROWS
 
 
-def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail):
+def _run_rows(csr, msg, red, nrows, feat_len, ld, eid, ufeat2, efeat2, elen, out, arg):
+    """The one-wave-per-row kernel over the first ``nrows`` rows of the
+    schedule (ufeat rows at stride ``ld`` when it is nonzero)."""
+    if ld:
+        check_call(LIB.dglhip_gspmm_strided_device(
+            msg, red, nrows, feat_len, ld, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
+            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(csr.row_order), _stream_of(out.device)))
+    else:
+        check_call(LIB.dglhip_gspmm_device(
+            msg, red, nrows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
+            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
+            _stream_of(out.device)))
+
+
+def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
     dev = out.device
     for maxd, (rows, sp, cols), n in tail:
         if maxd == 0 and red == RED_SUM_ACCUM:
             continue  # nothing to add
         check_call(LIB.dglhip_gspmm_short_rows_device(
             msg, red, n, feat_len, maxd, csr.num_rows, ptr(rows), ptr(sp), ptr(cols),
-            ptr(ufeat2), ptr(out), _stream_of(dev)))
+            ptr(ufeat2), ptr(out), ld, _stream_of(dev)))
 
 
 _PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")

@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from ... import function as fn
 from ... import kernel
 from ...base import DGLError
-from .linear import NodeLinear
+from .linear import NodeLinear, sage_dense
 
 __all__ = ["GraphConv", "GATConv", "SAGEConv", "RelGraphConv"]
 
@@ -117,13 +117,14 @@ class SAGEConv(nn.Module):
         self.activation = activation
 
     def forward(self, g, feat):
-        # fc_neigh (no bias) commutes with the mean: aggregate the narrower side
-        pre = self.fc_neigh.in_features > self.fc_neigh.out_features
-        g.ndata["_sage_h"] = self.fc_neigh(feat) if pre else feat
-        g.update_all(fn.copy_src("_sage_h", "_sage_m"), fn.mean("_sage_m", "_sage_n"))
-        g.ndata.pop("_sage_h")
-        neigh = g.ndata.pop("_sage_n")
-        rst = self.fc_self(feat) + (neigh if pre else self.fc_neigh(neigh))
+        def aggregate(x):
+            g.ndata["_sage_h"] = x
+            g.update_all(fn.copy_src("_sage_h", "_sage_m"), fn.mean("_sage_m", "_sage_n"))
+            g.ndata.pop("_sage_h")
+            return g.ndata.pop("_sage_n")
+        # fc_neigh (no bias) commutes with the mean: the narrower side is
+        # aggregated; both products and their sum fused (linear.sage_dense)
+        rst = sage_dense(feat, aggregate, self.fc_self, self.fc_neigh)
         return self.activation(rst) if self.activation else rst
 
 

@@ -164,7 +164,9 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
  * partial[c, :] (float32[num_chunks, feat_len] workspace), and heavy row
  * heavy_rows[h] = ((p[c0] + p[c0+1]) + ...) over its chunks
  * c0 = heavy_chunk_ptr[h] .. heavy_chunk_ptr[h+1]-1. Deterministic; differs
- * from the single chain only by re-association (fp32 tolerance, not bits). */
+ * from the single chain only by re-association (fp32 tolerance, not bits).
+ * ufeat_ld: row stride of ufeat in elements (0 = feat_len; an even padded
+ * width >= feat_len for line-aligned gathers, see dglhip_gspmm_strided_device). */
 int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 const int64_t* indptr, const int32_t* indices,
                                 const int64_t* eid, const float* ufeat,
@@ -174,7 +176,7 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                                 const int64_t* chunk_end, int64_t num_heavy,
                                 const int32_t* heavy_rows,
                                 const int64_t* heavy_chunk_ptr, float* partial,
-                                void* stream);
+                                int64_t ufeat_ld, void* stream);
 
 /* Range-list g-SpMM (sum): for every item i, out[i, :] = (accumulate ?
  * out[i, :] : 0) (+)= chain over slots [item_beg[i], item_end[i]) in slot
@@ -217,12 +219,14 @@ int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
  * power-law graph's degree-descending schedule where one wave per row leaves
  * the memory system idle. Longer items are still reduced correctly, in batches
  * of the kernel's depth. Results equal dglhip_gspmm_device's on the same rows
- * bit for bit. total_rows: rows of the whole output (non-temporal store rule). */
+ * bit for bit. total_rows: rows of the whole output (non-temporal store rule).
+ * ufeat_ld: row stride of ufeat in elements (0 = feat_len, else even and
+ * >= feat_len). */
 int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t num_items,
                                    int64_t feat_len, int64_t max_deg, int64_t total_rows,
                                    const int32_t* rows, const int64_t* slot_ptr,
                                    const int32_t* slot_cols, const float* ufeat, float* out,
-                                   void* stream);
+                                   int64_t ufeat_ld, void* stream);
 
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,

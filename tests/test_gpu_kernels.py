@@ -347,6 +347,42 @@ def test_padded_stride_gather(cuda, F, case):
         assert np.array_equal(padded.cpu().numpy(), O.spmm_coo(n, row, col, H))
 
 
+@pytest.mark.parametrize("F", [41, 24])
+@pytest.mark.parametrize("red", ["sum", "mean"])
+def test_padded_stride_with_split_and_tiers(cuda, F, red):
+    """The padded-stride gather composes with the heavy-row split (chunked
+    entry) and the short-row tiers (GraphSAGE's F = 41 layer on RMAT takes all
+    three): every combination of the three switches gives the same bits as
+    the plain gather under the same split setting, and the oracle for sum
+    without the split."""
+    rng = np.random.default_rng(F + 7)
+    n = 300_000
+    row, col = rand_graph(rng, n, n, 900_000, skew=True)
+    H = rng.uniform(-1, 1, (n, F)).astype(np.float32)
+    adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
+    Hd = torch.from_numpy(H).to(cuda)
+    assert kernel._pad_rows(kernel._MSG_NAMES["copy_u"], kernel._RED_NAMES[red], Hd, F)
+    outs = {}
+    for split in ("off", 2000):
+        for pad in ("auto", "off"):
+            for tiered in (True, False):
+                old_s, old_p = kernel.set_row_split(split), kernel.set_pad_rows(pad)
+                old_t = kernel.set_short_rows(tiered)
+                try:
+                    outs[(split, pad, tiered)] = kernel.gspmm(adj, "copy_u", red, Hd)
+                finally:
+                    kernel.set_row_split(old_s)
+                    kernel.set_pad_rows(old_p)
+                    kernel.set_short_rows(old_t)
+    for split in ("off", 2000):
+        ref = outs[(split, "off", False)]
+        for key, o in outs.items():
+            if key[0] == split:
+                assert torch.equal(o, ref), key
+    if red == "sum":
+        assert np.array_equal(outs[("off", "auto", True)].cpu().numpy(), O.spmm_coo(n, row, col, H))
+
+
 @pytest.mark.parametrize("red", ["sum", "mean"])
 @pytest.mark.parametrize("F", [128, 41, 2])
 def test_short_row_tiers(cuda, red, F):

@@ -79,6 +79,12 @@ for s in $STEPS; do
         rc=$?; tail -1 gpurun_out/emul_$tag.err; [ $rc -eq 0 ] || exit $rc
         python -c "import json; d=json.load(open('gpurun_out/emul_$tag.json')); print('$tag', d['ms_per_step'], d['roofline']['kernel_ms'])"
       done; done ;;
+    sageprof)
+      # kernel statistics of GraphSAGE-mean full-graph epochs on RMAT-$RMAT_SCALE (configs[3])
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sageprof -o run \
+        --output-format csv -- python examples/graphsage/train.py --graph rmat \
+        --rmat-scale ${RMAT_SCALE:-26} --gpu 0 --n-epochs ${EPOCHS:-4} > gpurun_out/sageprof.log 2>&1
+      rc=$?; tail -2 gpurun_out/sageprof.log; [ $rc -eq 0 ] || exit $rc ;;
     gcnprof)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/gcnprof -o run \
         --output-format csv -- python examples/gcn/gcn_spmv.py --dataset reddit --gpu 0 \

@@ -68,7 +68,7 @@ def main():
             for _ in range(args.iters):
                 _ffi.check_call(_ffi.LIB.dglhip_gspmm_short_rows_device(
                     0, 0, cnt_rows, F, maxd, n, _ffi.ptr(rows_t), _ffi.ptr(sp),
-                    _ffi.ptr(cols), _ffi.ptr(h), _ffi.ptr(out), stream))
+                    _ffi.ptr(cols), _ffi.ptr(h), _ffi.ptr(out), 0, stream))
             ms, cnt = kernel.timing_read()
             kernel.timing_enable(False)
         edges = int(deg[lo:hi].sum())
