@@ -467,7 +467,9 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
     ld = 0
-    if dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
+    if ufeat2 is not None and ufeat2.stride(0) != feat_len:
+        ld = ufeat2.stride(0)  # already row-padded by the caller (gspmm, _row_strided)
+    elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
         # source rows straddle cache lines: every schedule below gathers them
         # from a padded copy (same values, same chains: identical results,
         # fewer lines per row)
@@ -644,6 +646,13 @@ def _eid_major(adj):
     return fwd, False
 
 
+def _row_strided(t, F):
+    """A (rows, F) float32 view whose rows sit at an even stride > F (a
+    row-padded buffer): the strided g-SpMM entries read it as it is."""
+    return (t.dim() == 2 and t.dtype == torch.float32 and t.shape[1] == F and
+            t.stride(1) == 1 and t.stride(0) > F and t.stride(0) % 2 == 0)
+
+
 def _f32c(t):
     if t is None:
         return None
@@ -788,7 +797,11 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None, edge_order="
         F *= int(s)
     dev = (ufeat if ufeat is not None else efeat).device
     adj = adj.to(dev)
-    u2 = None if ufeat is None else _f32c(ufeat.reshape(ufeat.shape[0], F))
+    if ufeat is not None and _row_strided(ufeat, F) and dev.type == "cuda" and \
+            msg == MSG_COPY_U and red in (RED_SUM, RED_MEAN):
+        u2 = ufeat  # rows at a padded stride: gathered in place (_run_gspmm)
+    else:
+        u2 = None if ufeat is None else _f32c(ufeat.reshape(ufeat.shape[0], F))
     e2 = None
     if efeat is not None:
         ne = efeat.shape[0]

@@ -85,14 +85,90 @@ def _mm_t(x, w):
     return x.matmul(w.t())
 
 
+# -- MFMA node Linear (csrc/node_linear.hip) ----------------------------------
+# The narrow products of a GraphSAGE output layer (in 64/128/256, out <= 64)
+# run on the library's f32 MFMA kernels: both products of the input rows in one
+# pass, and the input gradient of both in one pass. Other shapes (and CPU
+# tensors) take torch's GEMMs, which run them at their rate already.
+
+def _mfma_fwd_ok(x, *ms):
+    return (x.is_cuda and x.dtype == torch.float32 and x.dim() == 2 and x.stride(1) == 1 and
+            x.stride(0) % 4 == 0 and x.shape[1] in (64, 128, 256) and x.data_ptr() % 16 == 0 and
+            all(1 <= m <= 64 for m in ms))
+
+
+def _mfma_dgrad_ok(k, *dys):
+    return k in (64, 128) and all(
+        d.is_cuda and d.dtype == torch.float32 and d.dim() == 2 and d.stride(1) == 1 and
+        1 <= d.shape[1] <= 64 for d in dys)
+
+
+def _w(t):
+    return None if t is None else t.detach().contiguous()
+
+
+def _node_linear2(x, w1, ld1, w2, b2):
+    """(y1 (n, m1) viewed out of rows padded to ld1, y2 = x W2^T + b2), one pass."""
+    from ... import _ffi, kernel
+    n, k = x.shape
+    m1, m2 = w1.shape[0], w2.shape[0]
+    w1, w2, b2 = _w(w1), _w(w2), _w(b2)
+    y1 = torch.empty(n, ld1, dtype=torch.float32, device=x.device)
+    y2 = torch.empty(n, m2, dtype=torch.float32, device=x.device)
+    _ffi.check_call(_ffi.LIB.dglhip_node_linear_device(
+        n, k, _ffi.ptr(x), x.stride(0), m1, _ffi.ptr(w1), None, _ffi.ptr(y1), ld1, m2,
+        _ffi.ptr(w2), _ffi.ptr(b2), _ffi.ptr(y2), m2, kernel._stream_of(x.device)))
+    return y1[:, :m1], y2
+
+
+def _mfma_cat_ok(x1, x2, m):
+    # up to 64 outputs (one pass over the inputs); at 128 outputs hipBLASLt's
+    # tiles run the two products as fast (43.3 vs 44.4 ms at 67M rows,
+    # tools/node_linear_bench.py)
+    return (1 <= m <= 64 and x1.shape == x2.shape and all(
+        t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and
+        t.stride(0) % 4 == 0 and t.shape[1] in (64, 128) and t.data_ptr() % 16 == 0
+        for t in (x1, x2)))
+
+
+def _node_linear_cat(x1, w1, x2, w2, b):
+    """x1 W1^T + x2 W2^T + b in one pass per 64 outputs."""
+    from ... import _ffi, kernel
+    n, k = x1.shape
+    m = w1.shape[0]
+    w1, w2, b = _w(w1), _w(w2), _w(b)
+    y = torch.empty(n, m, dtype=torch.float32, device=x1.device)
+    _ffi.check_call(_ffi.LIB.dglhip_node_linear_cat_device(
+        n, k, _ffi.ptr(x1), x1.stride(0), _ffi.ptr(x2), x2.stride(0), m, _ffi.ptr(w1),
+        _ffi.ptr(w2), _ffi.ptr(b), _ffi.ptr(y), m, kernel._stream_of(x1.device)))
+    return y
+
+
+def _node_dgrad2(k, dy1, w1, dy2, w2):
+    """dy1 W1 + dy2 W2 in one pass (n, k)."""
+    from ... import _ffi, kernel
+    n = dy1.shape[0]
+    w1, w2 = _w(w1), _w(w2)
+    dx = torch.empty(n, k, dtype=torch.float32, device=dy1.device)
+    _ffi.check_call(_ffi.LIB.dglhip_node_linear_dgrad_device(
+        n, k, dy1.shape[1], _ffi.ptr(dy1), dy1.stride(0), _ffi.ptr(w1), dy2.shape[1],
+        _ffi.ptr(dy2), dy2.stride(0), _ffi.ptr(w2), _ffi.ptr(dx), k,
+        kernel._stream_of(dy1.device)))
+    return dx
+
+
 class _DualLinearFn(torch.autograd.Function):
-    """out = x @ Ws^T + b + agg @ Wn^T as one GEMM and one accumulating GEMM
-    (beta = 1): no separate sum pass, and neither product is materialised."""
+    """out = x @ Ws^T + b + agg @ Wn^T as one product over the concatenated
+    inputs (the MFMA kernel: one pass over x and agg), or one GEMM and one
+    accumulating GEMM (beta = 1): no separate sum pass, and neither product
+    is materialised."""
 
     @staticmethod
     def forward(ctx, x, w_self, bias, agg, w_neigh):
         ctx.save_for_backward(x, w_self, agg, w_neigh)
         ctx.has_bias = bias is not None
+        if _mfma_cat_ok(x, agg, w_self.shape[0]):
+            return _node_linear_cat(x, w_self, agg, w_neigh, bias)
         out = torch.addmm(bias, x, w_self.t()) if bias is not None else _mm_t(x, w_self)
         out.addmm_(agg, w_neigh.t())
         return out
@@ -119,7 +195,15 @@ class _PreAggregateFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w_self, bias, w_neigh, aggregate):
-        pre = _mm_t(x, w_neigh)
+        self_out = None
+        if _mfma_fwd_ok(x, w_neigh.shape[0], w_self.shape[0]):
+            # both products in one pass over x; the aggregated one at a
+            # line-aligned row stride, gathered by the g-SpMM without a copy
+            from ... import kernel
+            pre, self_out = _node_linear2(x, w_neigh, kernel.padded_width(w_neigh.shape[0]),
+                                          w_self, bias)
+        else:
+            pre = _mm_t(x, w_neigh)
         if any(ctx.needs_input_grad):
             with torch.enable_grad():
                 pre_leaf = pre.detach().requires_grad_(True)
@@ -130,9 +214,13 @@ class _PreAggregateFn(torch.autograd.Function):
         # accumulate into the aggregate's own buffer (its backward does not
         # read it): no copy of an (N, out) tensor
         out = neigh.detach()
-        out.addmm_(x, w_self.t())
-        if bias is not None:
-            out.add_(bias)
+        if self_out is not None:
+            out.add_(self_out)
+            del self_out
+        else:
+            out.addmm_(x, w_self.t())
+            if bias is not None:
+                out.add_(bias)
         ctx.save_for_backward(x, w_self, w_neigh)
         ctx.graph = (pre_leaf, neigh) if pre_leaf is not None else None
         ctx.has_bias = bias is not None
@@ -149,8 +237,11 @@ class _PreAggregateFn(torch.autograd.Function):
         dpre = dpre.contiguous()
         dx = None
         if need[0]:
-            dx = dy.matmul(w_self)
-            dx.addmm_(dpre, w_neigh)
+            if _mfma_dgrad_ok(x.shape[1], dy, dpre):
+                dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh)
+            else:
+                dx = dy.matmul(w_self)
+                dx.addmm_(dpre, w_neigh)
         dws = _splitk_tn(dy, x.contiguous()) if need[1] else None
         db = _colsum(dy) if ctx.has_bias and need[2] else None
         dwn = _splitk_tn(dpre, x.contiguous()) if need[3] else None

@@ -228,6 +228,41 @@ int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t num_items,
                                    const int32_t* slot_cols, const float* ufeat, float* out,
                                    int64_t ufeat_ld, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* Dense per-node Linear on the f32 MFMA (the Linear that follows a g-SpMM;  */
+/* csrc/node_linear.hip). No reference counterpart: the reference runs these */
+/* products as torch nn.Linear (examples/pytorch/gcn/gcn_spmv.py:45-62).     */
+/* ------------------------------------------------------------------------ */
+/* y1 = x W1^T (+ b1) and, with m2 > 0, y2 = x W2^T (+ b2) in one pass over
+ * the num_rows rows of x (row stride ldx, a multiple of 4; 16-byte aligned).
+ * in_feats 64, 128 or 256; 1 <= m1 <= 64, 0 <= m2 <= 64; W row-major [m][in_feats]
+ * (nn.Linear's weight); b may be NULL; outputs at their own row strides. Each
+ * output element is one f32 fma chain over the inputs (exact f32). */
+int dglhip_node_linear_device(int64_t num_rows, int64_t in_feats, const float* x, int64_t ldx,
+                              int64_t m1, const float* w1, const float* b1, float* y1,
+                              int64_t ldy1, int64_t m2, const float* w2, const float* b2,
+                              float* y2, int64_t ldy2, void* stream);
+
+/* y = x1 W1^T + x2 W2^T (+ b): one output from two inputs of in_feats (64 or
+ * 128) columns each (GraphSAGE's fc_self(h) + fc_neigh(agg)); W1, W2 [m][in_feats],
+ * 1 <= m <= 128 (one pass over the inputs per 64 outputs). */
+int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const float* x1,
+                                  int64_t ldx1, const float* x2, int64_t ldx2, int64_t m,
+                                  const float* w1, const float* w2, const float* b, float* y,
+                                  int64_t ldy, void* stream);
+
+/* Tuning knob of the three node-Linear entries: lanes per workgroup (256 or
+ * 512) and workgroups per CU; 0 restores the automatic choice. Results do not
+ * depend on it. */
+int dglhip_set_node_linear_variant(int threads, int wgs_per_cu);
+
+/* Input gradient of the first: dx = dy1 W1 + dy2 W2 (m2 = 0: dy1 W1 only);
+ * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx. */
+int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t m1,
+                                    const float* dy1, int64_t lddy1, const float* w1, int64_t m2,
+                                    const float* dy2, int64_t lddy2, const float* w2, float* dx,
+                                    int64_t lddx, void* stream);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,
