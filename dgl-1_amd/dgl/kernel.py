@@ -49,8 +49,9 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 
 
 # Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device):
-#   "auto" : (default) rows are cut into chunks of max(4096, nnz / 12000) slots,
-#            but only when the longest row is the launch's critical path: a row
+#   "auto" : (default) rows longer than max(4096, nnz / 12000) slots are cut
+#            into chunks (CSR.split_plan sizes them to fill the chip), but only
+#            when the longest row is the launch's critical path: a row
 #            is one wave's sequential chain, the launch spreads its slots over
 #            ~7168 resident waves (256 CUs x 4 SIMDs x 7), and rows start
 #            longest-first, so a row longer than twice a wave's share
@@ -70,6 +71,10 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 _ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
 _CRITICAL_SHARE = 3584  # half the resident waves of a full-chip launch
 _CRITICAL_MIN = 16384   # rows up to this length are never split by "auto"
+# chunk length of the split rows: their slots over this many waves (half the
+# chip's resident waves), chunks of at least _CHUNK_MIN slots
+_CHUNK_WAVES = 4096
+_CHUNK_MIN = 1024
 
 
 def set_row_split(policy):
@@ -173,12 +178,18 @@ class CSR(object):
             self._num_nonempty = int((ip[1:] > ip[:-1]).sum()) if self.num_rows else 0
         return self._num_nonempty
 
-    def split_plan(self, threshold, skip_empty=False):
+    def split_plan(self, threshold, skip_empty=False, chunk=None):
         """Launch plan cutting rows longer than ``threshold`` slots into chunks
-        (cached per threshold): dict of device tensors for
+        of ``chunk`` slots (cached per arguments): dict of device tensors for
         dglhip_gspmm_chunked_device. ``skip_empty`` leaves rows without slots
-        out of the light list (accumulating launches need not touch them)."""
-        key = (threshold, bool(skip_empty))
+        out of the light list (accumulating launches need not touch them).
+        ``chunk`` None: enough chunks to spread the heavy rows' slots over
+        _CHUNK_WAVES waves (at least _CHUNK_MIN slots each, at most
+        ``threshold``). The chunk launch runs alone before the light rows, so
+        it must fill the chip: with chunks of ``threshold`` slots RMAT-26's 27
+        hub rows made 88 chunks, 88 waves chaining 89k gathers each for 6.6 ms
+        of a 82 ms call."""
+        key = (threshold, bool(skip_empty), chunk)
         if key in self._plans:
             return self._plans[key]
         ip = self.host_indptr.numpy()
@@ -190,6 +201,10 @@ class CSR(object):
         heavy_mask = deg[order] > threshold
         light = order[~heavy_mask].astype(np.int32)
         heavy = order[heavy_mask]
+        if chunk is None:
+            heavy_slots = int(deg[heavy].sum())
+            chunk = min(threshold, max(_CHUNK_MIN, -(-heavy_slots // _CHUNK_WAVES)))
+        threshold = int(chunk)  # the cut length below
         nchunks = (deg[heavy] + threshold - 1) // threshold
         ptr = np.concatenate([[0], np.cumsum(nchunks)]).astype(np.int64)
         rep = np.repeat(np.arange(len(heavy)), nchunks)
@@ -480,7 +495,8 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     tiered = (dev.type == "cuda" and _TIERED and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and
               red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM))
     if split:
-        p = csr.split_plan(split, skip_empty=skip)
+        # "auto" sizes the chunks to fill the chip; an explicit policy is the chunk length
+        p = csr.split_plan(split, skip_empty=skip, chunk=None if _ROW_SPLIT == "auto" else split)
         partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
         light = p["light"]
         n_light, tail = light.numel(), []
