@@ -482,8 +482,8 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
     skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
     ld = 0
-    if ufeat2 is not None and ufeat2.stride(0) != feat_len:
-        ld = ufeat2.stride(0)  # already row-padded by the caller (gspmm, _row_strided)
+    if ufeat2 is not None and ufeat2.shape[0] > 1 and _row_strided(ufeat2, feat_len):
+        ld = ufeat2.stride(0)  # already row-padded by the caller (gspmm)
     elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
         # source rows straddle cache lines: every schedule below gathers them
         # from a padded copy (same values, same chains: identical results,

@@ -256,7 +256,8 @@ def sage_dense(h, aggregate, fc_self, fc_neigh):
     accumulating GEMM in both directions, which at 10^7-10^8 nodes saves a
     pass over an (N, out) tensor per direction and two (N, out) buffers of
     peak memory (RMAT-26: 34 GB each)."""
-    if h.dim() != 2:
+    if h.dim() != 2 or fc_neigh.bias is not None:
+        # (a bias on fc_neigh would not commute with the mean's empty rows)
         return fc_self(h) + fc_neigh(aggregate(h))
     if fc_neigh.in_features > fc_neigh.out_features:
         return _PreAggregateFn.apply(h, fc_self.weight, fc_self.bias, fc_neigh.weight,
