@@ -224,6 +224,30 @@ def timed_steps(step, steps, warmup, world, dev):
     return elapsed, kms / steps
 
 
+def exchange_block(pg, h_local, steps, world, dev):
+    """N > 1: the halo exchange of one step alone (the pack, then RCCL's
+    all_gather_into_tensor or all_to_all_single, as the step issues it, in
+    one piece), timed like the step; with the step's own time it shows how
+    much of the exchange the pipelined segments hide."""
+    from dgl.distributed import _AllGatherRows, _AllToAllRows
+    if pg.halo_mode == "alltoall":
+        def step():
+            _AllToAllRows.apply(h_local, pg.send_idx, pg.send_splits, pg.recv_splits, pg.group,
+                                pg.halo_dtype)
+        recv_rows = sum(pg.recv_splits)
+    else:
+        def step():
+            _AllGatherRows.apply(h_local, pg.max_rows, pg.group, pg.halo_dtype)
+        recv_rows = (world - 1) * pg.max_rows
+    el, _ = timed_steps(step, steps, 1, world, dev)
+    per = el / steps
+    nbytes = recv_rows * FEAT * (2 if pg.halo_dtype is not None else 4)
+    return {"ms_per_step": per * 1e3, "mode": pg.halo_mode, "recv_bytes_rank0": nbytes,
+            "recv_GBs_rank0": nbytes / per / 1e9,
+            "note": "the step's halo exchange alone (max over ranks); rank 0's received "
+                    "bytes over that time"}
+
+
 def rmat_leg(args, world, rank, dev, pmc=None):
     """RMAT strong scaling on the same ranks: one fixed graph, 1-D dst-row
     partition, heavy rows chunked (kernel.set_row_split("auto"))."""
@@ -263,6 +287,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
         elapsed, kms = timed_steps(step, steps, 2, world, dev)
+        exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
         roof = None
         if not dist.is_initialized():
             # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
@@ -285,7 +310,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
                           "%d nodes, %d edges, feat=%d, heavy rows chunked"
                           % (args.rmat_scale, n, E, FEAT),
                 "parallelism": par, "kernel_ms_rank0": kms, "roofline": roof,
-                "cpu_baseline": cpu}
+                "halo_exchange": exch, "cpu_baseline": cpu}
     finally:
         kernel.set_row_split(old)
 
@@ -529,6 +554,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if dist.is_initialized():
+        result["halo_exchange"] = exchange_block(pg, h_local, args.steps, world, dev)
     if dist.is_initialized() and args.halo_dtype == "fp32" and not args.no_bf16_leg:
         # the opt-in bf16 halo on the same partition (not the headline: remote
         # rows are rounded to bf16, so rows are no longer bit-exact)
