@@ -41,6 +41,7 @@ struct LinOut {
   float* y;         // rows at stride ldy
   int64_t ldy;
   int m;
+  int relu;         // store max(y, 0) (the activation fused into the store)
 };
 
 // y_o = [x1 | x2] [W_o | Wb_o]^T + b_o for T1 (T2) 16-column tiles of output
@@ -127,7 +128,7 @@ __global__ __launch_bounds__(512) void node_linear_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t orow = r0 + 4 * h + i;
-        if (orow < n) o.y[orow * o.ldy + c] = acc[t][i];
+        if (orow < n) o.y[orow * o.ldy + c] = o.relu ? fmaxf(acc[t][i], 0.0f) : acc[t][i];
       }
     }
 #pragma unroll
@@ -331,8 +332,8 @@ int dglhip_node_linear_device(int64_t num_rows, int64_t in_feats, const float* x
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(x && w1 && y1 && (m2 == 0 || (w2 && y2)), "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(x) % 16 == 0, "x must be 16-byte aligned");
-  LinOut o1{w1, nullptr, b1, y1, ldy1, static_cast<int>(m1)};
-  LinOut o2{w2, nullptr, b2, y2, ldy2, static_cast<int>(m2)};
+  LinOut o1{w1, nullptr, b1, y1, ldy1, static_cast<int>(m1), 0};
+  LinOut o2{w2, nullptr, b2, y2, ldy2, static_cast<int>(m2), 0};
   const int t1 = static_cast<int>((m1 + 15) / 16), t2 = static_cast<int>((m2 + 15) / 16);
   switch (in_feats / 64) {
     case 1: dispatch_fwd<1>(t1, t2, num_rows, x, ldx, o1, o2, stream); break;
@@ -355,7 +356,7 @@ int dglhip_set_node_linear_variant(int threads, int wgs_per_cu) {
 int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const float* x1,
                                   int64_t ldx1, const float* x2, int64_t ldx2, int64_t m,
                                   const float* w1, const float* w2, const float* b, float* y,
-                                  int64_t ldy, void* stream_) {
+                                  int64_t ldy, int relu, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0, "negative row count");
@@ -373,7 +374,7 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
   // per operand); wider outputs take one pass per 64 columns
   for (int64_t c0 = 0; c0 < m; c0 += 64) {
     LinOut o{w1 + c0 * in_feats, w2 + c0 * in_feats, b ? b + c0 : nullptr, y + c0, ldy,
-             static_cast<int>(std::min<int64_t>(64, m - c0))};
+             static_cast<int>(std::min<int64_t>(64, m - c0)), relu ? 1 : 0};
     if (in_feats == 64) launch_fwd<1, 1, 4, 0>(num_rows, x1, ldx1, x2, ldx2, o, o, stream);
     else launch_fwd<2, 2, 4, 0>(num_rows, x1, ldx1, x2, ldx2, o, o, stream);
   }

@@ -93,7 +93,8 @@ def _load():
         "dglhip_node_linear_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _c_i64, _vp, _vp,
                                                _vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_node_linear_cat_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _c_i64,
-                                                   _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
+                                                   _c_i64, _vp, _vp, _vp, _vp, _c_i64, _c_int,
+                                                   _vp]),
         "dglhip_set_node_linear_variant": (_c_int, [_c_int, _c_int]),
         "dglhip_node_linear_dgrad_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp,
                                                      _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),

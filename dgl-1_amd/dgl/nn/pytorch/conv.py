@@ -124,8 +124,7 @@ class SAGEConv(nn.Module):
             return g.ndata.pop("_sage_n")
         # fc_neigh (no bias) commutes with the mean: the narrower side is
         # aggregated; both products and their sum fused (linear.sage_dense)
-        rst = sage_dense(feat, aggregate, self.fc_self, self.fc_neigh)
-        return self.activation(rst) if self.activation else rst
+        return sage_dense(feat, aggregate, self.fc_self, self.fc_neigh, self.activation)
 
 
 class RelGraphConv(nn.Module):

@@ -121,18 +121,19 @@ def _node_linear2(x, w1, ld1, w2, b2):
     return y1[:, :m1], y2
 
 
-def _mfma_cat_ok(x1, x2, m):
-    # up to 64 outputs (one pass over the inputs); at 128 outputs hipBLASLt's
-    # tiles run the two products as fast (43.3 vs 44.4 ms at 67M rows,
-    # tools/node_linear_bench.py)
-    return (1 <= m <= 64 and x1.shape == x2.shape and all(
+def _mfma_cat_ok(x1, x2, m, relu=False):
+    # up to 64 outputs (one pass over the inputs), or 128 with the ReLU fused
+    # into the store; without it hipBLASLt's tiles run the two 128-output
+    # products as fast (43.3 vs 44.4 ms at 67M rows, tools/node_linear_bench.py)
+    return (1 <= m <= (128 if relu else 64) and x1.shape == x2.shape and all(
         t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and
         t.stride(0) % 4 == 0 and t.shape[1] in (64, 128) and t.data_ptr() % 16 == 0
         for t in (x1, x2)))
 
 
-def _node_linear_cat(x1, w1, x2, w2, b):
-    """x1 W1^T + x2 W2^T + b in one pass per 64 outputs."""
+def _node_linear_cat(x1, w1, x2, w2, b, relu=False):
+    """x1 W1^T + x2 W2^T + b (relu: max(., 0) fused into the store) in one
+    pass per 64 outputs."""
     from ... import _ffi, kernel
     n, k = x1.shape
     m = w1.shape[0]
@@ -140,7 +141,7 @@ def _node_linear_cat(x1, w1, x2, w2, b):
     y = torch.empty(n, m, dtype=torch.float32, device=x1.device)
     _ffi.check_call(_ffi.LIB.dglhip_node_linear_cat_device(
         n, k, _ffi.ptr(x1), x1.stride(0), _ffi.ptr(x2), x2.stride(0), m, _ffi.ptr(w1),
-        _ffi.ptr(w2), _ffi.ptr(b), _ffi.ptr(y), m, kernel._stream_of(x1.device)))
+        _ffi.ptr(w2), _ffi.ptr(b), _ffi.ptr(y), m, int(relu), kernel._stream_of(x1.device)))
     return y
 
 
@@ -158,24 +159,31 @@ def _node_dgrad2(k, dy1, w1, dy2, w2):
 
 
 class _DualLinearFn(torch.autograd.Function):
-    """out = x @ Ws^T + b + agg @ Wn^T as one product over the concatenated
-    inputs (the MFMA kernel: one pass over x and agg), or one GEMM and one
-    accumulating GEMM (beta = 1): no separate sum pass, and neither product
-    is materialised."""
+    """out = x @ Ws^T + b + agg @ Wn^T (relu: max(., 0)) as one product over
+    the concatenated inputs (the MFMA kernel: one pass over x and agg, the
+    ReLU in its store), or one GEMM and one accumulating GEMM (beta = 1): no
+    separate sum pass, and neither product is materialised. With relu the
+    output is saved and the backward masks dy by out > 0 (ReLU's own rule)."""
 
     @staticmethod
-    def forward(ctx, x, w_self, bias, agg, w_neigh):
-        ctx.save_for_backward(x, w_self, agg, w_neigh)
+    def forward(ctx, x, w_self, bias, agg, w_neigh, relu):
         ctx.has_bias = bias is not None
-        if _mfma_cat_ok(x, agg, w_self.shape[0]):
-            return _node_linear_cat(x, w_self, agg, w_neigh, bias)
-        out = torch.addmm(bias, x, w_self.t()) if bias is not None else _mm_t(x, w_self)
-        out.addmm_(agg, w_neigh.t())
+        ctx.relu = bool(relu)
+        if _mfma_cat_ok(x, agg, w_self.shape[0], relu):
+            out = _node_linear_cat(x, w_self, agg, w_neigh, bias, relu)
+        else:
+            out = torch.addmm(bias, x, w_self.t()) if bias is not None else _mm_t(x, w_self)
+            out.addmm_(agg, w_neigh.t())
+            if relu:
+                out.relu_()
+        ctx.save_for_backward(x, w_self, agg, w_neigh, out if relu else None)
         return out
 
     @staticmethod
     def backward(ctx, dy):
-        x, w_self, agg, w_neigh = ctx.saved_tensors
+        x, w_self, agg, w_neigh, out = ctx.saved_tensors
+        if ctx.relu:
+            dy = torch.ops.aten.threshold_backward(dy, out, 0)  # ReLU's own backward, one pass
         dy = dy.contiguous()
         need = ctx.needs_input_grad
         dx = dy.matmul(w_self) if need[0] else None
@@ -183,7 +191,7 @@ class _DualLinearFn(torch.autograd.Function):
         db = _colsum(dy) if ctx.has_bias and need[2] else None
         dagg = dy.matmul(w_neigh) if need[3] else None
         dwn = _splitk_tn(dy, agg.contiguous()) if need[4] else None
-        return dx, dws, db, dagg, dwn
+        return dx, dws, db, dagg, dwn, None
 
 
 class _PreAggregateFn(torch.autograd.Function):
@@ -248,21 +256,32 @@ class _PreAggregateFn(torch.autograd.Function):
         return dx, dws, db, dwn, None
 
 
-def sage_dense(h, aggregate, fc_self, fc_neigh):
+def _is_relu(act):
+    return act in (torch.relu, torch.nn.functional.relu) or isinstance(act, torch.nn.ReLU)
+
+
+def sage_dense(h, aggregate, fc_self, fc_neigh, activation=None):
     """GraphSAGE's dense step fc_self(h) + fc_neigh(aggregate(h)) on
     NodeLinear weights (fc_neigh without bias), shaped for full-graph node
     counts. fc_neigh commutes with the (linear) aggregation, so the narrower
     side is aggregated; the two products and their sum are one GEMM plus one
     accumulating GEMM in both directions, which at 10^7-10^8 nodes saves a
     pass over an (N, out) tensor per direction and two (N, out) buffers of
-    peak memory (RMAT-26: 34 GB each)."""
+    peak memory (RMAT-26: 34 GB each). ``activation`` is applied to the sum;
+    a ReLU on the widening / square layer is fused into the product's store
+    (its backward mask into the fused backward)."""
+    def act(t):
+        return activation(t) if activation is not None else t
     if h.dim() != 2 or fc_neigh.bias is not None:
         # (a bias on fc_neigh would not commute with the mean's empty rows)
-        return fc_self(h) + fc_neigh(aggregate(h))
+        return act(fc_self(h) + fc_neigh(aggregate(h)))
     if fc_neigh.in_features > fc_neigh.out_features:
-        return _PreAggregateFn.apply(h, fc_self.weight, fc_self.bias, fc_neigh.weight,
-                                     aggregate)
-    return _DualLinearFn.apply(h, fc_self.weight, fc_self.bias, aggregate(h), fc_neigh.weight)
+        return act(_PreAggregateFn.apply(h, fc_self.weight, fc_self.bias, fc_neigh.weight,
+                                         aggregate))
+    relu = _is_relu(activation)
+    out = _DualLinearFn.apply(h, fc_self.weight, fc_self.bias, aggregate(h), fc_neigh.weight,
+                              relu)
+    return out if relu else act(out)
 
 
 class NodeLinear(nn.Module):

@@ -52,9 +52,8 @@ class SAGELayer(nn.Module):
     def forward(self, h, aggregate):
         # fc_self(h) + fc_neigh(aggregate(h)), the narrower side aggregated,
         # both products and their sum fused (dgl.nn.pytorch.sage_dense)
-        h = sage_dense(h, aggregate, self.fc_self, self.fc_neigh)
-        # in place: the fused step's output is not saved for its backward
-        return self.activation(h, inplace=True) if self.activation else h
+        # the activation fused into the dense step where it can be (ReLU)
+        return sage_dense(h, aggregate, self.fc_self, self.fc_neigh, self.activation)
 
 
 class SAGE(nn.Module):

@@ -159,9 +159,19 @@ def test_sage_dense_matches_unfused(dims):
         torch.testing.assert_close(xb.grad, xa.grad, rtol=1e-4, atol=1e-4)
         for a, b in ((fs.weight, rs.weight), (fs.bias, rs.bias), (fnb.weight, rnb.weight)):
             torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-3)
-        # the activation may run in place on the fused output
-        torch.nn.functional.relu(sage_dense(x.clone().requires_grad_(True), aggregate, fs, fnb),
-                                 inplace=True).sum().backward()
+        # a ReLU fused into the step (widening / square) or applied after it
+        for p in (fs.weight, fs.bias, fnb.weight, rs.weight, rs.bias, rnb.weight):
+            p.grad = None
+        xc = x.clone().requires_grad_(True)
+        xd = x.clone().requires_grad_(True)
+        o1 = sage_dense(xc, aggregate, fs, fnb, torch.nn.functional.relu)
+        o2 = torch.relu(rs(xd) + rnb(aggregate(xd)))
+        torch.testing.assert_close(o1, o2, rtol=1e-5, atol=1e-5)
+        o1.backward(dy)
+        o2.backward(dy)
+        torch.testing.assert_close(xc.grad, xd.grad, rtol=1e-4, atol=1e-4)
+        for a, b in ((fs.weight, rs.weight), (fs.bias, rs.bias), (fnb.weight, rnb.weight)):
+            torch.testing.assert_close(a.grad, b.grad, rtol=1e-4, atol=1e-3)
         with torch.no_grad():  # inference path (no graph kept)
             torch.testing.assert_close(sage_dense(x, aggregate, fs, fnb), ref.detach(),
                                        rtol=1e-5, atol=1e-5)

@@ -163,6 +163,9 @@ def test_cat_exact_integers(cuda, k, m):
     # sage_dense routes up to 64 outputs here; the entry takes up to 128
     # (one pass per 64 columns)
     assert L._mfma_cat_ok(x1, x2, m) == (m <= 64)
+    assert L._mfma_cat_ok(x1, x2, m, relu=True)
     y = L._node_linear_cat(x1, w1, x2, w2, b)
     ref = x1.double() @ w1.double().t() + x2.double() @ w2.double().t() + b.double()
     assert torch.equal(y.double(), ref)
+    yr = L._node_linear_cat(x1, w1, x2, w2, b, relu=True)
+    assert torch.equal(yr.double(), ref.clamp(min=0))
