@@ -109,17 +109,33 @@ __global__ __launch_bounds__(512) void node_linear_fwd_kernel(
     f32x4 acc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = f32x4{bias[t], bias[t], bias[t], bias[t]};
+    // weight operands of one float4 group (4 k-steps x T tiles) come from LDS
+    // one group ahead of the MFMAs that use them: the LDS latency overlaps
+    // the previous group's MFMAs instead of stalling each one
+    float bw[2][4][T];
+    auto load_w = [&](int g, float (&b)[4][T]) {
+      const int p = g >> 2, j = g & 3;
 #pragma unroll
-    for (int p = 0; p < KB; ++p)
+      for (int c = 0; c < 4; ++c) {
+        const float* wk = wt + (64 * p + 16 * j + 4 * h + c) * SW + r;
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+        for (int t = 0; t < T; ++t) b[c][t] = wk[16 * t];
+      }
+    };
+    load_w(0, bw[0]);
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          const float* wk = wt + (64 * p + 16 * j + 4 * h + c) * SW + r;
+    for (int g = 0; g < 4 * KB; ++g) {
+      if (g + 1 < 4 * KB) load_w(g + 1, bw[(g + 1) & 1]);
+      // keep the scheduler from sinking those reads back next to their MFMAs
+      __builtin_amdgcn_sched_barrier(0);
+      const int p = g >> 2, j = g & 3;
 #pragma unroll
-          for (int t = 0; t < T; ++t)
-            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p][j][c], wk[16 * t], acc[t], 0, 0, 0);
-        }
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p][j][c], bw[g & 1][c][t], acc[t], 0,
+                                                        0, 0);
+    }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
       const LinOut& o = t < T1 ? o1 : o2;
@@ -190,12 +206,21 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
     f32x4 acc[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
+    // weight operands one step ahead of their MFMAs (see the forward kernel)
+    float bw[2][KT];
+    auto load_w = [&](int s, float (&b)[KT]) {
       const float* ws = wl + (4 * s + h) * SK + r;
 #pragma unroll
+      for (int t = 0; t < KT; ++t) b[t] = ws[16 * t];
+    };
+    load_w(0, bw[0]);
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (s + 1 < S) load_w(s + 1, bw[(s + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
       for (int t = 0; t < KT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], ws[16 * t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[s & 1][t], acc[t], 0, 0, 0);
     }
 #pragma unroll
     for (int t = 0; t < KT; ++t)
