@@ -122,3 +122,52 @@ def test_gat_hip_graph_replay_matches_eager():
     assert graph["hip_graph"]
     assert not [w for w in caught if "AccumulateGrad" in str(w.message)]
     assert abs(graph["loss"] - eager["loss"]) < 1e-6 * max(1.0, abs(eager["loss"]))
+
+
+def test_gcn_cora_training_trajectory_equals_reference_arithmetic():
+    """configs[0] on the host: 2-layer GCN training through the engine's host
+    g-SpMM and through the reference's CPU arithmetic (torch.sparse.mm on the
+    uncoalesced COO, forward and its autograd backward) follow the SAME
+    trajectory, loss for loss and weight for weight: every g-SpMM and its
+    transpose reproduce the reference's chains bit for bit."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "cpu_gcn_cora", os.path.join(os.path.dirname(__file__), "..", "tools", "cpu_gcn_cora.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    import torch
+    import dgl
+    import dgl.function as fn
+    from dgl import data
+    ds = data.load_data("cora", seed=0, device="cpu")
+    src, dst = ds.graph
+    n = ds.num_nodes
+    loops = torch.arange(n)
+    src, dst = torch.cat([src, loops]), torch.cat([dst, loops])
+    g = dgl.DGLGraph((src, dst))
+    norm = torch.bincount(dst, minlength=n).float().clamp(min=1).pow(-0.5).unsqueeze(1)
+
+    def engine(h):
+        g.ndata["h"] = h
+        g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h"))
+        return g.ndata.pop("h")
+
+    A = torch.sparse_coo_tensor(torch.stack([dst, src]), torch.ones(src.numel()), (n, n))
+    runs = []
+    for spmm in (engine, lambda h: torch.sparse.mm(A, h)):
+        torch.manual_seed(0)
+        model = mod.GCN(ds.features.shape[1], 16, ds.num_labels, spmm)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+        losses = []
+        for _ in range(30):
+            loss = torch.nn.functional.cross_entropy(model(ds.features, norm)[ds.train_mask],
+                                                     ds.labels[ds.train_mask])
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            losses.append(loss.item())
+        runs.append((losses, [p.detach().clone() for p in model.parameters()]))
+    assert runs[0][0] == runs[1][0]
+    for a, b in zip(runs[0][1], runs[1][1]):
+        assert torch.equal(a, b)
