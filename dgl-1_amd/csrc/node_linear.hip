@@ -352,9 +352,9 @@ int dglhip_node_linear_device(int64_t num_rows, int64_t in_feats, const float* x
                "node Linear on the MFMA: in_feats must be 64, 128 or 256, got " << in_feats);
   DGLHIP_CHECK(m1 >= 1 && m1 <= 64 && m2 >= 0 && m2 <= 64,
                "node Linear on the MFMA: 1..64 (+ 0..64) outputs, got " << m1 << ", " << m2);
+  if (num_rows == 0) return 0;  // empty tensors may carry any strides and null pointers
   DGLHIP_CHECK(ldx >= in_feats && ldx % 4 == 0, "ldx " << ldx << ": >= in_feats, multiple of 4");
   DGLHIP_CHECK(ldy1 >= m1 && (m2 == 0 || ldy2 >= m2), "output row stride below its width");
-  if (num_rows == 0) return 0;
   DGLHIP_CHECK(x && w1 && y1 && (m2 == 0 || (w2 && y2)), "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(x) % 16 == 0, "x must be 16-byte aligned");
   LinOut o1{w1, nullptr, b1, y1, ldy1, static_cast<int>(m1), 0};
@@ -388,10 +388,10 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
   DGLHIP_CHECK(in_feats == 64 || in_feats == 128,
                "two-input node Linear on the MFMA: in_feats 64 or 128, got " << in_feats);
   DGLHIP_CHECK(m >= 1 && m <= 128, "two-input node Linear on the MFMA: 1..128 outputs, got " << m);
+  if (num_rows == 0) return 0;
   DGLHIP_CHECK(ldx1 >= in_feats && ldx2 >= in_feats && ldx1 % 4 == 0 && ldx2 % 4 == 0,
                "input row strides: >= in_feats, multiples of 4");
   DGLHIP_CHECK(ldy >= m, "output row stride below its width");
-  if (num_rows == 0) return 0;
   DGLHIP_CHECK(x1 && x2 && w1 && w2 && y, "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(x1) % 16 == 0 && reinterpret_cast<uintptr_t>(x2) % 16 == 0,
                "inputs must be 16-byte aligned");
@@ -419,9 +419,9 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
   const int s1 = round_steps(static_cast<int>(m1)), s2 = m2 == 0 ? 0 : round_steps(static_cast<int>(m2));
   DGLHIP_CHECK(m1 >= 1 && m1 <= 64 && m2 >= 0 && m2 <= 64 && s1 > 0 && s2 >= 0,
                "input gradient on the MFMA: 1..64 (+ 0..64) outputs, got " << m1 << ", " << m2);
+  if (num_rows == 0) return 0;
   DGLHIP_CHECK(lddy1 >= m1 && (m2 == 0 || lddy2 >= m2) && lddx >= in_feats,
                "row stride below the row width");
-  if (num_rows == 0) return 0;
   DGLHIP_CHECK(dy1 && w1 && dx && (m2 == 0 || (dy2 && w2)), "null pointer argument");
   GradIn g1{dy1, lddy1, w1, static_cast<int>(m1)};
   GradIn g2{dy2, lddy2, w2, static_cast<int>(m2)};

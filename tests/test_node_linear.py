@@ -169,3 +169,21 @@ def test_cat_exact_integers(cuda, k, m):
     assert torch.equal(y.double(), ref)
     yr = L._node_linear_cat(x1, w1, x2, w2, b, relu=True)
     assert torch.equal(yr.double(), ref.clamp(min=0))
+
+
+@pytest.mark.parametrize("n", [0, 1, 15, 17])
+def test_tiny_row_counts(cuda, n):
+    """Empty inputs return without a launch; 1..17 rows (one partial block or
+    a full one plus one row) match the float64 product exactly."""
+    rng = np.random.default_rng(n)
+    k, m = 128, 41
+    x = _ints(rng, (n, k)).to(cuda)
+    w1, w2 = _ints(rng, (m, k), -2, 3).to(cuda), _ints(rng, (m, k), -2, 3).to(cuda)
+    b = _ints(rng, (m,)).to(cuda)
+    y1, y2 = L._node_linear2(x, w1, 48, w2, b)
+    assert y1.shape == (n, m) and y2.shape == (n, m)
+    assert torch.equal(y1.double(), x.double() @ w1.double().t())
+    assert torch.equal(y2.double(), x.double() @ w2.double().t() + b.double())
+    dy1, dy2 = _ints(rng, (n, m)).to(cuda), _ints(rng, (n, m)).to(cuda)
+    dx = L._node_dgrad2(k, dy1, w1, dy2, w2)
+    assert torch.equal(dx.double(), dy1.double() @ w1.double() + dy2.double() @ w2.double())
