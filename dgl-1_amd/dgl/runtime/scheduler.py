@@ -97,9 +97,18 @@ class _Edges(object):
         return self._val
 
 
+def _all_nodes(g, recv_nodes):
+    """Receiver ids; None stands for every node (update_all), whose id list is
+    made only when a UDF or fallback reducer needs it: the kernel path of a
+    whole-graph update_all touches no O(N) host array."""
+    if recv_nodes is None:
+        return torch.arange(g.number_of_nodes(), dtype=torch.int64)
+    return recv_nodes
+
+
 def _bucket_fn(g, rfunc, recv_nodes, msg_dst):
     return var.FUNC(lambda msgs: degree_bucketing.bucket_reduce(
-        g, rfunc, recv_nodes, msg_dst, msgs, g._node_frame), "reduce_func")
+        g, rfunc, _all_nodes(g, recv_nodes), msg_dst, msgs, g._node_frame), "reduce_func")
 
 
 def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out):
@@ -112,7 +121,8 @@ def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out):
     ir.CALL_(var.FUNC(check, "check_msg"))
     m = ir.READ_COL(msgs, var.STR(rfn.msg_field))
     fallback = var.FUNC(lambda mt: degree_bucketing.bucket_reduce(
-        g, rfn, recv_nodes, msg_dst, {rfn.msg_field: mt}, g._node_frame)[rfn.out_field],
+        g, rfn, _all_nodes(g, recv_nodes), msg_dst, {rfn.msg_field: mt},
+        g._node_frame)[rfn.out_field],
         "bucket_" + rfn.name)
     r = ir.SPMV_E2V(inc, m, var.STR(rfn.kernel_reduce), fallback)
     ir.WRITE_COL_(out, var.STR(rfn.out_field), r)
@@ -171,7 +181,7 @@ def _apply_with_accum(g, nodes, reduced, apply_func):
     """Apply function over node data updated with the reduced values."""
     if not apply_func:
         return reduced
-    ids = torch.arange(g.number_of_nodes()) if nodes is None else nodes
+    ids = _all_nodes(g, nodes)
     data = ir.UPDATE_DICT(ir.READ_ROW(var.FEAT_DICT(g._node_frame, "nf"), var.IDX(nodes)),
                           reduced)
     fn = var.FUNC(lambda nd: apply_func(NodeBatch(g, ids, nd)), "apply_func")
@@ -194,8 +204,7 @@ def schedule_update_all(g, message_func, reduce_func, apply_func):
             _apply_nodes(g, None, apply_func, inplace=False)
         return
     edges = _Edges(g._graph.edges)
-    recv = torch.arange(g.number_of_nodes(), dtype=torch.int64)
-    reduced = _send_reduce(g, message_func, reduce_func, edges, recv, True)
+    reduced = _send_reduce(g, message_func, reduce_func, edges, None, True)
     final = _apply_with_accum(g, None, reduced, apply_func)
     ir.WRITE_DICT_(var.FEAT_DICT(g._node_frame, "nf"), final)
 
@@ -278,7 +287,7 @@ def schedule_recv(g, recv_nodes, reduce_func, apply_func, inplace):
 
 
 def _apply_nodes(g, v, apply_func, inplace):
-    ids = torch.arange(g.number_of_nodes()) if v is None else v
+    ids = _all_nodes(g, v)
     fn = var.FUNC(lambda nd: apply_func(NodeBatch(g, ids, nd)), "apply_func")
     out = ir.NODE_UDF(fn, ir.READ_ROW(var.FEAT_DICT(g._node_frame, "nf"), var.IDX(v)))
     _write_rows(g, v, out, inplace)
