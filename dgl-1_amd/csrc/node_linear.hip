@@ -162,11 +162,15 @@ struct GradIn {
 };
 
 // dx = dy1 W1 + dy2 W2 over S1 (S2) 4-wide steps of output 1's (2's) columns;
-// KT 16-column tiles of dx.
+// KT 16-column tiles of dx. With a gate (the ReLU output that x is), the
+// store is ReLU's backward rule: 0 where gate <= 0 (torch threshold_backward,
+// NaN gates pass the gradient), so the mask costs no pass of its own.
 template <int KT, int S1, int S2>
 __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn g1, GradIn g2,
                                                               float* __restrict__ dx,
-                                                              int64_t lddx) {
+                                                              int64_t lddx,
+                                                              const float* __restrict__ gate,
+                                                              int64_t ldg) {
   constexpr int K = 16 * KT;
   constexpr int S = S1 + S2;
   constexpr int SK = K + 16;  // rows 4s + h of one MFMA land 16 banks apart
@@ -203,6 +207,17 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
     const int64_t r0 = blk * 16;
     float an[S];  // the next block's gradient rows, in flight during the MFMAs
     if (blk + nwaves < nblk) load_block(blk + nwaves, an);
+    // this block's gate values, in flight during the MFMAs as well
+    float gv[KT][4];
+    if (gate != nullptr) {
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int64_t orow = r0 + 4 * h + i;
+          gv[t][i] = orow < n ? gate[orow * ldg + 16 * t + r] : 0.0f;
+        }
+    }
     f32x4 acc[KT];
 #pragma unroll
     for (int t = 0; t < KT; ++t) acc[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
@@ -227,7 +242,10 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int64_t orow = r0 + 4 * h + i;
-        if (orow < n) dx[orow * lddx + 16 * t + r] = acc[t][i];
+        if (orow < n) {
+          const float v = gate != nullptr && gv[t][i] <= 0.0f ? 0.0f : acc[t][i];
+          dx[orow * lddx + 16 * t + r] = v;
+        }
       }
 #pragma unroll
     for (int s = 0; s < S; ++s) a[s] = an[s];
@@ -288,12 +306,17 @@ void dispatch_fwd(int t1, int t2, int64_t n, const float* x, int64_t ldx, const 
   }
 }
 
+struct Gate {
+  const float* p;
+  int64_t ld;
+};
+
 template <int KT, int S1, int S2>
 void launch_bwd(int64_t n, const GradIn& g1, const GradIn& g2, float* dx, int64_t lddx,
-                hipStream_t stream) {
+                const Gate& gate, hipStream_t stream) {
   constexpr int lds = 4 * (S1 + S2) * (16 * KT + 16) * 4;
   hipLaunchKernelGGL((node_linear_bwd_kernel<KT, S1, S2>), dim3(persistent_blocks(n, lds)),
-                     dim3(nl_threads()), 0, stream, n, g1, g2, dx, lddx);
+                     dim3(nl_threads()), 0, stream, n, g1, g2, dx, lddx, gate.p, gate.ld);
 }
 
 // reduction widths up to 64 per input: S = ceil(m / 4) rounded up to a listed
@@ -310,26 +333,26 @@ inline int round_steps(int m) {
 
 template <int KT, int S1>
 void dispatch_bwd_s2(int s2, int64_t n, const GradIn& g1, const GradIn& g2, float* dx,
-                     int64_t lddx, hipStream_t st) {
+                     int64_t lddx, const Gate& gt, hipStream_t st) {
   switch (s2) {
-    case 0: return launch_bwd<KT, S1, 0>(n, g1, g2, dx, lddx, st);
-    case 2: return launch_bwd<KT, S1, 2>(n, g1, g2, dx, lddx, st);
-    case 4: return launch_bwd<KT, S1, 4>(n, g1, g2, dx, lddx, st);
-    case 8: return launch_bwd<KT, S1, 8>(n, g1, g2, dx, lddx, st);
-    case 11: return launch_bwd<KT, S1, 11>(n, g1, g2, dx, lddx, st);
-    default: return launch_bwd<KT, S1, 16>(n, g1, g2, dx, lddx, st);
+    case 0: return launch_bwd<KT, S1, 0>(n, g1, g2, dx, lddx, gt, st);
+    case 2: return launch_bwd<KT, S1, 2>(n, g1, g2, dx, lddx, gt, st);
+    case 4: return launch_bwd<KT, S1, 4>(n, g1, g2, dx, lddx, gt, st);
+    case 8: return launch_bwd<KT, S1, 8>(n, g1, g2, dx, lddx, gt, st);
+    case 11: return launch_bwd<KT, S1, 11>(n, g1, g2, dx, lddx, gt, st);
+    default: return launch_bwd<KT, S1, 16>(n, g1, g2, dx, lddx, gt, st);
   }
 }
 
 template <int KT>
 void dispatch_bwd(int s1, int s2, int64_t n, const GradIn& g1, const GradIn& g2, float* dx,
-                  int64_t lddx, hipStream_t st) {
+                  int64_t lddx, const Gate& gt, hipStream_t st) {
   switch (s1) {
-    case 2: return dispatch_bwd_s2<KT, 2>(s2, n, g1, g2, dx, lddx, st);
-    case 4: return dispatch_bwd_s2<KT, 4>(s2, n, g1, g2, dx, lddx, st);
-    case 8: return dispatch_bwd_s2<KT, 8>(s2, n, g1, g2, dx, lddx, st);
-    case 11: return dispatch_bwd_s2<KT, 11>(s2, n, g1, g2, dx, lddx, st);
-    default: return dispatch_bwd_s2<KT, 16>(s2, n, g1, g2, dx, lddx, st);
+    case 2: return dispatch_bwd_s2<KT, 2>(s2, n, g1, g2, dx, lddx, gt, st);
+    case 4: return dispatch_bwd_s2<KT, 4>(s2, n, g1, g2, dx, lddx, gt, st);
+    case 8: return dispatch_bwd_s2<KT, 8>(s2, n, g1, g2, dx, lddx, gt, st);
+    case 11: return dispatch_bwd_s2<KT, 11>(s2, n, g1, g2, dx, lddx, gt, st);
+    default: return dispatch_bwd_s2<KT, 16>(s2, n, g1, g2, dx, lddx, gt, st);
   }
 }
 
@@ -395,8 +418,10 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
   DGLHIP_CHECK(x1 && x2 && w1 && w2 && y, "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(x1) % 16 == 0 && reinterpret_cast<uintptr_t>(x2) % 16 == 0,
                "inputs must be 16-byte aligned");
-  // at most 64 outputs per pass (4 tiles: 8 tiles would spill at 128 inputs
-  // per operand); wider outputs take one pass per 64 columns
+  // at most 64 outputs per pass (4 tiles): one pass over 128 outputs (8
+  // tiles, 135 KB of weights in LDS, one wave per SIMD, no spills) took 44.6
+  // ms at 67M rows against 42.1 for two passes (tools/node_linear_bench.py);
+  // wider outputs take one pass per 64 columns
   for (int64_t c0 = 0; c0 < m; c0 += 64) {
     LinOut o{w1 + c0 * in_feats, w2 + c0 * in_feats, b ? b + c0 : nullptr, y + c0, ldy,
              static_cast<int>(std::min<int64_t>(64, m - c0)), relu ? 1 : 0};
@@ -410,7 +435,7 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
 int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t m1,
                                     const float* dy1, int64_t lddy1, const float* w1, int64_t m2,
                                     const float* dy2, int64_t lddy2, const float* w2, float* dx,
-                                    int64_t lddx, void* stream_) {
+                                    int64_t lddx, const float* gate, int64_t ldg, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0, "negative row count");
@@ -423,10 +448,12 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
   DGLHIP_CHECK(lddy1 >= m1 && (m2 == 0 || lddy2 >= m2) && lddx >= in_feats,
                "row stride below the row width");
   DGLHIP_CHECK(dy1 && w1 && dx && (m2 == 0 || (dy2 && w2)), "null pointer argument");
+  DGLHIP_CHECK(gate == nullptr || ldg >= in_feats, "gate row stride below in_feats");
   GradIn g1{dy1, lddy1, w1, static_cast<int>(m1)};
   GradIn g2{dy2, lddy2, w2, static_cast<int>(m2)};
-  if (in_feats == 64) dispatch_bwd<4>(s1, s2, num_rows, g1, g2, dx, lddx, stream);
-  else dispatch_bwd<8>(s1, s2, num_rows, g1, g2, dx, lddx, stream);
+  const Gate gt{gate, ldg};
+  if (in_feats == 64) dispatch_bwd<4>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
+  else dispatch_bwd<8>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "node Linear input-gradient launch failed");
   API_END();
 }

@@ -1,0 +1,234 @@
+// Weighted softmax cross-entropy over node rows: the loss of a full-graph node
+// classifier (GraphSAGE / GCN output layer, BASELINE configs[1], configs[3]),
+//   loss = sum_i w_i (logsumexp(z_i) - z_i[y_i]),
+// and its gradient dz_ij = g w_i (softmax(z_i)_j - [j == y_i]) for the
+// upstream scalar g. The same value as PyTorch's
+// (F.cross_entropy(z, y, reduction="none") * w).sum(), which at 10^7-10^8 rows
+// of a few dozen classes runs as five passes over the logits forward and
+// backward (log-softmax, the nll gather, a zero fill, the nll scatter, the
+// log-softmax backward: 28 ms per RMAT-26 epoch); here one read forward and one
+// read + one write backward.
+//
+// Layout: a workgroup stages a tile of kRows rows into LDS with coalesced
+// 16-B loads (rows at an odd LDS stride SC, so the one-row-per-lane pass that
+// follows is free of bank conflicts), each lane reduces its row (max, sum of
+// exponentials, log) and the backward writes its gradient row back into the
+// tile, which then leaves with coalesced stores. The loss sum is per-lane,
+// then per workgroup in a fixed tree, then over the workgroups in index order
+// (deterministic). Rows whose label is outside [0, C) (PyTorch's ignore_index,
+// -100) contribute nothing.
+#include "common.h"
+#include "launch.h"
+
+#include <hip/hip_runtime.h>
+
+namespace dglhip {
+
+namespace {
+
+constexpr int kRows = 256;         // rows per tile = lanes per workgroup
+constexpr int kMaxClasses = 64;
+constexpr int kMaxBlocks = 1024;   // workspace floats of the forward
+
+// tile[r * SC + c] = z[(r0 + r) * ld + c] for r < nrows, c < C
+__device__ inline void load_tile(const float* __restrict__ z, int64_t ld, int64_t r0, int nrows,
+                                 int C, int SC, float* tile) {
+  const int total = nrows * C;
+  if (ld == C && SC == C) {
+    const float* base = z + r0 * C;
+    if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {
+      const int n4 = total >> 2;
+      for (int i = threadIdx.x; i < n4; i += blockDim.x)
+        reinterpret_cast<float4*>(tile)[i] = reinterpret_cast<const float4*>(base)[i];
+      for (int i = (n4 << 2) + threadIdx.x; i < total; i += blockDim.x) tile[i] = base[i];
+    } else {
+      for (int i = threadIdx.x; i < total; i += blockDim.x) tile[i] = base[i];
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int r = i / C, c = i - r * C;
+    tile[r * SC + c] = z[(r0 + r) * ld + c];
+  }
+}
+
+__device__ inline void store_tile(float* __restrict__ out, int64_t ld, int64_t r0, int nrows,
+                                  int C, int SC, const float* tile) {
+  const int total = nrows * C;
+  if (ld == C && SC == C) {
+    float* base = out + r0 * C;
+    if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {
+      const int n4 = total >> 2;
+      for (int i = threadIdx.x; i < n4; i += blockDim.x)
+        reinterpret_cast<float4*>(base)[i] = reinterpret_cast<const float4*>(tile)[i];
+      for (int i = (n4 << 2) + threadIdx.x; i < total; i += blockDim.x) base[i] = tile[i];
+    } else {
+      for (int i = threadIdx.x; i < total; i += blockDim.x) base[i] = tile[i];
+    }
+    return;
+  }
+  for (int i = threadIdx.x; i < total; i += blockDim.x) {
+    const int r = i / C, c = i - r * C;
+    out[(r0 + r) * ld + c] = tile[r * SC + c];
+  }
+}
+
+// max and log(sum exp(z - max)) of one staged row
+__device__ inline void row_lse(const float* row, int C, float& m, float& lse) {
+  m = row[0];
+  for (int c = 1; c < C; ++c) m = fmaxf(m, row[c]);
+  float s = 0.0f;
+  for (int c = 0; c < C; ++c) s += expf(row[c] - m);
+  lse = logf(s);
+}
+
+__global__ __launch_bounds__(kRows) void xent_fwd_kernel(int64_t n, int C, int SC,
+                                                         const float* __restrict__ z, int64_t ld,
+                                                         const int64_t* __restrict__ labels,
+                                                         const float* __restrict__ w,
+                                                         float* __restrict__ partial) {
+  extern __shared__ float tile[];
+  float acc = 0.0f;
+  const int64_t ntiles = (n + kRows - 1) / kRows;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t r0 = t * kRows;
+    const int nrows = static_cast<int>(n - r0 < kRows ? n - r0 : kRows);
+    __syncthreads();  // the previous tile's rows are consumed
+    load_tile(z, ld, r0, nrows, C, SC, tile);
+    __syncthreads();
+    const int r = threadIdx.x;
+    if (r < nrows) {
+      const int64_t y = labels[r0 + r];
+      if (y >= 0 && y < C) {
+        const float* row = tile + r * SC;
+        float m, lse;
+        row_lse(row, C, m, lse);
+        const float nll = -((row[y] - m) - lse);
+        acc += w != nullptr ? nll * w[r0 + r] : nll;
+      }
+    }
+  }
+  // workgroup sum in a fixed tree
+  __syncthreads();
+  tile[threadIdx.x] = acc;
+  __syncthreads();
+  for (int s = kRows / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) tile[threadIdx.x] += tile[threadIdx.x + s];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = tile[0];
+}
+
+// loss = the workgroups' partial sums, in index order
+__global__ void xent_sum_kernel(int nparts, const float* __restrict__ partial,
+                                float* __restrict__ loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    float s = 0.0f;
+    for (int i = 0; i < nparts; ++i) s += partial[i];
+    loss[0] = s;
+  }
+}
+
+__global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int SC,
+                                                         const float* __restrict__ z, int64_t ld,
+                                                         const int64_t* __restrict__ labels,
+                                                         const float* __restrict__ w,
+                                                         const float* __restrict__ grad_loss,
+                                                         float* __restrict__ dz, int64_t ldd) {
+  extern __shared__ float tile[];
+  const float g = grad_loss[0];
+  const int64_t ntiles = (n + kRows - 1) / kRows;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t r0 = t * kRows;
+    const int nrows = static_cast<int>(n - r0 < kRows ? n - r0 : kRows);
+    __syncthreads();
+    load_tile(z, ld, r0, nrows, C, SC, tile);
+    __syncthreads();
+    const int r = threadIdx.x;
+    if (r < nrows) {
+      float* row = tile + r * SC;
+      const int64_t y = labels[r0 + r];
+      if (y >= 0 && y < C) {
+        float m, lse;
+        row_lse(row, C, m, lse);
+        const float gw = w != nullptr ? g * w[r0 + r] : g;
+        for (int c = 0; c < C; ++c) {
+          const float p = expf((row[c] - m) - lse);
+          row[c] = c == y ? gw * p - gw : gw * p;
+        }
+      } else {
+        for (int c = 0; c < C; ++c) row[c] = 0.0f;
+      }
+    }
+    __syncthreads();
+    store_tile(dz, ldd, r0, nrows, C, SC, tile);
+  }
+}
+
+inline int xent_grid(int64_t n, int SC) {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  const int lds = kRows * SC * 4;
+  const int per_cu = std::max(1, std::min(8, (160 * 1024) / lds));
+  const int64_t tiles = (n + kRows - 1) / kRows;
+  return static_cast<int>(std::max<int64_t>(1, std::min<int64_t>({tiles, int64_t(cus) * per_cu,
+                                                                    int64_t(kMaxBlocks)})));
+}
+
+inline int lds_stride(int C) { return C | 1; }
+
+}  // namespace
+
+}  // namespace dglhip
+
+using namespace dglhip;
+
+extern "C" {
+
+int dglhip_xent_workspace_floats() { return kMaxBlocks; }
+
+int dglhip_xent_fwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                           int64_t ld, const int64_t* labels, const float* weight, float* loss,
+                           float* workspace, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0, "negative row count");
+  DGLHIP_CHECK(num_classes >= 1 && num_classes <= kMaxClasses,
+               "cross-entropy rows: 1.." << kMaxClasses << " classes, got " << num_classes);
+  DGLHIP_CHECK(loss && workspace, "null pointer argument");
+  const int C = static_cast<int>(num_classes), SC = lds_stride(C);
+  if (num_rows == 0) {
+    hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(64), 0, stream, 0, workspace, loss);
+  } else {
+    DGLHIP_CHECK(ld >= num_classes, "row stride " << ld << " below the class count");
+    DGLHIP_CHECK(logits && labels, "null pointer argument");
+    const int grid = xent_grid(num_rows, SC);
+    hipLaunchKernelGGL(xent_fwd_kernel, dim3(grid), dim3(kRows), kRows * SC * 4, stream,
+                       num_rows, C, SC, logits, ld, labels, weight, workspace);
+    hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(64), 0, stream, grid, workspace, loss);
+  }
+  DGLHIP_CHECK(hipGetLastError() == hipSuccess, "cross-entropy launch failed");
+  API_END();
+}
+
+int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                           int64_t ld, const int64_t* labels, const float* weight,
+                           const float* grad_loss, float* dlogits, int64_t ldd, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0, "negative row count");
+  DGLHIP_CHECK(num_classes >= 1 && num_classes <= kMaxClasses,
+               "cross-entropy rows: 1.." << kMaxClasses << " classes, got " << num_classes);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(ld >= num_classes && ldd >= num_classes, "row stride below the class count");
+  DGLHIP_CHECK(logits && labels && grad_loss && dlogits, "null pointer argument");
+  const int C = static_cast<int>(num_classes), SC = lds_stride(C);
+  hipLaunchKernelGGL(xent_bwd_kernel, dim3(xent_grid(num_rows, SC)), dim3(kRows), kRows * SC * 4,
+                     stream, num_rows, C, SC, logits, ld, labels, weight, grad_loss, dlogits, ldd);
+  DGLHIP_CHECK(hipGetLastError() == hipSuccess, "cross-entropy backward launch failed");
+  API_END();
+}
+
+}  // extern "C"

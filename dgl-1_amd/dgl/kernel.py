@@ -275,6 +275,13 @@ class CSR(object):
     def degrees(self):
         return self.indptr[1:] - self.indptr[:-1]
 
+    def mean_divisor(self):
+        """float32 (R, 1): each row's slot count, at least 1 (the mean's
+        divisor, the reference's degree-bucketing ``mean``); cached."""
+        if getattr(self, "_mean_div", None) is None:
+            self._mean_div = self.degrees().clamp(min=1).to(torch.float32).unsqueeze(1)
+        return self._mean_div
+
     def row_ids(self):
         """Row id of every slot (COO expansion), cached."""
         if self._row_ids is None:
@@ -721,8 +728,16 @@ class _GSpMM(torch.autograd.Function):
         need_e = ctx.needs_input_grad[6]
         F = dout.shape[1]
         if red == RED_MEAN:
-            deg = fwd.degrees().clamp(min=1).to(dout.dtype).unsqueeze(1)
-            dout = (dout / deg).contiguous()
+            deg = fwd.mean_divisor()
+            if need_u and not need_e and dout.is_cuda and \
+                    _pad_rows(MSG_COPY_U, RED_SUM, dout, F):
+                # the quotient written straight into the padded rows the
+                # transposed product gathers (one pass instead of the
+                # division's and the padding copy's)
+                buf = dout.new_empty(dout.shape[0], padded_width(F))
+                dout = torch.div(dout, deg, out=buf[:, :F])
+            else:
+                dout = (dout / deg).contiguous()
             red_b = RED_SUM
         else:
             red_b = red
@@ -826,7 +841,11 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None, edge_order="
     if num_edges is None:
         num_edges = 0 if e2 is None else e2.shape[0]
     out = _GSpMM.apply(adj, msg, red, F, num_edges, u2, e2, slot)
-    return out.reshape((adj.shape[0],) + fshape) if fshape else out.reshape(adj.shape[0])
+    shape = (adj.shape[0],) + fshape if fshape else (adj.shape[0],)
+    # the product's own tensor when no reshape is needed: a view would make
+    # a caller's in-place update of the result rebase its autograd graph
+    # (CopySlices: a zero fill and a copy of the whole gradient)
+    return out if tuple(out.shape) == shape else out.reshape(shape)
 
 
 def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1, edge_order="eid"):

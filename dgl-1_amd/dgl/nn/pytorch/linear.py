@@ -145,8 +145,9 @@ def _node_linear_cat(x1, w1, x2, w2, b, relu=False):
     return y
 
 
-def _node_dgrad2(k, dy1, w1, dy2, w2):
-    """dy1 W1 + dy2 W2 in one pass (n, k)."""
+def _node_dgrad2(k, dy1, w1, dy2, w2, gate=None):
+    """dy1 W1 + dy2 W2 in one pass (n, k); ``gate`` (n, k, unit column
+    stride): 0 where gate <= 0 (ReLU's backward applied in the store)."""
     from ... import _ffi, kernel
     n = dy1.shape[0]
     w1, w2 = _w(w1), _w(w2)
@@ -154,7 +155,7 @@ def _node_dgrad2(k, dy1, w1, dy2, w2):
     _ffi.check_call(_ffi.LIB.dglhip_node_linear_dgrad_device(
         n, k, dy1.shape[1], _ffi.ptr(dy1), dy1.stride(0), _ffi.ptr(w1), dy2.shape[1],
         _ffi.ptr(dy2), dy2.stride(0), _ffi.ptr(w2), _ffi.ptr(dx), k,
-        kernel._stream_of(dy1.device)))
+        _ffi.ptr(gate), 0 if gate is None else gate.stride(0), kernel._stream_of(dy1.device)))
     return dx
 
 
@@ -177,12 +178,15 @@ class _DualLinearFn(torch.autograd.Function):
             if relu:
                 out.relu_()
         ctx.save_for_backward(x, w_self, agg, w_neigh, out if relu else None)
+        ctx.out_ptr = out.data_ptr()
+        ctx.premasked = None
         return out
 
     @staticmethod
     def backward(ctx, dy):
         x, w_self, agg, w_neigh, out = ctx.saved_tensors
-        if ctx.relu:
+        premasked, ctx.premasked = ctx.premasked, None
+        if ctx.relu and premasked != (dy.data_ptr(), dy._version):
             dy = torch.ops.aten.threshold_backward(dy, out, 0)  # ReLU's own backward, one pass
         dy = dy.contiguous()
         need = ctx.needs_input_grad
@@ -220,18 +224,25 @@ class _PreAggregateFn(torch.autograd.Function):
             pre_leaf, neigh = None, aggregate(pre)
         del pre
         # accumulate into the aggregate's own buffer (its backward does not
-        # read it): no copy of an (N, out) tensor
-        out = neigh.detach()
-        if self_out is not None:
+        # read it): no copy of an (N, out) tensor. Not into a view: autograd
+        # would rebase the view's graph on the in-place update (a zero fill
+        # and a copy of the gradient); then into self_out (a + b == b + a)
+        if self_out is not None and neigh._base is not None:
+            out = self_out.add_(neigh.detach())
+            del self_out
+        elif self_out is not None:
+            out = neigh.detach()
             out.add_(self_out)
             del self_out
         else:
+            out = neigh.detach() if neigh._base is None else neigh.detach().clone()
             out.addmm_(x, w_self.t())
             if bias is not None:
                 out.add_(bias)
         ctx.save_for_backward(x, w_self, w_neigh)
         ctx.graph = (pre_leaf, neigh) if pre_leaf is not None else None
         ctx.has_bias = bias is not None
+        ctx.relu_node = _relu_producer(x)
         return out
 
     @staticmethod
@@ -244,9 +255,18 @@ class _PreAggregateFn(torch.autograd.Function):
         (dpre,) = torch.autograd.grad(neigh, pre_leaf, dy)
         dpre = dpre.contiguous()
         dx = None
+        node, ctx.relu_node = ctx.relu_node, None
         if need[0]:
             if _mfma_dgrad_ok(x.shape[1], dy, dpre):
-                dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh)
+                # x is a fused-ReLU layer's output: its backward mask (out > 0
+                # is x > 0) is applied in this product's store, and that
+                # layer skips its own pass over the gradient when it receives
+                # this very tensor unmodified (same storage, same version:
+                # a gradient summed with another consumer's is masked there)
+                gate = x if node is not None else None
+                dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh, gate=gate)
+                if gate is not None:
+                    node.premasked = (dx.data_ptr(), dx._version)
             else:
                 dx = dy.matmul(w_self)
                 dx.addmm_(dpre, w_neigh)
@@ -254,6 +274,17 @@ class _PreAggregateFn(torch.autograd.Function):
         db = _colsum(dy) if ctx.has_bias and need[2] else None
         dwn = _splitk_tn(dpre, x.contiguous()) if need[3] else None
         return dx, dws, db, dwn, None
+
+
+def _relu_producer(x):
+    """The _DualLinearFn node whose fused-ReLU output ``x`` is (the tensor
+    itself, not a view or an in-place update of it), else None."""
+    node = x.grad_fn
+    if (isinstance(node, _DualLinearFn._backward_cls) and getattr(node, "relu", False) and
+            getattr(node, "out_ptr", None) == x.data_ptr() and x._base is None and
+            x.is_contiguous()):
+        return node
+    return None
 
 
 def _is_relu(act):

@@ -1,0 +1,71 @@
+"""Weighted softmax cross-entropy over node rows, the loss of a full-graph
+node classifier (csrc/node_loss.hip).
+
+``weighted_cross_entropy(z, y, w)`` is the value of
+
+    (F.cross_entropy(z, y, reduction="none") * w).sum()
+
+(the masked training loss of the examples when ``w`` is the float training
+mask; the reference's examples reduce ``F.cross_entropy`` / ``nll_loss`` over
+``logits[train_mask]``, examples/pytorch/gcn/gcn_spmv.py:113-118). At 10^7-10^8
+rows PyTorch runs it as five passes over the logits (log-softmax, the nll
+gather, a zero fill, the nll scatter, the log-softmax backward); on a ROCm
+device with 1..64 classes it is one kernel forward (one read) and one
+backward (one read, one write), the upstream gradient read on the device.
+Other devices and shapes compute the expression above with PyTorch's own
+operators. Results agree with it to fp32 rounding (the sums associate
+differently); labels outside [0, C) contribute nothing (PyTorch's
+ignore_index = -100; other out-of-range labels are an error there).
+"""
+import torch
+import torch.nn.functional as F
+
+__all__ = ["weighted_cross_entropy"]
+
+_MAX_CLASSES = 64
+
+
+def _fused_ok(z, y, w):
+    return (z.is_cuda and z.dtype == torch.float32 and z.dim() == 2 and z.stride(1) == 1 and
+            1 <= z.shape[1] <= _MAX_CLASSES and y.dim() == 1 and y.shape[0] == z.shape[0] and
+            y.dtype == torch.int64 and y.device == z.device and
+            (w is None or (w.dim() == 1 and w.shape[0] == z.shape[0] and
+                           w.dtype == torch.float32 and w.device == z.device)))
+
+
+class _WeightedXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, y, w):
+        from ... import _ffi, kernel
+        y = y.contiguous()
+        w = None if w is None else w.detach().contiguous()
+        n, C = z.shape
+        loss = torch.empty((), dtype=torch.float32, device=z.device)
+        ws = torch.empty(_ffi.LIB.dglhip_xent_workspace_floats(), dtype=torch.float32,
+                         device=z.device)
+        _ffi.check_call(_ffi.LIB.dglhip_xent_fwd_device(
+            n, C, _ffi.ptr(z), z.stride(0), _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(loss),
+            _ffi.ptr(ws), kernel._stream_of(z.device)))
+        ctx.save_for_backward(z, y, w)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        from ... import _ffi, kernel
+        z, y, w = ctx.saved_tensors
+        n, C = z.shape
+        g = g.detach().to(torch.float32).contiguous()
+        dz = torch.empty(n, C, dtype=torch.float32, device=z.device)
+        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_device(
+            n, C, _ffi.ptr(z), z.stride(0), _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(g), _ffi.ptr(dz),
+            C, kernel._stream_of(z.device)))
+        return dz, None, None
+
+
+def weighted_cross_entropy(logits, labels, weight=None):
+    """sum_i weight_i * cross_entropy(logits_i, labels_i) (weight None: all
+    ones), differentiable in ``logits``; see the module docstring."""
+    if _fused_ok(logits, labels, weight) and (weight is None or not weight.requires_grad):
+        return _WeightedXentFn.apply(logits, labels, weight)
+    ce = F.cross_entropy(logits, labels, reduction="none")
+    return (ce * weight).sum() if weight is not None else ce.sum()

@@ -37,7 +37,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph, data, kernel  # noqa: E402
 from dgl.distributed import PartitionedGraph, balanced_bounds  # noqa: E402
-from dgl.nn.pytorch import NodeLinear, sage_dense  # noqa: E402
+from dgl.nn.pytorch import NodeLinear, sage_dense, weighted_cross_entropy  # noqa: E402
 
 
 class SAGELayer(nn.Module):
@@ -150,10 +150,10 @@ def run(args):
         # per-row losses of every node, masked: at 10^7-10^8 nodes the
         # reducing nll_loss kernel runs as one workgroup (RMAT-26: 118 ms of a
         # 616 ms epoch), and logits[train] adds a gather and its scatter
-        # backward; the unreduced loss and the masked sum are elementwise
-        # passes (same per-row arithmetic)
-        loss = (F.cross_entropy(logits, labels, reduction="none") * train_w).sum() \
-            * (world / max(n_train_global, 1))
+        # backward. weighted_cross_entropy is
+        # (F.cross_entropy(logits, labels, reduction="none") * train_w).sum()
+        # as one pass over the logits forward and one backward
+        loss = weighted_cross_entropy(logits, labels, train_w) * (world / max(n_train_global, 1))
         opt.zero_grad()
         loss.backward()
         opt.step()

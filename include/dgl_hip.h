@@ -258,11 +258,39 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
 int dglhip_set_node_linear_variant(int threads, int wgs_per_cu);
 
 /* Input gradient of the first: dx = dy1 W1 + dy2 W2 (m2 = 0: dy1 W1 only);
- * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx. */
+ * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx. gate
+ * (optional, rows at stride ldg): x's own values when x is a ReLU output; dx
+ * is then 0 where gate <= 0 (ReLU's backward rule, torch threshold_backward),
+ * the mask applied in the store instead of a pass of its own. */
 int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t m1,
                                     const float* dy1, int64_t lddy1, const float* w1, int64_t m2,
                                     const float* dy2, int64_t lddy2, const float* w2, float* dx,
-                                    int64_t lddx, void* stream);
+                                    int64_t lddx, const float* gate, int64_t ldg, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Weighted softmax cross-entropy over node rows (csrc/node_loss.hip): the   */
+/* loss of a full-graph node classifier. No reference counterpart: the       */
+/* reference's examples call torch's F.cross_entropy / nll_loss             */
+/* (examples/pytorch/gcn/gcn_spmv.py:113-118).                              */
+/* ------------------------------------------------------------------------ */
+/* Floats of the forward's workspace (per-workgroup partial sums). */
+int dglhip_xent_workspace_floats(void);
+
+/* *loss = sum_i w_i (logsumexp(z_i) - z_i[labels_i]) over num_rows rows of
+ * num_classes (1..64) logits at row stride ld; weight NULL = all ones; rows
+ * whose label is outside [0, num_classes) (ignore_index) add nothing. The sum
+ * runs per lane, per workgroup in a fixed tree, then over the workgroups in
+ * order: deterministic. loss and workspace are device pointers. */
+int dglhip_xent_fwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                           int64_t ld, const int64_t* labels, const float* weight, float* loss,
+                           float* workspace, void* stream);
+
+/* dlogits_ij = g w_i (softmax(z_i)_j - [j == labels_i]) with g = *grad_loss
+ * (a device scalar: no host round trip); ignored rows get zeros; dlogits at
+ * row stride ldd. */
+int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                           int64_t ld, const int64_t* labels, const float* weight,
+                           const float* grad_loss, float* dlogits, int64_t ldd, void* stream);
 
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,

@@ -77,7 +77,7 @@ def test_dgrad_exact_integers(cuda, k, m1, m2):
         dx = torch.empty(n, k, device=cuda)
         _ffi.check_call(_ffi.LIB.dglhip_node_linear_dgrad_device(
             n, k, m1, _ffi.ptr(dy1), m1, _ffi.ptr(w1), 0, None, 0, None, _ffi.ptr(dx), k,
-            kernel._stream_of(cuda)))
+            None, 0, kernel._stream_of(cuda)))
         ref = dy1.double() @ w1.double()
     assert torch.equal(dx.double(), ref)
 
@@ -187,3 +187,78 @@ def test_tiny_row_counts(cuda, n):
     dy1, dy2 = _ints(rng, (n, m)).to(cuda), _ints(rng, (n, m)).to(cuda)
     dx = L._node_dgrad2(k, dy1, w1, dy2, w2)
     assert torch.equal(dx.double(), dy1.double() @ w1.double() + dy2.double() @ w2.double())
+
+
+@pytest.mark.parametrize("k", [64, 128])
+def test_dgrad_gate_is_relu_backward(cuda, k):
+    """A gated input gradient equals threshold_backward(dy1 W1 + dy2 W2, gate,
+    0) bit for bit: zero where the gate is <= 0 (both zeros), NaN gates pass
+    the gradient (torch's rule)."""
+    rng = np.random.default_rng(k + 1)
+    n, m = 1000 + 7, 41
+    dy1, dy2 = _ints(rng, (n, m)).to(cuda), _ints(rng, (n, m)).to(cuda)
+    w1, w2 = _ints(rng, (m, k), -2, 3).to(cuda), _ints(rng, (m, k), -2, 3).to(cuda)
+    gbuf = _ints(rng, (n, k + 8), -2, 3).to(cuda)
+    gbuf[::7, 5] = -0.0
+    gbuf[::11, 9] = float("nan")
+    gate = gbuf[:, :k]
+    plain = L._node_dgrad2(k, dy1, w1, dy2, w2)
+    gated = L._node_dgrad2(k, dy1, w1, dy2, w2, gate=gate)
+    ref = torch.ops.aten.threshold_backward(plain, gate, 0)
+    assert torch.equal(gated, ref)
+    assert bool((gated[gate <= 0] == 0).all()) and bool((gated[gate > 0] == plain[gate > 0]).all())
+
+
+@pytest.mark.parametrize("extra_consumer", [False, True])
+def test_relu_mask_across_layers_equals_unfused(cuda, monkeypatch, extra_consumer):
+    """Two sage_dense layers (128 -> 128 ReLU -> 41): the first layer's ReLU
+    mask applied in the second layer's input-gradient store gives the same
+    gradients, bit for bit, as the first layer's own threshold_backward pass;
+    with a second consumer of the hidden rows the gradients are summed and
+    the first layer masks the sum itself."""
+    import copy
+    rng = np.random.default_rng(11)
+    n, m = 60_000, 500_000
+    g = dgl.DGLGraph((torch.from_numpy(rng.integers(0, n, m)),
+                      torch.from_numpy(rng.integers(0, n, m))))
+
+    def aggregate(x):
+        g.ndata["x"] = x
+        g.update_all(fn.copy_src("x", "m"), fn.mean("m", "a"))
+        g.ndata.pop("x")
+        return g.ndata.pop("a")
+
+    torch.manual_seed(0)
+    mods = [NodeLinear(128, 128), NodeLinear(128, 128, bias=False), NodeLinear(128, 41),
+            NodeLinear(128, 41, bias=False)]
+    mods = [mm.to(cuda) for mm in mods]
+    x = torch.randn(n, 128, device=cuda)
+    dy = torch.randn(n, 41, device=cuda)
+
+    def run(ms):
+        h = sage_dense(x, aggregate, ms[0], ms[1], torch.relu)
+        out = sage_dense(h, aggregate, ms[2], ms[3])
+        loss = (out * dy).sum()
+        if extra_consumer:
+            loss = loss + (h * h[:, :1]).sum()
+        loss.backward()
+        return [p.grad for mm in ms for p in mm.parameters()]
+
+    calls = []
+    orig = L._node_dgrad2
+
+    def spy(*a, **kw):
+        calls.append(kw.get("gate") is not None)
+        return orig(*a, **kw)
+    monkeypatch.setattr(L, "_node_dgrad2", spy)
+    fused = run(mods)
+    assert calls == [True]
+    ref_mods = copy.deepcopy(mods)
+    for p in (p for mm in ref_mods for p in mm.parameters()):
+        p.grad = None
+    monkeypatch.setattr(L, "_relu_producer", lambda t: None)
+    calls.clear()
+    plain = run(ref_mods)
+    assert calls == [False]
+    for a, b in zip(fused, plain):
+        assert torch.equal(a, b)
