@@ -30,22 +30,52 @@ constexpr int kRows = 256;         // rows per tile = lanes per workgroup
 constexpr int kMaxClasses = 64;
 constexpr int kMaxBlocks = 1024;   // workspace floats of the forward
 
-// tile[r * SC + c] = z[(r0 + r) * ld + c] for r < nrows, c < C
+// Staging of one tile's rows, tile[r * SC + c] = z[(r0 + r) * ld + c].
+//
+// NS > 0 (rows packed back to back at an odd width C = SC from a 16-byte
+// aligned start, so a tile is one float4 run of nrows * C floats, at most NS
+// float4 per lane): the run is loaded into registers one tile AHEAD and copied
+// into LDS when its turn comes, so the next tile's loads are in flight while
+// this tile's rows are reduced. NS = 0: loaded element by element straight
+// into LDS (padded strides, even widths).
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int NS>
+struct Ahead {
+  f32x4 v[NS > 0 ? NS : 1];
+  float tail;
+};
+
+// e0: the tile's first element (a multiple of 4: kRows * C floats per tile)
+template <int NS>
+__device__ inline void fetch_ahead(Ahead<NS>& a, const float* __restrict__ z, int64_t e0,
+                                   int total) {
+  const int n4 = total >> 2;
+  const f32x4* b4 = reinterpret_cast<const f32x4*>(z) + (e0 >> 2);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int i = threadIdx.x + s * kRows;
+    if (i < n4) a.v[s] = b4[i];
+  }
+  const int t = (n4 << 2) + threadIdx.x;
+  if (t < total) a.tail = z[e0 + t];
+}
+
+template <int NS>
+__device__ inline void commit_ahead(const Ahead<NS>& a, int total, float* tile) {
+  const int n4 = total >> 2;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int i = threadIdx.x + s * kRows;
+    if (i < n4) reinterpret_cast<f32x4*>(tile)[i] = a.v[s];
+  }
+  const int t = (n4 << 2) + threadIdx.x;
+  if (t < total) tile[t] = a.tail;
+}
+
 __device__ inline void load_tile(const float* __restrict__ z, int64_t ld, int64_t r0, int nrows,
                                  int C, int SC, float* tile) {
   const int total = nrows * C;
-  if (ld == C && SC == C) {
-    const float* base = z + r0 * C;
-    if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {
-      const int n4 = total >> 2;
-      for (int i = threadIdx.x; i < n4; i += blockDim.x)
-        reinterpret_cast<float4*>(tile)[i] = reinterpret_cast<const float4*>(base)[i];
-      for (int i = (n4 << 2) + threadIdx.x; i < total; i += blockDim.x) tile[i] = base[i];
-    } else {
-      for (int i = threadIdx.x; i < total; i += blockDim.x) tile[i] = base[i];
-    }
-    return;
-  }
   for (int i = threadIdx.x; i < total; i += blockDim.x) {
     const int r = i / C, c = i - r * C;
     tile[r * SC + c] = z[(r0 + r) * ld + c];
@@ -55,16 +85,12 @@ __device__ inline void load_tile(const float* __restrict__ z, int64_t ld, int64_
 __device__ inline void store_tile(float* __restrict__ out, int64_t ld, int64_t r0, int nrows,
                                   int C, int SC, const float* tile) {
   const int total = nrows * C;
-  if (ld == C && SC == C) {
+  if (ld == C && SC == C && (reinterpret_cast<uintptr_t>(out + r0 * C) & 15) == 0) {
     float* base = out + r0 * C;
-    if ((reinterpret_cast<uintptr_t>(base) & 15) == 0) {
-      const int n4 = total >> 2;
-      for (int i = threadIdx.x; i < n4; i += blockDim.x)
-        reinterpret_cast<float4*>(base)[i] = reinterpret_cast<const float4*>(tile)[i];
-      for (int i = (n4 << 2) + threadIdx.x; i < total; i += blockDim.x) base[i] = tile[i];
-    } else {
-      for (int i = threadIdx.x; i < total; i += blockDim.x) base[i] = tile[i];
-    }
+    const int n4 = total >> 2;
+    for (int i = threadIdx.x; i < n4; i += blockDim.x)
+      reinterpret_cast<float4*>(base)[i] = reinterpret_cast<const float4*>(tile)[i];
+    for (int i = (n4 << 2) + threadIdx.x; i < total; i += blockDim.x) base[i] = tile[i];
     return;
   }
   for (int i = threadIdx.x; i < total; i += blockDim.x) {
@@ -82,6 +108,11 @@ __device__ inline void row_lse(const float* row, int C, float& m, float& lse) {
   lse = logf(s);
 }
 
+__device__ inline int tile_rows(int64_t n, int64_t r0) {
+  return static_cast<int>(n - r0 < kRows ? n - r0 : kRows);
+}
+
+template <int NS>
 __global__ __launch_bounds__(kRows) void xent_fwd_kernel(int64_t n, int C, int SC,
                                                          const float* __restrict__ z, int64_t ld,
                                                          const int64_t* __restrict__ labels,
@@ -90,22 +121,27 @@ __global__ __launch_bounds__(kRows) void xent_fwd_kernel(int64_t n, int C, int S
   extern __shared__ float tile[];
   float acc = 0.0f;
   const int64_t ntiles = (n + kRows - 1) / kRows;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  Ahead<NS> ahead;
+  int64_t t = blockIdx.x;
+  if (NS > 0 && t < ntiles) fetch_ahead(ahead, z, t * kRows * C, tile_rows(n, t * kRows) * C);
+  for (; t < ntiles; t += gridDim.x) {
     const int64_t r0 = t * kRows;
-    const int nrows = static_cast<int>(n - r0 < kRows ? n - r0 : kRows);
-    __syncthreads();  // the previous tile's rows are consumed
-    load_tile(z, ld, r0, nrows, C, SC, tile);
-    __syncthreads();
+    const int nrows = tile_rows(n, r0);
     const int r = threadIdx.x;
-    if (r < nrows) {
-      const int64_t y = labels[r0 + r];
-      if (y >= 0 && y < C) {
-        const float* row = tile + r * SC;
-        float m, lse;
-        row_lse(row, C, m, lse);
-        const float nll = -((row[y] - m) - lse);
-        acc += w != nullptr ? nll * w[r0 + r] : nll;
-      }
+    const int64_t y = r < nrows ? labels[r0 + r] : -1;
+    const float wr = (r < nrows && w != nullptr) ? w[r0 + r] : 1.0f;
+    __syncthreads();  // the previous tile's rows are consumed
+    if (NS > 0) commit_ahead(ahead, nrows * C, tile);
+    else load_tile(z, ld, r0, nrows, C, SC, tile);
+    __syncthreads();
+    const int64_t tn = t + gridDim.x;  // the next tile's loads overlap this one's rows
+    if (NS > 0 && tn < ntiles) fetch_ahead(ahead, z, tn * kRows * C, tile_rows(n, tn * kRows) * C);
+    if (r < nrows && y >= 0 && y < C) {
+      const float* row = tile + r * SC;
+      float m, lse;
+      row_lse(row, C, m, lse);
+      const float nll = -((row[y] - m) - lse);
+      acc += w != nullptr ? nll * wr : nll;
     }
   }
   // workgroup sum in a fixed tree
@@ -129,6 +165,7 @@ __global__ void xent_sum_kernel(int nparts, const float* __restrict__ partial,
   }
 }
 
+template <int NS>
 __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int SC,
                                                          const float* __restrict__ z, int64_t ld,
                                                          const int64_t* __restrict__ labels,
@@ -138,20 +175,27 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
   extern __shared__ float tile[];
   const float g = grad_loss[0];
   const int64_t ntiles = (n + kRows - 1) / kRows;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  Ahead<NS> ahead;
+  int64_t t = blockIdx.x;
+  if (NS > 0 && t < ntiles) fetch_ahead(ahead, z, t * kRows * C, tile_rows(n, t * kRows) * C);
+  for (; t < ntiles; t += gridDim.x) {
     const int64_t r0 = t * kRows;
-    const int nrows = static_cast<int>(n - r0 < kRows ? n - r0 : kRows);
-    __syncthreads();
-    load_tile(z, ld, r0, nrows, C, SC, tile);
-    __syncthreads();
+    const int nrows = tile_rows(n, r0);
     const int r = threadIdx.x;
+    const int64_t y = r < nrows ? labels[r0 + r] : -1;
+    const float wr = (r < nrows && w != nullptr) ? w[r0 + r] : 1.0f;
+    __syncthreads();  // the previous tile has left LDS
+    if (NS > 0) commit_ahead(ahead, nrows * C, tile);
+    else load_tile(z, ld, r0, nrows, C, SC, tile);
+    __syncthreads();
+    const int64_t tn = t + gridDim.x;
+    if (NS > 0 && tn < ntiles) fetch_ahead(ahead, z, tn * kRows * C, tile_rows(n, tn * kRows) * C);
     if (r < nrows) {
       float* row = tile + r * SC;
-      const int64_t y = labels[r0 + r];
       if (y >= 0 && y < C) {
         float m, lse;
         row_lse(row, C, m, lse);
-        const float gw = w != nullptr ? g * w[r0 + r] : g;
+        const float gw = w != nullptr ? g * wr : g;
         for (int c = 0; c < C; ++c) {
           const float p = expf((row[c] - m) - lse);
           row[c] = c == y ? gw * p - gw : gw * p;
@@ -179,6 +223,19 @@ inline int xent_grid(int64_t n, int SC) {
 
 inline int lds_stride(int C) { return C | 1; }
 
+// rows packed back to back at an odd width, from a 16-byte aligned start: each
+// tile is one float4 run (a tile's offset, kRows * C floats, is a multiple of 4)
+inline bool flat(const float* z, int64_t ld, int C, int SC) {
+  return ld == C && SC == C && (reinterpret_cast<uintptr_t>(z) & 15) == 0;
+}
+
+// float4 registers per lane that hold one tile of C-float rows (C / 4 rounded
+// up to a compiled count)
+inline int ahead_slots(int C) {
+  const int s = (C + 3) / 4;
+  return s <= 4 ? 4 : s <= 8 ? 8 : s <= 12 ? 12 : 16;
+}
+
 }  // namespace
 
 }  // namespace dglhip
@@ -205,8 +262,18 @@ int dglhip_xent_fwd_device(int64_t num_rows, int64_t num_classes, const float* l
     DGLHIP_CHECK(ld >= num_classes, "row stride " << ld << " below the class count");
     DGLHIP_CHECK(logits && labels, "null pointer argument");
     const int grid = xent_grid(num_rows, SC);
-    hipLaunchKernelGGL(xent_fwd_kernel, dim3(grid), dim3(kRows), kRows * SC * 4, stream,
-                       num_rows, C, SC, logits, ld, labels, weight, workspace);
+    const int ns = flat(logits, ld, C, SC) ? ahead_slots(C) : 0;
+    auto fwd = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(grid), dim3(kRows), kRows * SC * 4, stream, num_rows, C, SC,
+                         logits, ld, labels, weight, workspace);
+    };
+    switch (ns) {
+      case 4: fwd(xent_fwd_kernel<4>); break;
+      case 8: fwd(xent_fwd_kernel<8>); break;
+      case 12: fwd(xent_fwd_kernel<12>); break;
+      case 16: fwd(xent_fwd_kernel<16>); break;
+      default: fwd(xent_fwd_kernel<0>); break;
+    }
     hipLaunchKernelGGL(xent_sum_kernel, dim3(1), dim3(64), 0, stream, grid, workspace, loss);
   }
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "cross-entropy launch failed");
@@ -225,8 +292,19 @@ int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* l
   DGLHIP_CHECK(ld >= num_classes && ldd >= num_classes, "row stride below the class count");
   DGLHIP_CHECK(logits && labels && grad_loss && dlogits, "null pointer argument");
   const int C = static_cast<int>(num_classes), SC = lds_stride(C);
-  hipLaunchKernelGGL(xent_bwd_kernel, dim3(xent_grid(num_rows, SC)), dim3(kRows), kRows * SC * 4,
-                     stream, num_rows, C, SC, logits, ld, labels, weight, grad_loss, dlogits, ldd);
+  const int grid = xent_grid(num_rows, SC);
+  const int ns = flat(logits, ld, C, SC) ? ahead_slots(C) : 0;
+  auto bwd = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(kRows), kRows * SC * 4, stream, num_rows, C, SC,
+                       logits, ld, labels, weight, grad_loss, dlogits, ldd);
+  };
+  switch (ns) {
+    case 4: bwd(xent_bwd_kernel<4>); break;
+    case 8: bwd(xent_bwd_kernel<8>); break;
+    case 12: bwd(xent_bwd_kernel<12>); break;
+    case 16: bwd(xent_bwd_kernel<16>); break;
+    default: bwd(xent_bwd_kernel<0>); break;
+  }
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "cross-entropy backward launch failed");
   API_END();
 }

@@ -99,6 +99,7 @@ def _load():
         "dglhip_node_linear_dgrad_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp,
                                                      _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp,
                                                      _c_i64, _vp]),
+        "dglhip_div_rows_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
         "dglhip_xent_workspace_floats": (_c_int, []),
         "dglhip_xent_fwd_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_xent_bwd_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp,

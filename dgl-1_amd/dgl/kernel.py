@@ -734,8 +734,12 @@ class _GSpMM(torch.autograd.Function):
                 # the quotient written straight into the padded rows the
                 # transposed product gathers (one pass instead of the
                 # division's and the padding copy's)
-                buf = dout.new_empty(dout.shape[0], padded_width(F))
-                dout = torch.div(dout, deg, out=buf[:, :F])
+                ld = padded_width(F)
+                buf = dout.new_empty(dout.shape[0], ld)
+                check_call(LIB.dglhip_div_rows_device(
+                    dout.shape[0], F, ptr(dout), dout.stride(0), ptr(deg), ptr(buf), ld,
+                    _stream_of(dout.device)))
+                dout = buf[:, :F]
             else:
                 dout = (dout / deg).contiguous()
             red_b = RED_SUM

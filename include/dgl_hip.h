@@ -267,6 +267,14 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
                                     const float* dy2, int64_t lddy2, const float* w2, float* dx,
                                     int64_t lddx, const float* gate, int64_t ldg, void* stream);
 
+/* out[r, :F] = x[r, :F] / divisor[r] (IEEE division: torch.div's bits) over
+ * num_rows rows of feat_len (1..4096) floats, x and out at their own row
+ * strides: the mean reducer's backward dC / deg written into the row-padded
+ * buffer the transposed g-SpMM gathers (csrc/rowops.hip). out's pad columns
+ * [feat_len, ldo) may be overwritten (with zeros). */
+int dglhip_div_rows_device(int64_t num_rows, int64_t feat_len, const float* x, int64_t ldx,
+                           const float* divisor, float* out, int64_t ldo, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* Weighted softmax cross-entropy over node rows (csrc/node_loss.hip): the   */
 /* loss of a full-graph node classifier. No reference counterpart: the       */
