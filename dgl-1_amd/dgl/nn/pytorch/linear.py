@@ -252,6 +252,19 @@ class _PreAggregateFn(torch.autograd.Function):
         ctx.graph = None
         dy = dy.contiguous()
         need = ctx.needs_input_grad
+        dws = None
+        side = _side_stream(dy.device) if (_OVERLAP and dy.is_cuda and need[1]) else None
+        if side is not None:
+            # the self weight's gradient needs only dy: its MFMA product runs on
+            # a side stream while the transposed aggregation (a byte-bound
+            # gather) runs on this one (the byte-bound bias column sums stay
+            # here: beside the gather they only slow both)
+            main = torch.cuda.current_stream(dy.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                dws = _splitk_tn(dy, x.contiguous())
+            for t in (dy, x):
+                t.record_stream(side)
         (dpre,) = torch.autograd.grad(neigh, pre_leaf, dy)
         dpre = dpre.contiguous()
         dx = None
@@ -270,10 +283,27 @@ class _PreAggregateFn(torch.autograd.Function):
             else:
                 dx = dy.matmul(w_self)
                 dx.addmm_(dpre, w_neigh)
-        dws = _splitk_tn(dy, x.contiguous()) if need[1] else None
+        if side is None:
+            dws = _splitk_tn(dy, x.contiguous()) if need[1] else None
         db = _colsum(dy) if ctx.has_bias and need[2] else None
         dwn = _splitk_tn(dpre, x.contiguous()) if need[3] else None
+        if side is not None:
+            main.wait_stream(side)
+            dws.record_stream(main)
         return dx, dws, db, dwn, None
+
+
+_OVERLAP = True
+_SIDE = {}
+
+
+def _side_stream(device):
+    """One side stream per device for gradients that can run beside the
+    aggregation's backward."""
+    key = torch.device(device).index
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(device=device)
+    return _SIDE[key]
 
 
 def _relu_producer(x):
