@@ -28,6 +28,7 @@
 
 #include <hip/hip_runtime.h>
 
+
 namespace dglhip {
 
 namespace {
@@ -76,36 +77,32 @@ __global__ __launch_bounds__(512) void node_linear_fwd_kernel(
     const int c = 16 * (t < T1 ? t : t - T1) + r;
     bias[t] = (o.b != nullptr && c < o.m) ? o.b[c] : 0.0f;
   }
-  // the 16 rows of x a block needs, as MFMA operands (zero past the end)
-  auto load_block = [&](int64_t blk, f32x4 (&a)[KB][4]) {
+  // pass p (64 input columns) of the 16 rows of x a block needs, as MFMA
+  // operands (zero past the end)
+  auto load_pass = [&](int64_t blk, int p, f32x4 (&ap)[4]) {
     const int64_t row = blk * 16 + r;
     if (row < n) {
-      const float* xr1 = x1 + row * ldx1 + 4 * h;
-      const float* xr2 = x2 + row * ldx2 + 4 * h;
+      const float* xr = p < KB1 ? x1 + row * ldx1 + 64 * p + 4 * h
+                                : x2 + row * ldx2 + 64 * (p - KB1) + 4 * h;
 #pragma unroll
-      for (int p = 0; p < KB; ++p)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          a[p][j] = *reinterpret_cast<const f32x4*>(
-              p < KB1 ? xr1 + 64 * p + 16 * j : xr2 + 64 * (p - KB1) + 16 * j);
+      for (int j = 0; j < 4; ++j) ap[j] = *reinterpret_cast<const f32x4*>(xr + 16 * j);
     } else {
 #pragma unroll
-      for (int p = 0; p < KB; ++p)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[p][j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+      for (int j = 0; j < 4; ++j) ap[j] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
     }
   };
   int64_t blk = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
   f32x4 a[KB][4];
-  if (blk < nblk) load_block(blk, a);
+  if (blk < nblk) {
+#pragma unroll
+    for (int p = 0; p < KB; ++p) load_pass(blk, p, a[p]);
+  }
   for (; blk < nblk; blk += nwaves) {
     // the weight operands are loop-invariant: without this the compiler keeps
     // all of them in registers across blocks (K/4 x T values) and spills
     asm volatile("" ::: "memory");
     const int64_t r0 = blk * 16;
-    // the next block's rows are in flight while this block's MFMAs run
-    f32x4 an[KB][4];
-    if (blk + nwaves < nblk) load_block(blk + nwaves, an);
+    const int64_t next = blk + nwaves;
     f32x4 acc[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) acc[t] = f32x4{bias[t], bias[t], bias[t], bias[t]};
@@ -135,6 +132,9 @@ __global__ __launch_bounds__(512) void node_linear_fwd_kernel(
         for (int t = 0; t < T; ++t)
           acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[p][j][c], bw[g & 1][c][t], acc[t], 0,
                                                         0, 0);
+      // the pass's operands are consumed: the next block's pass p loads into
+      // the same registers, in flight during this block's remaining passes
+      if (j == 3 && next < nblk) load_pass(next, p, a[p]);
     }
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -147,10 +147,6 @@ __global__ __launch_bounds__(512) void node_linear_fwd_kernel(
         if (orow < n) o.y[orow * o.ldy + c] = o.relu ? fmaxf(acc[t][i], 0.0f) : acc[t][i];
       }
     }
-#pragma unroll
-    for (int p = 0; p < KB; ++p)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[p][j] = an[p][j];
   }
 }
 
@@ -281,6 +277,17 @@ void launch_fwd(int64_t n, const float* x1, int64_t ldx1, const float* x2, int64
   hipLaunchKernelGGL((node_linear_fwd_kernel<KB1, KB2, T1, T2>),
                      dim3(persistent_blocks(n, lds)), dim3(nl_threads()), 0, stream, n, x1, ldx1, x2,
                      ldx2, o1, o2);
+}
+
+// 65..128 outputs of two 128-column inputs in ONE pass over the inputs (8
+// tiles; the weights take 135 KB of LDS, one 512-lane workgroup per CU, 256
+// registers a lane): 38.4 ms at 67M rows against 41.4 for one pass per 64
+// outputs and 43 for hipBLASLt (tools/node_linear_bench.py)
+void launch_fwd_wide(int64_t n, const float* x1, int64_t ldx1, const float* x2, int64_t ldx2,
+                     const LinOut& o, hipStream_t stream) {
+  constexpr int lds = 64 * 4 * (16 * 8 + 4) * 4;
+  hipLaunchKernelGGL((node_linear_fwd_kernel<2, 2, 8, 0>), dim3(persistent_blocks(n, lds)),
+                     dim3(nl_threads()), 0, stream, n, x1, ldx1, x2, ldx2, o, o);
 }
 
 template <int KB, int T1>
@@ -418,10 +425,13 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
   DGLHIP_CHECK(x1 && x2 && w1 && w2 && y, "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(x1) % 16 == 0 && reinterpret_cast<uintptr_t>(x2) % 16 == 0,
                "inputs must be 16-byte aligned");
-  // at most 64 outputs per pass (4 tiles): one pass over 128 outputs (8
-  // tiles, 135 KB of weights in LDS, one wave per SIMD, no spills) took 44.6
-  // ms at 67M rows against 42.1 for two passes (tools/node_linear_bench.py);
-  // wider outputs take one pass per 64 columns
+  // otherwise at most 64 outputs per pass (4 tiles), one pass per 64 columns
+  if (in_feats == 128 && m > 64) {
+    LinOut o{w1, w2, b, y, ldy, static_cast<int>(m), relu ? 1 : 0};
+    launch_fwd_wide(num_rows, x1, ldx1, x2, ldx2, o, stream);
+    DGLHIP_CHECK(hipGetLastError() == hipSuccess, "two-input node Linear launch failed");
+    return 0;
+  }
   for (int64_t c0 = 0; c0 < m; c0 += 64) {
     LinOut o{w1 + c0 * in_feats, w2 + c0 * in_feats, b ? b + c0 : nullptr, y + c0, ldy,
              static_cast<int>(std::min<int64_t>(64, m - c0)), relu ? 1 : 0};

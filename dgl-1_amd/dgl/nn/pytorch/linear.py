@@ -122,10 +122,12 @@ def _node_linear2(x, w1, ld1, w2, b2):
 
 
 def _mfma_cat_ok(x1, x2, m, relu=False):
-    # up to 64 outputs (one pass over the inputs), or 128 with the ReLU fused
-    # into the store; without it hipBLASLt's tiles run the two 128-output
-    # products as fast (43.3 vs 44.4 ms at 67M rows, tools/node_linear_bench.py)
-    return (1 <= m <= (128 if relu else 64) and x1.shape == x2.shape and all(
+    # up to 64 outputs, or 128 from 128-column inputs (one pass over the
+    # inputs: 38.4 ms at 67M rows vs 43 for hipBLASLt's two products,
+    # tools/node_linear_bench.py), or 128 from 64-column inputs with the ReLU
+    # fused into the store (two passes)
+    k = x1.shape[1] if x1.dim() == 2 else 0
+    return (1 <= m <= (128 if (relu or k == 128) else 64) and x1.shape == x2.shape and all(
         t.is_cuda and t.dtype == torch.float32 and t.dim() == 2 and t.stride(1) == 1 and
         t.stride(0) % 4 == 0 and t.shape[1] in (64, 128) and t.data_ptr() % 16 == 0
         for t in (x1, x2)))

@@ -246,7 +246,7 @@ int dglhip_node_linear_device(int64_t num_rows, int64_t in_feats, const float* x
 /* y = x1 W1^T + x2 W2^T (+ b), relu != 0: max(that, 0): one output from two
  * inputs of in_feats (64 or 128) columns each (GraphSAGE's fc_self(h) +
  * fc_neigh(agg) and its activation); W1, W2 [m][in_feats], 1 <= m <= 128 (one
- * pass over the inputs per 64 outputs). */
+ * pass over the inputs; with in_feats 64 and m > 64, one per 64 outputs). */
 int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const float* x1,
                                   int64_t ldx1, const float* x2, int64_t ldx2, int64_t m,
                                   const float* w1, const float* w2, const float* b, float* y,

@@ -152,7 +152,7 @@ def test_sage_dense_mfma_matches_unfused(cuda):
                                    atol=1e-5 * float(b.grad.abs().max()))
 
 
-@pytest.mark.parametrize("k,m", [(128, 128), (128, 41), (64, 100), (64, 16)])
+@pytest.mark.parametrize("k,m", [(128, 128), (128, 100), (128, 65), (128, 41), (64, 100), (64, 16)])
 def test_cat_exact_integers(cuda, k, m):
     """y = x1 W1^T + x2 W2^T + b (sage_dense's square / widening layer)."""
     rng = np.random.default_rng(k + m)
@@ -160,9 +160,9 @@ def test_cat_exact_integers(cuda, k, m):
     x1, x2 = _ints(rng, (n, k)).to(cuda), _ints(rng, (n, k)).to(cuda)
     w1, w2 = _ints(rng, (m, k), -2, 3).to(cuda), _ints(rng, (m, k), -2, 3).to(cuda)
     b = _ints(rng, (m,)).to(cuda)
-    # sage_dense routes up to 64 outputs here; the entry takes up to 128
-    # (one pass per 64 columns)
-    assert L._mfma_cat_ok(x1, x2, m) == (m <= 64)
+    # sage_dense routes up to 64 outputs here, 128 from 128-column inputs
+    # (one pass), or 128 with a fused ReLU
+    assert L._mfma_cat_ok(x1, x2, m) == (m <= 64 or k == 128)
     assert L._mfma_cat_ok(x1, x2, m, relu=True)
     y = L._node_linear_cat(x1, w1, x2, w2, b)
     ref = x1.double() @ w1.double().t() + x2.double() @ w2.double().t() + b.double()
