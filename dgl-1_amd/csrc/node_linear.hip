@@ -158,9 +158,14 @@ struct GradIn {
 };
 
 // dx = dy1 W1 + dy2 W2 over S1 (S2) 4-wide steps of output 1's (2's) columns;
-// KT 16-column tiles of dx. With a gate (the ReLU output that x is), the
-// store is ReLU's backward rule: 0 where gate <= 0 (torch threshold_backward,
-// NaN gates pass the gradient), so the mask costs no pass of its own.
+// KT 16-column tiles of dx. Computed transposed, dxᵀ = Wᵀ dyᵀ: the weights
+// are the MFMA's A operand and the gradient rows its B operand, so a lane's
+// four accumulator registers are four consecutive columns of ONE dx row (D
+// row 4(l>>4)+i = dx column, D column l&15 = dx row): each tile leaves as one
+// 16-byte store per lane (and the gate arrives as one 16-byte load) instead
+// of four scalar ones. With a gate (the ReLU output that x is), the store is
+// ReLU's backward rule: 0 where gate <= 0 (torch threshold_backward, NaN
+// gates pass the gradient), so the mask costs no pass of its own.
 template <int KT, int S1, int S2>
 __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn g1, GradIn g2,
                                                               float* __restrict__ dx,
@@ -185,34 +190,31 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
   const int lane = threadIdx.x & 63, r = lane & 15, h = lane >> 4;
   const int64_t nwaves = int64_t(gridDim.x) * (blockDim.x >> 6);
   const int64_t nblk = (n + 15) / 16;
-  auto load_block = [&](int64_t blk, float (&a)[S]) {
+  // step s of the gradient rows a block needs: row r, column 4s + h
+  auto load_step = [&](int64_t blk, int s) -> float {
     const int64_t row = blk * 16 + r;
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-      const bool first = s < S1;
-      const GradIn& g = first ? g1 : g2;
-      const int col = 4 * (first ? s : s - S1) + h;
-      a[s] = (row < n && col < g.m) ? g.dy[row * g.lddy + col] : 0.0f;
-    }
+    const bool first = s < S1;
+    const GradIn& g = first ? g1 : g2;
+    const int col = 4 * (first ? s : s - S1) + h;
+    return (row < n && col < g.m) ? g.dy[row * g.lddy + col] : 0.0f;
   };
   int64_t blk = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
   float a[S];
-  if (blk < nblk) load_block(blk, a);
+  if (blk < nblk) {
+#pragma unroll
+    for (int s = 0; s < S; ++s) a[s] = load_step(blk, s);
+  }
   for (; blk < nblk; blk += nwaves) {
     asm volatile("" ::: "memory");  // weight operands re-read from LDS per block
-    const int64_t r0 = blk * 16;
-    float an[S];  // the next block's gradient rows, in flight during the MFMAs
-    if (blk + nwaves < nblk) load_block(blk + nwaves, an);
-    // this block's gate values, in flight during the MFMAs as well
-    float gv[KT][4];
-    if (gate != nullptr) {
+    const int64_t row = blk * 16 + r;  // this lane's dx row
+    const int64_t next = blk + nwaves;
+    // this row's gate values (4 consecutive columns per tile), in flight
+    // during the MFMAs
+    f32x4 gv[KT];
+    if (gate != nullptr && row < n) {
 #pragma unroll
       for (int t = 0; t < KT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int64_t orow = r0 + 4 * h + i;
-          gv[t][i] = orow < n ? gate[orow * ldg + 16 * t + r] : 0.0f;
-        }
+        gv[t] = *reinterpret_cast<const f32x4*>(gate + row * ldg + 16 * t + 4 * h);
     }
     f32x4 acc[KT];
 #pragma unroll
@@ -231,20 +233,21 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int t = 0; t < KT; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], bw[s & 1][t], acc[t], 0, 0, 0);
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(bw[s & 1][t], a[s], acc[t], 0, 0, 0);
+      // step s's operand is consumed: the next block's loads into its register
+      if (next < nblk) a[s] = load_step(next, s);
     }
+    if (row < n) {
 #pragma unroll
-    for (int t = 0; t < KT; ++t)
+      for (int t = 0; t < KT; ++t) {
+        f32x4 v = acc[t];
+        if (gate != nullptr) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t orow = r0 + 4 * h + i;
-        if (orow < n) {
-          const float v = gate != nullptr && gv[t][i] <= 0.0f ? 0.0f : acc[t][i];
-          dx[orow * lddx + 16 * t + r] = v;
+          for (int i = 0; i < 4; ++i) v[i] = gv[t][i] <= 0.0f ? 0.0f : v[i];
         }
+        *reinterpret_cast<f32x4*>(dx + row * lddx + 16 * t + 4 * h) = v;
       }
-#pragma unroll
-    for (int s = 0; s < S; ++s) a[s] = an[s];
+    }
   }
 }
 
@@ -459,6 +462,11 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
                "row stride below the row width");
   DGLHIP_CHECK(dy1 && w1 && dx && (m2 == 0 || (dy2 && w2)), "null pointer argument");
   DGLHIP_CHECK(gate == nullptr || ldg >= in_feats, "gate row stride below in_feats");
+  // dx and the gate move as 16-byte vectors
+  DGLHIP_CHECK(lddx % 4 == 0 && reinterpret_cast<uintptr_t>(dx) % 16 == 0,
+               "dx: 16-byte aligned rows (row stride a multiple of 4)");
+  DGLHIP_CHECK(gate == nullptr || (ldg % 4 == 0 && reinterpret_cast<uintptr_t>(gate) % 16 == 0),
+               "gate: 16-byte aligned rows (row stride a multiple of 4)");
   GradIn g1{dy1, lddy1, w1, static_cast<int>(m1)};
   GradIn g2{dy2, lddy2, w2, static_cast<int>(m2)};
   const Gate gt{gate, ldg};

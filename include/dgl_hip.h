@@ -258,7 +258,7 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
 int dglhip_set_node_linear_variant(int threads, int wgs_per_cu);
 
 /* Input gradient of the first: dx = dy1 W1 + dy2 W2 (m2 = 0: dy1 W1 only);
- * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx. gate
+ * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx (16-byte aligned rows). gate
  * (optional, rows at stride ldg): x's own values when x is a ReLU output; dx
  * is then 0 where gate <= 0 (ReLU's backward rule, torch threshold_backward),
  * the mask applied in the store instead of a pass of its own. */
