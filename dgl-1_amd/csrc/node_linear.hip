@@ -171,7 +171,8 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
                                                               float* __restrict__ dx,
                                                               int64_t lddx,
                                                               const float* __restrict__ gate,
-                                                              int64_t ldg) {
+                                                              int64_t ldg,
+                                                              float* __restrict__ part) {
   constexpr int K = 16 * KT;
   constexpr int S = S1 + S2;
   constexpr int SK = K + 16;  // rows 4s + h of one MFMA land 16 banks apart
@@ -198,12 +199,17 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
     const int col = 4 * (first ? s : s - S1) + h;
     return (row < n && col < g.m) ? g.dy[row * g.lddy + col] : 0.0f;
   };
-  int64_t blk = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  const int64_t wave = int64_t(blockIdx.x) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  int64_t blk = wave;
   float a[S];
   if (blk < nblk) {
 #pragma unroll
     for (int s = 0; s < S; ++s) a[s] = load_step(blk, s);
   }
+  // column sums of the stored dx over this lane's rows (part != null)
+  f32x4 cs[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) cs[t] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
   for (; blk < nblk; blk += nwaves) {
     asm volatile("" ::: "memory");  // weight operands re-read from LDS per block
     const int64_t row = blk * 16 + r;  // this lane's dx row
@@ -246,9 +252,41 @@ __global__ __launch_bounds__(512) void node_linear_bwd_kernel(int64_t n, GradIn 
           for (int i = 0; i < 4; ++i) v[i] = gv[t][i] <= 0.0f ? 0.0f : v[i];
         }
         *reinterpret_cast<f32x4*>(dx + row * lddx + 16 * t + 4 * h) = v;
+        if (part != nullptr) cs[t] += v;
       }
     }
   }
+  if (part != nullptr) {
+    // this wave's column sums: the 16 lanes of a column group (same h) summed
+    // in a fixed butterfly, one row of K partials per wave
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float v = cs[t][i];
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off, 64);
+        if (r == 0) part[wave * K + 16 * t + 4 * h + i] = v;
+      }
+  }
+}
+
+// colsum[c] = the waves' partial column sums: one workgroup per column, lane
+// j summing waves j, j + 256, ... in order, then a fixed tree over the lanes
+__global__ __launch_bounds__(256) void colsum_partials_kernel(int64_t nparts, int K,
+                                                              const float* __restrict__ part,
+                                                              float* __restrict__ colsum) {
+  __shared__ float red[256];
+  const int c = blockIdx.x;
+  float s = 0.0f;
+  for (int64_t w = threadIdx.x; w < nparts; w += 256) s += part[w * K + c];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) colsum[c] = red[0];
 }
 
 // Persistent grid: the weights are staged in LDS once per workgroup and the
@@ -316,17 +354,33 @@ void dispatch_fwd(int t1, int t2, int64_t n, const float* x, int64_t ldx, const 
   }
 }
 
+// what the input-gradient store does besides storing: the ReLU gate, and the
+// per-wave column-sum partials (with the grid it used, for the final sum)
 struct Gate {
   const float* p;
   int64_t ld;
+  float* part;
+  int64_t nparts;  // set by the launch: waves of the grid
 };
 
 template <int KT, int S1, int S2>
 void launch_bwd(int64_t n, const GradIn& g1, const GradIn& g2, float* dx, int64_t lddx,
-                const Gate& gate, hipStream_t stream) {
+                Gate& gate, hipStream_t stream) {
   constexpr int lds = 4 * (S1 + S2) * (16 * KT + 16) * 4;
-  hipLaunchKernelGGL((node_linear_bwd_kernel<KT, S1, S2>), dim3(persistent_blocks(n, lds)),
-                     dim3(nl_threads()), 0, stream, n, g1, g2, dx, lddx, gate.p, gate.ld);
+  const int64_t grid = persistent_blocks(n, lds);
+  gate.nparts = grid * (nl_threads() / 64);
+  hipLaunchKernelGGL((node_linear_bwd_kernel<KT, S1, S2>), dim3(grid), dim3(nl_threads()), 0,
+                     stream, n, g1, g2, dx, lddx, gate.p, gate.ld, gate.part);
+}
+
+// upper bound of launch_bwd's waves: 4 workgroups per CU of up to 512 lanes
+// (persistent_blocks) or the tuning knob's count
+inline int64_t max_bwd_waves() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  return int64_t(cus) * 8 * 8;
 }
 
 // reduction widths up to 64 per input: S = ceil(m / 4) rounded up to a listed
@@ -343,7 +397,7 @@ inline int round_steps(int m) {
 
 template <int KT, int S1>
 void dispatch_bwd_s2(int s2, int64_t n, const GradIn& g1, const GradIn& g2, float* dx,
-                     int64_t lddx, const Gate& gt, hipStream_t st) {
+                     int64_t lddx, Gate& gt, hipStream_t st) {
   switch (s2) {
     case 0: return launch_bwd<KT, S1, 0>(n, g1, g2, dx, lddx, gt, st);
     case 2: return launch_bwd<KT, S1, 2>(n, g1, g2, dx, lddx, gt, st);
@@ -356,7 +410,7 @@ void dispatch_bwd_s2(int s2, int64_t n, const GradIn& g1, const GradIn& g2, floa
 
 template <int KT>
 void dispatch_bwd(int s1, int s2, int64_t n, const GradIn& g1, const GradIn& g2, float* dx,
-                  int64_t lddx, const Gate& gt, hipStream_t st) {
+                  int64_t lddx, Gate& gt, hipStream_t st) {
   switch (s1) {
     case 2: return dispatch_bwd_s2<KT, 2>(s2, n, g1, g2, dx, lddx, gt, st);
     case 4: return dispatch_bwd_s2<KT, 4>(s2, n, g1, g2, dx, lddx, gt, st);
@@ -400,6 +454,10 @@ int dglhip_node_linear_device(int64_t num_rows, int64_t in_feats, const float* x
   }
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "node Linear launch failed");
   API_END();
+}
+
+int64_t dglhip_node_linear_dgrad_workspace_floats(int64_t in_feats) {
+  return max_bwd_waves() * in_feats;
 }
 
 int dglhip_set_node_linear_variant(int threads, int wgs_per_cu) {
@@ -448,7 +506,8 @@ int dglhip_node_linear_cat_device(int64_t num_rows, int64_t in_feats, const floa
 int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t m1,
                                     const float* dy1, int64_t lddy1, const float* w1, int64_t m2,
                                     const float* dy2, int64_t lddy2, const float* w2, float* dx,
-                                    int64_t lddx, const float* gate, int64_t ldg, void* stream_) {
+                                    int64_t lddx, const float* gate, int64_t ldg, float* colsum,
+                                    float* workspace, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0, "negative row count");
@@ -457,7 +516,11 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
   const int s1 = round_steps(static_cast<int>(m1)), s2 = m2 == 0 ? 0 : round_steps(static_cast<int>(m2));
   DGLHIP_CHECK(m1 >= 1 && m1 <= 64 && m2 >= 0 && m2 <= 64 && s1 > 0 && s2 >= 0,
                "input gradient on the MFMA: 1..64 (+ 0..64) outputs, got " << m1 << ", " << m2);
-  if (num_rows == 0) return 0;
+  if (num_rows == 0) {
+    if (colsum != nullptr) DGLHIP_CHECK(hipMemsetAsync(colsum, 0, in_feats * 4, stream) == hipSuccess,
+                                        "column-sum clear failed");
+    return 0;
+  }
   DGLHIP_CHECK(lddy1 >= m1 && (m2 == 0 || lddy2 >= m2) && lddx >= in_feats,
                "row stride below the row width");
   DGLHIP_CHECK(dy1 && w1 && dx && (m2 == 0 || (dy2 && w2)), "null pointer argument");
@@ -469,9 +532,16 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
                "gate: 16-byte aligned rows (row stride a multiple of 4)");
   GradIn g1{dy1, lddy1, w1, static_cast<int>(m1)};
   GradIn g2{dy2, lddy2, w2, static_cast<int>(m2)};
-  const Gate gt{gate, ldg};
+  DGLHIP_CHECK(colsum == nullptr || workspace != nullptr, "column sums need the workspace");
+  Gate gt{gate, ldg, colsum != nullptr ? workspace : nullptr, 0};
   if (in_feats == 64) dispatch_bwd<4>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
   else dispatch_bwd<8>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
+  DGLHIP_CHECK(gt.nparts <= max_bwd_waves(), "column-sum workspace too small");
+  if (colsum != nullptr) {
+    const int K = static_cast<int>(in_feats);
+    hipLaunchKernelGGL(colsum_partials_kernel, dim3(K), dim3(256), 0, stream, gt.nparts, K,
+                       workspace, colsum);
+  }
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "node Linear input-gradient launch failed");
   API_END();
 }

@@ -98,7 +98,8 @@ def _load():
         "dglhip_set_node_linear_variant": (_c_int, [_c_int, _c_int]),
         "dglhip_node_linear_dgrad_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp,
                                                      _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp,
-                                                     _c_i64, _vp]),
+                                                     _c_i64, _vp, _vp, _vp]),
+        "dglhip_node_linear_dgrad_workspace_floats": (_c_i64, [_c_i64]),
         "dglhip_div_rows_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _vp]),
         "dglhip_xent_workspace_floats": (_c_int, []),
         "dglhip_xent_fwd_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp]),

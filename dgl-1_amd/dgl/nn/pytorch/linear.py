@@ -147,18 +147,26 @@ def _node_linear_cat(x1, w1, x2, w2, b, relu=False):
     return y
 
 
-def _node_dgrad2(k, dy1, w1, dy2, w2, gate=None):
+def _node_dgrad2(k, dy1, w1, dy2, w2, gate=None, colsum=False):
     """dy1 W1 + dy2 W2 in one pass (n, k); ``gate`` (n, k, unit column
-    stride): 0 where gate <= 0 (ReLU's backward applied in the store)."""
+    stride): 0 where gate <= 0 (ReLU's backward applied in the store).
+    ``colsum``: also return dx's column sums, summed as the kernel stores."""
     from ... import _ffi, kernel
     n = dy1.shape[0]
     w1, w2 = _w(w1), _w(w2)
-    dx = torch.empty(n, k, dtype=torch.float32, device=dy1.device)
+    dev = dy1.device
+    dx = torch.empty(n, k, dtype=torch.float32, device=dev)
+    cs = ws = None
+    if colsum:
+        cs = torch.empty(k, dtype=torch.float32, device=dev)
+        ws = torch.empty(_ffi.LIB.dglhip_node_linear_dgrad_workspace_floats(k),
+                         dtype=torch.float32, device=dev)
     _ffi.check_call(_ffi.LIB.dglhip_node_linear_dgrad_device(
         n, k, dy1.shape[1], _ffi.ptr(dy1), dy1.stride(0), _ffi.ptr(w1), dy2.shape[1],
         _ffi.ptr(dy2), dy2.stride(0), _ffi.ptr(w2), _ffi.ptr(dx), k,
-        _ffi.ptr(gate), 0 if gate is None else gate.stride(0), kernel._stream_of(dy1.device)))
-    return dx
+        _ffi.ptr(gate), 0 if gate is None else gate.stride(0), _ffi.ptr(cs), _ffi.ptr(ws),
+        kernel._stream_of(dev)))
+    return (dx, cs) if colsum else dx
 
 
 class _DualLinearFn(torch.autograd.Function):
@@ -188,13 +196,18 @@ class _DualLinearFn(torch.autograd.Function):
     def backward(ctx, dy):
         x, w_self, agg, w_neigh, out = ctx.saved_tensors
         premasked, ctx.premasked = ctx.premasked, None
-        if ctx.relu and premasked != (dy.data_ptr(), dy._version):
+        colsum = None
+        if premasked is not None and premasked[:2] == (dy.data_ptr(), dy._version):
+            colsum = premasked[2]  # dy's column sums, taken as it was stored
+        elif ctx.relu:
             dy = torch.ops.aten.threshold_backward(dy, out, 0)  # ReLU's own backward, one pass
         dy = dy.contiguous()
         need = ctx.needs_input_grad
         dx = dy.matmul(w_self) if need[0] else None
         dws = _splitk_tn(dy, x.contiguous()) if need[1] else None
-        db = _colsum(dy) if ctx.has_bias and need[2] else None
+        db = None
+        if ctx.has_bias and need[2]:
+            db = colsum if colsum is not None else _colsum(dy)
         dagg = dy.matmul(w_neigh) if need[3] else None
         dwn = _splitk_tn(dy, agg.contiguous()) if need[4] else None
         return dx, dws, db, dagg, dwn, None
@@ -278,10 +291,15 @@ class _PreAggregateFn(torch.autograd.Function):
                 # layer skips its own pass over the gradient when it receives
                 # this very tensor unmodified (same storage, same version:
                 # a gradient summed with another consumer's is masked there)
+                # (and, for that layer's bias gradient, dx's column sums are
+                # taken as the store writes them)
                 gate = x if node is not None else None
-                dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh, gate=gate)
                 if gate is not None:
-                    node.premasked = (dx.data_ptr(), dx._version)
+                    dx, cs = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh, gate=gate,
+                                          colsum=node.has_bias)
+                    node.premasked = (dx.data_ptr(), dx._version, cs)
+                else:
+                    dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh)
             else:
                 dx = dy.matmul(w_self)
                 dx.addmm_(dpre, w_neigh)

@@ -261,11 +261,19 @@ int dglhip_set_node_linear_variant(int threads, int wgs_per_cu);
  * in_feats 64 or 128; dy rows at their own strides; dx at stride lddx (16-byte aligned rows). gate
  * (optional, rows at stride ldg): x's own values when x is a ReLU output; dx
  * is then 0 where gate <= 0 (ReLU's backward rule, torch threshold_backward),
- * the mask applied in the store instead of a pass of its own. */
+ * the mask applied in the store instead of a pass of its own. colsum
+ * (optional, in_feats floats): the column sums of the stored dx (the bias
+ * gradient of the layer whose output x is), per lane, per wave in a fixed
+ * butterfly and over the waves in order; workspace holds the per-wave
+ * partials (dglhip_node_linear_dgrad_workspace_floats(in_feats) floats). */
 int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t m1,
                                     const float* dy1, int64_t lddy1, const float* w1, int64_t m2,
                                     const float* dy2, int64_t lddy2, const float* w2, float* dx,
-                                    int64_t lddx, const float* gate, int64_t ldg, void* stream);
+                                    int64_t lddx, const float* gate, int64_t ldg, float* colsum,
+                                    float* workspace, void* stream);
+
+/* Floats of the input-gradient entry's column-sum workspace. */
+int64_t dglhip_node_linear_dgrad_workspace_floats(int64_t in_feats);
 
 /* out[r, :F] = x[r, :F] / divisor[r] (IEEE division: torch.div's bits) over
  * num_rows rows of feat_len (1..4096) floats, x and out at their own row
