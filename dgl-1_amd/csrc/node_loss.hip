@@ -17,6 +17,7 @@
 // then per workgroup in a fixed tree, then over the workgroups in index order
 // (deterministic). Rows whose label is outside [0, C) (PyTorch's ignore_index,
 // -100) contribute nothing.
+#include "../../include/dgl_hip.h"
 #include "common.h"
 #include "launch.h"
 
@@ -171,9 +172,12 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
                                                          const int64_t* __restrict__ labels,
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ grad_loss,
-                                                         float* __restrict__ dz, int64_t ldd) {
+                                                         float* __restrict__ dz, int64_t ldd,
+                                                         float* __restrict__ colpart) {
   extern __shared__ float tile[];
   const float g = grad_loss[0];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  float col = 0.0f;  // colpart: this wave's running sum of column `lane`
   const int64_t ntiles = (n + kRows - 1) / kRows;
   Ahead<NS> ahead;
   int64_t t = blockIdx.x;
@@ -206,6 +210,55 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
     }
     __syncthreads();
     store_tile(dz, ldd, r0, nrows, C, SC, tile);
+    if (colpart != nullptr && lane < C) {
+      // the gradient rows' column sums, read back from the tile: wave w sums
+      // rows [64 w, 64 w + 64) of column `lane` in row order (lanes read
+      // consecutive LDS words: no bank conflict); the next tile waits on the
+      // __syncthreads at the loop's head
+      const int rb = wv * 64, re = nrows < rb + 64 ? nrows : rb + 64;
+      const float* tc = tile + lane;
+      float s = 0.0f;
+      if (re - rb == 64) {  // full tiles: the reads issue ahead of the adds
+#pragma unroll 16
+        for (int rr = rb; rr < rb + 64; ++rr) s += tc[rr * SC];
+      } else {
+        for (int rr = rb; rr < re; ++rr) s += tc[rr * SC];
+      }
+      col += s;
+    }
+  }
+  if (colpart != nullptr) {
+    // the workgroup's partial: its four waves in order
+    __syncthreads();
+    if (lane < C) tile[wv * C + lane] = col;
+    __syncthreads();
+    if (threadIdx.x < C) {
+      float s = tile[threadIdx.x];
+      for (int w = 1; w < kRows / 64; ++w) s += tile[w * C + threadIdx.x];
+      colpart[int64_t(blockIdx.x) * C + threadIdx.x] = s;
+    }
+  }
+}
+
+// colsum[c] = the workgroups' partial column sums: kSegs contiguous runs of
+// partials, each summed in index order by one thread, then the runs in order
+// (a fixed association: deterministic; kSegs loads in flight per column)
+constexpr int kSegs = 16;
+__global__ __launch_bounds__(kSegs * 64) void xent_colsum_kernel(
+    int nparts, int C, const float* __restrict__ colpart, float* __restrict__ colsum) {
+  __shared__ float seg_sum[kSegs * 64];
+  const int c = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const int per = (nparts + kSegs - 1) / kSegs;
+  const int i0 = seg * per, i1 = nparts < i0 + per ? nparts : i0 + per;
+  float s = 0.0f;
+  if (c < C)
+    for (int i = i0; i < i1; ++i) s += colpart[int64_t(i) * C + c];
+  seg_sum[threadIdx.x] = s;
+  __syncthreads();
+  if (seg == 0 && c < C) {
+    float t = seg_sum[c];
+    for (int k = 1; k < kSegs; ++k) t += seg_sum[k * 64 + c];
+    colsum[c] = t;
   }
 }
 
@@ -283,20 +336,39 @@ int dglhip_xent_fwd_device(int64_t num_rows, int64_t num_classes, const float* l
 int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
                            int64_t ld, const int64_t* labels, const float* weight,
                            const float* grad_loss, float* dlogits, int64_t ldd, void* stream_) {
+  return dglhip_xent_bwd_colsum_device(num_rows, num_classes, logits, ld, labels, weight,
+                                       grad_loss, dlogits, ldd, nullptr, nullptr, stream_);
+}
+
+int dglhip_xent_colsum_workspace_floats(int64_t num_classes) {
+  return static_cast<int>(kMaxBlocks * std::max<int64_t>(1, num_classes));
+}
+
+int dglhip_xent_bwd_colsum_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                                  int64_t ld, const int64_t* labels, const float* weight,
+                                  const float* grad_loss, float* dlogits, int64_t ldd,
+                                  float* colsum, float* workspace, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0, "negative row count");
   DGLHIP_CHECK(num_classes >= 1 && num_classes <= kMaxClasses,
                "cross-entropy rows: 1.." << kMaxClasses << " classes, got " << num_classes);
-  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(colsum == nullptr || workspace != nullptr, "column sums need the workspace");
+  if (num_rows == 0) {
+    if (colsum != nullptr)
+      DGLHIP_CHECK(hipMemsetAsync(colsum, 0, num_classes * 4, stream) == hipSuccess,
+                   "column-sum fill failed");
+    return 0;
+  }
   DGLHIP_CHECK(ld >= num_classes && ldd >= num_classes, "row stride below the class count");
   DGLHIP_CHECK(logits && labels && grad_loss && dlogits, "null pointer argument");
   const int C = static_cast<int>(num_classes), SC = lds_stride(C);
   const int grid = xent_grid(num_rows, SC);
   const int ns = flat(logits, ld, C, SC) ? ahead_slots(C) : 0;
+  float* colpart = colsum != nullptr ? workspace : nullptr;
   auto bwd = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kRows), kRows * SC * 4, stream, num_rows, C, SC,
-                       logits, ld, labels, weight, grad_loss, dlogits, ldd);
+                       logits, ld, labels, weight, grad_loss, dlogits, ldd, colpart);
   };
   switch (ns) {
     case 4: bwd(xent_bwd_kernel<4>); break;
@@ -305,6 +377,9 @@ int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* l
     case 16: bwd(xent_bwd_kernel<16>); break;
     default: bwd(xent_bwd_kernel<0>); break;
   }
+  if (colsum != nullptr)
+    hipLaunchKernelGGL(xent_colsum_kernel, dim3(1), dim3(kSegs * 64), 0, stream, grid, C, colpart,
+                       colsum);
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "cross-entropy backward launch failed");
   API_END();
 }

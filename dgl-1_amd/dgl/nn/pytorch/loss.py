@@ -12,7 +12,10 @@ rows PyTorch runs it as five passes over the logits (log-softmax, the nll
 gather, a zero fill, the nll scatter, the log-softmax backward); on a ROCm
 device with 1..64 classes it is one kernel forward (one read) and one
 backward (one read, one write), the upstream gradient read on the device.
-Other devices and shapes compute the expression above with PyTorch's own
+When the logits are the output of a NodeLinear / sage_dense with a bias, the
+backward also returns that bias's gradient (dz's column sums) from the same
+kernel, read back from the tile it stores (no separate column reduce over
+the rows). Other devices and shapes compute the expression above with PyTorch's own
 operators. Results agree with it to fp32 rounding (the sums associate
 differently); labels outside [0, C) contribute nothing (PyTorch's
 ignore_index = -100; other out-of-range labels are an error there).
@@ -33,6 +36,18 @@ def _fused_ok(z, y, w):
                            w.dtype == torch.float32 and w.device == z.device)))
 
 
+def _bias_producer(z):
+    """The NodeLinear / sage_dense autograd node whose output ``z`` is (the
+    tensor itself) and that will want dz's column sums for its bias, else
+    None: the loss backward then sums them from its tile as it stores dz."""
+    node = z.grad_fn
+    if (node is not None and getattr(node, "wants_dy_colsum", False) and
+            getattr(node, "out_ptr", None) == z.data_ptr() and z._base is None and
+            z.is_contiguous()):
+        return node
+    return None
+
+
 class _WeightedXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, y, w):
@@ -47,6 +62,7 @@ class _WeightedXentFn(torch.autograd.Function):
             n, C, _ffi.ptr(z), z.stride(0), _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(loss),
             _ffi.ptr(ws), kernel._stream_of(z.device)))
         ctx.save_for_backward(z, y, w)
+        ctx.bias_node = _bias_producer(z)
         return loss
 
     @staticmethod
@@ -56,9 +72,18 @@ class _WeightedXentFn(torch.autograd.Function):
         n, C = z.shape
         g = g.detach().to(torch.float32).contiguous()
         dz = torch.empty(n, C, dtype=torch.float32, device=z.device)
-        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_device(
+        node, ctx.bias_node = ctx.bias_node, None
+        cs = ws = None
+        if node is not None:
+            cs = torch.empty(C, dtype=torch.float32, device=z.device)
+            ws = torch.empty(_ffi.LIB.dglhip_xent_colsum_workspace_floats(C),
+                             dtype=torch.float32, device=z.device)
+        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_colsum_device(
             n, C, _ffi.ptr(z), z.stride(0), _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(g), _ffi.ptr(dz),
-            C, kernel._stream_of(z.device)))
+            C, _ffi.ptr(cs), _ffi.ptr(ws), kernel._stream_of(z.device)))
+        if node is not None:
+            # the producing Linear's bias gradient, summed as dz was stored
+            node.dy_colsum = (dz.data_ptr(), dz._version, cs)
         return dz, None, None
 
 

@@ -308,6 +308,20 @@ int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* l
                            int64_t ld, const int64_t* labels, const float* weight,
                            const float* grad_loss, float* dlogits, int64_t ldd, void* stream);
 
+/* Floats of the column-sum workspace of dglhip_xent_bwd_colsum_device. */
+int dglhip_xent_colsum_workspace_floats(int64_t num_classes);
+
+/* dglhip_xent_bwd_device, and colsum[j] = sum_i dlogits_ij (the output layer's
+ * bias gradient) taken from the gradient rows as they are stored: per wave in
+ * row order, per workgroup over its waves in order, then over the workgroups
+ * in 16 contiguous runs summed in order, the runs in order (deterministic). colsum NULL = no sums (workspace unused);
+ * both are device pointers. Replaces the separate column reduce of the bias
+ * gradient (nn.Linear's autograd: torch's sum over dim 0). */
+int dglhip_xent_bwd_colsum_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                                  int64_t ld, const int64_t* labels, const float* weight,
+                                  const float* grad_loss, float* dlogits, int64_t ldd,
+                                  float* colsum, float* workspace, void* stream);
+
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t feat_len, const int64_t* indptr,

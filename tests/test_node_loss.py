@@ -88,3 +88,74 @@ def test_fused_path_runs_native():
     assert L._fused_ok(z, y, w)
     out = weighted_cross_entropy(z.requires_grad_(True), y, w)
     assert type(out.grad_fn).__name__ == "_WeightedXentFnBackward"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,C", [(0, 41), (1, 41), (255, 41), (257, 7), (5000, 1), (70001, 41),
+                                 (3001, 64), (1 << 20, 41)])
+def test_bwd_column_sums(n, C):
+    """dglhip_xent_bwd_colsum_device: the same dz as the plain backward (bit
+    for bit) and colsum = dz.sum(0) to fp32 summation tolerance, reruns
+    bit-identical."""
+    from dgl import _ffi, kernel
+    dev = torch.device("cuda", 0)
+    z, y, w = _case(n, C, dev, seed=7 + n, ignore=min(n, 11))
+    g = torch.tensor(0.75, device=dev)
+    ws = torch.empty(_ffi.LIB.dglhip_xent_colsum_workspace_floats(C), device=dev)
+    outs = []
+    for with_cs in (False, True, True):
+        dz = torch.full((n, C), float("nan"), device=dev)
+        cs = torch.full((C,), float("nan"), device=dev) if with_cs else None
+        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_colsum_device(
+            n, C, _ffi.ptr(z), C, _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(g), _ffi.ptr(dz), C,
+            _ffi.ptr(cs), _ffi.ptr(ws), kernel._stream_of(dev)))
+        outs.append((dz, cs))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[1][0], outs[2][0])
+    assert torch.equal(outs[1][1], outs[2][1])
+    ref = outs[0][0].double().sum(0)
+    tol = 1e-6 * (outs[0][0].double().abs().sum(0) + 1.0)
+    assert bool(((outs[1][1].double() - ref).abs() <= tol).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("narrow", [True, False])
+def test_output_bias_grad_from_loss_kernel(narrow, monkeypatch):
+    """The output layer's bias gradient comes from the loss kernel (no column
+    reduce over the rows in the Linear's backward) and equals the float64
+    expression's; weights and input gradients are unaffected."""
+    from dgl.nn.pytorch import NodeLinear, sage_dense
+    from dgl.nn.pytorch import linear as L
+    dev = torch.device("cuda", 0)
+    n, k, C = 70001, 128, 41
+    gen = torch.Generator().manual_seed(5)
+    x = torch.randn(n, k, generator=gen).to(dev)
+    y = torch.randint(0, C, (n,), generator=gen).to(dev)
+    w = (torch.rand(n, generator=gen) < 0.5).float().to(dev)
+    torch.manual_seed(0)
+    fc_self = NodeLinear(k, C).to(dev)
+    fc_neigh = NodeLinear(k, C, bias=False).to(dev)
+
+    def agg(t):  # a linear stand-in for the mean aggregation
+        return t * 0.5
+
+    def run():
+        xx = x.detach().clone().requires_grad_(True)
+        z = sage_dense(xx, agg, fc_self, fc_neigh) if narrow else fc_self(xx)
+        loss = weighted_cross_entropy(z, y, w) * 0.01
+        fc_self.zero_grad()
+        fc_neigh.zero_grad()
+        loss.backward()
+        return z.detach(), fc_self.bias.grad.clone(), fc_self.weight.grad.clone(), xx.grad
+
+    calls = []
+    real = L._colsum
+    monkeypatch.setattr(L, "_colsum", lambda a: calls.append(a.shape) or real(a))
+    z, db, dw, dx = run()
+    assert calls == []  # the bias gradient did not run a column reduce
+    # float64 reference from the same logits
+    z64 = z.double().requires_grad_(True)
+    (F.cross_entropy(z64, y, reduction="none") * w.double()).sum().mul(0.01).backward()
+    ref = z64.grad.sum(0)
+    assert torch.allclose(db.double(), ref, atol=1e-6, rtol=1e-5)
+    assert torch.allclose(dw.double(), z64.grad.t().matmul(x.double()), atol=1e-4, rtol=1e-4)
+    assert dx is not None and bool(torch.isfinite(dx).all())

@@ -101,6 +101,11 @@ for s in $STEPS; do
       timeout -k 10 300 python -u -m pytest tests/test_distributed.py -m gpu -x -v --timeout 240 \
         --timeout-method thread -p no:cacheprovider > gpurun_out/pytest_dist.log 2>&1
       rc=$?; tail -3 gpurun_out/pytest_dist.log; ok $rc || exit $rc ;;
+    relabel)
+      timeout -k 10 300 python tools/relabel_study.py > gpurun_out/relabel_reddit.json 2> gpurun_out/relabel.err &&
+      timeout -k 10 600 python tools/relabel_study.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} \
+        --feats ${RMAT_FEATS:-128} > gpurun_out/relabel_rmat.json 2>> gpurun_out/relabel.err
+      rc=$?; cat gpurun_out/relabel.err | tail -8; [ $rc -eq 0 ] || exit $rc ;;
     reducers)
       timeout -k 10 600 python tools/reducer_bench.py > gpurun_out/reducers.json 2> gpurun_out/reducers.err
       rc=$?; cat gpurun_out/reducers.json; tail -3 gpurun_out/reducers.err; [ $rc -eq 0 ] || exit $rc ;;
