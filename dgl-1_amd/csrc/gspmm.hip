@@ -332,7 +332,7 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
-  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
+  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 4, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;  // empty tensors may carry null pointers
   DGLHIP_CHECK(indptr != nullptr && out != nullptr, "null indptr/out");
@@ -349,9 +349,10 @@ int dglhip_gspmm_device(int msg_op, int reduce_op, int64_t num_rows,
     dispatch_max(msg_op, m, stream);
     return 0;
   }
-  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
+  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
   SumLaunch a{num_rows, feat_len, elen, indptr, indices, eid, ufeat, efeat, out, row_order,
-              nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+              nullptr, nullptr,
+              reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
               stream_output(num_rows, feat_len)};
   dispatch_sum(msg_op, mean, a, stream);
   API_END();
@@ -367,7 +368,7 @@ int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
   DGLHIP_CHECK(msg_op == DGLHIP_MSG_COPY_U || msg_op == DGLHIP_MSG_U_MUL_E,
                "strided source rows: copy_u or u_mul_e, got msg op " << msg_op);
   DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
-                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
                "strided source rows: sum / mean reducers only");
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   DGLHIP_CHECK(ufeat_ld >= feat_len, "ufeat_ld " << ufeat_ld << " < feat_len " << feat_len);
@@ -380,9 +381,11 @@ int dglhip_gspmm_strided_device(int msg_op, int reduce_op, int64_t num_rows,
   // a lane's vector of VEC features must not straddle padded rows: even strides only
   DGLHIP_CHECK(ufeat_ld == feat_len || ufeat_ld % 2 == 0, "odd padded stride " << ufeat_ld);
   SumLaunch a{num_rows, feat_len, use_e ? efeat_len : 1, indptr, indices, eid, ufeat, efeat, out,
-              row_order, nullptr, nullptr, reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+              row_order, nullptr, nullptr,
+              reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
               stream_output(num_rows, feat_len), ufeat_ld};
-  dispatch_sum(msg_op, reduce_op == DGLHIP_REDUCE_MEAN, a, stream);
+  dispatch_sum(msg_op, reduce_op == DGLHIP_REDUCE_MEAN || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
+               a, stream);
   API_END();
 }
 
@@ -400,7 +403,7 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
   DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
-                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
+                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
                "chunked rows support sum/mean only");
   DGLHIP_CHECK(num_light >= 0 && num_chunks >= 0 && num_heavy >= 0, "negative size");
   if (feat_len == 0) return 0;
@@ -417,8 +420,8 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
                    msg_op == DGLHIP_MSG_U_MUL_E,
                "strided source rows: copy_u or u_mul_e, got msg op " << msg_op);
   const int64_t elen = use_e ? efeat_len : 1;
-  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
-  const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM;
+  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
+  const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
   if (num_chunks > 0) {  // heavy-row chunks first: the longest work starts first
     SumLaunch c{num_chunks, feat_len, elen, indptr, indices, eid, ufeat, efeat, partial,
                 nullptr, chunk_beg, chunk_end, false, false, ufeat_ld};
@@ -433,7 +436,12 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   if (num_heavy > 0) {
     const int64_t blocks = (num_heavy + 3) / 4;
     timed_launch(stream, [&] {
-      if (mean)
+      if (mean && accum)
+        hipLaunchKernelGGL((gspmm_combine_kernel<true, true>),
+                           grid_1d(blocks), dim3(256), 0, stream,
+                           num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,
+                           out);
+      else if (mean)
         hipLaunchKernelGGL((gspmm_combine_kernel<true, false>),
                            grid_1d(blocks), dim3(256), 0, stream,
                            num_heavy, feat_len, indptr, heavy_rows, heavy_chunk_ptr, partial,

@@ -243,7 +243,9 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 // lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
 // or a slot range [chunk_beg[i], chunk_end[i]) whose sum goes to out[i, :]
 // (CHUNKED = true). With ACCUM the chain continues from the value already in
-// out[i, :] (segment-by-segment evaluation of one sequential chain).
+// out[i, :] (segment-by-segment evaluation of one sequential chain); with
+// MEAN and ACCUM on whole rows the row's mean is added to the value in
+// out[i, :] (out + mean: a sum of two terms, the same bits either way round).
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
           bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
@@ -276,7 +278,8 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   }
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
-    V acc = ACCUM ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
+    constexpr bool ADD_MEAN = MEAN && ACCUM && !CHUNKED;
+    V acc = (ACCUM && !ADD_MEAN) ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, ldu, f0, indices, ufeat);
     else if (copies_u(MSG) || eid != nullptr)  // uniform branch
@@ -287,13 +290,15 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
                                                       eid, ufeat, efeat);
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
+    if (ADD_MEAN) acc = ldv<VEC>(out + row * F + f0) + acc;
     store_row<VEC, POL>(out + row * F + f0, acc);
   }
 }
 
 // Combine the chunk partials of each heavy row in chunk order:
 // out[row] = ((p0 + p1) + p2) + ... (deterministic), then MEAN scaling; with
-// ACCUM the row's running value comes first: out[row] = ((out[row] + p0) + p1) ...
+// ACCUM the row's running value comes first: out[row] = ((out[row] + p0) + p1) ...;
+// with MEAN and ACCUM the mean is added to it: out[row] + (p0 + p1 + ...) / deg
 template <bool MEAN, bool ACCUM>
 __global__ __launch_bounds__(256) void gspmm_combine_kernel(
     int64_t num_heavy, int64_t F, const int64_t* __restrict__ indptr,
@@ -306,9 +311,10 @@ __global__ __launch_bounds__(256) void gspmm_combine_kernel(
   const int64_t c0 = heavy_chunk_ptr[wave], c1 = heavy_chunk_ptr[wave + 1];
   const float deg = static_cast<float>(indptr[row + 1] - indptr[row]);
   for (int64_t f = lane; f < F; f += 64) {
-    float acc = ACCUM ? out[row * F + f] + partial[c0 * F + f] : partial[c0 * F + f];
+    float acc = (ACCUM && !MEAN) ? out[row * F + f] + partial[c0 * F + f] : partial[c0 * F + f];
     for (int64_t c = c0 + 1; c < c1; ++c) acc += partial[c * F + f];
     if (MEAN && deg > 1.0f) acc = acc / deg;
+    if (MEAN && ACCUM) acc = out[row * F + f] + acc;
     out[row * F + f] = acc;
   }
 }
@@ -561,8 +567,8 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                          grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
-    else if (!a.chunk_beg && a.accumulate && !MEAN)
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, false, true>),
+    else if (!a.chunk_beg && a.accumulate)
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, false, true>),
                          grid_1d(blocks), dim3(256), 0, stream,
                          a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);

@@ -211,7 +211,7 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int num_threads) {
   API_BEGIN();
   DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
-  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 3, "unknown reduce op " << reduce_op);
+  DGLHIP_CHECK(reduce_op >= 0 && reduce_op <= 4, "unknown reduce op " << reduce_op);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   if (num_rows == 0 || feat_len == 0) return 0;
   if (msg_op == DGLHIP_MSG_COPY_U_BF16) {  // widen the rows once, then the fp32 path
@@ -226,9 +226,11 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
   const int64_t F = feat_len;
   const int64_t dpe = use_e ? F / efeat_len : 1;  // features per edge value
+  const bool add_mean = reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
   parallel_for(num_rows, nt, [&](int64_t b, int64_t e, int) {
+    std::vector<float> mean_row(add_mean ? F : 0);  // MEAN_ACCUM: the mean, then out + mean
     for (int64_t r = b; r < e; ++r) {
-      float* o = out + r * F;
+      float* o = add_mean ? mean_row.data() : out + r * F;
       const int64_t s = indptr[r], t = indptr[r + 1];
       if (reduce_op == DGLHIP_REDUCE_MAX) {
         for (int64_t f = 0; f < F; ++f) {
@@ -263,9 +265,13 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
           for (int64_t f = 0; f < F; ++f) o[f] = std::fma(er[f / dpe], ur[f], o[f]);
         }
       }
-      if (reduce_op == DGLHIP_REDUCE_MEAN && t - s > 1) {
+      if ((reduce_op == DGLHIP_REDUCE_MEAN || add_mean) && t - s > 1) {
         const float inv = static_cast<float>(t - s);
         for (int64_t f = 0; f < F; ++f) o[f] = o[f] / inv;
+      }
+      if (add_mean && t > s) {
+        float* dst = out + r * F;
+        for (int64_t f = 0; f < F; ++f) dst[f] = dst[f] + o[f];
       }
     }
   });

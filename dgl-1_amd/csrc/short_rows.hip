@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void gspmm_short_rows_kernel(
     V acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      acc[r] = (accum && row[r] >= 0) ? ldv<VEC>(out + row[r] * F + f0) : Vec<VEC>::zero();
+      acc[r] = (accum && !mean && row[r] >= 0) ? ldv<VEC>(out + row[r] * F + f0)
+                                               : Vec<VEC>::zero();
     if (MAXD > 0) {
       for (int64_t b = 0; b < dmax; b += MAXD) {  // one batch unless a row is long
         V v[R][MAXD > 0 ? MAXD : 1];
@@ -81,6 +82,7 @@ __global__ __launch_bounds__(256) void gspmm_short_rows_kernel(
       if (row[r] < 0) continue;
       V a = acc[r];
       if (mean && deg[r] > 1) a = a / Vec<VEC>::splat(static_cast<float>(deg[r]));
+      if (mean && accum) a = ldv<VEC>(out + row[r] * F + f0) + a;  // out + mean
       store_row<VEC, POL>(out + row[r] * F + f0, a);
     }
   }
@@ -135,8 +137,8 @@ extern "C" int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(copies_u(msg_op), "short-row g-SpMM: copy_u messages only, got " << msg_op);
   DGLHIP_CHECK(reduce_op == DGLHIP_REDUCE_SUM || reduce_op == DGLHIP_REDUCE_MEAN ||
-                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM,
-               "short-row g-SpMM: sum / mean / sum_accum only");
+                   reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM,
+               "short-row g-SpMM: sum / mean / sum_accum / mean_accum only");
   DGLHIP_CHECK(num_items >= 0 && feat_len >= 0 && max_deg >= 0, "negative size");
   if (num_items == 0 || feat_len == 0) return 0;
   DGLHIP_CHECK(out && rows && (max_deg == 0 || (slot_ptr && slot_cols && ufeat)),
@@ -144,8 +146,8 @@ extern "C" int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t
   DGLHIP_CHECK(ufeat_ld == 0 || ufeat_ld == feat_len || (ufeat_ld > feat_len && ufeat_ld % 2 == 0),
                "ufeat_ld " << ufeat_ld << ": 0, feat_len, or an even width > feat_len");
   const int64_t ldu = ufeat_ld ? ufeat_ld : feat_len;
-  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN;
-  const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM;
+  const bool mean = reduce_op == DGLHIP_REDUCE_MEAN || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
+  const bool accum = reduce_op == DGLHIP_REDUCE_SUM_ACCUM || reduce_op == DGLHIP_REDUCE_MEAN_ACCUM;
   // non-temporal output once the whole launch's output is past twice the
   // Infinity Cache (the main kernel's rule, decided on the full row count)
   const bool nt = stream_output(std::max(total_rows, num_items), feat_len);

@@ -38,6 +38,8 @@ MSG_COPY_U, MSG_U_MUL_E, MSG_COPY_E = 0, 1, 2
 MSG_COPY_U_BF16 = 3  # copy_u over bf16 source rows, widened exactly to fp32 (dgl_hip.h)
 RED_SUM, RED_MAX, RED_MEAN = 0, 1, 2
 RED_SUM_ACCUM = 3  # out += sum, each row's chain continued from out (include/dgl_hip.h)
+RED_MEAN_ACCUM = 4  # out = out + mean (include/dgl_hip.h)
+_ACCUM = (RED_SUM_ACCUM, RED_MEAN_ACCUM)
 ORDER_EID, ORDER_COL = 0, 1
 # edge values laid out in the forward CSR's slot order (edge_order="slot"):
 # kernels read / write slot k at row k, no eid indirection
@@ -487,7 +489,7 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     else:
         eid = csr.slot_eid if emap is None else emap
     split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
-    skip = red == RED_SUM_ACCUM and csr.row_order is not None  # empty rows: nothing to add
+    skip = red in _ACCUM and csr.row_order is not None  # empty rows: nothing to add
     ld = 0
     if ufeat2 is not None and ufeat2.shape[0] > 1 and _row_strided(ufeat2, feat_len):
         ld = ufeat2.stride(0)  # already row-padded by the caller (gspmm)
@@ -500,7 +502,7 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         up[:, :feat_len] = ufeat2
         ufeat2 = up
     tiered = (dev.type == "cuda" and _TIERED and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and
-              red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM))
+              red in (RED_SUM, RED_MEAN) + _ACCUM)
     if split:
         # "auto" sizes the chunks to fill the chip; an explicit policy is the chunk length
         p = csr.split_plan(split, skip_empty=skip, chunk=None if _ROW_SPLIT == "auto" else split)
@@ -575,7 +577,7 @@ def _run_rows(csr, msg, red, nrows, feat_len, ld, eid, ufeat2, efeat2, elen, out
 def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
     dev = out.device
     for maxd, (rows, sp, cols), n in tail:
-        if maxd == 0 and red == RED_SUM_ACCUM:
+        if maxd == 0 and red in _ACCUM:
             continue  # nothing to add
         check_call(LIB.dglhip_gspmm_short_rows_device(
             msg, red, n, feat_len, maxd, csr.num_rows, ptr(rows), ptr(sp), ptr(cols),
@@ -596,7 +598,7 @@ def set_pad_rows(policy):
 
 def _pad_rows(msg, red, ufeat2, feat_len):
     return (_PAD_ROWS == "auto" and msg in (MSG_COPY_U, MSG_U_MUL_E) and
-            red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM) and ufeat2 is not None and
+            red in (RED_SUM, RED_MEAN) + _ACCUM and ufeat2 is not None and
             ufeat2.dtype == torch.float32 and
             ufeat2.numel() * 4 >= _PAD_MIN_BYTES and padded_width(feat_len) != feat_len)
 
@@ -684,6 +686,23 @@ def _f32c(t):
     return t.contiguous()
 
 
+def _mean_scaled(fwd, dout, padded_ok):
+    """dC / deg, the mean reducer's backward ahead of the transposed product;
+    with ``padded_ok`` (only the node gradient reads it) written straight into
+    the padded rows that product gathers when the rows straddle lines (one pass
+    instead of the division's and the padding copy's)."""
+    deg = fwd.mean_divisor()
+    F = dout.shape[1]
+    if padded_ok and dout.is_cuda and _pad_rows(MSG_COPY_U, RED_SUM, dout, F):
+        ld = padded_width(F)
+        buf = dout.new_empty(dout.shape[0], ld)
+        check_call(LIB.dglhip_div_rows_device(
+            dout.shape[0], F, ptr(dout), dout.stride(0), ptr(deg), ptr(buf), ld,
+            _stream_of(dout.device)))
+        return buf[:, :F]
+    return (dout / deg).contiguous()
+
+
 class _GSpMM(torch.autograd.Function):
     """out = REDUCE over in-slots of MSG(ufeat[col], efeat[eid]).
 
@@ -728,20 +747,7 @@ class _GSpMM(torch.autograd.Function):
         need_e = ctx.needs_input_grad[6]
         F = dout.shape[1]
         if red == RED_MEAN:
-            deg = fwd.mean_divisor()
-            if need_u and not need_e and dout.is_cuda and \
-                    _pad_rows(MSG_COPY_U, RED_SUM, dout, F):
-                # the quotient written straight into the padded rows the
-                # transposed product gathers (one pass instead of the
-                # division's and the padding copy's)
-                ld = padded_width(F)
-                buf = dout.new_empty(dout.shape[0], ld)
-                check_call(LIB.dglhip_div_rows_device(
-                    dout.shape[0], F, ptr(dout), dout.stride(0), ptr(deg), ptr(buf), ld,
-                    _stream_of(dout.device)))
-                dout = buf[:, :F]
-            else:
-                dout = (dout / deg).contiguous()
+            dout = _mean_scaled(fwd, dout, padded_ok=need_u and not need_e)
             red_b = RED_SUM
         else:
             red_b = red
@@ -850,6 +856,52 @@ def gspmm(adj, msg, reduce, ufeat=None, efeat=None, num_edges=None, edge_order="
     # a caller's in-place update of the result rebase its autograd graph
     # (CopySlices: a zero fill and a copy of the whole gradient)
     return out if tuple(out.shape) == shape else out.reshape(shape)
+
+
+class _MeanAddInto(torch.autograd.Function):
+    """out <- out + mean over in-slots of ufeat[col] (copy_u + mean whose
+    store adds the row's mean to the value in ``out``, in place). Backward:
+    the incoming gradient for ``out``'s old value, the mean's transposed
+    product for ufeat."""
+
+    @staticmethod
+    def forward(ctx, adj, ufeat2, out, feat_len):
+        _run_gspmm(adj.fwd, MSG_COPY_U, RED_MEAN_ACCUM, ufeat2, None, 0, feat_len, False,
+                   out=out)
+        ctx.mark_dirty(out)
+        ctx.adj = adj
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        adj = ctx.adj
+        dout = dout.contiguous()
+        du = None
+        if ctx.needs_input_grad[1]:
+            d = _mean_scaled(adj.fwd, dout, padded_ok=True)
+            du, _ = _run_gspmm(adj.bwd, MSG_COPY_U, RED_SUM, d, None, 0, dout.shape[1], False)
+        return None, du, dout if ctx.needs_input_grad[2] else None, None
+
+
+def gspmm_mean_add(adj, ufeat, out):
+    """out <- out + mean over in-edges of ufeat[src] (copy_u + mean), in place
+    and differentiable: the value of ``out + gspmm(adj, "copy_u", "mean",
+    ufeat)`` bit for bit (a sum of two terms; rows without in-edges keep their
+    value), with the addition in the aggregation's own store instead of a pass
+    over both tensors (GraphSAGE's fc_self(h) + mean(fc_neigh(h)),
+    nn.pytorch.sage_dense). ``out``: contiguous float32 (num_rows, F) on the
+    features' device; ufeat may be row-padded (F columns of a wider row)."""
+    F = out.shape[1] if out.dim() == 2 else -1
+    dev = ufeat.device
+    if (out.dtype != torch.float32 or out.dim() != 2 or not out.is_contiguous() or
+            out.device != dev or ufeat.dim() != 2 or ufeat.shape[1] != F):
+        raise DGLError("gspmm_mean_add: out must be a contiguous float32 (num_rows, F) "
+                       "tensor beside (num_cols, F) features")
+    adj = adj.to(dev)
+    if out.shape[0] != adj.shape[0] or ufeat.shape[0] < adj.shape[1]:
+        raise DGLError("gspmm_mean_add: shapes do not match the adjacency")
+    u2 = ufeat if (_row_strided(ufeat, F) and dev.type == "cuda") else _f32c(ufeat)
+    return _MeanAddInto.apply(adj, u2, out, F)
 
 
 def gsddmm_dot(adj, lhs, rhs, num_edges, heads=1, edge_order="eid"):

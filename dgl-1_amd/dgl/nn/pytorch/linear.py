@@ -245,18 +245,26 @@ class _PreAggregateFn(torch.autograd.Function):
                                           w_self, bias)
         else:
             pre = _mm_t(x, w_neigh)
+        # an aggregation that can add its result into a tensor in its own
+        # store (``aggregate.add_into(h, out)``, e.g. kernel.gspmm_mean_add)
+        # takes self_out as that tensor: out = self_out + A(pre), no sum pass
+        add_into = getattr(aggregate, "add_into", None) if self_out is not None else None
+        agg = aggregate if add_into is None else (lambda t: add_into(t, self_out))
         if any(ctx.needs_input_grad):
             with torch.enable_grad():
                 pre_leaf = pre.detach().requires_grad_(True)
-                neigh = aggregate(pre_leaf)
+                neigh = agg(pre_leaf)
         else:  # inference: no graph to keep
-            pre_leaf, neigh = None, aggregate(pre)
+            pre_leaf, neigh = None, agg(pre)
         del pre
         # accumulate into the aggregate's own buffer (its backward does not
         # read it): no copy of an (N, out) tensor. Not into a view: autograd
         # would rebase the view's graph on the in-place update (a zero fill
         # and a copy of the gradient); then into self_out (a + b == b + a)
-        if self_out is not None and neigh._base is not None:
+        if add_into is not None:
+            out = neigh.detach()
+            del self_out
+        elif self_out is not None and neigh._base is not None:
             out = self_out.add_(neigh.detach())
             del self_out
         elif self_out is not None:
@@ -367,7 +375,10 @@ def sage_dense(h, aggregate, fc_self, fc_neigh, activation=None):
     pass over an (N, out) tensor per direction and two (N, out) buffers of
     peak memory (RMAT-26: 34 GB each). ``activation`` is applied to the sum;
     a ReLU on the widening / square layer is fused into the product's store
-    (its backward mask into the fused backward)."""
+    (its backward mask into the fused backward). An ``aggregate`` carrying
+    ``add_into(h, out)`` (out <- out + aggregate(h) in place, differentiable in
+    h; kernel.gspmm_mean_add for the mean) lets the narrowing layer add
+    fc_self(h) in the aggregation's own store."""
     def act(t):
         return activation(t) if activation is not None else t
     if h.dim() != 2 or fc_neigh.bias is not None:

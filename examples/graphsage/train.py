@@ -125,6 +125,10 @@ def run(args):
             g.ndata["h"] = h
             g.update_all(fn.copy_src("h", "m"), fn.mean("m", "neigh"))
             return g.ndata.pop("neigh")
+        # out + mean(h) in the aggregation's store (sage_dense's narrowing
+        # layer adds fc_self(h) there; the same bits as the sum of the two)
+        aggregate.add_into = lambda h, out: kernel.gspmm_mean_add(
+            g.sparse_adjacency(h.device), h, out)
     del src, dst
     if args.row_split is not None:
         kernel.set_row_split(args.row_split)

@@ -130,6 +130,10 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
 #define DGLHIP_REDUCE_SUM_ACCUM 3  /* out += sum: each row's chain continues from the
                                     * value already in out (segment-by-segment
                                     * evaluation of one product; new design) */
+#define DGLHIP_REDUCE_MEAN_ACCUM 4  /* out = out + mean: the row's mean added to the
+                                     * value already in out (GraphSAGE's
+                                     * fc_self(h) + mean(...) in the aggregation's
+                                     * own store; new design) */
 
 /* efeat_len: 0 (no edge feature), 1 (one scalar per edge, broadcast over the
  * feature row; the only case the reference specialises, message.py:37-44),
@@ -143,8 +147,8 @@ int dglhip_degree_bucketing_host(int64_t num_msgs, const int64_t* msg_recv,
  * row_order (int32[num_rows], may be NULL): launch schedule; rows are launched
  * in this order and results never depend on it. It may list a subset of the
  * CSR's rows (num_rows then counts the listed rows, indptr still spans the
- * CSR): rows not listed are not written, which SUM_ACCUM uses to skip rows
- * without slots.
+ * CSR): rows not listed are not written, which SUM_ACCUM and MEAN_ACCUM use
+ * to skip rows without slots.
  * Numerics: SUM/MEAN accumulate per output element in CSR slot order with
  * one fused multiply-add per slot (acc = fma(w, x, acc); copy: acc += x),
  * starting from +0.0 — the arithmetic of torch's CPU sparse x dense product
