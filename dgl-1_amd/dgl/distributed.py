@@ -180,20 +180,28 @@ class _PipelinedAggregate(torch.autograd.Function):
     last exchange; the received gradients are added in chunk order."""
 
     @staticmethod
-    def forward(ctx, h_local, pg, mean):
+    def forward(ctx, h_local, pg, mean, add_to=None):
         out = pg._pipelined_sum(h_local.detach())
-        if mean:
+        if add_to is not None:
+            # add_to + sum / deg in one pass (addcdiv: the quotient, then the
+            # sum of two terms -- the bits of add_to + (sum / deg))
+            add_to.addcdiv_(out, pg._mean_divisor(out.dtype))
+            ctx.mark_dirty(add_to)
+            out = add_to
+        elif mean:
             out = out / pg._mean_divisor(out.dtype)
-        ctx.pg, ctx.mean = pg, mean
+        ctx.pg, ctx.mean = pg, mean or add_to is not None
+        ctx.has_add = add_to is not None
         return out
 
     @staticmethod
     def backward(ctx, dout):
         pg = ctx.pg
         dout = dout.contiguous()
+        d_add = dout if (ctx.has_add and ctx.needs_input_grad[3]) else None
         if ctx.mean:
             dout = (dout / pg._mean_divisor(dout.dtype)).contiguous()
-        return pg._pipelined_backward(dout), None, None
+        return pg._pipelined_backward(dout), None, None, d_add
 
 
 class PartitionedGraph(object):
@@ -420,6 +428,16 @@ class PartitionedGraph(object):
             return _PipelinedAggregate.apply(h_local, self, reduce == "mean")
         full = self.gather_halo(h_local)
         return kernel.gspmm(self.adj, msg, reduce, full, efeat)
+
+    def mean_add(self, h_local, out):
+        """out <- out + update_all(h_local, copy_u, mean), in place and
+        differentiable in h_local: the bits of that sum of two tensors, without
+        a pass of its own (the pipelined path adds in the mean's division, the
+        exchanged one in the g-SpMM's store: kernel.gspmm_mean_add). GraphSAGE's
+        fc_self(h) + mean(...) (nn.pytorch.sage_dense's ``add_into``)."""
+        if self.chunks > 0:
+            return _PipelinedAggregate.apply(h_local, self, True, out)
+        return kernel.gspmm_mean_add(self.adj, self.gather_halo(h_local), out)
 
     def _pipelined_sum(self, h_local):
         if self.halo_mode == "alltoall":

@@ -116,6 +116,7 @@ def run(args):
 
         def aggregate(h):
             return pg.update_all(h, "copy_u", "mean")
+        aggregate.add_into = pg.mean_add  # out + mean(h) without a sum pass
         num_edges = int(src.numel())
     else:
         g = DGLGraph((src.cpu(), dst.cpu()))

@@ -68,6 +68,15 @@ def _worker(rank, world, port, n, F, halo="auto", graph="chung_lu"):
         gref = O.spmm_coo(n, src.numpy(), dst.numpy(), G.numpy())
         np.testing.assert_allclose(h_local.grad.numpy(), gref[lo:hi], rtol=1e-5, atol=1e-5)
         assert pg.num_local == hi - lo and pg.num_edges == int(sel.sum())
+        # mean_add (out + mean in the g-SpMM's store) == the sum of the two tensors
+        base = torch.randn(hi - lo, F, generator=gen)
+        h1 = H[lo:hi].clone().requires_grad_(True)
+        o1 = pg.mean_add(h1, base.clone())
+        o1.backward(G[lo:hi])
+        h2 = H[lo:hi].clone().requires_grad_(True)
+        o2 = base + pg.update_all(h2, "copy_u", "mean")
+        o2.backward(G[lo:hi])
+        assert torch.equal(o1.detach(), o2.detach()) and torch.equal(h1.grad, h2.grad)
     finally:
         dist.destroy_process_group()
 
@@ -198,6 +207,18 @@ def _pipe_worker(rank, world, port, graph="chung_lu"):
                 h2 = H[lo:hi].clone().requires_grad_(True)
                 pg.update_all(h2, "copy_u", reduce).backward(G[lo:hi])
                 assert torch.equal(h.grad, h2.grad)
+            # mean_add: base + mean in the division's pass, the same bits and
+            # gradients as the sum of the two tensors
+            base = torch.randn(hi - lo, F, generator=torch.Generator().manual_seed(4))
+            h3 = H[lo:hi].clone().requires_grad_(True)
+            b3 = base.clone().requires_grad_(True)
+            o3 = pg.mean_add(h3, b3.clone())
+            o3.backward(G[lo:hi])
+            h4 = H[lo:hi].clone().requires_grad_(True)
+            o4 = base + pg.update_all(h4, "copy_u", "mean")
+            o4.backward(G[lo:hi])
+            assert torch.equal(o3.detach(), o4.detach())
+            assert torch.equal(h3.grad, h4.grad) and torch.equal(b3.grad, G[lo:hi])
     finally:
         dist.destroy_process_group()
 
