@@ -173,7 +173,9 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
                                                          const float* __restrict__ w,
                                                          const float* __restrict__ grad_loss,
                                                          float* __restrict__ dz, int64_t ldd,
-                                                         float* __restrict__ colpart) {
+                                                         float* __restrict__ colpart,
+                                                         const float* __restrict__ divisor,
+                                                         float* __restrict__ dzs, int64_t ldds) {
   extern __shared__ float tile[];
   const float g = grad_loss[0];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -210,6 +212,24 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
     }
     __syncthreads();
     store_tile(dz, ldd, r0, nrows, C, SC, tile);
+    if (dzs != nullptr) {
+      // dz / divisor[row] at row stride ldds (a multiple of 4, pad columns
+      // zeroed): the mean aggregation's backward operand, written from the
+      // same tile as whole 16-byte groups (IEEE division: torch.div's bits)
+      float* base = dzs + r0 * ldds;
+      const int m = nrows * static_cast<int>(ldds);
+      // e / ldds as a multiply-high (exact for e < 2^16 <= 2^32 / ldds)
+      const uint32_t mo = static_cast<uint32_t>(((uint64_t(1) << 32) + ldds - 1) / ldds);
+      for (int e = 4 * threadIdx.x; e < m; e += 4 * kRows) {
+        const int rr = static_cast<int>(__umulhi(static_cast<uint32_t>(e), mo));
+        const int c = e - rr * static_cast<int>(ldds);
+        const float q = divisor[r0 + rr];
+        f32x4 v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = c + k < C ? tile[rr * SC + c + k] / q : 0.0f;
+        *reinterpret_cast<f32x4*>(base + e) = v;
+      }
+    }
     if (colpart != nullptr && lane < C) {
       // the gradient rows' column sums, read back from the tile: wave w sums
       // rows [64 w, 64 w + 64) of column `lane` in row order (lanes read
@@ -336,24 +356,31 @@ int dglhip_xent_fwd_device(int64_t num_rows, int64_t num_classes, const float* l
 int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* logits,
                            int64_t ld, const int64_t* labels, const float* weight,
                            const float* grad_loss, float* dlogits, int64_t ldd, void* stream_) {
-  return dglhip_xent_bwd_colsum_device(num_rows, num_classes, logits, ld, labels, weight,
-                                       grad_loss, dlogits, ldd, nullptr, nullptr, stream_);
+  return dglhip_xent_bwd_ex_device(num_rows, num_classes, logits, ld, labels, weight, grad_loss,
+                                   dlogits, ldd, nullptr, nullptr, nullptr, nullptr, 0, stream_);
 }
 
 int dglhip_xent_colsum_workspace_floats(int64_t num_classes) {
   return static_cast<int>(kMaxBlocks * std::max<int64_t>(1, num_classes));
 }
 
-int dglhip_xent_bwd_colsum_device(int64_t num_rows, int64_t num_classes, const float* logits,
-                                  int64_t ld, const int64_t* labels, const float* weight,
-                                  const float* grad_loss, float* dlogits, int64_t ldd,
-                                  float* colsum, float* workspace, void* stream_) {
+int dglhip_xent_bwd_ex_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                              int64_t ld, const int64_t* labels, const float* weight,
+                              const float* grad_loss, float* dlogits, int64_t ldd, float* colsum,
+                              float* workspace, const float* divisor, float* dlogits_scaled,
+                              int64_t ld_scaled, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0, "negative row count");
   DGLHIP_CHECK(num_classes >= 1 && num_classes <= kMaxClasses,
                "cross-entropy rows: 1.." << kMaxClasses << " classes, got " << num_classes);
   DGLHIP_CHECK(colsum == nullptr || workspace != nullptr, "column sums need the workspace");
+  DGLHIP_CHECK(dlogits_scaled == nullptr ||
+                   (divisor != nullptr && ld_scaled >= num_classes && ld_scaled % 4 == 0 &&
+                    ld_scaled <= 4 * kMaxClasses &&
+                    (reinterpret_cast<uintptr_t>(dlogits_scaled) & 15) == 0),
+               "scaled rows: a divisor, a 16-byte aligned output and a row stride >= the "
+               "class count that is a multiple of 4");
   if (num_rows == 0) {
     if (colsum != nullptr)
       DGLHIP_CHECK(hipMemsetAsync(colsum, 0, num_classes * 4, stream) == hipSuccess,
@@ -368,7 +395,8 @@ int dglhip_xent_bwd_colsum_device(int64_t num_rows, int64_t num_classes, const f
   float* colpart = colsum != nullptr ? workspace : nullptr;
   auto bwd = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(kRows), kRows * SC * 4, stream, num_rows, C, SC,
-                       logits, ld, labels, weight, grad_loss, dlogits, ldd, colpart);
+                       logits, ld, labels, weight, grad_loss, dlogits, ldd, colpart, divisor,
+                       dlogits_scaled, ld_scaled);
   };
   switch (ns) {
     case 4: bwd(xent_bwd_kernel<4>); break;

@@ -106,8 +106,8 @@ def _load():
         "dglhip_xent_bwd_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp,
                                             _c_i64, _vp]),
         "dglhip_xent_colsum_workspace_floats": (_c_int, [_c_i64]),
-        "dglhip_xent_bwd_colsum_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp,
-                                                   _vp, _c_i64, _vp, _vp, _vp]),
+        "dglhip_xent_bwd_ex_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp,
+                                               _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),
         "DGLFuncGetGlobal": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
         "DGLFuncListGlobalNames": (_c_int, [ctypes.POINTER(_c_int),

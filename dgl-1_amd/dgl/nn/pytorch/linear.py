@@ -282,6 +282,12 @@ class _PreAggregateFn(torch.autograd.Function):
         ctx.out_ptr = out.data_ptr()
         ctx.wants_dy_colsum = ctx.has_bias and ctx.needs_input_grad[2]
         ctx.dy_colsum = None
+        # the in-store mean-add's backward operand dy / deg can come from dy's
+        # producer (the loss kernel) as it stores dy
+        inner = neigh.grad_fn if (add_into is not None and pre_leaf is not None) else None
+        ctx.inner = inner if getattr(inner, "scale_spec", None) is not None else None
+        ctx.dy_scaled_spec = ctx.inner.scale_spec if ctx.inner is not None else None
+        ctx.dy_scaled = None
         ctx.relu_node = _relu_producer(x)
         return out
 
@@ -305,6 +311,10 @@ class _PreAggregateFn(torch.autograd.Function):
                 dws = _splitk_tn(dy, x.contiguous())
             for t in (dy, x):
                 t.record_stream(side)
+        scaled, ctx.dy_scaled = ctx.dy_scaled, None
+        inner, ctx.inner = ctx.inner, None
+        if inner is not None and scaled is not None and scaled[:2] == (dy.data_ptr(), dy._version):
+            inner.prescaled = scaled
         (dpre,) = torch.autograd.grad(neigh, pre_leaf, dy)
         dpre = dpre.contiguous()
         dx = None

@@ -15,7 +15,9 @@ backward (one read, one write), the upstream gradient read on the device.
 When the logits are the output of a NodeLinear / sage_dense with a bias, the
 backward also returns that bias's gradient (dz's column sums) from the same
 kernel, read back from the tile it stores (no separate column reduce over
-the rows). Other devices and shapes compute the expression above with PyTorch's own
+the rows); when they are a sage_dense output whose mean aggregation added into
+them (kernel.gspmm_mean_add), also dz / deg in the padded rows that
+aggregation's backward gathers (no division pass). Other devices and shapes compute the expression above with PyTorch's own
 operators. Results agree with it to fp32 rounding (the sums associate
 differently); labels outside [0, C) contribute nothing (PyTorch's
 ignore_index = -100; other out-of-range labels are an error there).
@@ -38,10 +40,13 @@ def _fused_ok(z, y, w):
 
 def _bias_producer(z):
     """The NodeLinear / sage_dense autograd node whose output ``z`` is (the
-    tensor itself) and that will want dz's column sums for its bias, else
-    None: the loss backward then sums them from its tile as it stores dz."""
+    tensor itself) and that will want dz's column sums for its bias, or dz
+    divided by its mean aggregation's degrees (``dy_scaled_spec``: divisor,
+    padded row stride), else None: the loss backward then takes them from its
+    tile as it stores dz."""
     node = z.grad_fn
-    if (node is not None and getattr(node, "wants_dy_colsum", False) and
+    if (node is not None and (getattr(node, "wants_dy_colsum", False) or
+                              getattr(node, "dy_scaled_spec", None) is not None) and
             getattr(node, "out_ptr", None) == z.data_ptr() and z._base is None and
             z.is_contiguous()):
         return node
@@ -73,17 +78,26 @@ class _WeightedXentFn(torch.autograd.Function):
         g = g.detach().to(torch.float32).contiguous()
         dz = torch.empty(n, C, dtype=torch.float32, device=z.device)
         node, ctx.bias_node = ctx.bias_node, None
-        cs = ws = None
-        if node is not None:
+        cs = ws = div = scaled = None
+        lds = 0
+        if node is not None and getattr(node, "wants_dy_colsum", False):
             cs = torch.empty(C, dtype=torch.float32, device=z.device)
             ws = torch.empty(_ffi.LIB.dglhip_xent_colsum_workspace_floats(C),
                              dtype=torch.float32, device=z.device)
-        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_colsum_device(
+        spec = getattr(node, "dy_scaled_spec", None) if node is not None else None
+        if spec is not None and spec[0].shape[0] == n:
+            div, lds = spec
+            scaled = torch.empty(n, lds, dtype=torch.float32, device=z.device)
+        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_ex_device(
             n, C, _ffi.ptr(z), z.stride(0), _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(g), _ffi.ptr(dz),
-            C, _ffi.ptr(cs), _ffi.ptr(ws), kernel._stream_of(z.device)))
-        if node is not None:
+            C, _ffi.ptr(cs), _ffi.ptr(ws), _ffi.ptr(div), _ffi.ptr(scaled), lds,
+            kernel._stream_of(z.device)))
+        if cs is not None:
             # the producing Linear's bias gradient, summed as dz was stored
             node.dy_colsum = (dz.data_ptr(), dz._version, cs)
+        if scaled is not None:
+            # dz / deg in the padded rows of the producer's mean aggregation
+            node.dy_scaled = (dz.data_ptr(), dz._version, scaled[:, :C])
         return dz, None, None
 
 

@@ -312,19 +312,28 @@ int dglhip_xent_bwd_device(int64_t num_rows, int64_t num_classes, const float* l
                            int64_t ld, const int64_t* labels, const float* weight,
                            const float* grad_loss, float* dlogits, int64_t ldd, void* stream);
 
-/* Floats of the column-sum workspace of dglhip_xent_bwd_colsum_device. */
+/* Floats of the column-sum workspace of dglhip_xent_bwd_ex_device. */
 int dglhip_xent_colsum_workspace_floats(int64_t num_classes);
 
-/* dglhip_xent_bwd_device, and colsum[j] = sum_i dlogits_ij (the output layer's
- * bias gradient) taken from the gradient rows as they are stored: per wave in
- * row order, per workgroup over its waves in order, then over the workgroups
- * in 16 contiguous runs summed in order, the runs in order (deterministic). colsum NULL = no sums (workspace unused);
- * both are device pointers. Replaces the separate column reduce of the bias
- * gradient (nn.Linear's autograd: torch's sum over dim 0). */
-int dglhip_xent_bwd_colsum_device(int64_t num_rows, int64_t num_classes, const float* logits,
-                                  int64_t ld, const int64_t* labels, const float* weight,
-                                  const float* grad_loss, float* dlogits, int64_t ldd,
-                                  float* colsum, float* workspace, void* stream);
+/* dglhip_xent_bwd_device, plus two optional outputs taken from the gradient
+ * rows as they are stored (no pass of their own):
+ * - colsum[j] = sum_i dlogits_ij (the output layer's bias gradient): per wave
+ *   in row order, per workgroup over its waves in order, then over the
+ *   workgroups in 16 contiguous runs summed in order, the runs in order
+ *   (deterministic). colsum NULL = no sums (workspace unused).
+ * - dlogits_scaled[i, j] = dlogits_ij / divisor[i] (IEEE division) at row
+ *   stride ld_scaled (a multiple of 4, >= num_classes, 16-byte aligned; pad
+ *   columns zeroed): the mean aggregation's backward operand dC / deg in the
+ *   padded rows its transposed g-SpMM gathers (dglhip_div_rows_device's
+ *   output). dlogits_scaled NULL = none.
+ * All pointers are device pointers. Replaces the separate column reduce of
+ * the bias gradient (nn.Linear's autograd: torch's sum over dim 0) and the
+ * mean backward's division pass. */
+int dglhip_xent_bwd_ex_device(int64_t num_rows, int64_t num_classes, const float* logits,
+                              int64_t ld, const int64_t* labels, const float* weight,
+                              const float* grad_loss, float* dlogits, int64_t ldd, float* colsum,
+                              float* workspace, const float* divisor, float* dlogits_scaled,
+                              int64_t ld_scaled, void* stream);
 
 /* Same contract on host memory (the CPU device of the engine; std::thread). */
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,

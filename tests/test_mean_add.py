@@ -88,10 +88,11 @@ def test_mean_add_device_schedules(F, split, tiered):
 
 
 @pytest.mark.gpu
-def test_sage_dense_add_into_equals_sum():
+def test_sage_dense_add_into_equals_sum(monkeypatch):
     """The narrowing SAGE layer with the aggregation's add_into: the same
     output, parameter gradients and input gradient as with the separate sum
-    (and the same loss-kernel bias gradient)."""
+    (and the same loss-kernel bias gradient); with add_into, the mean
+    backward's dC / deg comes from the loss kernel (no division pass)."""
     from dgl.nn.pytorch import weighted_cross_entropy
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(11)
@@ -112,8 +113,13 @@ def test_sage_dense_add_into_equals_sum():
         return aggregate(t)
     fused.add_into = lambda t, out: kernel.gspmm_mean_add(adj, t, out)
 
+    calls = []
+    real = kernel._mean_scaled
+    monkeypatch.setattr(kernel, "_mean_scaled",
+                        lambda *a, **k: calls.append(1) or real(*a, **k))
     res = []
     for agg in (aggregate, fused):
+        calls.clear()
         xx = x.detach().clone().requires_grad_(True)
         z = sage_dense(xx, agg, fc_self, fc_neigh)
         fc_self.zero_grad()
@@ -121,5 +127,6 @@ def test_sage_dense_add_into_equals_sum():
         (weighted_cross_entropy(z, y, w) * 1e-3).backward()
         res.append((z.detach(), xx.grad, fc_self.weight.grad.clone(), fc_self.bias.grad.clone(),
                     fc_neigh.weight.grad.clone()))
+        assert len(calls) == (1 if agg is aggregate else 0)
     for a, b in zip(*res):
         assert torch.equal(a, b)

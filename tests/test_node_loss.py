@@ -94,7 +94,7 @@ def test_fused_path_runs_native():
 @pytest.mark.parametrize("n,C", [(0, 41), (1, 41), (255, 41), (257, 7), (5000, 1), (70001, 41),
                                  (3001, 64), (1 << 20, 41)])
 def test_bwd_column_sums(n, C):
-    """dglhip_xent_bwd_colsum_device: the same dz as the plain backward (bit
+    """dglhip_xent_bwd_ex_device: the same dz as the plain backward (bit
     for bit) and colsum = dz.sum(0) to fp32 summation tolerance, reruns
     bit-identical."""
     from dgl import _ffi, kernel
@@ -102,16 +102,23 @@ def test_bwd_column_sums(n, C):
     z, y, w = _case(n, C, dev, seed=7 + n, ignore=min(n, 11))
     g = torch.tensor(0.75, device=dev)
     ws = torch.empty(_ffi.LIB.dglhip_xent_colsum_workspace_floats(C), device=dev)
+    div = torch.randint(1, 50, (n, 1), generator=torch.Generator().manual_seed(n)).float().to(dev)
+    lds = (C + 7) // 8 * 8
     outs = []
-    for with_cs in (False, True, True):
+    for with_cs, with_sc in ((False, False), (True, False), (True, True)):
         dz = torch.full((n, C), float("nan"), device=dev)
         cs = torch.full((C,), float("nan"), device=dev) if with_cs else None
-        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_colsum_device(
+        sc = torch.full((n, lds), float("nan"), device=dev) if with_sc else None
+        _ffi.check_call(_ffi.LIB.dglhip_xent_bwd_ex_device(
             n, C, _ffi.ptr(z), C, _ffi.ptr(y), _ffi.ptr(w), _ffi.ptr(g), _ffi.ptr(dz), C,
-            _ffi.ptr(cs), _ffi.ptr(ws), kernel._stream_of(dev)))
+            _ffi.ptr(cs), _ffi.ptr(ws), _ffi.ptr(div if with_sc else None), _ffi.ptr(sc),
+            lds if with_sc else 0, kernel._stream_of(dev)))
         outs.append((dz, cs))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[1][0], outs[2][0])
     assert torch.equal(outs[1][1], outs[2][1])
+    # dz / divisor at the padded stride (torch.div's bits), pad columns zero
+    assert torch.equal(sc[:, :C], outs[0][0] / div)
+    assert bool((sc[:, C:] == 0).all())
     ref = outs[0][0].double().sum(0)
     tol = 1e-6 * (outs[0][0].double().abs().sum(0) + 1.0)
     assert bool(((outs[1][1].double() - ref).abs() <= tol).all())
