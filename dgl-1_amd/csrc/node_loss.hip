@@ -199,12 +199,21 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
     if (r < nrows) {
       float* row = tile + r * SC;
       if (y >= 0 && y < C) {
-        float m, lse;
-        row_lse(row, C, m, lse);
-        const float gw = w != nullptr ? g * wr : g;
+        // one exp per element: e_c = exp(z_c - max) kept in the row, then
+        // gw * softmax = e_c * (gw / sum e)
+        float m = row[0];
+        for (int c = 1; c < C; ++c) m = fmaxf(m, row[c]);
+        float s = 0.0f;
         for (int c = 0; c < C; ++c) {
-          const float p = expf((row[c] - m) - lse);
-          row[c] = c == y ? gw * p - gw : gw * p;
+          const float e = expf(row[c] - m);
+          row[c] = e;
+          s += e;
+        }
+        const float gw = w != nullptr ? g * wr : g;
+        const float k = gw / s;
+        for (int c = 0; c < C; ++c) {
+          const float gp = row[c] * k;
+          row[c] = c == y ? gp - gw : gp;
         }
       } else {
         for (int c = 0; c < C; ++c) row[c] = 0.0f;
