@@ -15,14 +15,22 @@ at 1/2/4/8 GPUs". Workload (config.workload):
   rows 1-D partitioned over the ranks (dgl.distributed.PartitionedGraph); one
   step = RCCL all-gather of the node-feature halo + the local g-SpMM.
 
+Ranks: ``python bench.py --gpus N`` with N > 1 and no WORLD_SIZE in the
+environment starts ``python -m torch.distributed.run --nproc-per-node N
+bench.py ...`` as a CHILD process (before this process loads the HIP library
+or touches the GPU), relays its output and exits with its return code. Under
+an outer torchrun (WORLD_SIZE set) the script runs as one rank and refuses a
+WORLD_SIZE that disagrees with --gpus.
+
 Timing: W warm-up steps, then K steps bracketed by barrier + synchronize;
 the max over ranks is reported; value = all edges processed / that time.
 roofline: algorithmic bytes of one g-SpMM launch (SURVEY.md §8d:
 E*(4F+4) + R*(4F+8)) / the kernel's mean duration, measured with hipEvents
-recorded around every launch on its own stream inside the timed region.
+recorded around every launch on its own stream inside the timed region
+(rank 0's; ``per_rank`` lists every rank's).
 cpu_baseline: the reference's own CPU arithmetic (torch.sparse.mm on the
 uncoalesced COO, python/dgl/backend/pytorch/tensor.py:145-146) on a bounded
-sample of the same graph, rank 0 at N = 1 only.
+sample of the same graph, timed on rank 0 after the timed region, at every N.
 
 rmat26 (secondary block of the same JSON line, keyed rmat<scale>;
 --no-rmat-leg skips it): the
@@ -30,8 +38,8 @@ north star also asks for absolute edges/s on RMAT-26 at 1/2/4/8 GPUs next to
 the CPU baseline. After the headline timing (and with its memory released)
 the same ranks time one fixed Graph500 R-MAT graph (scale --rmat-scale, edge
 factor 16, 1.07B edges at 26): strong scaling, dst rows partitioned as above,
-heavy rows chunked. Its CPU baseline is the reference product on a compacted
-sample of that graph.
+heavy rows chunked. Its CPU baseline is the reference product on a sample of
+that graph (rank 0, after the timed region).
 
 Run: python bench.py [--gpus N --steps K --warmup W]
 """
@@ -40,6 +48,8 @@ from __future__ import absolute_import
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,9 +60,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "dgl-1_amd"))
 sys.path.insert(0, ROOT)
 
-import dgl  # noqa: E402
-import dgl.function as fn  # noqa: E402
-from dgl import data, kernel  # noqa: E402
+# bound by _load_dgl() once the launcher decision is made (loading
+# libdgl_hip.so is the first thing that may touch the GPU)
+dgl = fn = data = kernel = None
 
 FEAT = 128
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
@@ -62,26 +72,148 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def _load_dgl():
+    global dgl, fn, data, kernel
+    import dgl as _dgl
+    import dgl.function as _fn
+    from dgl import data as _data, kernel as _kernel
+    dgl, fn, data, kernel = _dgl, _fn, _data, _kernel
+
+
+def build_parser():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
+    ap.add_argument("--no-traffic", action="store_true",
+                    help="skip the rocprofv3 PMC passes that fill roofline.traffic")
+    ap.add_argument("--graph-scale", type=float, default=1.0,
+                    help="per-GPU graph size as a fraction of Reddit (testing only)")
+    ap.add_argument("--workload", default="reddit", choices=["reddit", "rmat"],
+                    help="reddit: weak-scaled Reddit-shaped graph (default, the driver's line); "
+                         "rmat: one fixed Graph500 R-MAT graph partitioned over the ranks "
+                         "(strong scaling, heavy rows chunked)")
+    ap.add_argument("--rmat-scale", type=int, default=26)
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="single-GPU study: build the x N graph, keep rank 0's partition and "
+                         "time its local g-SpMM against the full (all-gathered) feature matrix "
+                         "(no communication; not a driver line)")
+    ap.add_argument("--pipeline-chunks", type=int, default=4,
+                    help="N>1: halo all-gather chunks overlapped with the local g-SpMM "
+                         "(0 = one all-gather, then the kernel; bit-exact rows)")
+    ap.add_argument("--halo-dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="N>1: wire type of the exchanged remote rows (bf16 halves the "
+                         "exchange; rows then carry bf16 rounding of remote inputs)")
+    ap.add_argument("--no-bf16-leg", action="store_true",
+                    help="N>1: skip the secondary timing of the same step with the bf16 halo")
+    ap.add_argument("--no-train-leg", action="store_true",
+                    help="skip the secondary timing of a training step (forward + backward)")
+    ap.add_argument("--no-rmat-leg", action="store_true",
+                    help="skip the secondary RMAT strong-scaling block (rmat26)")
+    ap.add_argument("--dist-rehearsal", action="store_true",
+                    help="run the multi-rank code path (RCCL group, partition, collectives) "
+                         "on a world of one rank (single-GPU rehearsal; not a driver line)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
+                         "to rehearse the multi-rank path")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: run every leg through the library's host kernels with gloo "
+                         "(tests of the launcher and the multi-rank plumbing; not a driver line)")
+    return ap
+
+
+# ---------------------------------------------------------------------------
+# launcher: --gpus N > 1 without an outer torchrun
+# ---------------------------------------------------------------------------
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    try:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+    finally:
+        s.close()
+
+
+def launch_command(args, argv, env, port=None):
+    """The child command that runs this script as ``args.gpus`` ranks, or None
+    when this process is to run as a rank itself (one GPU, or WORLD_SIZE
+    already set by an outer launcher). Decided from argv and the environment
+    only: nothing here loads the HIP library or touches a device."""
+    if args.gpus <= 1 or "WORLD_SIZE" in env:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            "--nproc-per-node", str(args.gpus), "--master-addr", "127.0.0.1",
+            "--master-port", str(port if port is not None else _free_port()),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def relay(cmd, env=None):
+    """Run ``cmd`` as a child in its own process group, pass its stdout through
+    line by line (rank 0's JSON line among it), return its exit code. The
+    group is killed if this process is interrupted."""
+    env = dict(os.environ if env is None else env)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True,
+                            bufsize=1, universal_newlines=True)
+    try:
+        for line in proc.stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        return proc.wait()
+    except BaseException:
+        try:
+            os.killpg(proc.pid, 9)
+        except OSError:
+            pass
+        proc.wait()
+        raise
+
+
+def world_mismatch(args, env):
+    """Error text when an outer launcher's WORLD_SIZE disagrees with --gpus."""
+    world = int(env.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not (world == 1 and args.dist_rehearsal):
+        return "--gpus %d but WORLD_SIZE %d" % (args.gpus, world)
+    return None
+
+
+# ---------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def algorithmic_bytes(num_edges, num_rows, feat):
     """Gather model: each edge reads one int32 column id and one fp32 source
     row; each row reads its int64 indptr entry and writes one fp32 row."""
     return num_edges * (4 * feat + 4) + num_rows * (4 * feat + 8)
 
 
-def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
-    """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on the
-    in-edges of the first rows of the graph (bounded sample), timed at one
-    thread and at torch's default thread count (the setting the reference
-    runs with); ``value`` is the faster of the two. ``h_cpu`` None: the
-    sample's source columns are compacted and get random features (graphs
-    whose full feature matrix does not fit host memory)."""
-    threads = torch.get_num_threads()
+def cpu_sample(src, dst, n, target_edges):
+    """The CPU baseline's bounded sample: the in-edges (edge-id order) of the
+    first rows of the graph, ``target_edges`` of them, as host tensors
+    (rows, d, s). Taken before the edge lists are released; timed after the
+    timed region."""
     deg = torch.bincount(dst, minlength=n)
     cum = torch.cumsum(deg, 0)
     rows = int(torch.searchsorted(cum, torch.tensor(target_edges, device=cum.device))) + 1
     rows = min(rows, n)
     sel = dst < rows
-    s, d = src[sel].cpu(), dst[sel].cpu()
+    return rows, dst[sel].cpu(), src[sel].cpu()
+
+
+def cpu_baseline(sample, n, h_cpu, seconds_budget=20.0):
+    """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on
+    the sample, timed at one thread and at torch's default thread count (the
+    setting the reference runs with); ``value`` is the faster of the two.
+    ``h_cpu`` None: the sample's source columns are compacted and get random
+    features (graphs whose full feature matrix does not fit host memory)."""
+    rows, d, s = sample
+    threads = torch.get_num_threads()
     e = int(s.numel())
     ncols = n
     if h_cpu is None:
@@ -109,8 +241,9 @@ def cpu_baseline(src, dst, n, h_cpu, target_edges, seconds_budget=20.0):
             "build_kernel": build,
             "sample": "torch.sparse.mm on the reference's uncoalesced COO (fp32 ones, "
                       "edge-id order) over the in-edges of the first %d rows: %d edges x "
-                      "F=%d%s, %s call(s), torch %s, timed at %s thread(s) (torch default %d; "
-                      "value = the faster, at %d); host has %d cpus"
+                      "F=%d%s, %s call(s), torch %s, timed at %s thread(s) (torch default %d, "
+                      "the job's host-core share; value = the faster, at %d: the product "
+                      "is single-threaded in practice); host has %d cpus"
                       % (rows, e, h_cpu.shape[1],
                          "" if ncols == n else " (%d source columns compacted)" % ncols,
                          "/".join(str(v[1]) for _, v in sorted(runs.items())),
@@ -148,7 +281,6 @@ def pmc_traffic(child_args, per_call_calls=None):
     calls. Runs before this process touches the GPU; None if the profiler is
     unavailable."""
     import shutil
-    import subprocess
     import tempfile
     from tools.pmc_traffic import traffic, traffic_per_call
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
@@ -200,28 +332,65 @@ def describe_partition(pg, world, args):
 
 def timed_steps(step, steps, warmup, world, dev):
     """W warm-up steps, then K steps bracketed by barrier + synchronize; returns
-    (max-over-ranks seconds, this rank's g-SpMM kernel ms per step)."""
+    (max-over-ranks seconds, this rank's g-SpMM kernel ms per step). On the
+    host path (no device launches to time) the kernel ms is the rank's own
+    wall time per step."""
     for _ in range(warmup):
         step()
-    torch.cuda.synchronize()
+    _sync(dev)
     if dist.is_initialized():
         dist.barrier()
     kernel.timing_enable(True)
-    torch.cuda.synchronize()
+    _sync(dev)
     t_start = time.perf_counter()
     for _ in range(steps):
         step()
-    torch.cuda.synchronize()
+    _sync(dev)
+    own = time.perf_counter() - t_start
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kms, _ = kernel.timing_read()
+    kms, launches = kernel.timing_read()
     kernel.timing_enable(False)
+    if launches == 0:
+        kms = own * 1e3
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed, kms / steps
+
+
+def per_rank(values, world, dev):
+    """Every rank's tuple of floats, gathered to all ranks (a SUM all-reduce
+    over a rank-slotted tensor: works on every backend)."""
+    k = len(values)
+    t = torch.zeros(world * k, dtype=torch.float64, device=dev)
+    r = dist.get_rank() if dist.is_initialized() else 0
+    t[r * k:(r + 1) * k] = torch.tensor(values, dtype=torch.float64)
+    if dist.is_initialized():
+        dist.all_reduce(t)
+    t = t.cpu().tolist()
+    return [t[i * k:(i + 1) * k] for i in range(world)]
+
+
+def roofline_block(num_edges, num_rows, kms, world, dev, **extra):
+    """The g-SpMM roofline of this rank (algorithmic bytes of its launch(es)
+    per step over its kernel ms per step), with every rank's figures in
+    ``per_rank`` when N > 1."""
+    b = algorithmic_bytes(num_edges, num_rows, FEAT)
+    ach = b / (kms * 1e-3) / 1e9 if kms > 0 else None
+    roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": None if ach is None else ach / HBM_PEAK_GBS,
+            "kernel_ms": kms, "bytes_per_launch": b}
+    roof.update(extra)
+    if world > 1:
+        rows = per_rank([float(b), float(kms)], world, dev)
+        roof["per_rank"] = [{"rank": i, "bytes_per_step": r[0], "kernel_ms": r[1],
+                             "achieved": r[0] / (r[1] * 1e-3) / 1e9 if r[1] > 0 else None,
+                             "frac": r[0] / (r[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                             if r[1] > 0 else None} for i, r in enumerate(rows)]
+    return roof
 
 
 def exchange_block(pg, h_local, steps, world, dev):
@@ -259,13 +428,14 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         E = int(src.numel())
         gen = torch.Generator(device=dev)
         gen.manual_seed(1)
-        cpu = None
+        sample = None
+        if rank == 0 and not args.no_cpu_baseline:
+            sample = cpu_sample(src, dst, n, 2_000_000)
         if not dist.is_initialized():
-            if rank == 0 and not args.no_cpu_baseline:
-                cpu = cpu_baseline(src, dst, n, None, 2_000_000, seconds_budget=10.0)
             adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
             del src, dst
             h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+            local_edges, local_rows = E, n
 
             def step():
                 kernel.gspmm(adj, "copy_u", "sum", h)
@@ -279,30 +449,38 @@ def rmat_leg(args, world, rank, dev, pmc=None):
                                   halo_dtype=HALO_DTYPE[args.halo_dtype])
             del src, dst, sel
             h_local = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
+            local_edges, local_rows = pg.num_edges, pg.num_local
 
             def step():
                 pg.update_all(h_local)
             par = describe_partition(pg, world, args)
-        torch.cuda.synchronize()
+        _sync(dev)
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
         elapsed, kms = timed_steps(step, steps, 2, world, dev)
         exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
-        roof = None
-        if not dist.is_initialized():
-            # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
-            b = algorithmic_bytes(E, n, FEAT)
-            ach = b / (kms * 1e-3) / 1e9
-            roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": ach / HBM_PEAK_GBS, "traffic": None if pmc is None else pmc["bytes"],
-                    "kernel": "g-SpMM copy_u+sum, heavy rows chunked (light-row, chunk and "
-                              "combine kernels of one call)",
-                    "kernel_ms": kms, "bytes_per_launch": b,
-                    "traffic_source": None if pmc is None else
-                    "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes (bench.py --workload "
-                    "rmat), every g-SpMM kernel of a call summed, mean per call, read x2 (gfx950)",
-                    "regime": "HBM-bound random row gather (H = %.0f GB >> 256 MB Infinity Cache)"
-                              % (n * FEAT * 4 / 1e9)}
+        # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
+        roof = roofline_block(
+            local_edges, local_rows, kms, world, dev,
+            traffic=None if pmc is None else pmc["bytes"],
+            kernel="g-SpMM copy_u+sum, heavy rows chunked (light-row, chunk and combine "
+                   "kernels of one call%s)" % (", every segment of the pipelined partition"
+                                               if dist.is_initialized() else ""),
+            traffic_source=None if pmc is None else
+            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes (bench.py --workload "
+            "rmat), every g-SpMM kernel of a call summed, mean per call, read x2 (gfx950)",
+            regime="HBM-bound random row gather (H = %.0f GB >> 256 MB Infinity Cache)"
+                   % (n * FEAT * 4 / 1e9))
+        if dist.is_initialized():
+            roof["note"] = ("rank 0's local algorithmic bytes (its edges and rows) over rank "
+                            "0's g-SpMM kernel ms per step; per_rank: every rank")
+        cpu = None
+        if sample is not None:
+            t2 = time.time()
+            cpu = cpu_baseline(sample, n, None, seconds_budget=10.0)
+            log("rmat cpu baseline took %.1fs" % (time.time() - t2))
+        if dist.is_initialized():
+            dist.barrier()
         return {"value": E * steps / elapsed, "unit": "edges/s", "n_gpus": world,
                 "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
                 "scaling": "strong",
@@ -315,48 +493,27 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         kernel.set_row_split(old)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-edges", type=int, default=10_000_000)
-    ap.add_argument("--no-traffic", action="store_true",
-                    help="skip the rocprofv3 PMC passes that fill roofline.traffic")
-    ap.add_argument("--graph-scale", type=float, default=1.0,
-                    help="per-GPU graph size as a fraction of Reddit (testing only)")
-    ap.add_argument("--workload", default="reddit", choices=["reddit", "rmat"],
-                    help="reddit: weak-scaled Reddit-shaped graph (default, the driver's line); "
-                         "rmat: one fixed Graph500 R-MAT graph partitioned over the ranks "
-                         "(strong scaling, heavy rows chunked)")
-    ap.add_argument("--rmat-scale", type=int, default=26)
-    ap.add_argument("--emulate-world", type=int, default=0,
-                    help="single-GPU study: build the x N graph, keep rank 0's partition and "
-                         "time its local g-SpMM against the full (all-gathered) feature matrix "
-                         "(no communication; not a driver line)")
-    ap.add_argument("--pipeline-chunks", type=int, default=4,
-                    help="N>1: halo all-gather chunks overlapped with the local g-SpMM "
-                         "(0 = one all-gather, then the kernel; bit-exact rows)")
-    ap.add_argument("--halo-dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="N>1: wire type of the exchanged remote rows (bf16 halves the "
-                         "exchange; rows then carry bf16 rounding of remote inputs)")
-    ap.add_argument("--no-bf16-leg", action="store_true",
-                    help="N>1: skip the secondary timing of the same step with the bf16 halo")
-    ap.add_argument("--no-train-leg", action="store_true",
-                    help="skip the secondary timing of a training step (forward + backward)")
-    ap.add_argument("--no-rmat-leg", action="store_true",
-                    help="skip the secondary RMAT strong-scaling block (rmat26)")
-    ap.add_argument("--dist-rehearsal", action="store_true",
-                    help="run the multi-rank code path (RCCL group, partition, collectives) "
-                         "on a world of one rank (single-GPU rehearsal; not a driver line)")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
-                         "to rehearse the multi-rank path")
-    args = ap.parse_args()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = build_parser().parse_args(argv)
+    cmd = launch_command(args, argv, os.environ)
+    if cmd is not None:
+        # N ranks, one process per GPU: the child torchrun starts them; this
+        # process never loads the HIP library nor touches a device
+        log("starting %d ranks: %s" % (args.gpus, " ".join(cmd)))
+        return relay(cmd)
+    err = world_mismatch(args, os.environ)
+    if err is not None:
+        log("error: " + err)
+        return 2
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    on_cpu = args.device == "cpu"
+    if on_cpu:
+        args.no_traffic = True
+        if args.dist_backend == "nccl":
+            args.dist_backend = "gloo"
     pmc = None
     rmat_pmc = None
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
@@ -369,12 +526,14 @@ def main():
                                     "--steps", "2", "--warmup", "1", "--no-cpu-baseline",
                                     "--no-traffic"], per_call_calls=3)
         log("pmc traffic passes took %.1fs" % (time.time() - t0))
+    _load_dgl()
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world))
-    dev_index = local_rank % max(torch.cuda.device_count(), 1)
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
+    if on_cpu:
+        dev = torch.device("cpu")
+    else:
+        dev_index = local_rank % max(torch.cuda.device_count(), 1)
+        torch.cuda.set_device(dev_index)
+        dev = torch.device("cuda", dev_index)
     if world > 1 or args.dist_rehearsal:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -415,6 +574,11 @@ def main():
     gen.manual_seed(1)
     log("rank %d: graph %d nodes %d edges generated in %.1fs" % (rank, n, num_edges_total,
                                                                   time.time() - t0))
+    sample = h_cpu = None
+    want_cpu = (rank == 0 and not args.no_cpu_baseline and args.workload == "reddit"
+                and args.emulate_world <= 1)
+    if want_cpu:  # taken now, timed after the timed region
+        sample = cpu_sample(src, dst, n, args.cpu_sample_edges)
 
     if not dist.is_initialized() and args.workload == "rmat" and args.emulate_world <= 1:
         # 1.07B edges: build the device CSR directly (no host copy of the edge list)
@@ -473,15 +637,17 @@ def main():
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))
         h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         g.ndata["h"] = h
+        if want_cpu:
+            h_cpu = h.cpu()
         num_local_edges, num_rows = num_edges_total, n
         t1 = time.time()
         g.sparse_adjacency(dev)  # build + cache the device CSR (graph ingestion)
-        torch.cuda.synchronize()
+        _sync(dev)
         log("device CSR built in %.1fs" % (time.time() - t1))
 
         def step():
             g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
-        parallelism = "single GPU"
+        parallelism = "single GPU" if not on_cpu else "host (library host kernels)"
     else:
         from dgl.distributed import PartitionedGraph, balanced_bounds
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
@@ -492,6 +658,8 @@ def main():
                               halo_dtype=HALO_DTYPE[args.halo_dtype])
         h_full = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
         h_local = h_full[lo:hi].contiguous()
+        if want_cpu:
+            h_cpu = h_full.cpu()
         del h_full, sel
         num_local_edges, num_rows = pg.num_edges, pg.num_local
 
@@ -499,14 +667,24 @@ def main():
             pg.update_all(h_local)
         parallelism = describe_partition(pg, world, args)
     del src, dst
-    torch.cuda.synchronize()
-    log("setup done in %.1fs; peak HBM %.1f GB" % (time.time() - t0,
-                                                    torch.cuda.max_memory_allocated(dev) / 1e9))
+    _sync(dev)
+    if dev.type == "cuda":
+        log("setup done in %.1fs; peak HBM %.1f GB" % (
+            time.time() - t0, torch.cuda.max_memory_allocated(dev) / 1e9))
 
     elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
     value = num_edges_total * args.steps / elapsed
-    bytes_per_launch = algorithmic_bytes(num_local_edges, num_rows, FEAT)
-    achieved = bytes_per_launch / (kernel_ms * 1e-3) / 1e9
+    roof = roofline_block(
+        num_local_edges, num_rows, kernel_ms, world, dev,
+        traffic=None if pmc is None else pmc["bytes"],
+        kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
+            ", every segment of the pipelined partition" if dist.is_initialized() else ""),
+        traffic_source=None if pmc is None else
+        "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
+        regime=("L2/MALL-resident gather: H = %.0f MB fits the 256 MB Infinity Cache, "
+                "whose hits FETCH_SIZE counts as fetches; the DRAM-bound figure is the "
+                "rmat%d block's roofline" % (n * FEAT * 4 / 1e6, args.rmat_scale))
+        if n * FEAT * 4 < 256e6 else "HBM-bound gather (H exceeds the Infinity Cache)")
     result = {
         "metric": "edges/sec on update_all g-SpMM (copy_u+sum, feat=128)",
         "value": value,
@@ -535,25 +713,11 @@ def main():
             "feat": FEAT,
             "parallelism": parallelism,
         },
-        "roofline": {
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": None if pmc is None else pmc["bytes"],
-            "kernel": "gspmm_sum_kernel<copy_u> (rank 0)",
-            "kernel_ms": kernel_ms,
-            "bytes_per_launch": bytes_per_launch,
-            "traffic_source": None if pmc is None else
-            "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
-            "regime": ("L2/MALL-resident gather: H = %.0f MB fits the 256 MB Infinity Cache, "
-                       "whose hits FETCH_SIZE counts as fetches; the DRAM-bound figure is the "
-                       "rmat%d block's roofline" % (n * FEAT * 4 / 1e6, args.rmat_scale))
-            if n * FEAT * 4 < 256e6 else "HBM-bound gather (H exceeds the Infinity Cache)",
-        },
+        "roofline": roof,
         "cpu_baseline": None,
     }
+    if on_cpu:
+        result["device"] = "cpu (host kernels; plumbing test, not a measurement)"
     if dist.is_initialized():
         result["halo_exchange"] = exchange_block(pg, h_local, args.steps, world, dev)
     if dist.is_initialized() and args.halo_dtype == "fp32" and not args.no_bf16_leg:
@@ -598,18 +762,21 @@ def main():
                        % args.pipeline_chunks if dist.is_initialized() and
                        args.pipeline_chunks > 0 else "")}
         del h_tr, d_out
-    if rank == 0 and not dist.is_initialized() and not args.no_cpu_baseline:
+    if sample is not None:
+        # rank 0, after the timed region (the other ranks wait at the barrier)
         t2 = time.time()
-        gsrc, gdst = g._graph.src(), g._graph.dst()
-        result["cpu_baseline"] = cpu_baseline(gsrc, gdst, n, g.ndata["h"].cpu(),
-                                              args.cpu_sample_edges)
+        result["cpu_baseline"] = cpu_baseline(sample, n, h_cpu)
         log("cpu baseline took %.1fs" % (time.time() - t2))
+        sample = h_cpu = None
+    if dist.is_initialized():
+        dist.barrier()
     if not args.no_rmat_leg and args.workload == "reddit" and args.emulate_world <= 1:
         # release the headline leg before the 1.07B-edge graph
         step = g = h = adj = pg = h_local = None  # noqa: F841
         import gc
         gc.collect()
-        torch.cuda.empty_cache()
+        if dev.type == "cuda":
+            torch.cuda.empty_cache()
         key = "rmat%d" % args.rmat_scale
         if not dist.is_initialized():
             try:
@@ -623,7 +790,8 @@ def main():
     if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
