@@ -111,9 +111,12 @@ def _bucket_fn(g, rfunc, recv_nodes, msg_dst):
         g, rfunc, _all_nodes(g, recv_nodes), msg_dst, msgs, g._node_frame), "reduce_func")
 
 
-def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out):
+def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out, msg_eid=None):
     """A builtin reducer over materialised messages: SPMV_E2V (copy_e over the
-    incidence matrix), or degree bucketing when the messages are not float32."""
+    incidence matrix), or degree bucketing when the messages are not float32.
+    ``msg_eid``: ``msgs`` is the whole message frame and the incidence
+    matrix's columns are edge ids (build_inc_eid); the fallback then takes the
+    rows of those edges."""
     def check():
         if rfn.msg_field not in msgs.data:
             raise DGLError('Reduce function requires message field "%s", but no message '
@@ -121,7 +124,8 @@ def _builtin_over_messages(g, rfn, msgs, inc, recv_nodes, msg_dst, out):
     ir.CALL_(var.FUNC(check, "check_msg"))
     m = ir.READ_COL(msgs, var.STR(rfn.msg_field))
     fallback = var.FUNC(lambda mt: degree_bucketing.bucket_reduce(
-        g, rfn, _all_nodes(g, recv_nodes), msg_dst, {rfn.msg_field: mt},
+        g, rfn, _all_nodes(g, recv_nodes), msg_dst,
+        {rfn.msg_field: mt if msg_eid is None else mt[msg_eid.to(mt.device)]},
         g._node_frame)[rfn.out_field],
         "bucket_" + rfn.name)
     r = ir.SPMV_E2V(inc, m, var.STR(rfn.kernel_reduce), fallback)
@@ -269,13 +273,17 @@ def schedule_recv(g, recv_nodes, reduce_func, apply_func, inplace):
         return
     recv = torch.unique(recv_nodes, sorted=True)
     rfunc = _standardize(reduce_func, "reduce")
-    msgs = ir.READ_ROW(var.FEAT_DICT(g._msg_frame, "mf"), var.IDX(eid))
     out = ir.NEW_DICT()
     if is_iterable(rfunc):
-        inc = var.SPMAT(lambda dev: spmv.build_inc_dst(dst, recv, dev), "inc")
+        # the reference's e2v route (scheduler.py:451-456): incidence by edge id
+        # over the whole message frame, read in place
+        mf = var.FEAT_DICT(g._msg_frame, "mf")
+        m = g._msg_frame.num_rows
+        inc = var.SPMAT(lambda dev: spmv.build_inc_eid(m, eid, dst, recv, dev), "inc")
         for rfn in rfunc:
-            _builtin_over_messages(g, rfn, msgs, inc, recv, dst, out)
+            _builtin_over_messages(g, rfn, mf, inc, recv, dst, out, msg_eid=eid)
     else:
+        msgs = ir.READ_ROW(var.FEAT_DICT(g._msg_frame, "mf"), var.IDX(eid))
         out = ir.UPDATE_DICT(out, ir.DEGREE_BUCKETING(_bucket_fn(g, rfunc, recv, dst), msgs))
     _write_rows(g, recv, _apply_with_accum(g, recv, out, apply_func), inplace)
 

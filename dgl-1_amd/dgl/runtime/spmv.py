@@ -20,7 +20,7 @@ import torch
 from .. import kernel
 from ..base import DGLError
 
-__all__ = ["analyze_v2v", "build_adj_uv", "build_inc_dst", "kernel_feat_ok"]
+__all__ = ["analyze_v2v", "build_adj_uv", "build_inc_eid", "build_inc_dst", "kernel_feat_ok"]
 
 
 def kernel_feat_ok(mfn, nf, ef):
@@ -86,11 +86,23 @@ def build_adj_uv(num_nodes, u, v, eid, recv_nodes, device):
     return _remap_eid(adj, eid)
 
 
-def build_inc_dst(v, recv_nodes, device):
-    """(|recv|, len(v)) incidence of message positions (spmv.py:316-353)."""
+def build_inc_eid(m, eid, v, recv_nodes, device):
+    """(|recv|, m) incidence of messages by edge id (spmv.py:249-314): slot k
+    of row ``searchsorted(recv_nodes, v[k])`` is column ``eid[k]``, and its
+    slot eid is ``eid[k]`` too, so copy_e over it reads the message frame's
+    rows in place (no gathered copy of the pending messages). Receivers
+    without messages are empty rows (0 for sum, the initializer)."""
+    eid = torch.as_tensor(eid, dtype=torch.int64)
     rows = _relabel(recv_nodes, v)
-    pos = torch.arange(len(v), dtype=torch.int64)
-    return kernel.from_coo(len(recv_nodes), len(v), rows, pos, kernel.ORDER_EID, device)
+    adj = kernel.from_coo(len(recv_nodes), m, rows, eid, kernel.ORDER_EID, device)
+    return _remap_eid(adj, eid)
+
+
+def build_inc_dst(v, recv_nodes, device):
+    """(|recv|, len(v)) incidence of message positions (spmv.py:316-353):
+    build_inc_eid over positions 0..len(v)-1, as the reference defines it."""
+    return build_inc_eid(len(v), torch.arange(len(v), dtype=torch.int64), v, recv_nodes,
+                         device)
 
 
 class _RemappedAdj(kernel.SparseAdj):
