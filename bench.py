@@ -66,6 +66,12 @@ dgl = fn = data = kernel = None
 
 FEAT = 128
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# the guide's highest measured rate for uniformly random rows gathered from a
+# table past L2 and resident in the 256 MiB Infinity Cache (38 MB table, 8.6
+# TB/s; 7.4-7.9 at 151 MB): the ceiling of a gather whose table the Infinity
+# Cache holds (MI355X_MICROARCH.md "Indexed rows: gather into LDS")
+IC_GATHER_PEAK_GBS = 8600.0
+INFINITY_CACHE_BYTES = 256 << 20
 
 
 def log(*a):
@@ -374,23 +380,48 @@ def per_rank(values, world, dev):
     return [t[i * k:(i + 1) * k] for i in range(world)]
 
 
-def roofline_block(num_edges, num_rows, kms, world, dev, **extra):
+def gather_peak(table_bytes):
+    """(peak GB/s, source) of a row gather from a ``table_bytes`` table: the
+    guide's Infinity-Cache random-row rate while the table fits the cache,
+    else the HBM spec peak."""
+    if table_bytes < INFINITY_CACHE_BYTES:
+        return IC_GATHER_PEAK_GBS, (
+            "Infinity-Cache-resident gather (table %.0f MB < 256 MiB): the guide's measured "
+            "random-row rate from the Infinity Cache, 8.6 TB/s (MI355X_MICROARCH.md 'Indexed "
+            "rows'); no counter on this part separates Infinity-Cache hits from DRAM reads"
+            % (table_bytes / 1e6))
+    return HBM_PEAK_GBS, "HBM3E spec peak (MI355X_MICROARCH.md)"
+
+
+def roofline_block(num_edges, num_rows, kms, world, dev, table_bytes, **extra):
     """The g-SpMM roofline of this rank (algorithmic bytes of its launch(es)
-    per step over its kernel ms per step), with every rank's figures in
-    ``per_rank`` when N > 1."""
+    per step over its kernel ms per step) against the gather's ceiling for a
+    table of ``table_bytes`` (gather_peak), with every rank's figures in
+    ``per_rank`` when N > 1. ``effective_gather_frac`` is the same rate over
+    the 8 TB/s HBM spec: a figure of effective gather bandwidth, not of DRAM
+    bytes (FETCH_SIZE / TCC_EA0_RDREQ_DRAM count Infinity-Cache hits)."""
+    peak, source = gather_peak(table_bytes)
     b = algorithmic_bytes(num_edges, num_rows, FEAT)
     ach = b / (kms * 1e-3) / 1e9 if kms > 0 else None
-    roof = {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": None if ach is None else ach / HBM_PEAK_GBS,
-            "kernel_ms": kms, "bytes_per_launch": b}
+    roof = {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s",
+            "frac": None if ach is None else ach / peak,
+            "effective_gather_frac": None if ach is None else ach / HBM_PEAK_GBS,
+            "peak_source": source, "kernel_ms": kms, "bytes_per_launch": b}
     roof.update(extra)
     if world > 1:
         rows = per_rank([float(b), float(kms)], world, dev)
         roof["per_rank"] = [{"rank": i, "bytes_per_step": r[0], "kernel_ms": r[1],
                              "achieved": r[0] / (r[1] * 1e-3) / 1e9 if r[1] > 0 else None,
-                             "frac": r[0] / (r[1] * 1e-3) / 1e9 / HBM_PEAK_GBS
+                             "frac": r[0] / (r[1] * 1e-3) / 1e9 / peak
                              if r[1] > 0 else None} for i, r in enumerate(rows)]
     return roof
+
+
+def compulsory_bytes(num_edges, num_rows, num_sources, feat):
+    """Bytes a g-SpMM launch must move to or from DRAM at least: every
+    referenced source row once, the column ids and indptr once, the output
+    once (any cache re-use only lowers the rest)."""
+    return num_sources * 4 * feat + num_edges * 4 + num_rows * (4 * feat + 8)
 
 
 def exchange_block(pg, h_local, steps, world, dev):
@@ -428,6 +459,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         E = int(src.numel())
         gen = torch.Generator(device=dev)
         gen.manual_seed(1)
+        n_src = int((torch.bincount(src, minlength=n) > 0).sum())  # distinct sources
         sample = None
         if rank == 0 and not args.no_cpu_baseline:
             sample = cpu_sample(src, dst, n, 2_000_000)
@@ -461,7 +493,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
         # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
         roof = roofline_block(
-            local_edges, local_rows, kms, world, dev,
+            local_edges, local_rows, kms, world, dev, n * FEAT * 4,
             traffic=None if pmc is None else pmc["bytes"],
             kernel="g-SpMM copy_u+sum, heavy rows chunked (light-row, chunk and combine "
                    "kernels of one call%s)" % (", every segment of the pipelined partition"
@@ -474,6 +506,16 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         if dist.is_initialized():
             roof["note"] = ("rank 0's local algorithmic bytes (its edges and rows) over rank "
                             "0's g-SpMM kernel ms per step; per_rank: every rank")
+        else:
+            # DRAM bytes per call lie between the compulsory bytes (every
+            # referenced row once) and the fabric bytes (which include
+            # Infinity-Cache hits): no counter separates the two on gfx950
+            roof["dram_traffic"] = {
+                "lower_bound": compulsory_bytes(E, n, n_src, FEAT),
+                "upper_bound": None if pmc is None else pmc["bytes"],
+                "note": "compulsory bytes (%d distinct source rows once, ids, indptr, output) "
+                        "<= DRAM bytes <= fabric bytes (FETCH_SIZE x2 + WRITE_SIZE, which "
+                        "count Infinity-Cache hits)" % n_src}
         cpu = None
         if sample is not None:
             t2 = time.time()
@@ -675,16 +717,18 @@ def main(argv=None):
     elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
     value = num_edges_total * args.steps / elapsed
     roof = roofline_block(
-        num_local_edges, num_rows, kernel_ms, world, dev,
+        num_local_edges, num_rows, kernel_ms, world, dev, n * FEAT * 4,
         traffic=None if pmc is None else pmc["bytes"],
         kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
             ", every segment of the pipelined partition" if dist.is_initialized() else ""),
         traffic_source=None if pmc is None else
         "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
-        regime=("L2/MALL-resident gather: H = %.0f MB fits the 256 MB Infinity Cache, "
-                "whose hits FETCH_SIZE counts as fetches; the DRAM-bound figure is the "
-                "rmat%d block's roofline" % (n * FEAT * 4 / 1e6, args.rmat_scale))
-        if n * FEAT * 4 < 256e6 else "HBM-bound gather (H exceeds the Infinity Cache)")
+        regime=("Infinity-Cache-resident gather: H = %.0f MB fits the 256 MiB Infinity "
+                "Cache, whose hits FETCH_SIZE counts as fetches (traffic = fabric bytes, not "
+                "DRAM bytes); the DRAM-bound figure is the rmat%d block's roofline"
+                % (n * FEAT * 4 / 1e6, args.rmat_scale))
+        if n * FEAT * 4 < INFINITY_CACHE_BYTES else
+        "HBM-bound gather (H exceeds the Infinity Cache)")
     result = {
         "metric": "edges/sec on update_all g-SpMM (copy_u+sum, feat=128)",
         "value": value,

@@ -27,7 +27,7 @@ import os
 import numpy as np
 import torch
 
-from . import _ffi
+from . import _ffi, _handoff
 from ._ffi import LIB, check_call, ptr
 from .base import DGLError
 
@@ -886,9 +886,8 @@ class _MeanAddInto(torch.autograd.Function):
         given, ctx.prescaled = ctx.prescaled, None
         du = None
         if ctx.needs_input_grad[1]:
-            if given is not None and given[:2] == (dout.data_ptr(), dout._version):
-                d = given[2]  # dC / deg, written by dC's producer as it stored dC
-            else:
+            d = _handoff.take(given, dout)  # dC / deg, written by dC's producer
+            if d is None:
                 d = _mean_scaled(adj.fwd, dout, padded_ok=True)
             du, _ = _run_gspmm(adj.bwd, MSG_COPY_U, RED_SUM, d, None, 0, dout.shape[1], False)
         return None, du, dout if ctx.needs_input_grad[2] else None, None

@@ -23,6 +23,8 @@ import math
 import torch
 import torch.nn as nn
 
+from ..._handoff import GradHandoff, is_output, output_ref, take
+
 __all__ = ["NodeLinear", "sage_dense"]
 
 _ROWS_PER_CHUNK = 1 << 16
@@ -60,11 +62,11 @@ def _colsum(a):
 
 def _given_colsum(ctx, dy):
     """dy's column sums as the consumer's backward handed them over with dy
-    (the loss kernel, which sums them as it stores dy), else computed here."""
+    (the loss kernel, which sums them as it stores dy; a GradHandoff keyed on
+    that very tensor), else computed here."""
     given, ctx.dy_colsum = getattr(ctx, "dy_colsum", None), None
-    if given is not None and given[:2] == (dy.data_ptr(), dy._version):
-        return given[2]
-    return _colsum(dy)
+    cs = take(given, dy)
+    return cs if cs is not None else _colsum(dy)
 
 
 class _NodeLinearFn(torch.autograd.Function):
@@ -76,7 +78,7 @@ class _NodeLinearFn(torch.autograd.Function):
             out = torch.addmm(bias, x, weight.t())
         else:
             out = x.matmul(weight.t())
-        ctx.out_ptr = out.data_ptr()
+        ctx.out_ref = output_ref(out)
         ctx.wants_dy_colsum = ctx.has_bias and ctx.needs_input_grad[2]
         ctx.dy_colsum = None
         return out
@@ -202,7 +204,7 @@ class _DualLinearFn(torch.autograd.Function):
             if relu:
                 out.relu_()
         ctx.save_for_backward(x, w_self, agg, w_neigh, out if relu else None)
-        ctx.out_ptr = out.data_ptr()
+        ctx.out_ref = output_ref(out)
         ctx.premasked = None
         return out
 
@@ -211,8 +213,9 @@ class _DualLinearFn(torch.autograd.Function):
         x, w_self, agg, w_neigh, out = ctx.saved_tensors
         premasked, ctx.premasked = ctx.premasked, None
         colsum = None
-        if premasked is not None and premasked[:2] == (dy.data_ptr(), dy._version):
-            colsum = premasked[2]  # dy's column sums, taken as it was stored
+        got = take(premasked, dy)  # (dy's column sums or None,): dy already masked
+        if got is not None:
+            colsum = got[0]  # taken as dy was stored
         elif ctx.relu:
             dy = torch.ops.aten.threshold_backward(dy, out, 0)  # ReLU's own backward, one pass
         dy = dy.contiguous()
@@ -279,7 +282,7 @@ class _PreAggregateFn(torch.autograd.Function):
         ctx.save_for_backward(x, w_self, w_neigh)
         ctx.graph = (pre_leaf, neigh) if pre_leaf is not None else None
         ctx.has_bias = bias is not None
-        ctx.out_ptr = out.data_ptr()
+        ctx.out_ref = output_ref(out)
         ctx.wants_dy_colsum = ctx.has_bias and ctx.needs_input_grad[2]
         ctx.dy_colsum = None
         # the in-store mean-add's backward operand dy / deg can come from dy's
@@ -313,8 +316,10 @@ class _PreAggregateFn(torch.autograd.Function):
                 t.record_stream(side)
         scaled, ctx.dy_scaled = ctx.dy_scaled, None
         inner, ctx.inner = ctx.inner, None
-        if inner is not None and scaled is not None and scaled[:2] == (dy.data_ptr(), dy._version):
-            inner.prescaled = scaled
+        scaled = take(scaled, dy)
+        if inner is not None and scaled is not None:
+            # the mean-add's backward receives this same dy as its dout
+            inner.prescaled = GradHandoff(dy, scaled)
         (dpre,) = torch.autograd.grad(neigh, pre_leaf, dy)
         dpre = dpre.contiguous()
         dx = None
@@ -332,7 +337,7 @@ class _PreAggregateFn(torch.autograd.Function):
                 if gate is not None:
                     dx, cs = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh, gate=gate,
                                           colsum=node.has_bias)
-                    node.premasked = (dx.data_ptr(), dx._version, cs)
+                    node.premasked = GradHandoff(dx, (cs,))
                 else:
                     dx = _node_dgrad2(x.shape[1], dy, w_self, dpre, w_neigh)
             else:
@@ -366,8 +371,7 @@ def _relu_producer(x):
     itself, not a view or an in-place update of it), else None."""
     node = x.grad_fn
     if (isinstance(node, _DualLinearFn._backward_cls) and getattr(node, "relu", False) and
-            getattr(node, "out_ptr", None) == x.data_ptr() and x._base is None and
-            x.is_contiguous()):
+            is_output(node, x) and x.is_contiguous()):
         return node
     return None
 

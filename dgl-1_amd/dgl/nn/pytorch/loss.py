@@ -25,6 +25,8 @@ ignore_index = -100; other out-of-range labels are an error there).
 import torch
 import torch.nn.functional as F
 
+from ..._handoff import GradHandoff, is_output
+
 __all__ = ["weighted_cross_entropy"]
 
 _MAX_CLASSES = 64
@@ -47,8 +49,7 @@ def _bias_producer(z):
     node = z.grad_fn
     if (node is not None and (getattr(node, "wants_dy_colsum", False) or
                               getattr(node, "dy_scaled_spec", None) is not None) and
-            getattr(node, "out_ptr", None) == z.data_ptr() and z._base is None and
-            z.is_contiguous()):
+            is_output(node, z) and z.is_contiguous()):
         return node
     return None
 
@@ -94,10 +95,10 @@ class _WeightedXentFn(torch.autograd.Function):
             kernel._stream_of(z.device)))
         if cs is not None:
             # the producing Linear's bias gradient, summed as dz was stored
-            node.dy_colsum = (dz.data_ptr(), dz._version, cs)
+            node.dy_colsum = GradHandoff(dz, cs)
         if scaled is not None:
             # dz / deg in the padded rows of the producer's mean aggregation
-            node.dy_scaled = (dz.data_ptr(), dz._version, scaled[:, :C])
+            node.dy_scaled = GradHandoff(dz, scaled[:, :C])
         return dz, None, None
 
 
