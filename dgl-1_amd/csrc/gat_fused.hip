@@ -1,0 +1,195 @@
+// Fused GAT layer aggregation for gfx950: attention, attention dropout,
+// normaliser and head-broadcast aggregation in one pass over the CSR.
+//
+// The reference's GAT layer (examples/pytorch/gat/train.py:74-96) runs it as
+//   apply_edges(edge_attention)   a = clamp(exp(leaky_relu(a1[u] + a2[v])))
+//   attn_drop                     a_drop = dropout(a)
+//   update_all([src_mul_edge(ft, a_drop), copy_edge(a)], [sum -> ft, sum -> z])
+// i.e. an E x H attention tensor written, then read by an incidence SPMV over
+// E x H x D materialised messages and again by the normaliser's. Here one wave
+// owns one destination row v and, slot by slot in CSR order (u = indices[k]):
+//   a[k, h]            = clamp(exp(leaky_relu(el[u, h] + er[v, h], alpha)), lo, hi)
+//   w[k, h]            = keep(k, h) ? a[k, h] * scale : 0     (dropout; else a)
+//   ft_out[v, hD + d]  = fma chain over k of w[k, h] * ft[u, hD + d]
+//   z[v, h]            = add chain over k of a[k, h]
+// The per-edge expression is gsddmm_attention_vec_kernel's and the two chains
+// are gspmm_sum_kernel's (u_mul_e with per-head weights, copy_e), in the same
+// slot order, so the outputs equal the three-kernel path's bit for bit. The
+// E x H attention (and its dropped copy) are written, in CSR slot order, only
+// when the caller passes buffers for them (autograd needs them); the gathered
+// el row of a slot is one 4-B load per lane, shared by the D lanes of a head.
+//
+// Lane map: VEC consecutive features per lane (VEC divides D), a 64-lane pass
+// covers 64 * VEC features; the first lane of each head in a pass keeps and
+// stores that head's z and attention values. UNROLL slots are in flight.
+//
+// Dropout mask: keep(k, h) = hash(seed, k * H + h) >= threshold, a stateless
+// counter hash (gat_keep below, host and device), so the backward and the host
+// path reproduce it from (seed, slot, head) alone.
+
+#include "gspmm_impl.h"
+
+namespace dglhip {
+
+// lowbias32 (a 32-bit integer finaliser); two rounds over the 64-bit index
+__host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ bool gat_keep(uint64_t seed, int64_t idx, uint32_t thr) {
+  const uint64_t i = static_cast<uint64_t>(idx);
+  const uint32_t r = gat_mix32(gat_mix32(static_cast<uint32_t>(i) ^ static_cast<uint32_t>(seed)) ^
+                               (static_cast<uint32_t>(i >> 32) + static_cast<uint32_t>(seed >> 32) +
+                                0x9e3779b9u));
+  return r >= thr;
+}
+
+// keep iff hash >= threshold: P(keep) = 1 - p
+static inline uint32_t gat_drop_threshold(float p) {
+  const double t = static_cast<double>(p) * 4294967296.0;
+  return t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
+}
+
+template <int VEC, int UNROLL, bool DROP>
+__global__ __launch_bounds__(256) void gat_aggregate_kernel(
+    int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
+    const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
+    float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
+    const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
+    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out) {
+  typedef typename Vec<VEC>::T V;
+  const int lane = threadIdx.x & 63;
+  const int64_t it = block_linear() * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_rows) return;
+  int64_t row = row_order ? row_order[it] : it;
+  row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int64_t F = H * D;
+  const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
+  for (int64_t f0 = int64_t(lane) * VEC; f0 < F; f0 += 64 * VEC) {
+    const int64_t h = f0 / D;
+    const bool head_lane = f0 - h * D == 0;  // first lane of head h in this pass
+    const float r = er[row * H + h];
+    V acc = Vec<VEC>::zero();
+    float zacc = 0.0f;
+    auto attend = [&](float x) {
+      x = x + r;
+      x = x > 0.0f ? x : alpha * x;
+      if (apply_exp) x = __expf(x);
+      return fminf(fmaxf(x, lo), hi);
+    };
+    auto consume = [&](int64_t k, float l, V u) {
+      const float a = attend(l);
+      float w = a;
+      if (DROP) w = gat_keep(seed, k * H + h, thr) ? a * scale : 0.0f;
+      acc = Vec<VEC>::fma(Vec<VEC>::splat(w), u, acc);
+      zacc += a;
+      if (head_lane && a_out) {
+        a_out[k * H + h] = a;
+        if (DROP) w_out[k * H + h] = w;
+      }
+    };
+    int64_t k = beg;
+    for (; k + UNROLL <= end; k += UNROLL) {
+      float l[UNROLL];
+      V u[UNROLL];
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j) {
+        const int64_t src = indices[k + j];
+        l[j] = el[src * H + h];
+        u[j] = ldv<VEC>(ft + src * F + f0);
+      }
+#pragma unroll
+      for (int j = 0; j < UNROLL; ++j) consume(k + j, l[j], u[j]);
+    }
+    const int64_t rem = end - k;  // one predicated batch, as reduce_range's tail
+    if (rem > 0) {
+      float l[UNROLL];
+      V u[UNROLL];
+#pragma unroll
+      for (int j = 0; j < UNROLL - 1; ++j) {
+        if (j < rem) {
+          const int64_t src = indices[k + j];
+          l[j] = el[src * H + h];
+          u[j] = ldv<VEC>(ft + src * F + f0);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < UNROLL - 1; ++j)
+        if (j < rem) consume(k + j, l[j], u[j]);
+    }
+    stv<VEC>(out_ft + row * F + f0, acc);
+    if (head_lane) out_z[row * H + h] = zacc;
+  }
+}
+
+}  // namespace dglhip
+
+using namespace dglhip;
+
+extern "C" {
+
+int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t head_dim,
+                                const int64_t* indptr, const int32_t* indices,
+                                const int32_t* row_order, const float* el, const float* er,
+                                const float* ft, float alpha, float clamp_lo, float clamp_hi,
+                                int apply_exp, float drop_p, uint64_t seed,
+                                const int64_t* seed_offset, float* out_ft, float* out_z,
+                                float* attn_out, float* attn_drop_out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
+  DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && el && er && ft && out_ft && out_z, "null pointer argument");
+  const bool drop = drop_p > 0.0f;
+  DGLHIP_CHECK(!drop || (attn_out == nullptr) == (attn_drop_out == nullptr),
+               "with dropout, the attention and its dropped copy are written together");
+  const int64_t blocks = (num_rows + 3) / 4;
+  DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large");
+  const uint32_t thr = drop ? gat_drop_threshold(drop_p) : 0u;
+  const float scale = drop ? 1.0f / (1.0f - drop_p) : 1.0f;
+  const int64_t F = num_heads * head_dim;
+  // VEC 2 when a lane's two features stay in one head and rows are 8-B aligned
+  const bool v2 = head_dim % 2 == 0 && F >= 128 &&
+                  reinterpret_cast<uintptr_t>(ft) % 8 == 0 &&
+                  reinterpret_cast<uintptr_t>(out_ft) % 8 == 0;
+  timed_launch(stream, [&] {
+#define DGLHIP_GAT(VV, DD)                                                                 \
+  hipLaunchKernelGGL((gat_aggregate_kernel<VV, 16, DD>), grid_1d(blocks), dim3(256), 0,    \
+                     stream, num_rows, num_heads, head_dim, indptr, indices, row_order, el, \
+                     er, ft, alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale, \
+                     out_ft, out_z, attn_out, attn_drop_out)
+    if (v2) {
+      if (drop) DGLHIP_GAT(2, true); else DGLHIP_GAT(2, false);
+    } else {
+      if (drop) DGLHIP_GAT(1, true); else DGLHIP_GAT(1, false);
+    }
+#undef DGLHIP_GAT
+  });
+  API_END();
+}
+
+int dglhip_gat_dropout_mask_host(int64_t num_slots, int64_t num_heads, float drop_p,
+                                 uint64_t seed, uint8_t* keep) {
+  API_BEGIN();
+  DGLHIP_CHECK(num_slots >= 0 && num_heads >= 1, "bad sizes");
+  DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
+  if (num_slots == 0) return 0;
+  DGLHIP_CHECK(keep != nullptr, "null pointer argument");
+  const uint32_t thr = drop_p > 0.0f ? gat_drop_threshold(drop_p) : 0u;
+  const int64_t n = num_slots * num_heads;
+  parallel_for(n, default_num_threads(), [&](int64_t b, int64_t e, int) {
+    for (int64_t i = b; i < e; ++i) keep[i] = gat_keep(seed, i, thr) ? 1 : 0;
+  }, 1 << 16);
+  API_END();
+}
+
+}  // extern "C"

@@ -1135,3 +1135,163 @@ def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
     return _EdgeAttention.apply(adj, int(num_edges), float(alpha), float(clamp[0]),
                                 float(clamp[1]), bool(apply_exp),
                                 _f32c(a_src.reshape(-1, H)), _f32c(a_dst.reshape(-1, H)), slot)
+
+
+# ---------------------------------------------------------------------------
+# Fused GAT aggregation: attention + dropout + normaliser + head-broadcast sum
+# ---------------------------------------------------------------------------
+_GAT_SEED = {}
+
+
+def _gat_seed_offset(dev):
+    """A per-device int64 counter the fused kernel adds to its dropout seed,
+    advanced on the device at every call: a captured HIP graph draws a new
+    mask at every replay, and no host round trip is needed."""
+    key = str(dev)
+    if key not in _GAT_SEED:
+        base = int(torch.randint(0, 1 << 62, (1,)).item())  # torch's generator: manual_seed
+        _GAT_SEED[key] = (base, torch.zeros(1, dtype=torch.int64, device=dev))
+    base, off = _GAT_SEED[key]
+    off.add_(1)
+    return base, off
+
+
+def gat_dropout_mask(num_slots, num_heads, p, seed):
+    """bool (num_slots, num_heads): the (slot, head) pairs the fused kernel
+    keeps at dropout probability ``p`` under seed ``seed`` (its counter hash,
+    computed on the host)."""
+    keep = torch.empty(num_slots, num_heads, dtype=torch.uint8)
+    check_call(LIB.dglhip_gat_dropout_mask_host(num_slots, num_heads, float(p), int(seed),
+                                                ptr(keep)))
+    return keep.bool()
+
+
+def _attention_slots(fwd, el, er, alpha, lo, hi, apply_exp):
+    out = torch.empty(fwd.nnz, el.shape[1], dtype=torch.float32, device=el.device)
+    args = (fwd.num_rows, el.shape[1], ptr(fwd.indptr), ptr(fwd.indices), None, ptr(el),
+            ptr(er), float(alpha), float(lo), float(hi), 1 if apply_exp else 0, ptr(out))
+    if el.is_cuda:
+        check_call(LIB.dglhip_gsddmm_attention_device(*(args + (_stream_of(el.device),))))
+    else:
+        check_call(LIB.dglhip_gsddmm_attention_host(*(args + (0,))))
+    return out
+
+
+class _GATAggregate(torch.autograd.Function):
+    """(ft_sum, z) = (sum_k w[k,h] ft[u_k, h, :], sum_k a[k,h]) per destination
+    row and head, a = clamp(exp(leaky_relu(el[u] + er[v]))), w = dropout(a),
+    all in one kernel on the device (dglhip_gat_aggregate_device); a and w are
+    kept in CSR slot order only when a gradient is needed. The backward is the
+    three-kernel path's (the u_mul_e product over the transpose, the g-SDDMM
+    dot, the copy_e gather, the attention's backward): same bits."""
+
+    @staticmethod
+    def forward(ctx, adj, alpha, lo, hi, apply_exp, p, seed, seed_off, el, er, ft2, D):
+        fwd = adj.fwd
+        H = el.shape[1]
+        F = ft2.shape[1]
+        dev = ft2.device
+        need = any(ctx.needs_input_grad[8:11])
+        a = w = None
+        if dev.type == "cuda":
+            out_ft = torch.empty(fwd.num_rows, F, dtype=torch.float32, device=dev)
+            out_z = torch.empty(fwd.num_rows, H, dtype=torch.float32, device=dev)
+            if need:
+                a = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
+                w = torch.empty_like(a) if p > 0 else None
+            check_call(LIB.dglhip_gat_aggregate_device(
+                fwd.num_rows, H, D, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.row_order),
+                ptr(el), ptr(er), ptr(ft2), float(alpha), float(lo), float(hi),
+                1 if apply_exp else 0, float(p), int(seed), ptr(seed_off), ptr(out_ft),
+                ptr(out_z), ptr(a), ptr(w), _stream_of(dev)))
+        else:  # host: the same per-edge values and chains from the host kernels
+            a = _attention_slots(fwd, el, er, alpha, lo, hi, apply_exp)
+            w = None
+            if p > 0:
+                keep = gat_dropout_mask(fwd.nnz, H, p, seed)
+                w = torch.where(keep, a * (1.0 / (1.0 - p)), torch.zeros_like(a))
+            out_ft, _ = _run_gspmm(fwd, MSG_U_MUL_E, RED_SUM, ft2, w if p > 0 else a, H, F,
+                                   False, emap=SLOT)
+            out_z, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, a, H, H, False, emap=SLOT)
+            if not need:
+                a = w = None
+        ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp, ctx.p = adj, alpha, lo, hi, \
+            apply_exp, p
+        ctx.save_for_backward(ft2, a, w)
+        return out_ft, out_z
+
+    @staticmethod
+    def backward(ctx, d_ft, d_z):
+        ft2, a, w = ctx.saved_tensors
+        adj = ctx.adj
+        fwd = adj.fwd
+        H = a.shape[1]
+        F = ft2.shape[1]
+        need_el, need_er, need_ft = ctx.needs_input_grad[8:11]
+        d_el = d_er = d_ft2 = None
+        d_ft = torch.zeros_like(ft2) if d_ft is None else d_ft.contiguous()
+        wt = w if w is not None else a
+        if need_ft:
+            d_ft2, _ = _run_gspmm(adj.bwd, MSG_U_MUL_E, RED_SUM, d_ft, wt, H, F, False,
+                                  emap=_fwd_slot_of_bwd(adj))
+        if need_el or need_er:
+            d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
+            if w is not None:  # dropout's backward: the kept pairs, scaled
+                d_a = torch.where(w != 0, d_a * (1.0 / (1.0 - ctx.p)), torch.zeros_like(d_a))
+            if d_z is not None:
+                d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
+            # the attention's backward (_EdgeAttention.backward, slot order)
+            inside = (a > ctx.lo) & (a < ctx.hi)
+            if ctx.apply_exp:
+                slope = torch.where(a < 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                g = d_a * a * slope
+            else:
+                slope = torch.where(a < 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                g = d_a * slope
+            g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
+            if need_el:
+                d_el, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
+                                     emap=_fwd_slot_of_bwd(adj))
+            if need_er:
+                d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
+        return (None,) * 8 + (d_el, d_er, d_ft2, None)
+
+
+def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0,
+                  training=True, apply_exp=True, seed=None):
+    """One GAT layer's aggregation in one kernel (examples/pytorch/gat/train.py:74-96):
+    for every destination row v and head h, over v's in-edges u -> v in CSR
+    slot order,
+
+        a      = clamp(exp(leaky_relu(el[u, h] + er[v, h], alpha)), *clamp)
+        ft_sum = sum a_drop * ft[u, h, :]    (a_drop = dropout(a), training only)
+        z      = sum a
+
+    returned as (ft_sum (R, H, D), z (R, H, 1)), differentiable in ft, el, er.
+    ft (N, H, D); el (N, H[, 1]); er (R, H[, 1]). Equals edge_attention(...,
+    edge_order="slot") followed by gspmm(u_mul_e, sum) and gspmm(copy_e, sum)
+    bit for bit. The dropout mask is the kernel's counter hash of (seed,
+    slot, head) (gat_dropout_mask), not torch's generator; ``seed`` None draws
+    the seed from torch's generator once per device and advances a device
+    counter per call."""
+    p = float(attn_drop) if training else 0.0
+    if not 0.0 <= p < 1.0:
+        raise DGLError("attention dropout must be in [0, 1), got %r" % (attn_drop,))
+    dev = ft.device
+    adj = adj.to(dev)
+    N, H, D = ft.shape
+    el2 = _f32c(el.reshape(el.shape[0], H))
+    er2 = _f32c(er.reshape(er.shape[0], H))
+    ft2 = _f32c(ft.reshape(N, H * D))
+    if el2.shape[0] < adj.shape[1] or er2.shape[0] != adj.shape[0] or N < adj.shape[1]:
+        raise DGLError("gat_aggregate: feature rows do not match the adjacency")
+    seed_off = None
+    if p > 0 and seed is None:
+        if dev.type == "cuda":
+            seed, seed_off = _gat_seed_offset(dev)
+        else:
+            seed = int(torch.randint(0, 1 << 62, (1,)).item())
+    ft_sum, z = _GATAggregate.apply(adj, float(alpha), float(clamp[0]), float(clamp[1]),
+                                    bool(apply_exp), p, int(seed or 0), seed_off, el2, er2,
+                                    ft2, D)
+    return ft_sum.view(-1, H, D), z.view(-1, H, 1)

@@ -7,8 +7,8 @@ must drop in, so these modules package the example layers' computation (with
 the later-DGL module names and arguments) on top of:
 
 * GraphConv    : update_all(copy_src, sum) -> one g-SpMM (gcn_spmv.py:45-62)
-* GATConv      : fused attention g-SDDMM + per-head u_mul_e g-SpMM + copy_edge
-                 normaliser (gat/train.py:61-96), attention kept in CSR slot order
+* GATConv      : attention, dropout, per-head weighted sum and copy_edge
+                 normaliser in one kernel (gat/train.py:61-96, kernel.gat_aggregate)
 * SAGEConv     : update_all(copy_src, mean) -> g-SpMM mean
 * RelGraphConv : typed-edge block-diagonal g-SpMM (rgcn/layers.py:121-132)
 """
@@ -90,15 +90,15 @@ class GATConv(nn.Module):
         el = (ft * self.attn_l).sum(-1)  # N x H
         er = (ft * self.attn_r).sum(-1)
         adj = g.sparse_adjacency(feat.device)
-        # attention in the forward CSR's slot order: the two g-SpMMs then read
-        # it by slot (no per-edge eid gather) and its gradient comes back in
-        # the same layout; the arithmetic per element is unchanged
-        a = kernel.edge_attention(adj, el, er, g.number_of_edges(), self.negative_slope,
-                                  clamp=(-float("inf"), float("inf")), edge_order="slot")
-        a = a.unsqueeze(-1)  # E x H x 1
-        a_drop = self.attn_drop(a) if self.attn_drop is not None else a
-        ft_sum = kernel.gspmm(adj, "u_mul_e", "sum", ft, a_drop, edge_order="slot")
-        z = kernel.gspmm(adj, "copy_e", "sum", None, a, edge_order="slot")
+        # attention, its dropout, the weighted sum and the normaliser in one
+        # kernel (kernel.gat_aggregate); the attention is kept, in CSR slot
+        # order, only for the backward. Same per-element arithmetic as the
+        # attention g-SDDMM + u_mul_e + copy_e g-SpMMs (bit for bit without
+        # dropout); the dropout mask is the kernel's counter hash
+        ft_sum, z = kernel.gat_aggregate(
+            adj, ft, el, er, self.negative_slope, clamp=(-float("inf"), float("inf")),
+            attn_drop=self.attn_drop.p if self.attn_drop is not None else 0.0,
+            training=self.training)
         rst = ft_sum / z.clamp(min=1e-20)
         if self.res_fc is not None:
             rst = rst + self.res_fc(h).view(-1, self.num_heads, self.out_feats)

@@ -1,14 +1,17 @@
 """Graph Attention Network on the engine (counterpart of the reference's
 examples/pytorch/gat/train.py; BASELINE.json configs[2]: 8 heads on Pubmed).
 
-Per layer: the unnormalised attention exp(leaky_relu(a_l[src] + a_r[dst]))
-(E x H x 1) comes from one fused g-SDDMM kernel (dgl.kernel.edge_attention;
-``--udf`` runs the reference's edge UDF instead), then ONE
+Per layer, by default ONE kernel (dgl.kernel.gat_aggregate): the
+unnormalised attention exp(leaky_relu(a_l[src] + a_r[dst])), its dropout, the
+per-head weighted sum of the source features and the copy_edge normaliser, in
+one pass over each destination row's in-edges (the attention kept in CSR slot
+order only for the backward). ``--unfused`` runs the same arithmetic as three
+kernels (attention g-SDDMM, then ONE
 ``update_all([src_mul_edge('ft','a_drop','ft'), copy_edge('a','a')],
-[sum('ft','ft'), sum('a','z')])`` — on this engine both pairs are fused
-g-SpMMs (per-head edge weights broadcast over the head's features, and the
-copy_edge normaliser), where the reference materialises E x H x D messages
-and reduces them with an incidence-matrix SPMV.
+[sum('ft','ft'), sum('a','z')])`` whose pairs are fused g-SpMMs) with torch's
+dropout; ``--udf`` runs the reference's edge UDF for the attention. The
+reference materialises E x H x D messages and reduces them with an
+incidence-matrix SPMV.
 
   python examples/gat/train.py --dataset pubmed --gpu 0 [--hip-graph]
 
@@ -34,10 +37,11 @@ from dgl.data import load_data  # noqa: E402
 
 class GraphAttention(nn.Module):
     def __init__(self, g, in_dim, out_dim, num_heads, feat_drop, attn_drop, alpha, residual,
-                 udf=False):
+                 udf=False, unfused=False):
         super(GraphAttention, self).__init__()
         self.g = g
         self.udf = udf
+        self.unfused = unfused
         self.alpha = alpha
         self.num_heads = num_heads
         self.fc = nn.Linear(in_dim, num_heads * out_dim, bias=False)
@@ -66,16 +70,25 @@ class GraphAttention(nn.Module):
         if self.udf:  # the reference's edge UDF (gat/train.py:90-96)
             self.g.ndata.update({"ft": ft, "a1": a1.contiguous(), "a2": a2.contiguous()})
             self.g.apply_edges(self.edge_attention)
-        else:  # fused u_add_v -> leaky_relu -> exp -> clamp g-SDDMM
+            self.g.update_all([fn.src_mul_edge("ft", "a_drop", "ft"), fn.copy_edge("a", "a")],
+                              [fn.sum("ft", "ft"), fn.sum("a", "z")])
+            ret = self.g.ndata["ft"] / self.g.ndata["z"]
+        elif self.unfused:  # three kernels: attention g-SDDMM, u_mul_e and copy_e g-SpMMs
             self.g.ndata["ft"] = ft
             a = kernel.edge_attention(self.g.sparse_adjacency(h.device), a1, a2,
                                       self.g.number_of_edges(), self.alpha)
             a = a.unsqueeze(-1)  # E x H x 1
             a_drop = self.attn_drop(a) if self.attn_drop is not None else a
             self.g.edata.update({"a": a, "a_drop": a_drop})
-        self.g.update_all([fn.src_mul_edge("ft", "a_drop", "ft"), fn.copy_edge("a", "a")],
-                          [fn.sum("ft", "ft"), fn.sum("a", "z")])
-        ret = self.g.ndata["ft"] / self.g.ndata["z"]
+            self.g.update_all([fn.src_mul_edge("ft", "a_drop", "ft"), fn.copy_edge("a", "a")],
+                              [fn.sum("ft", "ft"), fn.sum("a", "z")])
+            ret = self.g.ndata["ft"] / self.g.ndata["z"]
+        else:  # one kernel: attention, dropout, weighted sum and normaliser
+            ft_sum, z = kernel.gat_aggregate(
+                self.g.sparse_adjacency(h.device), ft, a1, a2, self.alpha,
+                attn_drop=self.attn_drop.p if self.attn_drop is not None else 0.0,
+                training=self.training)
+            ret = ft_sum / z
         if self.residual:
             res = self.res_fc(h).reshape(ret.shape) if self.res_fc is not None \
                 else h.reshape(ret.shape)
@@ -91,16 +104,17 @@ class GraphAttention(nn.Module):
 
 class GAT(nn.Module):
     def __init__(self, g, num_layers, in_dim, num_hidden, num_classes, heads, activation,
-                 feat_drop, attn_drop, alpha, residual, udf=False):
+                 feat_drop, attn_drop, alpha, residual, udf=False, unfused=False):
         super(GAT, self).__init__()
         self.activation = activation
+        kw = {"udf": udf, "unfused": unfused}
         self.layers = nn.ModuleList([GraphAttention(g, in_dim, num_hidden, heads[0], feat_drop,
-                                                    attn_drop, alpha, False, udf)])
+                                                    attn_drop, alpha, False, **kw)])
         for i in range(1, num_layers):
             self.layers.append(GraphAttention(g, num_hidden * heads[i - 1], num_hidden, heads[i],
-                                              feat_drop, attn_drop, alpha, residual, udf))
+                                              feat_drop, attn_drop, alpha, residual, **kw))
         self.layers.append(GraphAttention(g, num_hidden * heads[-2], num_classes, heads[-1],
-                                          feat_drop, attn_drop, alpha, residual, udf))
+                                          feat_drop, attn_drop, alpha, residual, **kw))
 
     def forward(self, h):
         for layer in self.layers[:-1]:
@@ -117,7 +131,8 @@ def run(args):
     torch.manual_seed(args.seed)
     heads = [args.num_heads] * args.num_layers + [args.num_out_heads]
     model = GAT(g, args.num_layers, data.features.shape[1], args.num_hidden, data.num_labels,
-                heads, F.elu, args.in_drop, args.attn_drop, args.alpha, args.residual, args.udf)
+                heads, F.elu, args.in_drop, args.attn_drop, args.alpha, args.residual, args.udf,
+                args.unfused)
     model = model.to(device)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=args.weight_decay,
                            capturable=args.hip_graph)
@@ -198,6 +213,9 @@ def parser():
     p.add_argument("--alpha", type=float, default=0.2)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--udf", action="store_true", help="reference edge UDF for the attention")
+    p.add_argument("--unfused", action="store_true",
+                   help="attention g-SDDMM + u_mul_e and copy_e g-SpMMs as three kernels "
+                        "(torch dropout) instead of the one fused kernel")
     p.add_argument("--hip-graph", action="store_true",
                    help="capture the training step in a HIP graph and replay it (GPU)")
     return p

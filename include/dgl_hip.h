@@ -384,6 +384,36 @@ int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads,
                                  float alpha, float clamp_lo, float clamp_hi,
                                  int apply_exp, float* out, int num_threads);
 
+/* Fused GAT layer aggregation (gat/train.py:74-96: apply_edges(edge_attention),
+ * attn_drop, update_all([src_mul_edge, copy_edge], [sum, sum])) in one pass,
+ * one wave per destination row r, slots k of the row in CSR order, u = indices[k]:
+ *   a[k, h]         = clamp(act(el[u, h] + er[r, h]), lo, hi)   (act as above)
+ *   w[k, h]         = keep(s, k * H + h) ? a[k, h] / (1 - drop_p) : 0
+ *                     (w = a when drop_p == 0), s = seed + *seed_offset
+ *                     (seed_offset: a device int64, may be NULL: s = seed;
+ *                     a counter on the device keeps HIP-graph replays drawing
+ *                     fresh masks)
+ *   out_ft[r, hD+d] = sum_k w[k, h] * ft[u, hD+d]   (fma chain in slot order)
+ *   out_z[r, h]     = sum_k a[k, h]                 (add chain in slot order)
+ * el, er: [num_src, H], [num_rows, H]; ft: [num_src, H*D]; out_ft: [num_rows,
+ * H*D]; out_z: [num_rows, H]. attn_out / attn_drop_out ([nnz, H], CSR slot
+ * order) may be NULL (nothing stored); with dropout both or neither. The
+ * outputs equal dglhip_gsddmm_attention_device (slot order) followed by the
+ * u_mul_e and copy_e sums bit for bit. keep(): dglhip_gat_dropout_mask_host.
+ * row_order (int32[num_rows], may be NULL): launch schedule only. */
+int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t head_dim,
+                                const int64_t* indptr, const int32_t* indices,
+                                const int32_t* row_order, const float* el, const float* er,
+                                const float* ft, float alpha, float clamp_lo, float clamp_hi,
+                                int apply_exp, float drop_p, uint64_t seed,
+                                const int64_t* seed_offset, float* out_ft, float* out_z,
+                                float* attn_out, float* attn_drop_out, void* stream);
+
+/* The attention-dropout mask of dglhip_gat_aggregate_device: keep[i] = 1 for
+ * the kept (slot, head) pairs i = k * H + h, a stateless hash of (seed, i). */
+int dglhip_gat_dropout_mask_host(int64_t num_slots, int64_t num_heads, float drop_p,
+                                 uint64_t seed, uint8_t* keep);
+
 /* ------------------------------------------------------------------------ */
 /* Typed-edge block-diagonal g-SpMM (R-GCN block layer, examples/pytorch/    */
 /* rgcn/layers.py:121-132): with Fi = nb*si, Fo = nb*so,                     */

@@ -1,0 +1,192 @@
+"""The fused GAT aggregation (kernel.gat_aggregate, csrc/gat_fused.hip).
+
+* kernel level: attention + weighted sum + normaliser in one kernel equal the
+  three-kernel path (attention g-SDDMM in slot order, u_mul_e and copy_e
+  g-SpMMs) bit for bit, forward and every gradient, over head shapes
+  including Pubmed's (8 x 8, 8 x 3) and a Reddit-like row (8 x 16);
+* dropout: the kernel's mask is the host hash (gat_dropout_mask), so the
+  fused output equals the composition over that mask bit for bit, keeps
+  about 1 - p of the pairs, and a fresh device counter draws a fresh mask;
+* configs[2] at full size (Pubmed, 8 heads, -m gpu): per epoch, from the same
+  parameters, the fused model's logits and gradients equal the three-kernel
+  model's bit for bit and the reference UDF formulation's
+  (examples/pytorch/gat/train.py:61-96) within 1e-5, dropout 0.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import dgl
+from conftest import load_example
+from dgl import kernel
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+SHAPES = [(8, 8), (8, 3), (8, 16), (1, 128), (4, 32), (2, 5), (16, 4)]
+
+
+def _dev(device):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device(device)
+
+
+def _graph(n=3000, m=40000, seed=0):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, m)
+    # a few hub destinations: rows longer than one batch of slots in flight
+    dst = np.where(rng.random(m) < 0.1, rng.integers(0, 5, m), rng.integers(0, n, m))
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+    g.add_edges(g.nodes(), g.nodes())
+    return g
+
+
+def _inputs(n, H, D, dev, seed=1):
+    gen = torch.Generator().manual_seed(seed)
+    ft = torch.randn(n, H, D, generator=gen).to(dev).requires_grad_(True)
+    el = torch.randn(n, H, generator=gen).to(dev).requires_grad_(True)
+    er = torch.randn(n, H, generator=gen).to(dev).requires_grad_(True)
+    return ft, el, er
+
+
+def _unfused(adj, ft, el, er, alpha, clamp, E, keep=None, p=0.0):
+    a = kernel.edge_attention(adj, el, er, E, alpha, clamp=clamp, edge_order="slot")
+    w = a if keep is None else torch.where(keep, a * (1.0 / (1.0 - p)), torch.zeros_like(a))
+    fs = kernel.gspmm(adj, "u_mul_e", "sum", ft, w.unsqueeze(-1), edge_order="slot")
+    z = kernel.gspmm(adj, "copy_e", "sum", None, a.unsqueeze(-1), edge_order="slot")
+    return fs, z
+
+
+def _grads(outs, ins, seed=2):
+    gen = torch.Generator().manual_seed(seed)
+    loss = sum((o * torch.randn(o.shape, generator=gen).to(o.device)).sum() for o in outs)
+    return torch.autograd.grad(loss, ins)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("H,D", SHAPES)
+@pytest.mark.parametrize("clamp", [(-10.0, 10.0), (-float("inf"), float("inf"))])
+def test_fused_equals_three_kernels(device, H, D, clamp):
+    dev = _dev(device)
+    g = _graph()
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(g.number_of_nodes(), H, D, dev)
+    fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, clamp=clamp)
+    fs2, z2 = _unfused(adj, ft, el, er, 0.2, clamp, g.number_of_edges())
+    assert fs.shape == (g.number_of_nodes(), H, D) and z.shape == (g.number_of_nodes(), H, 1)
+    assert torch.equal(fs, fs2) and torch.equal(z, z2)
+    for a, b in zip(_grads((fs, z), (ft, el, er)), _grads((fs2, z2), (ft, el, er))):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_fused_no_grad_and_partial_grads(device):
+    dev = _dev(device)
+    g = _graph(n=500, m=5000)
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(g.number_of_nodes(), 8, 8, dev)
+    with torch.no_grad():
+        fs, z = kernel.gat_aggregate(adj, ft, el, er)
+    fs2, z2 = _unfused(adj, ft, el, er, 0.2, (-10.0, 10.0), g.number_of_edges())
+    assert torch.equal(fs, fs2) and torch.equal(z, z2.detach())
+    # only z used downstream, only ft requiring grad
+    ft2 = ft.detach().requires_grad_(True)
+    fs, z = kernel.gat_aggregate(adj, ft2, el.detach(), er.detach())
+    (d,) = torch.autograd.grad(fs.sum(), ft2)
+    fs3, _ = _unfused(adj, ft2, el.detach(), er.detach(), 0.2, (-10.0, 10.0),
+                      g.number_of_edges())
+    (d3,) = torch.autograd.grad(fs3.sum(), ft2)
+    assert torch.equal(d, d3)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("p", [0.1, 0.6])
+def test_dropout_mask_is_the_host_hash(device, p):
+    dev = _dev(device)
+    g = _graph()
+    adj = g.sparse_adjacency(dev)
+    H, D, E = 8, 8, g.number_of_edges()
+    ft, el, er = _inputs(g.number_of_nodes(), H, D, dev)
+    seed = 12345
+    fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, attn_drop=p, seed=seed)
+    keep = kernel.gat_dropout_mask(E, H, p, seed).to(dev)
+    assert abs(float(keep.float().mean()) - (1 - p)) < 0.01
+    fs2, z2 = _unfused(adj, ft, el, er, 0.2, (-10.0, 10.0), E, keep=keep, p=p)
+    assert torch.equal(fs, fs2) and torch.equal(z, z2)
+    for a, b in zip(_grads((fs, z), (ft, el, er)), _grads((fs2, z2), (ft, el, er))):
+        assert torch.equal(a, b)
+    # eval mode: no dropout
+    fs3, _ = kernel.gat_aggregate(adj, ft, el, er, 0.2, attn_drop=p, training=False)
+    fs4, _ = _unfused(adj, ft, el, er, 0.2, (-10.0, 10.0), E)
+    assert torch.equal(fs3, fs4)
+
+
+@pytest.mark.gpu
+def test_device_counter_draws_fresh_masks():
+    dev = _dev("cuda")
+    g = _graph(n=500, m=5000)
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(g.number_of_nodes(), 4, 8, dev)
+    with torch.no_grad():
+        a, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
+        b, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
+    assert not torch.equal(a, b)
+
+
+def test_bad_dropout_rejected():
+    g = _graph(n=50, m=200)
+    adj = g.sparse_adjacency("cpu")
+    ft, el, er = _inputs(g.number_of_nodes(), 2, 4, torch.device("cpu"))
+    with pytest.raises(dgl.DGLError):
+        kernel.gat_aggregate(adj, ft, el, er, attn_drop=1.0)
+
+
+# -- configs[2] at full size -------------------------------------------------
+gat_train = load_example("gat/train.py", "gat_train_fused")
+
+
+def _gat_model(data, g, dev, udf=False, unfused=False):
+    torch.manual_seed(0)
+    m = gat_train.GAT(g, 1, data.features.shape[1], 8, data.num_labels, [8, 8], F.elu,
+                      0.0, 0.0, 0.2, False, udf=udf, unfused=unfused)
+    return m.to(dev)
+
+
+def _step(model, data):
+    model.zero_grad(set_to_none=True)
+    logits = model(data.features)
+    loss = F.cross_entropy(logits[data.train_mask], data.labels[data.train_mask])
+    loss.backward()
+    return logits.detach(), [p.grad.detach().clone() for p in model.parameters()]
+
+
+@pytest.mark.gpu
+def test_gat_pubmed_fused_per_epoch_parity():
+    """BASELINE configs[2]: GAT, 8 heads, Pubmed shape (19,717 nodes, 88,651
+    edges + self-loops, 500 features, 3 classes). Five Adam epochs of the
+    fused model; at each, the three-kernel and UDF models take its parameters
+    and must give the same logits and gradients."""
+    dev = _dev("cuda")
+    data = gat_train.load_data("pubmed", seed=0, device=dev)
+    src, dst = data.graph
+    g = dgl.DGLGraph((src.cpu(), dst.cpu()))
+    g.add_edges(g.nodes(), g.nodes())
+    assert g.number_of_nodes() == 19717
+    fused = _gat_model(data, g, dev)
+    three = _gat_model(data, g, dev, unfused=True)
+    udf = _gat_model(data, g, dev, udf=True)
+    opt = torch.optim.Adam(fused.parameters(), lr=0.005, weight_decay=5e-4)
+    for epoch in range(5):
+        for other in (three, udf):
+            other.load_state_dict(copy.deepcopy(fused.state_dict()))
+        lf, gf = _step(fused, data)
+        lt, gt = _step(three, data)
+        lu, gu = _step(udf, data)
+        assert torch.equal(lf, lt), epoch
+        assert all(torch.equal(a, b) for a, b in zip(gf, gt)), epoch
+        torch.testing.assert_close(lf, lu, rtol=1e-5, atol=1e-5 * float(lu.abs().max()))
+        for a, b in zip(gf, gu):
+            torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-5 * float(b.abs().max()) + 1e-12)
+        opt.step()
