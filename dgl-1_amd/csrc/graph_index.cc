@@ -91,12 +91,71 @@ static int64_t first_invalid(int64_t n, Ok&& ok) {
   return bad.load() == n ? -1 : bad.load();
 }
 
+// Stable scatter of input entries into the CSR, parallel and O(n) reads in
+// total. The rows are split into `parts` nnz-balanced ranges and the input
+// into `parts` contiguous chunks. Pass 1: every chunk counts its entries per
+// range; pass 2: every chunk writes its entries' input positions into a
+// staging array grouped by (range, chunk) (offsets from a prefix sum in that
+// order); pass 3: every range places its staged entries, which are in input
+// order, row by row. So a row's slots keep input order whatever the thread
+// count, and each pass reads the input once (the earlier version had every
+// thread scan all n entries: n x threads reads).
+template <typename Pos>
+static void place_stable(int64_t n, const int64_t* row, const int64_t* col, const int64_t* id,
+                         const std::vector<int64_t>& bounds, CSR& c) {
+  const int parts = static_cast<int>(bounds.size()) - 1;
+  // range of each row: binary search over the (few) bounds
+  auto range_of = [&](int64_t r) {
+    return static_cast<int>(std::upper_bound(bounds.begin() + 1, bounds.end() - 1, r) -
+                            (bounds.begin() + 1));
+  };
+  std::vector<int64_t> cnt(static_cast<size_t>(parts) * parts, 0);  // [chunk][range]
+  auto chunk_beg = [&](int t) { return n * t / parts; };
+  parallel_for(parts, parts, [&](int64_t b, int64_t e, int) {
+    for (int64_t t = b; t < e; ++t) {
+      int64_t* ct = cnt.data() + t * parts;
+      for (int64_t i = chunk_beg(static_cast<int>(t)); i < chunk_beg(static_cast<int>(t) + 1); ++i)
+        ++ct[range_of(row[i])];
+    }
+  }, 2);
+  std::vector<int64_t> off(static_cast<size_t>(parts) * parts);  // (range, chunk) order
+  std::vector<int64_t> range_start(static_cast<size_t>(parts) + 1, n);
+  int64_t acc = 0;
+  for (int p = 0; p < parts; ++p) {
+    range_start[p] = acc;
+    for (int t = 0; t < parts; ++t) {
+      off[static_cast<size_t>(t) * parts + p] = acc;
+      acc += cnt[static_cast<size_t>(t) * parts + p];
+    }
+  }
+  std::vector<Pos> stage(static_cast<size_t>(n));
+  parallel_for(parts, parts, [&](int64_t b, int64_t e, int) {
+    for (int64_t t = b; t < e; ++t) {
+      int64_t* ot = off.data() + t * parts;
+      for (int64_t i = chunk_beg(static_cast<int>(t)); i < chunk_beg(static_cast<int>(t) + 1); ++i)
+        stage[ot[range_of(row[i])]++] = static_cast<Pos>(i);
+    }
+  }, 2);
+  parallel_for(parts, parts, [&](int64_t b, int64_t e, int) {
+    for (int64_t p = b; p < e; ++p) {
+      const int64_t r0 = bounds[p], r1 = bounds[p + 1];
+      if (r0 >= r1) continue;
+      id_vec pos(c.indptr.begin() + r0, c.indptr.begin() + r1);
+      for (int64_t s = range_start[p]; s < range_start[p + 1]; ++s) {
+        const int64_t i = static_cast<int64_t>(stage[s]);
+        const int64_t k = pos[row[i] - r0]++;
+        c.indices[k] = col[i];
+        c.eid[k] = id ? id[i] : i;
+      }
+    }
+  }, 2);
+}
+
 CSR build_csr(int64_t nrows, int64_t ncols, const int64_t* row, const int64_t* col,
               const int64_t* id, int64_t n, bool sort_cols) {
   // Stable counting sort by row. Degrees are counted with relaxed atomic adds;
-  // placement splits the rows into nnz-balanced ranges and every thread scans
-  // the entries in input order, placing only its own rows', so a row's slots
-  // keep input order whatever the thread count.
+  // placement (place_stable) splits the rows into nnz-balanced ranges, so a
+  // row's slots keep input order whatever the thread count.
   CSR c;
   const int64_t bad = first_invalid(n, [&](int64_t i) {
     return row[i] >= 0 && row[i] < nrows && col[i] >= 0 && col[i] < ncols;
@@ -119,20 +178,18 @@ CSR build_csr(int64_t nrows, int64_t ncols, const int64_t* row, const int64_t* c
                 c.indptr.begin() - 1;
     bounds[t] = std::max(bounds[t], bounds[t - 1]);
   }
-  parallel_for(parts, parts, [&](int64_t b, int64_t e, int) {
-    for (int64_t t = b; t < e; ++t) {
-      const int64_t r0 = bounds[t], r1 = bounds[t + 1];
-      if (r0 >= r1) continue;
-      id_vec pos(c.indptr.begin() + r0, c.indptr.begin() + r1);
-      for (int64_t i = 0; i < n; ++i) {
-        const int64_t r = row[i];
-        if (r < r0 || r >= r1) continue;
-        const int64_t k = pos[r - r0]++;
-        c.indices[k] = col[i];
-        c.eid[k] = id ? id[i] : i;
-      }
+  if (parts == 1) {
+    id_vec pos(c.indptr.begin(), c.indptr.end() - 1);
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t k = pos[row[i]]++;
+      c.indices[k] = col[i];
+      c.eid[k] = id ? id[i] : i;
     }
-  }, 2);
+  } else if (n <= int64_t(0xffffffff)) {
+    place_stable<uint32_t>(n, row, col, id, bounds, c);
+  } else {
+    place_stable<int64_t>(n, row, col, id, bounds, c);
+  }
   if (sort_cols) {
     parallel_for(nrows, num_threads(), [&](int64_t b, int64_t e, int) {
       std::vector<std::pair<int64_t, int64_t>> tmp;

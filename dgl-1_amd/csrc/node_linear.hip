@@ -363,12 +363,19 @@ struct Gate {
   int64_t nparts;  // set by the launch: waves of the grid
 };
 
+inline int64_t max_bwd_waves();
+
 template <int KT, int S1, int S2>
 void launch_bwd(int64_t n, const GradIn& g1, const GradIn& g2, float* dx, int64_t lddx,
                 Gate& gate, hipStream_t stream) {
   constexpr int lds = 4 * (S1 + S2) * (16 * KT + 16) * 4;
   const int64_t grid = persistent_blocks(n, lds);
   gate.nparts = grid * (nl_threads() / 64);
+  // every wave writes its column-sum partials: the grid must fit the
+  // workspace (sized by dglhip_node_linear_dgrad_workspace_floats) BEFORE the
+  // launch, whatever launch shape a tuning knob has set since the query
+  DGLHIP_CHECK(gate.part == nullptr || gate.nparts <= max_bwd_waves(),
+               "column-sum workspace too small for " << gate.nparts << " waves");
   hipLaunchKernelGGL((node_linear_bwd_kernel<KT, S1, S2>), dim3(grid), dim3(nl_threads()), 0,
                      stream, n, g1, g2, dx, lddx, gate.p, gate.ld, gate.part);
 }
@@ -536,7 +543,6 @@ int dglhip_node_linear_dgrad_device(int64_t num_rows, int64_t in_feats, int64_t 
   Gate gt{gate, ldg, colsum != nullptr ? workspace : nullptr, 0};
   if (in_feats == 64) dispatch_bwd<4>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
   else dispatch_bwd<8>(s1, s2, num_rows, g1, g2, dx, lddx, gt, stream);
-  DGLHIP_CHECK(gt.nparts <= max_bwd_waves(), "column-sum workspace too small");
   if (colsum != nullptr) {
     const int K = static_cast<int>(in_feats);
     hipLaunchKernelGGL(colsum_partials_kernel, dim3(K), dim3(256), 0, stream, gt.nparts, K,

@@ -15,8 +15,10 @@
 // exponentials, log) and the backward writes its gradient row back into the
 // tile, which then leaves with coalesced stores. The loss sum is per-lane,
 // then per workgroup in a fixed tree, then over the workgroups in index order
-// (deterministic). Rows whose label is outside [0, C) (PyTorch's ignore_index,
-// -100) contribute nothing.
+// (deterministic). Rows labelled -100 (PyTorch's ignore_index) contribute
+// nothing; any other label outside [0, C) is an error in PyTorch (an
+// exception, a device-side assert on the GPU): here it makes the loss NaN and
+// that row's gradient NaN, so a bad label set can never train silently.
 #include "../../include/dgl_hip.h"
 #include "common.h"
 #include "launch.h"
@@ -28,6 +30,7 @@ namespace dglhip {
 namespace {
 
 constexpr int kRows = 256;         // rows per tile = lanes per workgroup
+constexpr int64_t kIgnore = -100;  // PyTorch's default ignore_index
 constexpr int kMaxClasses = 64;
 constexpr int kMaxBlocks = 1024;   // workspace floats of the forward
 
@@ -143,6 +146,8 @@ __global__ __launch_bounds__(kRows) void xent_fwd_kernel(int64_t n, int C, int S
       row_lse(row, C, m, lse);
       const float nll = -((row[y] - m) - lse);
       acc += w != nullptr ? nll * wr : nll;
+    } else if (r < nrows && y != kIgnore) {
+      acc = __builtin_nanf("");  // out-of-range label: poison the loss
     }
   }
   // workgroup sum in a fixed tree
@@ -216,7 +221,8 @@ __global__ __launch_bounds__(kRows) void xent_bwd_kernel(int64_t n, int C, int S
           row[c] = c == y ? gp - gw : gp;
         }
       } else {
-        for (int c = 0; c < C; ++c) row[c] = 0.0f;
+        const float v = y == kIgnore ? 0.0f : __builtin_nanf("");
+        for (int c = 0; c < C; ++c) row[c] = v;
       }
     }
     __syncthreads();

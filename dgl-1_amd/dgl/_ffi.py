@@ -89,6 +89,7 @@ def _load():
         "dglhip_gsddmm_host": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                         _vp, _c_int]),
         "dglhip_timing_enable": (_c_int, [_c_int]),
+        "dglhip_gspmm_resident_waves": (_c_int, [_c_int, ctypes.POINTER(_c_i64)]),
         "dglhip_set_spmm_variant": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
         "dglhip_set_cache_policy": (_c_int, [_c_int]),
         "dglhip_set_sddmm_variant": (_c_int, [_c_int]),

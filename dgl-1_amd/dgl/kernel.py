@@ -50,33 +50,50 @@ _MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_
 _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 
 
-# Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device):
-#   "auto" : (default) rows longer than max(4096, nnz / 12000) slots are cut
-#            into chunks (CSR.split_plan sizes them to fill the chip), but only
-#            when the longest row is the launch's critical path: a row
-#            is one wave's sequential chain, the launch spreads its slots over
-#            ~7168 resident waves (256 CUs x 4 SIMDs x 7), and rows start
-#            longest-first, so a row longer than twice a wave's share
-#            (nnz / 3584 slots) outlasts the rest of the launch — and it must
-#            also be longer than 16,384 slots (~1.5 ms of chained gathers), below
-#            which the loss is bounded and every row stays one exact chain (a
-#            floor of 65,536 left the 60k-slot hub rows of RMAT-26's pipelined
-#            segments at 1/8 unsplit: 13.2 -> 24.3 ms per step, bench.py
-#            --emulate-world 8 --workload rmat).
+# Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device),
+# sized from the device: R = the headline kernel's resident waves
+# (dglhip_gspmm_resident_waves: compute units x waves per CU at its occupancy;
+# MI355X 256 x 28 = 7,168).
+#   "auto" : (default) a row is one wave's sequential chain, a launch spreads
+#            its slots over the R resident waves and rows start longest-first,
+#            so a row longer than twice a wave's share (nnz / (R / 2) slots)
+#            outlasts the rest of the launch. Only then — and only for rows
+#            longer than 16,384 slots (~1.5 ms of chained gathers), below which
+#            the loss is bounded and every row stays one exact chain — are the
+#            rows longer than max(4096, (7168 / 12000) x nnz / R) slots (nnz /
+#            12,000 on MI355X) cut into chunks, sized (CSR.split_plan) to spread
+#            their slots over 4R/7 waves (4,096 on MI355X). A floor of 65,536 left
+#            the 60k-slot hub rows of RMAT-26's pipelined segments at 1/8
+#            unsplit: 13.2 -> 24.3 ms per step (bench.py --emulate-world 8
+#            --workload rmat).
 #            RMAT-26 (max in-degree ~855k, 2.9x the share) is split: GraphSAGE-
 #            mean epoch 0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
 #            Reddit (max 21,657 <= 114.8M / 3584 = 32,045) is not, and stays
-#            bit-exact.
+#            bit-exact. A part with fewer resident waves has a longer share per
+#            wave and splits less.
 #   "off"  : every row is one sequential chain — bit-exact with the reference
 #            on every graph (the documented bit-exact switch)
 #   <int>  : explicit chunk length, applied whenever some row is longer
 _ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
-_CRITICAL_SHARE = 3584  # half the resident waves of a full-chip launch
+_REF_WAVES = 7168       # MI355X (and the host path, which never splits)
 _CRITICAL_MIN = 16384   # rows up to this length are never split by "auto"
-# chunk length of the split rows: their slots over this many waves (half the
-# chip's resident waves), chunks of at least _CHUNK_MIN slots
-_CHUNK_WAVES = 4096
+_CUT_NUM, _CUT_DEN = 7168, 12000  # cut rows longer than (7168/12000) of a wave's share
 _CHUNK_MIN = 1024
+_WAVES = {}
+
+
+def _resident_waves(device=None):
+    """R: the headline g-SpMM kernel's resident waves on ``device`` (queried
+    once per device from the library); _REF_WAVES for host / unknown devices."""
+    if device is None or torch.device(device).type != "cuda":
+        return _REF_WAVES
+    idx = torch.device(device).index
+    idx = torch.cuda.current_device() if idx is None else idx
+    if idx not in _WAVES:
+        w = ctypes.c_int64()
+        check_call(LIB.dglhip_gspmm_resident_waves(idx, ctypes.byref(w)))
+        _WAVES[idx] = int(w.value)
+    return _WAVES[idx]
 
 
 def set_row_split(policy):
@@ -87,13 +104,16 @@ def set_row_split(policy):
     return old
 
 
-def _split_threshold(csr):
+def _split_threshold(csr, waves=None):
+    """Rows longer than this many slots are chunked (0: none), for a launch
+    over ``csr`` on a part with ``waves`` resident waves (None: csr's device)."""
     pol = _ROW_SPLIT
     if pol in ("off", "0", "", "none", "None"):
         return 0
     if pol == "auto":
-        t = max(4096, csr.nnz // 12000)
-        return t if csr.max_degree > max(_CRITICAL_MIN, csr.nnz // _CRITICAL_SHARE) else 0
+        R = waves if waves is not None else _resident_waves(getattr(csr, "device", None))
+        t = max(4096, csr.nnz * _CUT_NUM // (_CUT_DEN * R))
+        return t if csr.max_degree > max(_CRITICAL_MIN, csr.nnz // (R // 2)) else 0
     t = int(pol)
     return t if csr.max_degree > t else 0
 
@@ -186,8 +206,8 @@ class CSR(object):
         dglhip_gspmm_chunked_device. ``skip_empty`` leaves rows without slots
         out of the light list (accumulating launches need not touch them).
         ``chunk`` None: enough chunks to spread the heavy rows' slots over
-        _CHUNK_WAVES waves (at least _CHUNK_MIN slots each, at most
-        ``threshold``). The chunk launch runs alone before the light rows, so
+        4R/7 waves (R = the device's resident waves; at least _CHUNK_MIN slots
+        each, at most ``threshold``). The chunk launch runs alone before the light rows, so
         it must fill the chip: with chunks of ``threshold`` slots RMAT-26's 27
         hub rows made 88 chunks, 88 waves chaining 89k gathers each for 6.6 ms
         of a 82 ms call."""
@@ -205,7 +225,8 @@ class CSR(object):
         heavy = order[heavy_mask]
         if chunk is None:
             heavy_slots = int(deg[heavy].sum())
-            chunk = min(threshold, max(_CHUNK_MIN, -(-heavy_slots // _CHUNK_WAVES)))
+            chunk_waves = _resident_waves(self.device) * 4 // 7  # 4,096 on MI355X
+            chunk = min(threshold, max(_CHUNK_MIN, -(-heavy_slots // chunk_waves)))
         threshold = int(chunk)  # the cut length below
         nchunks = (deg[heavy] + threshold - 1) // threshold
         ptr = np.concatenate([[0], np.cumsum(nchunks)]).astype(np.int64)
@@ -1156,6 +1177,13 @@ def _gat_seed_offset(dev):
     return base, off
 
 
+def gat_dropout_scale(p):
+    """The kept attention's scale 1 / (1 - p) as the fused kernel computes it
+    (float32 operands), so host compositions match its bits."""
+    one = np.float32(1.0)
+    return float(one / (one - np.float32(p)))
+
+
 def gat_dropout_mask(num_slots, num_heads, p, seed):
     """bool (num_slots, num_heads): the (slot, head) pairs the fused kernel
     keeps at dropout probability ``p`` under seed ``seed`` (its counter hash,
@@ -1209,7 +1237,7 @@ class _GATAggregate(torch.autograd.Function):
             w = None
             if p > 0:
                 keep = gat_dropout_mask(fwd.nnz, H, p, seed)
-                w = torch.where(keep, a * (1.0 / (1.0 - p)), torch.zeros_like(a))
+                w = torch.where(keep, a * gat_dropout_scale(p), torch.zeros_like(a))
             out_ft, _ = _run_gspmm(fwd, MSG_U_MUL_E, RED_SUM, ft2, w if p > 0 else a, H, F,
                                    False, emap=SLOT)
             out_z, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, a, H, H, False, emap=SLOT)
@@ -1237,7 +1265,7 @@ class _GATAggregate(torch.autograd.Function):
         if need_el or need_er:
             d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
             if w is not None:  # dropout's backward: the kept pairs, scaled
-                d_a = torch.where(w != 0, d_a * (1.0 / (1.0 - ctx.p)), torch.zeros_like(d_a))
+                d_a = torch.where(w != 0, d_a * gat_dropout_scale(ctx.p), torch.zeros_like(d_a))
             if d_z is not None:
                 d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
             # the attention's backward (_EdgeAttention.backward, slot order)

@@ -17,10 +17,12 @@ backward also returns that bias's gradient (dz's column sums) from the same
 kernel, read back from the tile it stores (no separate column reduce over
 the rows); when they are a sage_dense output whose mean aggregation added into
 them (kernel.gspmm_mean_add), also dz / deg in the padded rows that
-aggregation's backward gathers (no division pass). Other devices and shapes compute the expression above with PyTorch's own
-operators. Results agree with it to fp32 rounding (the sums associate
-differently); labels outside [0, C) contribute nothing (PyTorch's
-ignore_index = -100; other out-of-range labels are an error there).
+aggregation's backward gathers (no division pass). Other devices and shapes
+compute the expression above with PyTorch's own operators. Results agree with
+it to fp32 rounding (the sums associate differently). Rows labelled -100
+(PyTorch's ignore_index) contribute nothing; any other label outside [0, C)
+is an error in PyTorch, and makes the fused loss (and that row's gradient)
+NaN: never a silently different value.
 """
 import torch
 import torch.nn.functional as F
@@ -34,7 +36,7 @@ _MAX_CLASSES = 64
 
 def _fused_ok(z, y, w):
     return (z.is_cuda and z.dtype == torch.float32 and z.dim() == 2 and z.stride(1) == 1 and
-            1 <= z.shape[1] <= _MAX_CLASSES and y.dim() == 1 and y.shape[0] == z.shape[0] and
+            1 <= z.shape[1] <= _MAX_CLASSES and z.stride(0) >= z.shape[1] and y.dim() == 1 and y.shape[0] == z.shape[0] and
             y.dtype == torch.int64 and y.device == z.device and
             (w is None or (w.dim() == 1 and w.shape[0] == z.shape[0] and
                            w.dtype == torch.float32 and w.device == z.device)))

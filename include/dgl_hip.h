@@ -343,6 +343,12 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t efeat_len, float* out, int64_t* arg_out,
                       int num_threads);
 
+/* Resident waves of the headline g-SpMM kernel (F = 128 copy_u + sum) on
+ * `device`: compute units x the kernel's occupancy per CU (blocks of 4 waves).
+ * The heavy-row policy sizes its critical-path test and its chunk launches
+ * from it (dgl.kernel._resident_waves). MI355X: 256 CUs x 28 = 7168. */
+int dglhip_gspmm_resident_waves(int device, int64_t* waves);
+
 /* ------------------------------------------------------------------------ */
 /* g-SDDMM: per-edge products feeding the backward of u_mul_e and the GAT    */
 /* edge attention (gat/train.py:74-96).                                      */

@@ -53,7 +53,8 @@ def _inputs(n, H, D, dev, seed=1):
 
 def _unfused(adj, ft, el, er, alpha, clamp, E, keep=None, p=0.0):
     a = kernel.edge_attention(adj, el, er, E, alpha, clamp=clamp, edge_order="slot")
-    w = a if keep is None else torch.where(keep, a * (1.0 / (1.0 - p)), torch.zeros_like(a))
+    w = a if keep is None else torch.where(keep, a * kernel.gat_dropout_scale(p),
+                                           torch.zeros_like(a))
     fs = kernel.gspmm(adj, "u_mul_e", "sum", ft, w.unsqueeze(-1), edge_order="slot")
     z = kernel.gspmm(adj, "copy_e", "sum", None, a.unsqueeze(-1), edge_order="slot")
     return fs, z

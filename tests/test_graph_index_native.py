@@ -135,3 +135,23 @@ def test_bulk_construction_exports_without_permutation():
     g = dgl.DGLGraph((src, dst))
     assert torch.equal(g._graph.src(), src) and torch.equal(g._graph.dst(), dst)
     assert torch.equal(g.in_degrees(), torch.bincount(dst, minlength=n))
+
+
+@pytest.mark.parametrize("readonly", [False, True])
+def test_parallel_csr_build_is_stable(readonly):
+    """Past 2^20 edges the native CSR build places entries in parallel (rows in
+    nnz-balanced ranges, input in chunks staged per range: O(n) reads); a
+    row's slots must still come out in input (edge-id) order, or for the
+    immutable index in (neighbour, edge id) order, with hub rows that straddle
+    chunk boundaries."""
+    n, m = 20_000, 3_000_000
+    rng = np.random.default_rng(5)
+    src = rng.integers(0, n, m)
+    dst = np.where(rng.random(m) < 0.2, rng.integers(0, 3, m), rng.integers(0, n, m))
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)), readonly=readonly)
+    u, v, e = g.in_edges(g.nodes(), form="all")
+    u, v, e = u.numpy(), v.numpy(), e.numpy()
+    order = (np.lexsort((np.arange(m), src, dst)) if readonly
+             else np.lexsort((np.arange(m), dst)))
+    assert np.array_equal(v, dst[order]) and np.array_equal(u, src[order])
+    assert np.array_equal(src[e], u) and np.array_equal(dst[e], v)

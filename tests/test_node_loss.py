@@ -166,3 +166,41 @@ def test_output_bias_grad_from_loss_kernel(narrow, monkeypatch):
     assert torch.allclose(db.double(), ref, atol=1e-6, rtol=1e-5)
     assert torch.allclose(dw.double(), z64.grad.t().matmul(x.double()), atol=1e-4, rtol=1e-4)
     assert dx is not None and bool(torch.isfinite(dx).all())
+
+
+@pytest.mark.gpu
+def test_out_of_range_labels_are_loud():
+    """-100 rows are ignored as PyTorch ignores them; any other label outside
+    [0, C) (an error in PyTorch) makes the fused loss and that row's gradient
+    NaN instead of contributing nothing."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    z, y, w = _case(1000, 7, dev, ignore=50)
+    z = z.requires_grad_(True)
+    loss = weighted_cross_entropy(z, y, w)
+    ref, _ = _ref(z, y, w)
+    assert torch.isfinite(loss) and abs(float(loss) - float(ref)) <= 1e-5 * abs(float(ref))
+    for bad in (7, -1, 1 << 40):
+        yb = y.clone()
+        yb[123] = bad
+        zb = z.detach().clone().requires_grad_(True)
+        lb = weighted_cross_entropy(zb, yb, None)
+        assert torch.isnan(lb)
+        lb.backward()
+        assert torch.isnan(zb.grad[123]).all() and torch.isfinite(zb.grad[:123]).all()
+
+
+@pytest.mark.gpu
+def test_overlapping_rows_take_the_torch_path():
+    """A view whose rows overlap (row stride below the class count) is not
+    handed to the kernel; the result is PyTorch's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    base = torch.randn(4000, device=dev)
+    z = base.as_strided((1000, 8), (3, 1))
+    y = torch.randint(0, 8, (1000,), device=dev)
+    loss = weighted_cross_entropy(z, y)
+    ref = F.cross_entropy(z, y, reduction="none").sum()
+    assert torch.allclose(loss, ref, rtol=1e-6)
