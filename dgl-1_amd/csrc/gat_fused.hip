@@ -49,10 +49,31 @@ __host__ __device__ __forceinline__ bool gat_keep(uint64_t seed, int64_t idx, ui
   return r >= thr;
 }
 
+// study knob (dglhip_set_gat_variant): 0 automatic, 1 the per-lane kernel,
+// 2 the LDS-shared attention kernel (head counts 1, 2, 4, 8, 16)
+int g_gat_variant = 0;
+
 // keep iff hash >= threshold: P(keep) = 1 - p
 static inline uint32_t gat_drop_threshold(float p) {
   const double t = static_cast<double>(p) * 4294967296.0;
   return t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
+}
+
+// One row of VEC floats per lane through a buffer descriptor built from the
+// wave-uniform row address: a 32-bit per-lane byte offset instead of a 64-bit
+// address per gather (16 gathers in flight share one offset register).
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T gather_rsrc(const float* row, int64_t F,
+                                                            uint32_t voff) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(row), 0, static_cast<int>(F * sizeof(float)), 0x00020000);
+  if (VEC == 2) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, voff, 0, 0);
+    return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
+  }
+  const unsigned int w = __builtin_amdgcn_raw_buffer_load_b32(r, voff, 0, 0);
+  return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
 }
 
 template <int VEC, int UNROLL, bool DROP>
@@ -76,6 +97,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
   for (int64_t f0 = int64_t(lane) * VEC; f0 < F; f0 += 64 * VEC) {
     const int64_t h = f0 / D;
     const bool head_lane = f0 - h * D == 0;  // first lane of head h in this pass
+    const uint32_t voff = static_cast<uint32_t>(f0 * int64_t(sizeof(float)));
     const float r = er[row * H + h];
     V acc = Vec<VEC>::zero();
     float zacc = 0.0f;
@@ -104,7 +126,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
       for (int j = 0; j < UNROLL; ++j) {
         const int64_t src = indices[k + j];
         l[j] = el[src * H + h];
-        u[j] = ldv<VEC>(ft + src * F + f0);
+        u[j] = gather_rsrc<VEC>(ft + src * F, F, voff);
       }
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j) consume(k + j, l[j], u[j]);
@@ -118,7 +140,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
         if (j < rem) {
           const int64_t src = indices[k + j];
           l[j] = el[src * H + h];
-          u[j] = ldv<VEC>(ft + src * F + f0);
+          u[j] = gather_rsrc<VEC>(ft + src * F, F, voff);
         }
       }
 #pragma unroll
@@ -127,6 +149,136 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
     }
     stv<VEC>(out_ft + row * F + f0, acc);
     if (head_lane) out_z[row * H + h] = zacc;
+  }
+}
+
+// The same operation for H in {1, 2, 4, 8, 16}, with each (slot, head)
+// attention computed ONCE per batch instead of once per lane: a batch is U
+// slots; its U x H (slot, head) pairs are spread over the wave (lane l takes
+// head l % H of slots l / H, l / H + 64 / H, ...), each computed value goes to
+// the wave's LDS row of its head, and every lane then reads the U values of
+// its own head back (lanes of a head read the same words: broadcast). The
+// gathers of the batch's feature rows are issued before the attention is
+// computed, so the exp work overlaps their latency. gat_aggregate_kernel ran
+// the exp, the clamp and a 4-B logit gather per lane and slot (8x redundant
+// at 8 heads of 16 features). Same per-element arithmetic and chain order.
+// One batch of the LDS kernel: slots [k, k + nb) of the row (FULL: nb == U,
+// no predication; the row's last partial batch runs with FULL = false, as
+// reduce_range's predicated tail).
+template <int H, int VEC, bool DROP, bool FULL>
+__device__ __forceinline__ void gat_batch(
+    int64_t k, int nb, int64_t F, uint32_t voff, int64_t h, int hc, int jc, float rc,
+    const int32_t* __restrict__ indices, const float* __restrict__ el,
+    const float* __restrict__ ft, float alpha, float lo, float hi, int apply_exp,
+    uint64_t seed, uint32_t thr, float scale, float* la, float* lw, float* __restrict__ a_out,
+    float* __restrict__ w_out, typename Vec<VEC>::T& acc, float& zacc) {
+  typedef typename Vec<VEC>::T V;
+  constexpr int U = 16;
+  constexpr int SPP = 64 / H;               // slots covered per pass of the wave
+  constexpr int PPL = (U + SPP - 1) / SPP;  // attention values per lane per batch
+#pragma unroll
+  for (int i = 0; i < PPL; ++i) {
+    const int j = jc + SPP * i;
+    if ((SPP * PPL == U || j < U) && (FULL || j < nb)) {
+      const int64_t src = indices[k + j];
+      float x = el[src * H + hc] + rc;
+      x = x > 0.0f ? x : alpha * x;
+      if (apply_exp) x = __expf(x);
+      const float a = fminf(fmaxf(x, lo), hi);
+      la[hc * U + j] = a;
+      if (a_out) a_out[(k + j) * H + hc] = a;
+      if (DROP) {
+        const float w = gat_keep(seed, (k + j) * H + hc, thr) ? a * scale : 0.0f;
+        lw[hc * U + j] = w;
+        if (a_out) w_out[(k + j) * H + hc] = w;
+      }
+    }
+  }
+  // the batch's feature-row gathers (column ids through the scalar cache),
+  // issued after the attention so that its few registers and the 16 rows in
+  // flight are never live together (7 waves per SIMD); the other waves of the
+  // SIMD hide the logit gathers' latency
+  // row base from the scalar slot stream (SGPRs) + the lane's 32-bit byte
+  // offset: the saddr load form, one offset VGPR for all 16 gathers instead
+  // of a 64-bit address per gather (80 -> fewer VGPRs, more waves per SIMD)
+  V u[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (FULL || j < nb) u[j] = gather_rsrc<VEC>(ft + int64_t(indices[k + j]) * F, F, voff);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the head's values four at a time (one 16-B LDS read), consumed in slot order
+#pragma unroll
+  for (int q = 0; q < U / 4; ++q) {
+    const f32x4 t = *reinterpret_cast<const f32x4*>(la + h * U + 4 * q);
+    const float av[4] = {t.x, t.y, t.z, t.w};
+    f32x4 t2 = t;
+    if (DROP) t2 = *reinterpret_cast<const f32x4*>(lw + h * U + 4 * q);
+    const float wv[4] = {t2.x, t2.y, t2.z, t2.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int j = 4 * q + i;
+      if (FULL || j < nb) {
+        acc = Vec<VEC>::fma(Vec<VEC>::splat(wv[i]), u[j], acc);
+        zacc += av[i];
+      }
+    }
+  }
+  // the next batch overwrites the rows only after every lane has read them
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int H, int VEC, bool DROP>
+__global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
+    int64_t num_rows, int64_t D, const int64_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
+    const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
+    float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
+    const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
+    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out) {
+  typedef typename Vec<VEC>::T V;
+  constexpr int U = 16;
+  __shared__ float s_a[4][H * U];
+  __shared__ float s_w[4][DROP ? H * U : 1];
+  const int lane = threadIdx.x & 63;
+  const int wi = threadIdx.x >> 6;
+  const int64_t it = block_linear() * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_rows) return;
+  int64_t row = row_order ? row_order[it] : it;
+  row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int64_t F = H * D;
+  const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
+  // the pairs this lane computes: head hc of slots jc + (64 / H) * i
+  const int hc = lane % H, jc = lane / H;
+  const float rc = er[row * H + hc];
+  for (int64_t base = 0; base < F; base += 64 * VEC) {
+    // every lane takes part in the attention of each pass; lanes past F
+    // gather a valid row (feature 0) and store nothing
+    const int64_t f0 = base + int64_t(lane) * VEC;
+    const bool active = f0 < F;
+    const int64_t fa = active ? f0 : 0;
+    const int64_t h = fa / D;
+    const uint32_t voff = static_cast<uint32_t>(fa * int64_t(sizeof(float)));
+    V acc = Vec<VEC>::zero();
+    float zacc = 0.0f;
+    int64_t k = beg;
+    for (; k + U <= end; k += U)
+      gat_batch<H, VEC, DROP, true>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, alpha, lo, hi,
+                                    apply_exp, seed, thr, scale, s_a[wi], s_w[wi], a_out, w_out,
+                                    acc, zacc);
+    if (k < end)
+      gat_batch<H, VEC, DROP, false>(k, static_cast<int>(end - k), F, voff, h, hc, jc, rc, indices,
+                                     el, ft, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
+                                     s_w[wi], a_out, w_out, acc, zacc);
+    if (active) {
+      stv<VEC>(out_ft + row * F + f0, acc);
+      if (f0 - h * D == 0) out_z[row * H + h] = zacc;
+    }
   }
 }
 
@@ -161,6 +313,33 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
   const bool v2 = head_dim % 2 == 0 && F >= 128 &&
                   reinterpret_cast<uintptr_t>(ft) % 8 == 0 &&
                   reinterpret_cast<uintptr_t>(out_ft) % 8 == 0;
+  // per-(slot, head) attention through LDS for the common head counts on
+  // one-float lanes (rows of <= 64 floats or odd head widths: Pubmed's 8 x 8
+  // and 8 x 3, 0.015 vs 0.023 ms); two-float lanes (8 x 16 on the
+  // Reddit-shaped graph) run the per-lane kernel, 9.37 vs 9.87 ms
+  // (tools/gat_bench.py). Both are bound by the line rate: per slot the
+  // feature row's lines plus one line for the source's H logits.
+  const bool lds_heads = num_heads == 1 || num_heads == 2 || num_heads == 4 ||
+                         num_heads == 8 || num_heads == 16;
+  if (lds_heads && (g_gat_variant == 2 || (g_gat_variant == 0 && !v2))) {
+    timed_launch(stream, [&] {
+#define DGLHIP_GATL(HH, VV, DD)                                                            \
+  hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD>), grid_1d(blocks), dim3(256), 0, \
+                     stream, num_rows, head_dim, indptr, indices, row_order, el, er, ft,     \
+                     alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale,    \
+                     out_ft, out_z, attn_out, attn_drop_out)
+#define DGLHIP_GATH(HH)                                                                    \
+  if (num_heads == HH) {                                                                   \
+    if (v2) { if (drop) DGLHIP_GATL(HH, 2, true); else DGLHIP_GATL(HH, 2, false); }         \
+    else { if (drop) DGLHIP_GATL(HH, 1, true); else DGLHIP_GATL(HH, 1, false); }            \
+    return;                                                                                \
+  }
+      DGLHIP_GATH(1) DGLHIP_GATH(2) DGLHIP_GATH(4) DGLHIP_GATH(8) DGLHIP_GATH(16)
+#undef DGLHIP_GATH
+#undef DGLHIP_GATL
+    });
+    return 0;
+  }
   timed_launch(stream, [&] {
 #define DGLHIP_GAT(VV, DD)                                                                 \
   hipLaunchKernelGGL((gat_aggregate_kernel<VV, 16, DD>), grid_1d(blocks), dim3(256), 0,    \
@@ -174,6 +353,13 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
     }
 #undef DGLHIP_GAT
   });
+  API_END();
+}
+
+int dglhip_set_gat_variant(int variant) {
+  API_BEGIN();
+  DGLHIP_CHECK(variant >= 0 && variant <= 2, "unknown GAT kernel variant " << variant);
+  g_gat_variant = variant;
   API_END();
 }
 

@@ -25,15 +25,43 @@
 
 namespace dglhip {
 
+// GAT attention-gradient epilogue of the SDDMM dot (EPI = true): the dot
+// d_w[k, h] = <dC[row, h, :], ft[u, h, :]> becomes the gradient of the
+// attention's pre-activation, stored in slot order:
+//   t = d_w; t = keep ? t * scale : 0 (dropout: keep = w[k, h] != 0);
+//   t = t + dz[row, h] (the normaliser's gradient);
+//   g = (t * a) * (a < 1 ? alpha : 1) (exp; else t * (a < 0 ? alpha : 1));
+//   g = lo < a < hi ? g : 0
+// the float operations, and their order, of kernel._GATAggregate's torch
+// backward, so both give the same bits.
+struct GatEpi {
+  const float* a;     // attention, [nnz, H] slot order
+  const float* w;     // its dropped copy (NULL: no dropout)
+  const float* dz;    // normaliser gradient, [rows, H] (NULL: zero)
+  float alpha, lo, hi, scale;
+  int apply_exp;
+};
+
+__device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, int64_t H,
+                                         int64_t h, int64_t row) {
+  const float a = e.a[k * H + h];
+  if (e.w) t = e.w[k * H + h] != 0.0f ? t * e.scale : 0.0f;
+  if (e.dz) t = t + e.dz[row * H + h];
+  const float g = e.apply_exp ? (t * a) * (a < 1.0f ? e.alpha : 1.0f)
+                              : t * (a < 0.0f ? e.alpha : 1.0f);
+  return (a > e.lo && a < e.hi) ? g : 0.0f;
+}
+
 // SDDMM dot: one wave per row. One head (H == 1): per slot a wave-wide fma
 // dot product of two feature rows reduced in a fixed butterfly order. Several
 // heads: lane h computes head h's dot over its D = F / H features as one
 // sequential fma chain. Both orders are fixed, so results are deterministic.
+template <bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
     int64_t num_rows, int64_t F, int64_t H, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs,
-    float* __restrict__ out) {
+    float* __restrict__ out, GatEpi epi) {
   const int64_t wave = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (wave >= num_rows) return;
   const int lane = threadIdx.x & 63;
@@ -46,12 +74,12 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
       for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) out[eid ? eid[k] : k] = acc;
+      if (lane == 0) out[eid ? eid[k] : k] = EPI ? gat_epi(epi, acc, k, 1, 0, wave) : acc;
     } else {
       for (int64_t h = lane; h < H; h += 64) {
         float acc = 0.0f;
         for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);
-        out[(eid ? eid[k] : k) * H + h] = acc;
+        out[(eid ? eid[k] : k) * H + h] = EPI ? gat_epi(epi, acc, k, H, h, wave) : acc;
       }
     }
   }
@@ -128,11 +156,12 @@ __device__ __forceinline__ void slot_reduce_scatter(float* q, int j) {
 //     of the slot's heads (8 heads at D = 16: one 32-B run per slot).
 // The pairing of lanes is the full xor butterfly's (4, 2, 1 / 2, 1 / 1), so
 // results are deterministic and equal the butterfly's bits.
-template <int NB, int UNROLL, int H>
+template <int NB, int UNROLL, int H, bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
     int64_t num_rows, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
-    const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out) {
+    const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out,
+    GatEpi epi) {
   constexpr int F = NB * 32;
   constexpr int D = F / H;
   constexpr int LPH = D >= 32 ? 8 : D / 4;  // lanes sharing a head
@@ -181,11 +210,15 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
         slot_reduce_scatter<H, 8>(q, j);
         if (H >= 8) {
 #pragma unroll
-          for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t)
-            if (k < end) out[obase + j * (H / 8) + t] = q[t];
+          for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t) {
+            const int hh = j * (H / 8) + t;
+            if (k < end) out[obase + hh] = EPI ? gat_epi(epi, q[t], k, H, hh, row) : q[t];
+          }
         } else {
           constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
-          if (k < end && j % DUP == 0) out[obase + j / DUP] = q[0];
+          const int hh = j / DUP;
+          if (k < end && j % DUP == 0)
+            out[obase + hh] = EPI ? gat_epi(epi, q[0], k, H, hh, row) : q[0];
         }
       } else {
         constexpr int HPB = 8 / LPH;
@@ -193,11 +226,15 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
         slot_reduce_scatter<NB, LPH>(p, j);
         if (NB >= LPH) {
 #pragma unroll
-          for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t)
-            if (k < end) out[obase + (r * (NB / LPH) + t) * HPB + g] = p[t];
+          for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t) {
+            const int hh = (r * (NB / LPH) + t) * HPB + g;
+            if (k < end) out[obase + hh] = EPI ? gat_epi(epi, p[t], k, H, hh, row) : p[t];
+          }
         } else {
           constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
-          if (k < end && r % DUP == 0) out[obase + (r / DUP) * HPB + g] = p[0];
+          const int hh = (r / DUP) * HPB + g;
+          if (k < end && r % DUP == 0)
+            out[obase + hh] = EPI ? gat_epi(epi, p[0], k, H, hh, row) : p[0];
         }
       }
     }
@@ -485,18 +522,17 @@ int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
   API_END();
 }
 
-int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
-                         int64_t num_heads, const int64_t* indptr, const int32_t* indices,
-                         const int64_t* eid, const float* lhs,
-                         const float* rhs, float* out, void* stream_) {
-  API_BEGIN();
-  hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
-  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
-  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
-               "num_heads " << num_heads << " must divide feat_len " << feat_len);
-  if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
+}  // extern "C"
+
+namespace dglhip {
+
+// The SDDMM dot launch for one shape (the sliced kernel where it applies, the
+// generic one otherwise); EPI adds the GAT attention-gradient epilogue.
+template <bool EPI>
+static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_heads,
+                             const int64_t* indptr, const int32_t* indices, const int64_t* eid,
+                             const float* lhs, const float* rhs, float* out, const GatEpi& epi,
+                             hipStream_t stream) {
   const int64_t blocks = (num_rows + 3) / 4;
   DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large: " << blocks);
   const int64_t D = feat_len / num_heads;
@@ -508,8 +544,8 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                                              nb == 16);
   timed_launch(stream, [&] {
 #define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
-  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH>), grid_1d(blocks), dim3(256), 0, \
-                     stream, num_rows, indptr, indices, eid, lhs, rhs, out)
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI>), grid_1d(blocks), dim3(256), \
+                     0, stream, num_rows, indptr, indices, eid, lhs, rhs, out, epi)
 #define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
   if (num_heads == HH) {                                                                   \
     if (!g_sddmm_alt) DGLHIP_SDDMM_K(NB, U, HH);                                          \
@@ -538,11 +574,50 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
       DGLHIP_SDDMM_H(16, 1, 8) DGLHIP_SDDMM_H(16, 1, 16) DGLHIP_SDDMM_H(16, 1, 32)
       DGLHIP_SDDMM_H(16, 1, 64) DGLHIP_SDDMM_H(16, 1, 128)
     }
-    hipLaunchKernelGGL(gsddmm_dot_kernel, grid_1d(blocks), dim3(256), 0, stream, num_rows,
-                       feat_len, num_heads, indptr, indices, eid, lhs, rhs, out);
+    hipLaunchKernelGGL((gsddmm_dot_kernel<EPI>), grid_1d(blocks), dim3(256), 0, stream,
+                       num_rows, feat_len, num_heads, indptr, indices, eid, lhs, rhs, out, epi);
 #undef DGLHIP_SDDMM_K
 #undef DGLHIP_SDDMM_H
   });
+}
+
+}  // namespace dglhip
+
+extern "C" {
+
+int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
+                         int64_t num_heads, const int64_t* indptr, const int32_t* indices,
+                         const int64_t* eid, const float* lhs,
+                         const float* rhs, float* out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
+  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indices, eid, lhs, rhs, out,
+                          GatEpi{}, stream);
+  API_END();
+}
+
+int dglhip_gat_attention_grad_device(int64_t num_rows, int64_t feat_len, int64_t num_heads,
+                                     const int64_t* indptr, const int32_t* indices,
+                                     const float* dout, const float* ft, const float* attn,
+                                     const float* attn_drop, const float* dz, float alpha,
+                                     float clamp_lo, float clamp_hi, int apply_exp,
+                                     float drop_scale, float* grad, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && dout && ft && attn && grad, "null pointer argument");
+  const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp};
+  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, indptr, indices, nullptr, dout, ft,
+                         grad, epi, stream);
   API_END();
 }
 

@@ -1177,6 +1177,13 @@ def _gat_seed_offset(dev):
     return base, off
 
 
+def set_gat_variant(variant):
+    """Study knob for the fused GAT kernel: 0 automatic (default), 1 the
+    attention computed in every lane that consumes it, 2 once per (slot,
+    head) through LDS (1/2/4/8/16 heads). Same bits."""
+    check_call(LIB.dglhip_set_gat_variant(int(variant)))
+
+
 def gat_dropout_scale(p):
     """The kept attention's scale 1 / (1 - p) as the fused kernel computes it
     (float32 operands), so host compositions match its bits."""
@@ -1263,20 +1270,33 @@ class _GATAggregate(torch.autograd.Function):
             d_ft2, _ = _run_gspmm(adj.bwd, MSG_U_MUL_E, RED_SUM, d_ft, wt, H, F, False,
                                   emap=_fwd_slot_of_bwd(adj))
         if need_el or need_er:
-            d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
-            if w is not None:  # dropout's backward: the kept pairs, scaled
-                d_a = torch.where(w != 0, d_a * gat_dropout_scale(ctx.p), torch.zeros_like(d_a))
-            if d_z is not None:
-                d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
-            # the attention's backward (_EdgeAttention.backward, slot order)
-            inside = (a > ctx.lo) & (a < ctx.hi)
-            if ctx.apply_exp:
-                slope = torch.where(a < 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
-                g = d_a * a * slope
+            scale = gat_dropout_scale(ctx.p) if w is not None else 1.0
+            if ft2.is_cuda:
+                # the dot, dropout, normaliser and activation gradients in one
+                # pass (the g-SDDMM dot with the GAT epilogue): the torch ops
+                # below, fused, same bits
+                g = torch.empty_like(a)
+                dz = None if d_z is None else d_z.contiguous()
+                check_call(LIB.dglhip_gat_attention_grad_device(
+                    fwd.num_rows, F, H, ptr(fwd.indptr), ptr(fwd.indices), ptr(d_ft),
+                    ptr(ft2.contiguous()), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
+                    float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
+                    ptr(g), _stream_of(ft2.device)))
             else:
-                slope = torch.where(a < 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
-                g = d_a * slope
-            g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
+                d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
+                if w is not None:  # dropout's backward: the kept pairs, scaled
+                    d_a = torch.where(w != 0, d_a * scale, torch.zeros_like(d_a))
+                if d_z is not None:
+                    d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
+                # the attention's backward (_EdgeAttention.backward, slot order)
+                inside = (a > ctx.lo) & (a < ctx.hi)
+                if ctx.apply_exp:
+                    slope = torch.where(a < 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                    g = d_a * a * slope
+                else:
+                    slope = torch.where(a < 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                    g = d_a * slope
+                g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
             if need_el:
                 d_el, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
                                      emap=_fwd_slot_of_bwd(adj))

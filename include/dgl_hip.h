@@ -369,6 +369,22 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
                        const float* lhs, const float* rhs, float* out,
                        int num_threads);
 
+/* GAT attention gradient (the backward of dglhip_gat_aggregate_device with
+ * respect to the attention's pre-activation), in CSR slot order, one pass:
+ *   t = DOT(dout[r, h], ft[indices[k], h])   (the g-SDDMM dot above, same bits)
+ *   t = attn_drop ? (attn_drop[k, h] != 0 ? t * drop_scale : 0) : t
+ *   t = dz ? t + dz[r, h] : t                (the normaliser's gradient)
+ *   grad[k, h] = lo < a < hi ? (apply_exp ? (t * a) * s : t * s) : 0,
+ *   a = attn[k, h], s = alpha where a < 1 (exp) / a < 0, else 1
+ * attn, attn_drop, grad: [nnz, H] slot order; dout: [num_rows, F]; ft:
+ * [num_src, F]; dz: [num_rows, H] or NULL; attn_drop NULL without dropout. */
+int dglhip_gat_attention_grad_device(int64_t num_rows, int64_t feat_len, int64_t num_heads,
+                                     const int64_t* indptr, const int32_t* indices,
+                                     const float* dout, const float* ft, const float* attn,
+                                     const float* attn_drop, const float* dz, float alpha,
+                                     float clamp_lo, float clamp_hi, int apply_exp,
+                                     float drop_scale, float* grad, void* stream);
+
 /* Study knob: 1 = the sliced g-SDDMM dot runs at its alternative depth of
  * slots in flight (16 <-> 32, or 8 -> 16 for F >= 256), 0 = the default. */
 int dglhip_set_sddmm_variant(int alternate);
@@ -414,6 +430,11 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
                                 int apply_exp, float drop_p, uint64_t seed,
                                 const int64_t* seed_offset, float* out_ft, float* out_z,
                                 float* attn_out, float* attn_drop_out, void* stream);
+
+/* Study knob for dglhip_gat_aggregate_device: 0 (default) automatic; 1 = the
+ * attention computed in every lane that consumes it; 2 = once per (slot,
+ * head), shared through LDS (H in {1, 2, 4, 8, 16}). Same bits. */
+int dglhip_set_gat_variant(int variant);
 
 /* The attention-dropout mask of dglhip_gat_aggregate_device: keep[i] = 1 for
  * the kept (slot, head) pairs i = k * H + h, a stateless hash of (seed, i). */

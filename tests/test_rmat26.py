@@ -15,7 +15,11 @@
   (the summation error bound's own yardstick).
 * A 2-layer GraphSAGE-mean (in 128 -> hidden 128 -> 41 classes), forward +
   backward through the mean g-SpMM and its transposed backward on the same
-  graph: finite loss and gradients; the step time is written to
+  graph, with the edge lists and the sum test's features released first and
+  the transposed CSR built then (peak HBM of the step asserted <= 240 GB of
+  the 288): the first layer's aggregated rows (every chunked hub row and 2,000
+  random rows) within 1e-5 of the oracle's mean of the same input rows;
+  finite loss and gradients; the step time and peak go to
   gpurun_out/graphsage_rmat26_test.json.
 
 The reference path this replaces for mean is the degree-bucketing UDF
@@ -48,7 +52,6 @@ def rmat():
     t0 = time.time()
     src, dst, n = data.rmat(SCALE, 16, seed=0, device=dev)
     adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
-    adj.bwd  # the transposed CSR (GraphSAGE backward) while HBM is still free
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
     h = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
@@ -73,9 +76,10 @@ def _sample(rmat, threshold):
     return rows, deg[rows] > threshold, deg
 
 
-def _sub_csr(rmat, rows):
+def _sub_csr(rmat, rows, feats=None):
     """Slots of ``rows`` from the device CSR, checked against the edge list;
-    returns (sub_indptr, compacted cols, H rows of those cols) on the host."""
+    returns (sub_indptr, compacted cols, rows of those cols of ``feats``
+    (default the fixture's H)) on the host."""
     csr = rmat["adj"].fwd
     dev = rmat["dev"]
     r = torch.from_numpy(rows).to(dev)
@@ -95,7 +99,7 @@ def _sub_csr(rmat, rows):
     first[starts[lens > 0]] = True
     assert bool(((eids[1:] > eids[:-1]) | first[1:]).all())
     uniq, inv = torch.unique(cols, return_inverse=True)
-    hsub = rmat["h"].index_select(0, uniq).cpu().numpy()
+    hsub = (rmat["h"] if feats is None else feats).index_select(0, uniq).cpu().numpy()
     ip = np.concatenate([[0], np.cumsum(lens.cpu().numpy())]).astype(np.int64)
     ix = inv.cpu().numpy().astype(np.int64)
     return ip, ix, hsub
@@ -153,27 +157,51 @@ def test_rmat26_heavy_rows_vs_oracle(rmat, reduce):
 
 def test_rmat26_graphsage_mean_fwd_bwd(rmat):
     """2-layer GraphSAGE-mean forward + backward at full size (configs[3] model
-    on one GPU); the step time goes to gpurun_out/."""
+    on one GPU); the step time and peak HBM go to gpurun_out/."""
     import torch.nn.functional as F
     from conftest import load_example
     sage = load_example("graphsage/train.py", "sage_rmat26")
     dev, n = rmat["dev"], rmat["n"]
     adj = rmat["adj"]
-    # the edge list is not needed any more: make room for activations
-    rmat.pop("src")
-    rmat.pop("dst")
-    rmat.pop("h")
+    rmat.pop("h")  # the sum test's features
     if dev.type == "cuda":
         torch.cuda.empty_cache()
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
     feats = 0.1 * torch.randn(n, FEAT, generator=gen, device=dev)
     labels = torch.randint(0, 41, (n,), generator=gen, device=dev)
+    # the rows the first layer's aggregation is checked on: every chunked hub
+    # row and 2,000 random rows, their slots checked against the edge list
+    old = kernel.set_row_split("auto")
+    try:
+        threshold = kernel._split_threshold(adj.fwd)
+    finally:
+        kernel.set_row_split(old)
+    deg = (adj.fwd.host_indptr[1:] - adj.fwd.host_indptr[:-1]).numpy()
+    rng = np.random.default_rng(11)
+    rows = np.unique(np.concatenate([np.nonzero(deg > threshold)[0],
+                                     rng.choice(n, 2000, replace=False)]))
+    ip, ix, hsub = _sub_csr(rmat, rows, feats)
+    # the edge lists are not needed any more: make room for activations, then
+    # build the transposed CSR (the backward's) before the step
+    rmat.pop("src")
+    rmat.pop("dst")
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
+    adj.bwd
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+        torch.cuda.reset_peak_memory_stats(dev)
     torch.manual_seed(0)
     model = sage.SAGE(FEAT, 128, 41, 1, 0.0).to(dev)
+    seen = []
+    sel = torch.from_numpy(rows).to(dev)
 
     def aggregate(x):
-        return kernel.gspmm(adj, "copy_u", "mean", x)
+        out = kernel.gspmm(adj, "copy_u", "mean", x)
+        if not seen:  # the first layer's aggregation of the input features
+            seen.append(out.detach().index_select(0, sel).cpu().numpy())
+        return out
 
     old = kernel.set_row_split("auto")
     times = []
@@ -192,15 +220,31 @@ def test_rmat26_graphsage_mean_fwd_bwd(rmat):
             del logits
     finally:
         kernel.set_row_split(old)
+    peak = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else None
     assert torch.isfinite(loss).item()
     for p in model.parameters():
         assert p.grad is not None and torch.isfinite(p.grad).all().item()
+    # the model's first aggregation against the oracle's mean of the same rows
+    pos = np.arange(len(ix), dtype=np.int64)
+    ref = O.spmm_csr(ip, ix, pos, hsub, num_threads=16)
+    absref = O.spmm_csr(ip, ix, pos, np.abs(hsub), num_threads=16)
+    d = deg[rows].astype(np.float32)[:, None]
+    ref = np.where(d > 0, ref / np.maximum(d, 1), 0).astype(np.float32)
+    absref = absref / np.maximum(d, 1)
+    worst = float((np.abs(seen[0] - ref) / (1e-5 * absref + 1e-30)).max())
+    heavy = int((deg[rows] > threshold).sum())
     rec = {"graph": "rmat-%d" % SCALE, "nodes": n, "edges": int(adj.fwd.nnz),
            "model": "GraphSAGE-mean 128-128-41, 2 layers, fwd+bwd (no optimizer)",
-           "step_s": times, "loss": float(loss.item()),
-           "peak_hbm_gb": torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda"
-           else None}
+           "step_s": times, "loss": float(loss.item()), "peak_hbm_gb": peak,
+           "peak_scope": "the model step (edge lists released, transposed CSR built, "
+                         "peak stats reset before it)",
+           "first_layer_rows_checked": int(len(rows)), "chunked_rows_checked": heavy,
+           "worst_err_over_1e-5_sum_abs_over_deg": worst}
     print(rec, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.path.join("gpurun_out", "graphsage_rmat26_test.json"), "w") as f:
         json.dump(rec, f)
+    assert heavy > 0
+    assert worst <= 1.0
+    if peak is not None:
+        assert peak <= 240.0, "model step peaked at %.1f GB" % peak

@@ -74,8 +74,20 @@ def bench_graph(name, adj, n, E, H, D, iters):
         kernel.gspmm(adj, "u_mul_e", "sum", ft, a, edge_order="slot")
         kernel.gspmm(adj, "copy_e", "sum", None, a, edge_order="slot")
 
+    def variant(v, fn):
+        def run():
+            kernel.set_gat_variant(v)
+            try:
+                fn()
+            finally:
+                kernel.set_gat_variant(0)
+        return run
+
     for key, fn, stored in (("fused", fused_ng, 0), ("fused+a", fused_g, 4 * H),
-                            ("fused+drop", fused_drop, 8 * H), ("unfused", unfused, None)):
+                            ("fused+drop", fused_drop, 8 * H),
+                            ("per_lane_kernel", variant(1, fused_ng), 0),
+                            ("lds_kernel", variant(2, fused_ng), 0),
+                            ("unfused", unfused, None)):
         t = timed(fn, iters)
         entry = {"kernel_ms": round(t, 3)}
         if stored is not None:
@@ -102,10 +114,33 @@ def bench_graph(name, adj, n, E, H, D, iters):
     return res
 
 
+def fwd_bwd_only(iters):
+    """Reddit-shaped 8 x 16 forward + backward of the fused path only (for a
+    rocprofv3 kernel breakdown)."""
+    dev = torch.device("cuda", 0)
+    src, dst, n = data.reddit_like(device=dev)
+    E = int(src.numel())
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    del src, dst
+    ft = (torch.rand(n, 8, 16, device=dev) * 2 - 1).requires_grad_(True)
+    el = (torch.rand(n, 8, device=dev) - 0.5).requires_grad_(True)
+    er = (torch.rand(n, 8, device=dev) - 0.5).requires_grad_(True)
+    gout = torch.rand(n, 8, 16, device=dev)
+    gz = torch.rand(n, 8, 1, device=dev)
+
+    def fb():
+        fs, z = kernel.gat_aggregate(adj, ft, el, er)
+        torch.autograd.backward([fs, z], [gout, gz])
+    print(json.dumps({"edges": E, "fwd_bwd_wall_ms": round(wall(fb, iters), 3)}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--fwd-bwd-only", action="store_true")
     args = ap.parse_args()
+    if args.fwd_bwd_only:
+        return fwd_bwd_only(args.iters)
     dev = torch.device("cuda", 0)
     out = []
     src, dst, n = data.reddit_like(device=dev)
