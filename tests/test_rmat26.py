@@ -60,7 +60,11 @@ def rmat():
         torch.cuda.synchronize()
     print("rmat-%d: %d nodes, %d edges, setup %.1fs" % (SCALE, n, src.numel(), time.time() - t0),
           flush=True)
-    yield {"adj": adj, "h": h, "n": n, "src": src, "dst": dst, "dev": dev}
+    res = {"adj": adj, "h": h, "n": n, "src": src, "dst": dst, "dev": dev}
+    # the dict is the only owner: tests that pop an entry free it (this frame
+    # stays alive until teardown and would otherwise pin 51 GB of them)
+    del adj, h, src, dst
+    yield res
     if dev.type == "cuda":
         torch.cuda.empty_cache()
 
@@ -208,12 +212,18 @@ def test_rmat26_graphsage_mean_fwd_bwd(rmat):
 
     old = kernel.set_row_split("auto")
     times = []
+    mem = {}
+    if dev.type == "cuda":
+        mem["at_step_start_gb"] = torch.cuda.memory_allocated(dev) / 1e9
     try:
         for _ in range(2):
             if dev.type == "cuda":
                 torch.cuda.synchronize()
             t0 = time.time()
             logits = model(feats, aggregate)
+            if dev.type == "cuda" and "after_forward_gb" not in mem:
+                mem["after_forward_gb"] = torch.cuda.memory_allocated(dev) / 1e9
+                mem["forward_peak_gb"] = torch.cuda.max_memory_allocated(dev) / 1e9
             # the engine's node-row loss (the example's): no log-softmax copy
             loss = weighted_cross_entropy(logits, labels) / n
             model.zero_grad(set_to_none=True)
@@ -242,7 +252,7 @@ def test_rmat26_graphsage_mean_fwd_bwd(rmat):
            "step_s": times, "loss": float(loss.item()), "peak_hbm_gb": peak,
            "peak_scope": "the model step (edge lists released, transposed CSR built, "
                          "peak stats reset before it)",
-           "first_layer_rows_checked": int(len(rows)), "chunked_rows_checked": heavy,
+           "memory": mem, "first_layer_rows_checked": int(len(rows)), "chunked_rows_checked": heavy,
            "worst_err_over_1e-5_sum_abs_over_deg": worst}
     print(rec, flush=True)
     os.makedirs("gpurun_out", exist_ok=True)
