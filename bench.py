@@ -216,16 +216,20 @@ def cpu_baseline(sample, n, h_cpu, seconds_budget=20.0):
     """The reference path on host cores: torch.sparse.mm(COO(dst, src), H) on
     the sample, timed at one thread and at torch's default thread count (the
     setting the reference runs with); ``value`` is the faster of the two.
-    ``h_cpu`` None: the sample's source columns are compacted and get random
-    features (graphs whose full feature matrix does not fit host memory)."""
+    ``h_cpu`` None: a full-size (n, F) table whose pages are touched only for
+    the sample's source rows (random features there): the gathers spread over
+    the whole table's address range, as on the GPU, without allocating it
+    (RMAT-26: 34 GB of address space, the sample's rows resident)."""
     rows, d, s = sample
     threads = torch.get_num_threads()
     e = int(s.numel())
     ncols = n
+    touched = None
     if h_cpu is None:
-        uniq, s = torch.unique(s, return_inverse=True)
-        ncols = int(uniq.numel())
-        h_cpu = torch.rand(ncols, FEAT) * 2 - 1
+        uniq = torch.unique(s)
+        touched = int(uniq.numel())
+        h_cpu = torch.empty(n, FEAT)  # untouched pages are never materialised
+        h_cpu[uniq] = torch.rand(touched, FEAT) * 2 - 1
     A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (rows, ncols))
     runs = {}
     try:
@@ -251,7 +255,9 @@ def cpu_baseline(sample, n, h_cpu, seconds_budget=20.0):
                       "the job's host-core share; value = the faster, at %d: the product "
                       "is single-threaded in practice); host has %d cpus"
                       % (rows, e, h_cpu.shape[1],
-                         "" if ncols == n else " (%d source columns compacted)" % ncols,
+                         "" if touched is None else
+                         " (the full %d-row table's address range; its %d referenced rows "
+                         "resident)" % (n, touched),
                          "/".join(str(v[1]) for _, v in sorted(runs.items())),
                          torch.__version__, " and ".join(str(k) for k in sorted(runs)),
                          threads, best, os.cpu_count() or 0)}
