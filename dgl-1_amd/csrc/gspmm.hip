@@ -318,6 +318,7 @@ __global__ __launch_bounds__(256) void gsddmm_attention_vec_kernel(
 Timing g_timing;
 int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
 int g_cache_policy = -1;
+int g_gather_buf = 0;
 int g_sddmm_alt = 0;
 
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
@@ -638,6 +639,14 @@ int dglhip_set_sddmm_variant(int alternate) {
   API_BEGIN();
   DGLHIP_CHECK(alternate == 0 || alternate == 1, "unsupported g-SDDMM variant " << alternate);
   g_sddmm_alt = alternate;
+  API_END();
+}
+
+int dglhip_set_gather_mode(int buffer_descriptors) {
+  API_BEGIN();
+  DGLHIP_CHECK(buffer_descriptors == 0 || buffer_descriptors == 1,
+               "unknown gather mode " << buffer_descriptors);
+  g_gather_buf = buffer_descriptors;
   API_END();
 }
 

@@ -109,10 +109,38 @@ __device__ __forceinline__ f32x4 gather_bf16<4>(const float* ufeat, int32_t col,
 //  POL_NT_OUT  : only the output store non-temporal.
 enum { POL_DEFAULT = 0, POL_NT = 1, POL_HOT = 2, POL_NT_OUT = 3 };
 
-template <int VEC, int POL>
+// BUF: the row is wave-uniform (a whole wave per row, the column id from the
+// scalar slot stream): gather it through a buffer descriptor built from the
+// row's address, so every gather in flight shares the lane's one 32-bit byte
+// offset instead of holding a 64-bit address of its own (VGPRs -> waves per
+// SIMD). Same loads, same values.
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T gather_row_buf(const float* row, int64_t F,
+                                                               int64_t f0) {
+  typedef typename Vec<VEC>::T V;
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(row), 0, static_cast<int>(F * int64_t(sizeof(float))), 0x00020000);
+  const uint32_t off = static_cast<uint32_t>(f0 * int64_t(sizeof(float)));
+  if (VEC == 4) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return *reinterpret_cast<const V*>(&w);
+  }
+  if (VEC == 2) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+    return *reinterpret_cast<const V*>(&w);
+  }
+  const unsigned int w = __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+  return *reinterpret_cast<const V*>(&w);
+}
+
+template <int VEC, int POL, bool BUF = false>
 __device__ __forceinline__ typename Vec<VEC>::T gather_row(const float* __restrict__ ufeat,
                                                            int32_t col, int64_t F, int64_t f0) {
   typedef typename Vec<VEC>::T V;
+  if (BUF && (POL == POL_DEFAULT || POL == POL_NT_OUT))
+    return gather_row_buf<VEC>(ufeat + int64_t(col) * F, F, f0);
   if (POL == POL_NT) {
     return __builtin_nontemporal_load(reinterpret_cast<const V*>(ufeat + int64_t(col) * F + f0));
   } else if (POL == POL_HOT) {
@@ -143,7 +171,7 @@ enum { EM_FULL = 0, EM_SCALAR = 1, EM_HEAD = 2 };
 //  COPY_U : u                     U_MUL_E: w * u (fused into the reducer)
 //  COPY_E : e
 // `eoff` is the edge-feature column of f0 (f0, 0 or f0 / D by EM).
-template <int VEC, int MSG, int EM, int POL = POL_DEFAULT>
+template <int VEC, int MSG, int EM, int POL = POL_DEFAULT, bool BUF = false>
 struct SlotLoad {
   typedef typename Vec<VEC>::T V;
   V u;
@@ -154,7 +182,7 @@ struct SlotLoad {
                                        int32_t src, int64_t edge) {
     // ldu: row stride of ufeat in elements (F, or a padded width)
     if (MSG == DGLHIP_MSG_COPY_U_BF16) u = gather_bf16<VEC>(ufeat, src, ldu, f0);
-    else if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL>(ufeat, src, ldu, f0);
+    else if (MSG != DGLHIP_MSG_COPY_E) u = gather_row<VEC, POL, BUF>(ufeat, src, ldu, f0);
     if (!copies_u(MSG)) {
       if (EM == EM_FULL) e = ldv<VEC>(efeat + edge * F + f0);
       else e = Vec<VEC>::splat(efeat[edge * elen + eoff]);
@@ -164,7 +192,8 @@ struct SlotLoad {
 
 // Sequential reduction of slots [beg, end) of one row for the VEC features at
 // f0: the fma chain the reference's product runs (see the file header).
-template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID, int POL = POL_DEFAULT>
+template <int VEC, int UNROLL, int MSG, int EM, bool USE_EID, int POL = POL_DEFAULT,
+          bool BUF = false>
 __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     typename Vec<VEC>::T acc, int64_t beg, int64_t end, int64_t ldu, int64_t F, int64_t f0,
     int64_t elen, int64_t eoff, const int32_t* __restrict__ indices,
@@ -172,7 +201,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
     const float* __restrict__ efeat) {
   int64_t k = beg;
   for (; k + UNROLL <= end; k += UNROLL) {
-    SlotLoad<VEC, MSG, EM, POL> s[UNROLL];
+    SlotLoad<VEC, MSG, EM, POL, BUF> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j)
       s[j].load(ufeat, efeat, ldu, F, f0, elen, eoff, indices[k + j],
@@ -189,7 +218,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range(
   // load latencies per row, which dominates rows shorter than UNROLL)
   const int64_t rem = end - k;
   if (rem > 0) {
-    SlotLoad<VEC, MSG, EM, POL> s[UNROLL];
+    SlotLoad<VEC, MSG, EM, POL, BUF> s[UNROLL];
 #pragma unroll
     for (int j = 0; j < UNROLL - 1; ++j)
       if (j < rem)
@@ -247,7 +276,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 // MEAN and ACCUM on whole rows the row's mean is added to the value in
 // out[i, :] (out + mean: a sum of two terms, the same bits either way round).
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
-          bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT>
+          bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT, bool BUF = false>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     int64_t num_items, int64_t F, int64_t elen, int64_t ldu,
     const int64_t* __restrict__ indptr,
@@ -283,8 +312,8 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, ldu, f0, indices, ufeat);
     else if (copies_u(MSG) || eid != nullptr)  // uniform branch
-      acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL>(acc, beg, end, ldu, F, f0, elen, eoff,
-                                                          indices, eid, ufeat, efeat);
+      acc = reduce_range<VEC, UNROLL, MSG, EM, true, POL, BUF && GROUP == 64>(
+          acc, beg, end, ldu, F, f0, elen, eoff, indices, eid, ufeat, efeat);
     else
       acc = reduce_range<VEC, UNROLL, MSG, EM, false>(acc, beg, end, ldu, F, f0, elen, eoff, indices,
                                                       eid, ufeat, efeat);
@@ -535,6 +564,9 @@ extern int g_var_vec, g_var_group, g_var_unroll, g_var_pipe;
 // Cache policy for copy_u + sum at VEC 2 x 64 lanes (dglhip_set_cache_policy).
 // -1: automatic (non-temporal output past 512 MiB, default otherwise).
 extern int g_cache_policy;
+// Row gathers of copy_u + sum at VEC 2 x 64 lanes through buffer descriptors
+// (dglhip_set_gather_mode): 1 on, 0 global loads.
+extern int g_gather_buf;
 
 template <int VEC, int GROUP, int MSG, int EM, bool MEAN, int UNROLL_OVERRIDE = 0,
           bool PIPE = false>
@@ -552,12 +584,18 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                   : g_cache_policy >= 0 ? g_cache_policy
                   : a.nt_out ? POL_NT_OUT : POL_DEFAULT;
   timed_launch(stream, [&] {
-#define DGLHIP_POL_LAUNCH(CH, P)                                                           \
-  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P>), \
+#define DGLHIP_POL_LAUNCH_B(CH, P, B)                                                      \
+  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P, B>), \
                      grid_1d(blocks), dim3(256), 0, stream, a.num_items,   \
                      a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
                      a.row_order, a.chunk_beg, a.chunk_end)
-    if (POL_OK && pol != POL_DEFAULT && !a.accumulate) {
+#define DGLHIP_POL_LAUNCH(CH, P) DGLHIP_POL_LAUNCH_B(CH, P, false)
+    if (POL_OK && g_gather_buf && !a.accumulate && (pol == POL_DEFAULT || pol == POL_NT_OUT)) {
+      // row gathers through buffer descriptors (gather_row_buf)
+      const bool ch = a.chunk_beg != nullptr;
+      if (pol == POL_DEFAULT) { if (ch) DGLHIP_POL_LAUNCH_B(true, POL_DEFAULT, true); else DGLHIP_POL_LAUNCH_B(false, POL_DEFAULT, true); }
+      else { if (ch) DGLHIP_POL_LAUNCH_B(true, POL_NT_OUT, true); else DGLHIP_POL_LAUNCH_B(false, POL_NT_OUT, true); }
+    } else if (POL_OK && pol != POL_DEFAULT && !a.accumulate) {
       const bool ch = a.chunk_beg != nullptr;
       if (pol == POL_NT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT); else DGLHIP_POL_LAUNCH(false, POL_NT); }
       else if (pol == POL_HOT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_HOT); else DGLHIP_POL_LAUNCH(false, POL_HOT); }
@@ -583,6 +621,7 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                          a.num_items, a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat,
                          a.out, a.row_order, a.chunk_beg, a.chunk_end);
 #undef DGLHIP_POL_LAUNCH
+#undef DGLHIP_POL_LAUNCH_B
   });
 }
 

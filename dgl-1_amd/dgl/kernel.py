@@ -1032,6 +1032,12 @@ def gspmm_ranges(msg, beg, end, accumulate, indices, out, ufeat=None, efeat=None
     return out
 
 
+def set_gather_mode(buffer_descriptors):
+    """Study knob: the copy_u + sum kernel's row gathers through buffer
+    descriptors (True) or global loads (False); same values."""
+    check_call(LIB.dglhip_set_gather_mode(1 if buffer_descriptors else 0))
+
+
 def set_sddmm_variant(alternate):
     """Study knob: run the sliced g-SDDMM dot at its alternative depth of
     slots in flight (1) or the default (0)."""
