@@ -76,14 +76,48 @@ __device__ __forceinline__ typename Vec<VEC>::T gather_rsrc(const float* row, in
   return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
 }
 
-template <int VEC, int UNROLL, bool DROP>
+// Tables under 4 GB: one descriptor over the whole table, the row's byte
+// offset as the (wave-uniform, SGPR) soffset and the lane's as voffset: no
+// per-gather descriptor (4 SGPRs each, 16 in flight) and no per-gather VGPR.
+struct GatTable {
+  __amdgpu_buffer_rsrc_t r;
+};
+
+__device__ __forceinline__ GatTable gat_table(const float* ft, int64_t bytes) {
+  return GatTable{__builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(ft), 0,
+                                                    static_cast<int>(bytes), 0x00020000)};
+}
+
+template <int VEC>
+__device__ __forceinline__ typename Vec<VEC>::T gather_soff(const GatTable& t, int64_t src,
+                                                            int64_t F, uint32_t voff) {
+  const uint32_t soff = static_cast<uint32_t>(src * F * int64_t(sizeof(float)));
+  if (VEC == 2) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(t.r, voff, soff, 0);
+    return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
+  }
+  const unsigned int w = __builtin_amdgcn_raw_buffer_load_b32(t.r, voff, soff, 0);
+  return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
+}
+
+template <int VEC, bool SMALL>
+__device__ __forceinline__ typename Vec<VEC>::T gat_gather(const float* ft, const GatTable& t,
+                                                           int64_t src, int64_t F,
+                                                           uint32_t voff) {
+  if (SMALL) return gather_soff<VEC>(t, src, F, voff);
+  return gather_rsrc<VEC>(ft + src * F, F, voff);
+}
+
+template <int VEC, int UNROLL, bool DROP, bool SMALL>
 __global__ __launch_bounds__(256) void gat_aggregate_kernel(
     int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
     const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
     float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
     const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
-    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out) {
+    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out,
+    int64_t table_bytes) {
   typedef typename Vec<VEC>::T V;
   const int lane = threadIdx.x & 63;
   const int64_t it = block_linear() * (blockDim.x >> 6) +
@@ -94,6 +128,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
   const int64_t beg = indptr[row], end = indptr[row + 1];
   const int64_t F = H * D;
   const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
+  const GatTable tab = gat_table(ft, SMALL ? table_bytes : 0);
   for (int64_t f0 = int64_t(lane) * VEC; f0 < F; f0 += 64 * VEC) {
     const int64_t h = f0 / D;
     const bool head_lane = f0 - h * D == 0;  // first lane of head h in this pass
@@ -126,7 +161,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
       for (int j = 0; j < UNROLL; ++j) {
         const int64_t src = indices[k + j];
         l[j] = el[src * H + h];
-        u[j] = gather_rsrc<VEC>(ft + src * F, F, voff);
+        u[j] = gat_gather<VEC, SMALL>(ft, tab, src, F, voff);
       }
 #pragma unroll
       for (int j = 0; j < UNROLL; ++j) consume(k + j, l[j], u[j]);
@@ -140,7 +175,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
         if (j < rem) {
           const int64_t src = indices[k + j];
           l[j] = el[src * H + h];
-          u[j] = gather_rsrc<VEC>(ft + src * F, F, voff);
+          u[j] = gat_gather<VEC, SMALL>(ft, tab, src, F, voff);
         }
       }
 #pragma unroll
@@ -165,11 +200,11 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
 // One batch of the LDS kernel: slots [k, k + nb) of the row (FULL: nb == U,
 // no predication; the row's last partial batch runs with FULL = false, as
 // reduce_range's predicated tail).
-template <int H, int VEC, bool DROP, bool FULL>
+template <int H, int VEC, bool DROP, bool SMALL, bool FULL>
 __device__ __forceinline__ void gat_batch(
     int64_t k, int nb, int64_t F, uint32_t voff, int64_t h, int hc, int jc, float rc,
     const int32_t* __restrict__ indices, const float* __restrict__ el,
-    const float* __restrict__ ft, float alpha, float lo, float hi, int apply_exp,
+    const float* __restrict__ ft, const GatTable& tab, float alpha, float lo, float hi, int apply_exp,
     uint64_t seed, uint32_t thr, float scale, float* la, float* lw, float* __restrict__ a_out,
     float* __restrict__ w_out, typename Vec<VEC>::T& acc, float& zacc) {
   typedef typename Vec<VEC>::T V;
@@ -204,7 +239,7 @@ __device__ __forceinline__ void gat_batch(
   V u[U];
 #pragma unroll
   for (int j = 0; j < U; ++j)
-    if (FULL || j < nb) u[j] = gather_rsrc<VEC>(ft + int64_t(indices[k + j]) * F, F, voff);
+    if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, indices[k + j], F, voff);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -231,16 +266,18 @@ __device__ __forceinline__ void gat_batch(
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int H, int VEC, bool DROP>
+template <int H, int VEC, bool DROP, bool SMALL>
 __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     int64_t num_rows, int64_t D, const int64_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
     const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
     float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
     const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
-    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out) {
+    float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out,
+    int64_t table_bytes) {
   typedef typename Vec<VEC>::T V;
   constexpr int U = 16;
+  const GatTable tab = gat_table(ft, SMALL ? table_bytes : 0);
   __shared__ float s_a[4][H * U];
   __shared__ float s_w[4][DROP ? H * U : 1];
   const int lane = threadIdx.x & 63;
@@ -268,12 +305,13 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     float zacc = 0.0f;
     int64_t k = beg;
     for (; k + U <= end; k += U)
-      gat_batch<H, VEC, DROP, true>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, alpha, lo, hi,
+      gat_batch<H, VEC, DROP, SMALL, true>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab,
+                                           alpha, lo, hi,
                                     apply_exp, seed, thr, scale, s_a[wi], s_w[wi], a_out, w_out,
                                     acc, zacc);
     if (k < end)
-      gat_batch<H, VEC, DROP, false>(k, static_cast<int>(end - k), F, voff, h, hc, jc, rc, indices,
-                                     el, ft, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
+      gat_batch<H, VEC, DROP, SMALL, false>(k, static_cast<int>(end - k), F, voff, h, hc, jc,
+                                            rc, indices, el, ft, tab, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
                                      s_w[wi], a_out, w_out, acc, zacc);
     if (active) {
       stv<VEC>(out_ft + row * F + f0, acc);
@@ -288,8 +326,8 @@ using namespace dglhip;
 
 extern "C" {
 
-int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t head_dim,
-                                const int64_t* indptr, const int32_t* indices,
+int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_heads,
+                                int64_t head_dim, const int64_t* indptr, const int32_t* indices,
                                 const int32_t* row_order, const float* el, const float* er,
                                 const float* ft, float alpha, float clamp_lo, float clamp_hi,
                                 int apply_exp, float drop_p, uint64_t seed,
@@ -297,7 +335,7 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
                                 float* attn_out, float* attn_drop_out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rows >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
+  DGLHIP_CHECK(num_rows >= 0 && num_src >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
   DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(indptr && indices && el && er && ft && out_ft && out_z, "null pointer argument");
@@ -309,6 +347,10 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
   const uint32_t thr = drop ? gat_drop_threshold(drop_p) : 0u;
   const float scale = drop ? 1.0f / (1.0f - drop_p) : 1.0f;
   const int64_t F = num_heads * head_dim;
+  // the source table in bytes: under 4 GB one descriptor spans it (row
+  // offsets as soffset), else one descriptor per gathered row
+  const int64_t tbytes = num_src * F * int64_t(sizeof(float));
+  const bool small = tbytes < (int64_t(1) << 31);
   // VEC 2 when a lane's two features stay in one head and rows are 8-B aligned
   const bool v2 = head_dim % 2 == 0 && F >= 128 &&
                   reinterpret_cast<uintptr_t>(ft) % 8 == 0 &&
@@ -323,34 +365,39 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t hea
                          num_heads == 8 || num_heads == 16;
   if (lds_heads && (g_gat_variant == 2 || (g_gat_variant == 0 && !v2))) {
     timed_launch(stream, [&] {
-#define DGLHIP_GATL(HH, VV, DD)                                                            \
-  hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD>), grid_1d(blocks), dim3(256), 0, \
-                     stream, num_rows, head_dim, indptr, indices, row_order, el, er, ft,     \
+#define DGLHIP_GATL(HH, VV, DD, SM)                                                        \
+  hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD, SM>), grid_1d(blocks), dim3(256), \
+                     0, stream, num_rows, head_dim, indptr, indices, row_order, el, er, ft,  \
                      alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale,    \
-                     out_ft, out_z, attn_out, attn_drop_out)
+                     out_ft, out_z, attn_out, attn_drop_out, tbytes)
+#define DGLHIP_GATS(HH, VV, DD) \
+  if (small) DGLHIP_GATL(HH, VV, DD, true); else DGLHIP_GATL(HH, VV, DD, false);
 #define DGLHIP_GATH(HH)                                                                    \
   if (num_heads == HH) {                                                                   \
-    if (v2) { if (drop) DGLHIP_GATL(HH, 2, true); else DGLHIP_GATL(HH, 2, false); }         \
-    else { if (drop) DGLHIP_GATL(HH, 1, true); else DGLHIP_GATL(HH, 1, false); }            \
+    if (v2) { if (drop) { DGLHIP_GATS(HH, 2, true) } else { DGLHIP_GATS(HH, 2, false) } }   \
+    else { if (drop) { DGLHIP_GATS(HH, 1, true) } else { DGLHIP_GATS(HH, 1, false) } }      \
     return;                                                                                \
   }
       DGLHIP_GATH(1) DGLHIP_GATH(2) DGLHIP_GATH(4) DGLHIP_GATH(8) DGLHIP_GATH(16)
 #undef DGLHIP_GATH
+#undef DGLHIP_GATS
 #undef DGLHIP_GATL
     });
     return 0;
   }
   timed_launch(stream, [&] {
-#define DGLHIP_GAT(VV, DD)                                                                 \
-  hipLaunchKernelGGL((gat_aggregate_kernel<VV, 16, DD>), grid_1d(blocks), dim3(256), 0,    \
+#define DGLHIP_GAT(VV, DD, SM)                                                             \
+  hipLaunchKernelGGL((gat_aggregate_kernel<VV, 16, DD, SM>), grid_1d(blocks), dim3(256), 0, \
                      stream, num_rows, num_heads, head_dim, indptr, indices, row_order, el, \
                      er, ft, alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale, \
-                     out_ft, out_z, attn_out, attn_drop_out)
+                     out_ft, out_z, attn_out, attn_drop_out, tbytes)
+#define DGLHIP_GATS(VV, DD) if (small) DGLHIP_GAT(VV, DD, true); else DGLHIP_GAT(VV, DD, false);
     if (v2) {
-      if (drop) DGLHIP_GAT(2, true); else DGLHIP_GAT(2, false);
+      if (drop) { DGLHIP_GATS(2, true) } else { DGLHIP_GATS(2, false) }
     } else {
-      if (drop) DGLHIP_GAT(1, true); else DGLHIP_GAT(1, false);
+      if (drop) { DGLHIP_GATS(1, true) } else { DGLHIP_GATS(1, false) }
     }
+#undef DGLHIP_GATS
 #undef DGLHIP_GAT
   });
   API_END();

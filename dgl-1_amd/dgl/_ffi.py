@@ -75,7 +75,8 @@ def _load():
         "dglhip_gsddmm_attention_host": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                   ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                                   _c_int, _vp, _c_int]),
-        "dglhip_gat_aggregate_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
+        "dglhip_gat_aggregate_device": (_c_int, [_c_i64, _c_i64, _c_i64, _c_i64, _vp, _vp, _vp,
+                                                 _vp, _vp,
                                                  _vp, ctypes.c_float, ctypes.c_float,
                                                  ctypes.c_float, _c_int, ctypes.c_float,
                                                  ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),

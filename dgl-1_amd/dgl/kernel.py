@@ -1281,7 +1281,7 @@ class _GATAggregate(torch.autograd.Function):
                 a = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
                 w = torch.empty_like(a) if p > 0 else None
             check_call(LIB.dglhip_gat_aggregate_device(
-                fwd.num_rows, H, D, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.row_order),
+                fwd.num_rows, ft2.shape[0], H, D, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.row_order),
                 ptr(el), ptr(er), ptr(ft2), float(alpha), float(lo), float(hi),
                 1 if apply_exp else 0, float(p), int(seed), ptr(seed_off), ptr(out_ft),
                 ptr(out_z), ptr(a), ptr(w), _stream_of(dev)))

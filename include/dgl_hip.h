@@ -423,14 +423,15 @@ int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads,
  *                     fresh masks)
  *   out_ft[r, hD+d] = sum_k w[k, h] * ft[u, hD+d]   (fma chain in slot order)
  *   out_z[r, h]     = sum_k a[k, h]                 (add chain in slot order)
- * el, er: [num_src, H], [num_rows, H]; ft: [num_src, H*D]; out_ft: [num_rows,
+ * el, er: [num_src, H], [num_rows, H]; ft: [num_src, H*D] (num_src: the column
+ * count, every index below it); out_ft: [num_rows,
  * H*D]; out_z: [num_rows, H]. attn_out / attn_drop_out ([nnz, H], CSR slot
  * order) may be NULL (nothing stored); with dropout both or neither. The
  * outputs equal dglhip_gsddmm_attention_device (slot order) followed by the
  * u_mul_e and copy_e sums bit for bit. keep(): dglhip_gat_dropout_mask_host.
  * row_order (int32[num_rows], may be NULL): launch schedule only. */
-int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_heads, int64_t head_dim,
-                                const int64_t* indptr, const int32_t* indices,
+int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_heads,
+                                int64_t head_dim, const int64_t* indptr, const int32_t* indices,
                                 const int32_t* row_order, const float* el, const float* er,
                                 const float* ft, float alpha, float clamp_lo, float clamp_hi,
                                 int apply_exp, float drop_p, uint64_t seed,

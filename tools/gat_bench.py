@@ -87,6 +87,8 @@ def bench_graph(name, adj, n, E, H, D, iters):
                             ("fused+drop", fused_drop, 8 * H),
                             ("per_lane_kernel", variant(1, fused_ng), 0),
                             ("lds_kernel", variant(2, fused_ng), 0),
+                            ("per_lane_kernel+drop", variant(1, fused_drop), 8 * H),
+                            ("lds_kernel+drop", variant(2, fused_drop), 8 * H),
                             ("unfused", unfused, None)):
         t = timed(fn, iters)
         entry = {"kernel_ms": round(t, 3)}
