@@ -72,6 +72,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Cache holds (MI355X_MICROARCH.md "Indexed rows: gather into LDS")
 IC_GATHER_PEAK_GBS = 8600.0
 INFINITY_CACHE_BYTES = 256 << 20
+# the guide's measured rate for indexed rows gathered from an XCD's L2 (rows
+# shared by every workgroup: 16.8-18.8 TB/s chip-wide): the ceiling of the
+# source-blocked schedule, whose blocks of ~7.5 MiB the 4 MiB L2s serve
+L2_GATHER_PEAK_GBS = 18800.0
 
 
 def log(*a):
@@ -386,10 +390,18 @@ def per_rank(values, world, dev):
     return [t[i * k:(i + 1) * k] for i in range(world)]
 
 
-def gather_peak(table_bytes):
-    """(peak GB/s, source) of a row gather from a ``table_bytes`` table: the
-    guide's Infinity-Cache random-row rate while the table fits the cache,
-    else the HBM spec peak."""
+def gather_peak(table_bytes, blocks=0):
+    """(peak GB/s, source) of a row gather from a ``table_bytes`` table: with
+    the source-blocked schedule (``blocks`` > 0) the guide's L2 indexed-row
+    rate; else the Infinity-Cache random-row rate while the table fits the
+    cache, else the HBM spec peak."""
+    if blocks:
+        return L2_GATHER_PEAK_GBS, (
+            "source-blocked gather (%d launches of ~%.1f MB slices of the %.0f MB table, "
+            "each continuing every row's chain): the slices are served by the XCDs' 4 MiB "
+            "L2s; the guide's measured rate for indexed rows from L2, 16.8-18.8 TB/s "
+            "chip-wide (MI355X_MICROARCH.md 'Indexed rows'), upper end"
+            % (blocks, table_bytes / blocks / 1e6, table_bytes / 1e6))
     if table_bytes < INFINITY_CACHE_BYTES:
         return IC_GATHER_PEAK_GBS, (
             "Infinity-Cache-resident gather (table %.0f MB < 256 MiB): the guide's measured "
@@ -399,14 +411,14 @@ def gather_peak(table_bytes):
     return HBM_PEAK_GBS, "HBM3E spec peak (MI355X_MICROARCH.md)"
 
 
-def roofline_block(num_edges, num_rows, kms, world, dev, table_bytes, **extra):
+def roofline_block(num_edges, num_rows, kms, world, dev, table_bytes, blocks=0, **extra):
     """The g-SpMM roofline of this rank (algorithmic bytes of its launch(es)
     per step over its kernel ms per step) against the gather's ceiling for a
     table of ``table_bytes`` (gather_peak), with every rank's figures in
     ``per_rank`` when N > 1. ``effective_gather_frac`` is the same rate over
     the 8 TB/s HBM spec: a figure of effective gather bandwidth, not of DRAM
     bytes (FETCH_SIZE / TCC_EA0_RDREQ_DRAM count Infinity-Cache hits)."""
-    peak, source = gather_peak(table_bytes)
+    peak, source = gather_peak(table_bytes, blocks)
     b = algorithmic_bytes(num_edges, num_rows, FEAT)
     ach = b / (kms * 1e-3) / 1e9 if kms > 0 else None
     roof = {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s",
@@ -566,8 +578,9 @@ def main(argv=None):
     rmat_pmc = None
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
         t0 = time.time()  # before this process initialises the GPU
+        # every g-SpMM kernel of the 3 calls (warm-up + 2 steps), per call
         pmc = pmc_traffic(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
-                           "--no-rmat-leg", "--no-train-leg"])
+                           "--no-rmat-leg", "--no-train-leg"], per_call_calls=3)
         if not args.no_rmat_leg and args.emulate_world <= 1:
             # the rmat leg's kernels: every g-SpMM kernel of a call, per call
             rmat_pmc = pmc_traffic(["--workload", "rmat", "--rmat-scale", str(args.rmat_scale),
@@ -595,6 +608,7 @@ def main(argv=None):
 
     t0 = time.time()
     real_reddit = None
+    blocks = 0
     if args.workload == "rmat":
         src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
         kernel.set_row_split("auto")
@@ -696,6 +710,12 @@ def main(argv=None):
         def step():
             g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
         parallelism = "single GPU" if not on_cpu else "host (library host kernels)"
+        blocks = kernel.blocked_schedule(g.sparse_adjacency(dev), h)
+        if blocks:
+            parallelism += (", source-blocked schedule: %d launches over contiguous source "
+                            "blocks, every row's chain continued block by block (the edges "
+                            "are numbered source-major, so the chains are the edge-id "
+                            "chains: bit-identical)" % blocks)
     else:
         from dgl.distributed import PartitionedGraph, balanced_bounds
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
@@ -723,13 +743,20 @@ def main(argv=None):
     elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
     value = num_edges_total * args.steps / elapsed
     roof = roofline_block(
-        num_local_edges, num_rows, kernel_ms, world, dev, n * FEAT * 4,
+        num_local_edges, num_rows, kernel_ms, world, dev, n * FEAT * 4, blocks,
         traffic=None if pmc is None else pmc["bytes"],
         kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
-            ", every segment of the pipelined partition" if dist.is_initialized() else ""),
+            ", every segment of the pipelined partition" if dist.is_initialized() else
+            ", every block launch and short-row tier of one call" if blocks else ""),
         traffic_source=None if pmc is None else
-        "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, mean per launch, read x2 (gfx950)",
-        regime=("Infinity-Cache-resident gather: H = %.0f MB fits the 256 MiB Infinity "
+        "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes, every g-SpMM kernel of a "
+        "call summed, mean per call, read x2 (gfx950); EA requests: bytes the L2s did "
+        "not serve",
+        regime=("L2-served gather: H = %.0f MB in %d source blocks of %.1f MB; traffic "
+                "(EA requests) = the bytes the L2s did not serve, from the Infinity Cache "
+                "(H and out fit it) or DRAM" % (n * FEAT * 4 / 1e6, blocks,
+                                                n * FEAT * 4 / blocks / 1e6)) if blocks else
+        ("Infinity-Cache-resident gather: H = %.0f MB fits the 256 MiB Infinity "
                 "Cache, whose hits FETCH_SIZE counts as fetches (traffic = fabric bytes, not "
                 "DRAM bytes); the DRAM-bound figure is the rmat%d block's roofline"
                 % (n * FEAT * 4 / 1e6, args.rmat_scale))

@@ -540,6 +540,11 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     dev = (ufeat2 if ufeat2 is not None else efeat2).device
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
+    if (out is None and dev.type == "cuda" and msg == MSG_COPY_U and
+            red in (RED_SUM, RED_MEAN) and efeat2 is None):
+        blocks = _block_plan(csr, ufeat2, feat_len)
+        if blocks is not None:
+            return _run_blocked(csr, blocks, red, ufeat2, feat_len), None
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
@@ -643,6 +648,119 @@ def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
         check_call(LIB.dglhip_gspmm_short_rows_device(
             msg, red, n, feat_len, maxd, csr.num_rows, ptr(rows), ptr(sp), ptr(cols),
             ptr(ufeat2), ptr(out), ld, _stream_of(dev)))
+
+
+# Source-blocked schedule (copy_u with sum / mean): the
+# columns are cut into B contiguous blocks of about _BLOCK_BYTES of feature
+# rows each, every block a CSR of its own over all rows, run as B launches
+# that continue each row's chain (SUM_ACCUM). All 8 XCDs then gather from the
+# same slice of H at a time, which their 4 MiB L2s serve, instead of from the
+# whole table through the Infinity Cache (Reddit-shaped graph, F = 128: 7.41
+# -> 4.21 ms at B = 16, tools/blocked_study.py). Used only where it keeps
+# every chain: when along each row's slots (edge-id order) the sources'
+# blocks never decrease — then block by block IS the row's order, and the
+# results are bit-identical (true of graphs whose edges are numbered
+# source-major, as the (src, dst)-sorted loaders, the synthetic generators and
+# the transposed CSR of any such graph give them). Other graphs, tables that
+# fit one L2 or exceed the Infinity Cache, and rows too short to split keep
+# the one-launch schedule.
+_BLOCKED = os.environ.get("DGLHIP_BLOCKED", "auto")
+_BLOCK_BYTES = 15 << 19         # ~7.5 MiB of feature rows per block
+_BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
+_BLOCK_TABLE_MAX = 256 << 20    # above: out's per-block pass outweighs the L2 hits
+_BLOCK_MIN_SLOTS = 8            # slots per row and block, on average
+
+
+def set_blocked(policy):
+    """Source-blocked schedule for copy_u sum / mean: "auto" (default: where
+    it keeps the chains bit-identical and the table size pays) or "off";
+    returns the old policy."""
+    global _BLOCKED
+    old = _BLOCKED
+    _BLOCKED = str(policy)
+    return old
+
+
+def _block_count(csr, table_bytes):
+    if _BLOCKED == "off" or csr.num_rows == 0 or csr.nnz == 0:
+        return 0
+    if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
+        return 0
+    B = -(-table_bytes // _BLOCK_BYTES)
+    B = min(B, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
+    return int(B) if B >= 2 else 0
+
+
+def _block_plan(csr, ufeat2, feat_len):
+    """The segment CSRs of the blocked schedule for ``csr`` (cached), or None
+    when the schedule does not apply or would reorder some row's chain."""
+    ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
+    B = _block_count(csr, csr.num_cols * max(ld, feat_len) * 4)
+    if not B:
+        return None
+    key = ("blocked", B)
+    if key in csr._plans:
+        return csr._plans[key]
+    dev = csr.device
+    bs = -(-csr.num_cols // B)
+    blk = torch.div(csr.indices, bs, rounding_mode="floor")  # int32, block of each slot
+    first = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
+    starts = csr.indptr[:-1][csr.degrees() > 0]
+    first[starts] = True
+    monotone = not bool(((blk[1:] < blk[:-1]) & ~first[1:]).any())
+    plan = None
+    if monotone:
+        rid = torch.repeat_interleave(torch.arange(csr.num_rows, device=dev), csr.degrees(),
+                                      output_size=csr.nnz)
+        counts = torch.bincount(rid * B + blk.long(), minlength=csr.num_rows * B)
+        counts = counts.view(csr.num_rows, B)
+        del rid
+        plan = []
+        for b in range(B):
+            sel = blk == b
+            ip = torch.zeros(csr.num_rows + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(counts[:, b], 0, out=ip[1:])
+            host_ip = ip.cpu()
+            ro = torch.empty(csr.num_rows, dtype=torch.int32)
+            check_call(LIB.dglhip_rows_by_degree_host(csr.num_rows, ptr(host_ip), ptr(ro)))
+            # copy_u never reads edge ids: the segments carry none
+            plan.append(CSR(ip, csr.indices[sel], None, csr.num_cols, ro.to(dev), host_ip))
+            del sel
+    del blk, first
+    csr._plans[key] = plan
+    return plan
+
+
+def blocked_schedule(adj, ufeat):
+    """The number of source blocks the copy_u sum / mean g-SpMM of ``ufeat``
+    over ``adj`` runs in (0: one launch), e.g. for a roofline's regime."""
+    adj = adj.to(ufeat.device)
+    if ufeat.device.type != "cuda":
+        return 0
+    u2 = ufeat.reshape(ufeat.shape[0], -1)
+    plan = _block_plan(adj.fwd, u2, u2.shape[1])
+    return 0 if plan is None else len(plan)
+
+
+def _run_blocked(csr, blocks, red, ufeat2, feat_len):
+    """copy_u + sum (mean) over the segment CSRs, each row's chain continued
+    block by block: the first block writes every row, the others add to rows
+    that have slots in them; mean divides by the degree last (the kernel's own
+    division: IEEE, by max(deg, 1))."""
+    if not _row_strided(ufeat2, feat_len) and _pad_rows(MSG_COPY_U, RED_SUM, ufeat2, feat_len):
+        # line-straddling rows: one padded copy for every block's launch
+        ld = padded_width(feat_len)
+        up = ufeat2.new_empty(ufeat2.shape[0], ld)
+        up[:, :feat_len] = ufeat2
+        ufeat2 = up[:, :feat_len]
+    out, _ = _run_gspmm(blocks[0], MSG_COPY_U, RED_SUM, ufeat2, None, 0, feat_len, False,
+                        out=torch.empty(csr.num_rows, feat_len, dtype=torch.float32,
+                                        device=ufeat2.device))
+    for seg in blocks[1:]:
+        _run_gspmm(seg, MSG_COPY_U, RED_SUM_ACCUM, ufeat2, None, 0, feat_len, False, out=out)
+    if red == RED_MEAN:
+        out.div_(csr.mean_divisor())
+    return out
 
 
 _PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")

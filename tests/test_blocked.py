@@ -1,0 +1,133 @@
+"""The source-blocked schedule of copy_u + sum / mean (kernel._block_plan,
+DESIGN.md §4.1): B launches over per-block segment CSRs, each row's chain
+continued block by block. It is used only when, along every row's slots
+(edge-id order), the source blocks never decrease — then the blocked chain IS
+the row's chain and the results are bit-identical to the one-launch schedule
+(and the oracle). These tests check the plan's gate (monotone graphs get it,
+others do not), the bits on the host and on the device (forward, mean, the
+transposed backward, line-straddling F), and that the bench graph takes it.
+"""
+import numpy as np
+import pytest
+import torch
+
+import dgl
+import dgl.function as fn
+from dgl import kernel
+from oracle import oracle as O
+
+
+def _graph(n, m, seed, sorted_src):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, m)
+    dst = rng.integers(0, n, m)
+    if sorted_src:  # edges numbered source-major, as (src, dst)-sorted loaders give them
+        o = np.lexsort((dst, src))
+        src, dst = src[o], dst[o]
+    return src, dst
+
+
+@pytest.fixture
+def small_blocks(monkeypatch):
+    monkeypatch.setattr(kernel, "_BLOCK_TABLE_MIN", 0)
+    monkeypatch.setattr(kernel, "_BLOCK_BYTES", 1 << 16)
+
+
+def test_plan_gate_and_host_bits(small_blocks):
+    n, m = 2000, 200_000
+    src, dst = _graph(n, m, 0, True)
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                           kernel.ORDER_EID, "cpu")
+    h = torch.randn(n, 128, generator=torch.Generator().manual_seed(1))
+    plan = kernel._block_plan(csr, h, 128)
+    assert plan is not None and len(plan) >= 2
+    assert sum(p.nnz for p in plan) == csr.nnz
+    ref = torch.from_numpy(O.spmm_coo(n, dst, src, h.numpy()))
+    out = torch.empty(n, 128)
+    kernel._run_gspmm(plan[0], kernel.MSG_COPY_U, kernel.RED_SUM, h, None, 0, 128, False,
+                      out=out)
+    for seg in plan[1:]:
+        kernel._run_gspmm(seg, kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, h, None, 0, 128,
+                          False, out=out)
+    assert torch.equal(out, ref)
+    # edges in random order: some row's blocks decrease -> no plan
+    src2, dst2 = _graph(n, m, 0, False)
+    csr2 = kernel.build_csr(n, n, torch.from_numpy(dst2), torch.from_numpy(src2),
+                            kernel.ORDER_EID, "cpu")
+    assert kernel._block_plan(csr2, h, 128) is None
+    # off switch
+    old = kernel.set_blocked("off")
+    try:
+        assert kernel._block_count(csr, 1 << 30) == 0
+    finally:
+        kernel.set_blocked(old)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [128, 41])
+@pytest.mark.parametrize("reduce", ["sum", "mean"])
+def test_blocked_device_bits(F, reduce):
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000  # 61 MB table at F = 128: 8 blocks; 3 at F = 41
+    src, dst = _graph(n, m, 3, True)
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+    gen = torch.Generator().manual_seed(4)
+    H = torch.randn(n, F, generator=gen)
+    G = torch.randn(n, F, generator=gen)
+    red = fn.sum if reduce == "sum" else fn.mean
+
+    def run(policy):
+        old = kernel.set_blocked(policy)
+        try:
+            h = H.to(dev).requires_grad_(True)
+            g.ndata["h"] = h
+            kernel.timing_enable(True)
+            g.update_all(fn.copy_src("h", "m"), red("m", "o"))
+            g.ndata["o"].backward(G.to(dev))
+            torch.cuda.synchronize()
+            _, launches = kernel.timing_read()
+            kernel.timing_enable(False)
+            return g.ndata["o"].detach().cpu(), h.grad.cpu(), launches
+        finally:
+            kernel.set_blocked(old)
+    o1, g1, n1 = run("auto")
+    o0, g0, n0 = run("off")
+    adj = g.sparse_adjacency(dev)
+    assert kernel._block_plan(adj.fwd, H.to(dev), F) is not None
+    assert n1 > n0  # the blocked launches ran, forward and backward
+    assert torch.equal(o1, o0) and torch.equal(g1, g0)
+    if reduce == "sum":
+        assert np.array_equal(o1.numpy(), O.spmm_coo(n, dst, src, H.numpy()))
+
+
+@pytest.mark.gpu
+def test_random_order_graph_keeps_one_launch():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 60_000, 6_000_000
+    src, dst = _graph(n, m, 5, False)
+    adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                          kernel.ORDER_EID, dev)
+    h = torch.randn(n, 128, device=dev)
+    assert kernel._block_plan(adj.fwd, h, 128) is None
+    out = kernel.gspmm(adj, "copy_u", "sum", h)
+    assert np.array_equal(out.cpu().numpy(), O.spmm_coo(n, dst, src, h.cpu().numpy()))
+
+
+@pytest.mark.gpu
+def test_bench_graph_takes_the_blocked_schedule():
+    """The Reddit-shaped bench graph (edges numbered source-major by the
+    generator) qualifies in both directions."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from dgl import data
+    dev = torch.device("cuda", 0)
+    src, dst, n = data.reddit_like(device=dev)
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    h = torch.empty(n, 128, device=dev)
+    plan = kernel._block_plan(adj.fwd, h, 128)
+    assert plan is not None and len(plan) >= 8
+    assert kernel._block_plan(adj.bwd, h, 128) is not None
