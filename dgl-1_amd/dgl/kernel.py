@@ -540,11 +540,11 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     dev = (ufeat2 if ufeat2 is not None else efeat2).device
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
-    if (out is None and dev.type == "cuda" and msg == MSG_COPY_U and
-            red in (RED_SUM, RED_MEAN) and efeat2 is None):
+    if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
+            red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)):
         blocks = _block_plan(csr, ufeat2, feat_len)
         if blocks is not None:
-            return _run_blocked(csr, blocks, red, ufeat2, feat_len), None
+            return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out), None
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
@@ -665,10 +665,11 @@ def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
 # fit one L2 or exceed the Infinity Cache, and rows too short to split keep
 # the one-launch schedule.
 _BLOCKED = os.environ.get("DGLHIP_BLOCKED", "auto")
-_BLOCK_BYTES = 15 << 19         # ~7.5 MiB of feature rows per block
+_BLOCK_BYTES = int(os.environ.get("DGLHIP_BLOCK_BYTES", 15 << 19))  # ~7.5 MiB per block
 _BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
 _BLOCK_TABLE_MAX = 256 << 20    # above: out's per-block pass outweighs the L2 hits
-_BLOCK_MIN_SLOTS = 8            # slots per row and block, on average
+# slots per row and block, on average (the rows' per-block pass must pay)
+_BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
 
 
 def set_blocked(policy):
@@ -682,7 +683,7 @@ def set_blocked(policy):
 
 
 def _block_count(csr, table_bytes):
-    if _BLOCKED == "off" or csr.num_rows == 0 or csr.nnz == 0:
+    if csr.num_rows == 0 or csr.nnz == 0:
         return 0
     if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
         return 0
@@ -691,19 +692,37 @@ def _block_count(csr, table_bytes):
     return int(B) if B >= 2 else 0
 
 
+def _column_span(csr):
+    """(lo, hi): the range of columns the slots reference (cached); a segment
+    of a pipelined partition references one chunk of its halo buffer."""
+    span = csr._plans.get("span")
+    if span is None:
+        if csr.nnz:
+            lo, hi = torch.aminmax(csr.indices)
+            span = (int(lo), int(hi) + 1)
+        else:
+            span = (0, 0)
+        csr._plans["span"] = span
+    return span
+
+
 def _block_plan(csr, ufeat2, feat_len):
     """The segment CSRs of the blocked schedule for ``csr`` (cached), or None
-    when the schedule does not apply or would reorder some row's chain."""
+    when the schedule does not apply or would reorder some row's chain. The
+    blocks cut the referenced column range evenly."""
+    if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
+        return None
     ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
-    B = _block_count(csr, csr.num_cols * max(ld, feat_len) * 4)
+    lo, hi = _column_span(csr)
+    B = _block_count(csr, (hi - lo) * max(ld, feat_len) * ufeat2.element_size())
     if not B:
         return None
     key = ("blocked", B)
     if key in csr._plans:
         return csr._plans[key]
     dev = csr.device
-    bs = -(-csr.num_cols // B)
-    blk = torch.div(csr.indices, bs, rounding_mode="floor")  # int32, block of each slot
+    bs = -(-(hi - lo) // B)
+    blk = torch.div(csr.indices - lo, bs, rounding_mode="floor")  # block of each slot
     first = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
     starts = csr.indptr[:-1][csr.degrees() > 0]
     first[starts] = True
@@ -724,7 +743,9 @@ def _block_plan(csr, ufeat2, feat_len):
             ro = torch.empty(csr.num_rows, dtype=torch.int32)
             check_call(LIB.dglhip_rows_by_degree_host(csr.num_rows, ptr(host_ip), ptr(ro)))
             # copy_u never reads edge ids: the segments carry none
-            plan.append(CSR(ip, csr.indices[sel], None, csr.num_cols, ro.to(dev), host_ip))
+            seg = CSR(ip, csr.indices[sel], None, csr.num_cols, ro.to(dev), host_ip)
+            seg._plans["segment"] = True  # not blocked again
+            plan.append(seg)
             del sel
     del blk, first
     csr._plans[key] = plan
@@ -742,22 +763,24 @@ def blocked_schedule(adj, ufeat):
     return 0 if plan is None else len(plan)
 
 
-def _run_blocked(csr, blocks, red, ufeat2, feat_len):
-    """copy_u + sum (mean) over the segment CSRs, each row's chain continued
-    block by block: the first block writes every row, the others add to rows
-    that have slots in them; mean divides by the degree last (the kernel's own
+def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None):
+    """copy_u (fp32 or bf16 rows) + sum (mean) over the segment CSRs, each row's chain continued
+    block by block: the first block writes every row (unless ``red`` is
+    SUM_ACCUM: then every block adds to ``out``), the others add to rows that
+    have slots in them; mean divides by the degree last (the kernel's own
     division: IEEE, by max(deg, 1))."""
-    if not _row_strided(ufeat2, feat_len) and _pad_rows(MSG_COPY_U, RED_SUM, ufeat2, feat_len):
+    if not _row_strided(ufeat2, feat_len) and _pad_rows(msg, RED_SUM, ufeat2, feat_len):
         # line-straddling rows: one padded copy for every block's launch
         ld = padded_width(feat_len)
         up = ufeat2.new_empty(ufeat2.shape[0], ld)
         up[:, :feat_len] = ufeat2
         ufeat2 = up[:, :feat_len]
-    out, _ = _run_gspmm(blocks[0], MSG_COPY_U, RED_SUM, ufeat2, None, 0, feat_len, False,
-                        out=torch.empty(csr.num_rows, feat_len, dtype=torch.float32,
-                                        device=ufeat2.device))
+    if out is None:
+        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
+    first = RED_SUM_ACCUM if red == RED_SUM_ACCUM else RED_SUM
+    _run_gspmm(blocks[0], msg, first, ufeat2, None, 0, feat_len, False, out=out)
     for seg in blocks[1:]:
-        _run_gspmm(seg, MSG_COPY_U, RED_SUM_ACCUM, ufeat2, None, 0, feat_len, False, out=out)
+        _run_gspmm(seg, msg, RED_SUM_ACCUM, ufeat2, None, 0, feat_len, False, out=out)
     if red == RED_MEAN:
         out.div_(csr.mean_divisor())
     return out

@@ -58,7 +58,7 @@ def test_plan_gate_and_host_bits(small_blocks):
     # off switch
     old = kernel.set_blocked("off")
     try:
-        assert kernel._block_count(csr, 1 << 30) == 0
+        assert kernel._block_plan(csr, h, 128) is None
     finally:
         kernel.set_blocked(old)
 
@@ -131,3 +131,40 @@ def test_bench_graph_takes_the_blocked_schedule():
     plan = kernel._block_plan(adj.fwd, h, 128)
     assert plan is not None and len(plan) >= 8
     assert kernel._block_plan(adj.bwd, h, 128) is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_blocked_accumulate_over_a_column_span(dtype):
+    """gspmm_into with accumulate over a CSR whose slots reference one range
+    of a larger buffer (a pipelined partition's halo chunk): the blocks cut
+    that range, every block adds to ``out``; bits equal the one-launch path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m, base = 120_000, 8_000_000, 150_000
+    src, dst = _graph(n, m, 6, True)
+    csr = kernel.build_csr(n, 3 * n, torch.from_numpy(dst), torch.from_numpy(src + base),
+                           kernel.ORDER_EID, dev)
+    gen = torch.Generator().manual_seed(7)
+    buf = (torch.rand(3 * n, 128, generator=gen) * 2 - 1).to(dev).to(dtype)
+    init = (torch.rand(n, 128, generator=gen) * 2 - 1).to(dev)
+
+    def run(policy, accumulate):
+        old = kernel.set_blocked(policy)
+        try:
+            out = init.clone()
+            kernel.timing_enable(True)
+            kernel.gspmm_into(csr, out, buf, accumulate=accumulate)
+            torch.cuda.synchronize()
+            _, launches = kernel.timing_read()
+            kernel.timing_enable(False)
+            return out.cpu(), launches
+        finally:
+            kernel.set_blocked(old)
+    assert kernel._column_span(csr) == (base + int(src.min()), base + int(src.max()) + 1)
+    for acc in (False, True):
+        o1, n1 = run("auto", acc)
+        o0, n0 = run("off", acc)
+        assert n1 > n0
+        assert torch.equal(o1, o0)
