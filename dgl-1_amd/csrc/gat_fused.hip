@@ -23,6 +23,14 @@
 // covers 64 * VEC features; the first lane of each head in a pass keeps and
 // stores that head's z and attention values. UNROLL slots are in flight.
 //
+// Row ranges: a row's slots are [row_beg[row], row_end[row]) of the CSR
+// (row_beg = indptr, row_end = indptr + 1 for the whole row). The
+// source-blocked schedule (kernel.py _block_cuts) runs one launch per source
+// block over the sub-range of each row whose sources lie in it, with
+// ``accumulate`` continuing both chains from out_ft / out_z: when the blocks
+// never decrease along a row's slots this is the row's own chain, and slot
+// indices (dropout hash, attention positions) stay the CSR's.
+//
 // Dropout mask: keep(k, h) = hash(seed, k * H + h) >= threshold, a stateless
 // counter hash (gat_keep below, host and device), so the backward and the host
 // path reproduce it from (seed, slot, head) alone.
@@ -111,8 +119,8 @@ __device__ __forceinline__ typename Vec<VEC>::T gat_gather(const float* ft, cons
 
 template <int VEC, int UNROLL, bool DROP, bool SMALL>
 __global__ __launch_bounds__(256) void gat_aggregate_kernel(
-    int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ indptr,
-    const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
+    int64_t num_rows, int64_t H, int64_t D, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
     const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
     float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
     const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
@@ -125,7 +133,8 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
   if (it >= num_rows) return;
   int64_t row = row_order ? row_order[it] : it;
   row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
-  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int64_t beg = row_beg[row], end = row_end[row];
+  if (accumulate && beg == end) return;  // nothing to add: the row keeps its value
   const int64_t F = H * D;
   const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
   const GatTable tab = gat_table(ft, SMALL ? table_bytes : 0);
@@ -134,8 +143,8 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
     const bool head_lane = f0 - h * D == 0;  // first lane of head h in this pass
     const uint32_t voff = static_cast<uint32_t>(f0 * int64_t(sizeof(float)));
     const float r = er[row * H + h];
-    V acc = Vec<VEC>::zero();
-    float zacc = 0.0f;
+    V acc = accumulate ? ldv<VEC>(out_ft + row * F + f0) : Vec<VEC>::zero();
+    float zacc = accumulate ? out_z[row * H + h] : 0.0f;
     auto attend = [&](float x) {
       x = x + r;
       x = x > 0.0f ? x : alpha * x;
@@ -268,8 +277,8 @@ __device__ __forceinline__ void gat_batch(
 
 template <int H, int VEC, bool DROP, bool SMALL>
 __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
-    int64_t num_rows, int64_t D, const int64_t* __restrict__ indptr,
-    const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
+    int64_t num_rows, int64_t D, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
     const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
     float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
     const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
@@ -287,7 +296,8 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
   if (it >= num_rows) return;
   int64_t row = row_order ? row_order[it] : it;
   row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
-  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int64_t beg = row_beg[row], end = row_end[row];
+  if (accumulate && beg == end) return;  // nothing to add: the row keeps its value
   const int64_t F = H * D;
   const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
   // the pairs this lane computes: head hc of slots jc + (64 / H) * i
@@ -303,6 +313,10 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     const uint32_t voff = static_cast<uint32_t>(fa * int64_t(sizeof(float)));
     V acc = Vec<VEC>::zero();
     float zacc = 0.0f;
+    if (accumulate && active) {
+      acc = ldv<VEC>(out_ft + row * F + f0);
+      if (f0 - h * D == 0) zacc = out_z[row * H + h];
+    }
     int64_t k = beg;
     for (; k + U <= end; k += U)
       gat_batch<H, VEC, DROP, SMALL, true>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab,
@@ -326,19 +340,20 @@ using namespace dglhip;
 
 extern "C" {
 
-int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_heads,
-                                int64_t head_dim, const int64_t* indptr, const int32_t* indices,
-                                const int32_t* row_order, const float* el, const float* er,
-                                const float* ft, float alpha, float clamp_lo, float clamp_hi,
-                                int apply_exp, float drop_p, uint64_t seed,
-                                const int64_t* seed_offset, float* out_ft, float* out_z,
-                                float* attn_out, float* attn_drop_out, void* stream_) {
+int dglhip_gat_aggregate_ranges_device(
+    int64_t num_rows, int64_t num_src, int64_t num_heads, int64_t head_dim,
+    const int64_t* row_beg, const int64_t* row_end, int accumulate, const int32_t* indices,
+    const int32_t* row_order, const float* el, const float* er, const float* ft, float alpha,
+    float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* out_ft, float* out_z, float* attn_out,
+    float* attn_drop_out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && num_src >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
   DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
   if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && el && er && ft && out_ft && out_z, "null pointer argument");
+  DGLHIP_CHECK(row_beg && row_end && indices && el && er && ft && out_ft && out_z,
+               "null pointer argument");
   const bool drop = drop_p > 0.0f;
   DGLHIP_CHECK(!drop || (attn_out == nullptr) == (attn_drop_out == nullptr),
                "with dropout, the attention and its dropped copy are written together");
@@ -361,13 +376,19 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
   // Reddit-shaped graph) run the per-lane kernel, 9.37 vs 9.87 ms
   // (tools/gat_bench.py). Both are bound by the line rate: per slot the
   // feature row's lines plus one line for the source's H logits.
+  // Under the source-blocked schedule (row sub-ranges, not whole rows) the
+  // gathers come from L2 and the per-lane attention's exp and hash work
+  // becomes the bound: the LDS kernel there for every width (Reddit-shaped
+  // 8 x 16: 7.39 vs 11.37 ms, with dropout 9.44 vs 17.04).
+  const bool whole_rows = row_end == row_beg + 1;
   const bool lds_heads = num_heads == 1 || num_heads == 2 || num_heads == 4 ||
                          num_heads == 8 || num_heads == 16;
-  if (lds_heads && (g_gat_variant == 2 || (g_gat_variant == 0 && !v2))) {
+  if (lds_heads && (g_gat_variant == 2 || (g_gat_variant == 0 && (!v2 || !whole_rows)))) {
     timed_launch(stream, [&] {
 #define DGLHIP_GATL(HH, VV, DD, SM)                                                        \
   hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD, SM>), grid_1d(blocks), dim3(256), \
-                     0, stream, num_rows, head_dim, indptr, indices, row_order, el, er, ft,  \
+                     0, stream, num_rows, head_dim, row_beg, row_end, accumulate, indices,   \
+                     row_order, el, er, ft,                                                  \
                      alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale,    \
                      out_ft, out_z, attn_out, attn_drop_out, tbytes)
 #define DGLHIP_GATS(HH, VV, DD) \
@@ -388,7 +409,8 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
   timed_launch(stream, [&] {
 #define DGLHIP_GAT(VV, DD, SM)                                                             \
   hipLaunchKernelGGL((gat_aggregate_kernel<VV, 16, DD, SM>), grid_1d(blocks), dim3(256), 0, \
-                     stream, num_rows, num_heads, head_dim, indptr, indices, row_order, el, \
+                     stream, num_rows, num_heads, head_dim, row_beg, row_end, accumulate,   \
+                     indices, row_order, el,                                                 \
                      er, ft, alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale, \
                      out_ft, out_z, attn_out, attn_drop_out, tbytes)
 #define DGLHIP_GATS(VV, DD) if (small) DGLHIP_GAT(VV, DD, true); else DGLHIP_GAT(VV, DD, false);
@@ -401,6 +423,19 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
 #undef DGLHIP_GAT
   });
   API_END();
+}
+
+int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_heads,
+                                int64_t head_dim, const int64_t* indptr, const int32_t* indices,
+                                const int32_t* row_order, const float* el, const float* er,
+                                const float* ft, float alpha, float clamp_lo, float clamp_hi,
+                                int apply_exp, float drop_p, uint64_t seed,
+                                const int64_t* seed_offset, float* out_ft, float* out_z,
+                                float* attn_out, float* attn_drop_out, void* stream) {
+  return dglhip_gat_aggregate_ranges_device(
+      num_rows, num_src, num_heads, head_dim, indptr, indptr ? indptr + 1 : nullptr, 0, indices,
+      row_order, el, er, ft, alpha, clamp_lo, clamp_hi, apply_exp, drop_p, seed, seed_offset,
+      out_ft, out_z, attn_out, attn_drop_out, stream);
 }
 
 int dglhip_set_gat_variant(int variant) {

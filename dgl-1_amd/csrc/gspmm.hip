@@ -58,8 +58,8 @@ __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, in
 // sequential fma chain. Both orders are fixed, so results are deterministic.
 template <bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
-    int64_t num_rows, int64_t F, int64_t H, const int64_t* __restrict__ indptr,
-    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    int64_t num_rows, int64_t F, int64_t H, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs,
     float* __restrict__ out, GatEpi epi) {
   const int64_t wave = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   const int lane = threadIdx.x & 63;
   const float* a = lhs + wave * F;
   const int64_t D = F / H;
-  for (int64_t k = indptr[wave]; k < indptr[wave + 1]; ++k) {
+  for (int64_t k = row_beg[wave]; k < row_end[wave]; ++k) {
     const float* c = rhs + int64_t(indices[k]) * F;
     if (H == 1) {
       float acc = 0.0f;
@@ -158,7 +158,7 @@ __device__ __forceinline__ void slot_reduce_scatter(float* q, int j) {
 // results are deterministic and equal the butterfly's bits.
 template <int NB, int UNROLL, int H, bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
-    int64_t num_rows, const int64_t* __restrict__ indptr,
+    int64_t num_rows, const int64_t* __restrict__ row_beg, const int64_t* __restrict__ row_end,
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out,
     GatEpi epi) {
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   if (row >= num_rows) return;
   const int lane = threadIdx.x & 63;
   const int s = lane >> 3, j = lane & 7;
-  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int64_t beg = row_beg[row], end = row_end[row];
   if (beg == end) return;
   f32x4 a[NB];
 #pragma unroll
@@ -528,10 +528,12 @@ int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
 namespace dglhip {
 
 // The SDDMM dot launch for one shape (the sliced kernel where it applies, the
-// generic one otherwise); EPI adds the GAT attention-gradient epilogue.
+// generic one otherwise); EPI adds the GAT attention-gradient epilogue. Row
+// r's slots are [row_beg[r], row_end[r]) (indptr, indptr + 1 for whole rows).
 template <bool EPI>
 static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_heads,
-                             const int64_t* indptr, const int32_t* indices, const int64_t* eid,
+                             const int64_t* row_beg, const int64_t* row_end,
+                             const int32_t* indices, const int64_t* eid,
                              const float* lhs, const float* rhs, float* out, const GatEpi& epi,
                              hipStream_t stream) {
   const int64_t blocks = (num_rows + 3) / 4;
@@ -546,7 +548,7 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
   timed_launch(stream, [&] {
 #define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
   hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI>), grid_1d(blocks), dim3(256), \
-                     0, stream, num_rows, indptr, indices, eid, lhs, rhs, out, epi)
+                     0, stream, num_rows, row_beg, row_end, indices, eid, lhs, rhs, out, epi)
 #define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
   if (num_heads == HH) {                                                                   \
     if (!g_sddmm_alt) DGLHIP_SDDMM_K(NB, U, HH);                                          \
@@ -576,7 +578,8 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
       DGLHIP_SDDMM_H(16, 1, 64) DGLHIP_SDDMM_H(16, 1, 128)
     }
     hipLaunchKernelGGL((gsddmm_dot_kernel<EPI>), grid_1d(blocks), dim3(256), 0, stream,
-                       num_rows, feat_len, num_heads, indptr, indices, eid, lhs, rhs, out, epi);
+                       num_rows, feat_len, num_heads, row_beg, row_end, indices, eid, lhs, rhs,
+                       out, epi);
 #undef DGLHIP_SDDMM_K
 #undef DGLHIP_SDDMM_H
   });
@@ -598,8 +601,27 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
-  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indices, eid, lhs, rhs, out,
-                          GatEpi{}, stream);
+  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indptr + 1, indices, eid, lhs,
+                          rhs, out, GatEpi{}, stream);
+  API_END();
+}
+
+int dglhip_gat_attention_grad_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* indices, const float* dout, const float* ft,
+    const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(row_beg && row_end && indices && dout && ft && attn && grad,
+               "null pointer argument");
+  const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp};
+  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, indices, nullptr, dout,
+                         ft, grad, epi, stream);
   API_END();
 }
 
@@ -608,18 +630,10 @@ int dglhip_gat_attention_grad_device(int64_t num_rows, int64_t feat_len, int64_t
                                      const float* dout, const float* ft, const float* attn,
                                      const float* attn_drop, const float* dz, float alpha,
                                      float clamp_lo, float clamp_hi, int apply_exp,
-                                     float drop_scale, float* grad, void* stream_) {
-  API_BEGIN();
-  hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
-  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
-               "num_heads " << num_heads << " must divide feat_len " << feat_len);
-  if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && dout && ft && attn && grad, "null pointer argument");
-  const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp};
-  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, indptr, indices, nullptr, dout, ft,
-                         grad, epi, stream);
-  API_END();
+                                     float drop_scale, float* grad, void* stream) {
+  return dglhip_gat_attention_grad_ranges_device(
+      num_rows, feat_len, num_heads, indptr, indptr ? indptr + 1 : nullptr, indices, dout, ft,
+      attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, apply_exp, drop_scale, grad, stream);
 }
 
 int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {

@@ -80,11 +80,22 @@ def _load():
                                                  _vp, ctypes.c_float, ctypes.c_float,
                                                  ctypes.c_float, _c_int, ctypes.c_float,
                                                  ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "dglhip_gat_aggregate_ranges_device": (_c_int, [_c_i64, _c_i64, _c_i64, _c_i64, _vp,
+                                                        _vp, _c_int, _vp, _vp, _vp, _vp, _vp,
+                                                        ctypes.c_float, ctypes.c_float,
+                                                        ctypes.c_float, _c_int, ctypes.c_float,
+                                                        ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
+                                                        _vp]),
         "dglhip_set_gat_variant": (_c_int, [_c_int]),
         "dglhip_gat_attention_grad_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp,
                                                       _vp, _vp, _vp, ctypes.c_float,
                                                       ctypes.c_float, ctypes.c_float, _c_int,
                                                       ctypes.c_float, _vp, _vp]),
+        "dglhip_gat_attention_grad_ranges_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp,
+                                                             _vp, _vp, _vp, _vp, _vp, _vp,
+                                                             ctypes.c_float, ctypes.c_float,
+                                                             ctypes.c_float, _c_int,
+                                                             ctypes.c_float, _vp, _vp]),
         "dglhip_gat_dropout_mask_host": (_c_int, [_c_i64, _c_i64, ctypes.c_float, ctypes.c_uint64,
                                                   _vp]),
         "dglhip_degree_bucketing_host": (_c_int, [_c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp]),

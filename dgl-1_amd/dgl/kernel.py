@@ -721,19 +721,9 @@ def _block_plan(csr, ufeat2, feat_len):
     if key in csr._plans:
         return csr._plans[key]
     dev = csr.device
-    bs = -(-(hi - lo) // B)
-    blk = torch.div(csr.indices - lo, bs, rounding_mode="floor")  # block of each slot
-    first = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
-    starts = csr.indptr[:-1][csr.degrees() > 0]
-    first[starts] = True
-    monotone = not bool(((blk[1:] < blk[:-1]) & ~first[1:]).any())
+    blk, counts = _block_counts(csr, B, lo, hi)
     plan = None
-    if monotone:
-        rid = torch.repeat_interleave(torch.arange(csr.num_rows, device=dev), csr.degrees(),
-                                      output_size=csr.nnz)
-        counts = torch.bincount(rid * B + blk.long(), minlength=csr.num_rows * B)
-        counts = counts.view(csr.num_rows, B)
-        del rid
+    if counts is not None:
         plan = []
         for b in range(B):
             sel = blk == b
@@ -747,9 +737,68 @@ def _block_plan(csr, ufeat2, feat_len):
             seg._plans["segment"] = True  # not blocked again
             plan.append(seg)
             del sel
-    del blk, first
+    del blk
     csr._plans[key] = plan
     return plan
+
+
+def _block_counts(csr, B, lo, hi):
+    """(block of each slot, per-row slot counts (num_rows, B)) for B even
+    blocks of columns [lo, hi), or (None, None) when some row's blocks
+    decrease along its slots (blocking would reorder its chain)."""
+    dev = csr.device
+    bs = -(-(hi - lo) // B)
+    blk = torch.div(csr.indices - lo, bs, rounding_mode="floor")  # block of each slot
+    first = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
+    first[csr.indptr[:-1][csr.degrees() > 0]] = True
+    monotone = not bool(((blk[1:] < blk[:-1]) & ~first[1:]).any())
+    del first
+    if not monotone:
+        return None, None
+    rid = torch.repeat_interleave(torch.arange(csr.num_rows, device=dev), csr.degrees(),
+                                  output_size=csr.nnz)
+    counts = torch.bincount(rid * B + blk.long(), minlength=csr.num_rows * B)
+    return blk, counts.view(csr.num_rows, B)
+
+
+def _block_cuts(csr, row_bytes):
+    """The blocked schedule as row ranges (cached): B + 1 int64 arrays, row r's
+    slots of block b being [cuts[b][r], cuts[b + 1][r]) of the CSR itself
+    (cuts[0] = indptr[:-1], cuts[B] = indptr[1:]), for kernels that keep the
+    CSR's slot indices (the fused GAT layer). ``row_bytes``: bytes gathered
+    per source. None when the schedule does not apply."""
+    if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
+        return None
+    lo, hi = _column_span(csr)
+    B = _block_count(csr, (hi - lo) * row_bytes)
+    if not B:
+        return None
+    key = ("cuts", B)
+    if key not in csr._plans:
+        blk, counts = _block_counts(csr, B, lo, hi)
+        cuts = None
+        if counts is not None:
+            del blk
+            start = csr.indptr[:-1]
+            cum = torch.cumsum(counts, 1)
+            cuts = [start.contiguous()] + [(start + cum[:, b]).contiguous() for b in range(B)]
+            del cum, counts
+        csr._plans[key] = cuts
+    return csr._plans[key]
+
+
+def _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, eid):
+    """sum over ``csr`` (edge values at rows ``eid`` per slot) as one
+    dglhip_gspmm_ranges_device launch per source block, every row's chain
+    continued block by block (the rows' sub-ranges ``cuts``, _block_cuts):
+    the one-launch bits when the blocks never decrease along each row."""
+    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
+    for b in range(len(cuts) - 1):
+        check_call(LIB.dglhip_gspmm_ranges_device(
+            msg, csr.num_rows, feat_len, ptr(cuts[b]), ptr(cuts[b + 1]), 1 if b else 0,
+            ptr(csr.indices), ptr(eid), ptr(ufeat2), ptr(efeat2), elen, ptr(out),
+            _stream_of(out.device)))
+    return out
 
 
 def blocked_schedule(adj, ufeat):
@@ -1421,11 +1470,18 @@ class _GATAggregate(torch.autograd.Function):
             if need:
                 a = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
                 w = torch.empty_like(a) if p > 0 else None
-            check_call(LIB.dglhip_gat_aggregate_device(
-                fwd.num_rows, ft2.shape[0], H, D, ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.row_order),
-                ptr(el), ptr(er), ptr(ft2), float(alpha), float(lo), float(hi),
-                1 if apply_exp else 0, float(p), int(seed), ptr(seed_off), ptr(out_ft),
-                ptr(out_z), ptr(a), ptr(w), _stream_of(dev)))
+            # source-blocked (exact where the blocks never decrease along a
+            # row): one launch per block, both chains continued
+            cuts = _block_cuts(fwd, (F + H) * 4)
+            if cuts is None:
+                cuts = [fwd.indptr, fwd.indptr[1:]]
+            for b in range(len(cuts) - 1):
+                check_call(LIB.dglhip_gat_aggregate_ranges_device(
+                    fwd.num_rows, ft2.shape[0], H, D, ptr(cuts[b]), ptr(cuts[b + 1]),
+                    1 if b else 0, ptr(fwd.indices), ptr(fwd.row_order), ptr(el), ptr(er),
+                    ptr(ft2), float(alpha), float(lo), float(hi), 1 if apply_exp else 0,
+                    float(p), int(seed), ptr(seed_off), ptr(out_ft), ptr(out_z), ptr(a), ptr(w),
+                    _stream_of(dev)))
         else:  # host: the same per-edge values and chains from the host kernels
             a = _attention_slots(fwd, el, er, alpha, lo, hi, apply_exp)
             w = None
@@ -1454,8 +1510,14 @@ class _GATAggregate(torch.autograd.Function):
         d_ft = torch.zeros_like(ft2) if d_ft is None else d_ft.contiguous()
         wt = w if w is not None else a
         if need_ft:
-            d_ft2, _ = _run_gspmm(adj.bwd, MSG_U_MUL_E, RED_SUM, d_ft, wt, H, F, False,
-                                  emap=_fwd_slot_of_bwd(adj))
+            emap = _fwd_slot_of_bwd(adj)
+            cuts = _block_cuts(adj.bwd, F * 4) if ft2.is_cuda else None
+            if cuts is not None:  # source-blocked: dft rows of one block at a time
+                d_ft2 = _gspmm_ranges_blocked(adj.bwd, cuts, MSG_U_MUL_E, d_ft, wt, H, F,
+                                              adj.bwd.slot_eid if emap is None else emap)
+            else:
+                d_ft2, _ = _run_gspmm(adj.bwd, MSG_U_MUL_E, RED_SUM, d_ft, wt, H, F, False,
+                                      emap=emap)
         if need_el or need_er:
             scale = gat_dropout_scale(ctx.p) if w is not None else 1.0
             if ft2.is_cuda:
@@ -1464,11 +1526,16 @@ class _GATAggregate(torch.autograd.Function):
                 # below, fused, same bits
                 g = torch.empty_like(a)
                 dz = None if d_z is None else d_z.contiguous()
-                check_call(LIB.dglhip_gat_attention_grad_device(
-                    fwd.num_rows, F, H, ptr(fwd.indptr), ptr(fwd.indices), ptr(d_ft),
-                    ptr(ft2.contiguous()), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
-                    float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
-                    ptr(g), _stream_of(ft2.device)))
+                # every slot's value is its own: the source blocks' sub-ranges
+                # (ft rows of one block at a time) give the same bits
+                cuts = _block_cuts(fwd, F * 4) or [fwd.indptr, fwd.indptr[1:]]
+                ft2c = ft2.contiguous()
+                for b in range(len(cuts) - 1):
+                    check_call(LIB.dglhip_gat_attention_grad_ranges_device(
+                        fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]), ptr(fwd.indices),
+                        ptr(d_ft), ptr(ft2c), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
+                        float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
+                        ptr(g), _stream_of(ft2.device)))
             else:
                 d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
                 if w is not None:  # dropout's backward: the kept pairs, scaled

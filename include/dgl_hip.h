@@ -438,6 +438,33 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
                                 const int64_t* seed_offset, float* out_ft, float* out_z,
                                 float* attn_out, float* attn_drop_out, void* stream);
 
+/* dglhip_gat_attention_grad_device over row ranges: row r's slots are
+ * [row_beg[r], row_end[r]) (slot indices stay the CSR's). Every slot's value
+ * is independent, so launches over the source blocks' sub-ranges give the
+ * one-launch bits (the GAT backward under the source-blocked schedule). */
+int dglhip_gat_attention_grad_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* indices, const float* dout, const float* ft,
+    const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream);
+
+/* dglhip_gat_aggregate_device over row ranges: row r's slots are
+ * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
+ * attention positions stay the CSR's); with accumulate != 0 both chains
+ * continue from out_ft / out_z and rows with an empty range are left as they
+ * are. One launch per contiguous source block, in block order, over the
+ * sub-ranges of rows whose sources never decrease in block along the row,
+ * gives the one-launch bits (the source-blocked schedule).
+ * dglhip_gat_aggregate_device is this with row_beg = indptr,
+ * row_end = indptr + 1, accumulate = 0. */
+int dglhip_gat_aggregate_ranges_device(
+    int64_t num_rows, int64_t num_src, int64_t num_heads, int64_t head_dim,
+    const int64_t* row_beg, const int64_t* row_end, int accumulate, const int32_t* indices,
+    const int32_t* row_order, const float* el, const float* er, const float* ft, float alpha,
+    float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* out_ft, float* out_z, float* attn_out,
+    float* attn_drop_out, void* stream);
+
 /* Study knob for dglhip_gat_aggregate_device: 0 (default) automatic; 1 = the
  * attention computed in every lane that consumes it; 2 = once per (slot,
  * head), shared through LDS (H in {1, 2, 4, 8, 16}). Same bits. */

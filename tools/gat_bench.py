@@ -5,6 +5,7 @@ call, hipEvent pairs on the launch stream) of
 * fused      kernel.gat_aggregate under no_grad (nothing per edge stored)
 * fused+a    the same with autograd on (the E x H attention stored, slot order)
 * fused+drop the same with attention dropout 0.6 (the dropped copy stored too)
+* *_one_launch  the same with the source-blocked schedule off
 * unfused    edge_attention(slot) + u_mul_e sum + copy_e sum (the r02 path)
 and the forward + backward ms of the fused and unfused paths.
 Algorithmic bytes of the fused forward: per edge the gathered feature row
@@ -74,6 +75,15 @@ def bench_graph(name, adj, n, E, H, D, iters):
         kernel.gspmm(adj, "u_mul_e", "sum", ft, a, edge_order="slot")
         kernel.gspmm(adj, "copy_e", "sum", None, a, edge_order="slot")
 
+    def one_launch(fn):
+        def run():
+            old = kernel.set_blocked("off")
+            try:
+                fn()
+            finally:
+                kernel.set_blocked(old)
+        return run
+
     def variant(v, fn):
         def run():
             kernel.set_gat_variant(v)
@@ -85,6 +95,8 @@ def bench_graph(name, adj, n, E, H, D, iters):
 
     for key, fn, stored in (("fused", fused_ng, 0), ("fused+a", fused_g, 4 * H),
                             ("fused+drop", fused_drop, 8 * H),
+                            ("fused_one_launch", one_launch(fused_ng), 0),
+                            ("fused+drop_one_launch", one_launch(fused_drop), 8 * H),
                             ("per_lane_kernel", variant(1, fused_ng), 0),
                             ("lds_kernel", variant(2, fused_ng), 0),
                             ("per_lane_kernel+drop", variant(1, fused_drop), 8 * H),
@@ -112,6 +124,7 @@ def bench_graph(name, adj, n, E, H, D, iters):
         torch.autograd.backward([fs, z], [gout, gz])
 
     res["fwd_bwd_wall_ms"] = {"fused": round(wall(fb_fused, iters), 3),
+                              "fused_one_launch": round(wall(one_launch(fb_fused), iters), 3),
                               "unfused": round(wall(fb_unfused, iters), 3)}
     return res
 
