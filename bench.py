@@ -762,6 +762,14 @@ def main(argv=None):
                 % (n * FEAT * 4 / 1e6, args.rmat_scale))
         if n * FEAT * 4 < INFINITY_CACHE_BYTES else
         "HBM-bound gather (H exceeds the Infinity Cache)")
+    if blocks:
+        roof["launches_per_call"] = blocks  # bytes_per_launch / kernel_ms: per call
+        if pmc is not None and kernel_ms > 0:
+            # the bytes the L2s did not serve, against the rate the fabric
+            # serves random rows at (the Infinity-Cache row rate)
+            rate = pmc["bytes"] / (kernel_ms * 1e-3) / 1e9
+            roof["l2_miss_traffic_GBs"] = rate
+            roof["l2_miss_traffic_frac"] = rate / IC_GATHER_PEAK_GBS
     result = {
         "metric": "edges/sec on update_all g-SpMM (copy_u+sum, feat=128)",
         "value": value,

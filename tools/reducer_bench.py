@@ -48,7 +48,7 @@ def main():
             kernel.gspmm(adj, msg, red, h, e, edge_order=order)
         ms, cnt = kernel.timing_read()
         kernel.timing_enable(False)
-        t = ms / max(cnt, 1)
+        t = ms / args.iters  # per call (a blocked call launches several kernels)
         per_edge = 4 * F + 4 + ((12 if order == "eid" else 4) if e is not None else 0)
         per_row = 4 * F + 8
         byts = E * per_edge + n * per_row
@@ -72,7 +72,7 @@ def main():
                 ms, cnt = kernel.timing_read()
                 kernel.timing_enable(False)
                 kernel.set_sddmm_variant(0)
-                t = ms / max(cnt, 1)
+                t = ms / args.iters  # per call (a blocked call launches several kernels)
                 byts = E * (4 * F + 4 + (8 if order == "eid" else 0) + 4 * heads) + \
                     n * (4 * F + 8)
                 res.append({"msg": "sddmm_dot", "reduce": "heads=%d" % heads,
@@ -92,7 +92,7 @@ def main():
             kernel.edge_attention(adj, a1, a2, E, edge_order=order)
         ms, cnt = kernel.timing_read()
         kernel.timing_enable(False)
-        t = ms / max(cnt, 1)
+        t = ms / args.iters  # per call (a blocked call launches several kernels)
         byts = E * (4 + 32 + 32 + (8 if order == "eid" else 0)) + n * (32 + 8)
         res.append({"msg": "edge_attention", "reduce": "heads=8", "edge_order": order,
                     "kernel_ms": round(t, 3), "edges_per_s": E / (t * 1e-3),
