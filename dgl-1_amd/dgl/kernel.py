@@ -665,7 +665,7 @@ def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
 # fit one L2 or exceed the Infinity Cache, and rows too short to split keep
 # the one-launch schedule.
 _BLOCKED = os.environ.get("DGLHIP_BLOCKED", "auto")
-_BLOCK_BYTES = int(os.environ.get("DGLHIP_BLOCK_BYTES", 15 << 19))  # ~7.5 MiB per block
+_BLOCK_BYTES = int(os.environ.get("DGLHIP_BLOCK_BYTES", 6 << 20))  # 6 MiB per block
 _BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
 _BLOCK_TABLE_MAX = 256 << 20    # above: out's per-block pass outweighs the L2 hits
 # slots per row and block, on average (the rows' per-block pass must pay)
@@ -682,12 +682,12 @@ def set_blocked(policy):
     return old
 
 
-def _block_count(csr, table_bytes):
+def _block_count(csr, table_bytes, block_bytes=None):
     if csr.num_rows == 0 or csr.nnz == 0:
         return 0
     if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
         return 0
-    B = -(-table_bytes // _BLOCK_BYTES)
+    B = -(-table_bytes // (block_bytes or _BLOCK_BYTES))
     B = min(B, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
     return int(B) if B >= 2 else 0
 
@@ -761,7 +761,12 @@ def _block_counts(csr, B, lo, hi):
     return blk, counts.view(csr.num_rows, B)
 
 
-def _block_cuts(csr, row_bytes):
+# the fused GAT kernels' blocks: their per-row work (the attention through LDS)
+# makes a row's pass per block dearer than copy_u's, so fewer, larger blocks
+_GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11 MiB
+
+
+def _block_cuts(csr, row_bytes, block_bytes=None):
     """The blocked schedule as row ranges (cached): B + 1 int64 arrays, row r's
     slots of block b being [cuts[b][r], cuts[b + 1][r]) of the CSR itself
     (cuts[0] = indptr[:-1], cuts[B] = indptr[1:]), for kernels that keep the
@@ -770,7 +775,7 @@ def _block_cuts(csr, row_bytes):
     if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
         return None
     lo, hi = _column_span(csr)
-    B = _block_count(csr, (hi - lo) * row_bytes)
+    B = _block_count(csr, (hi - lo) * row_bytes, block_bytes or _GAT_BLOCK_BYTES)
     if not B:
         return None
     key = ("cuts", B)
@@ -1457,12 +1462,14 @@ class _GATAggregate(torch.autograd.Function):
     dot, the copy_e gather, the attention's backward): same bits."""
 
     @staticmethod
-    def forward(ctx, adj, alpha, lo, hi, apply_exp, p, seed, seed_off, el, er, ft2, D):
+    def forward(ctx, adj, alpha, lo, hi, apply_exp, p, seed, seed_off, el, er, ft2, D, grad_mode):
         fwd = adj.fwd
         H = el.shape[1]
         F = ft2.shape[1]
         dev = ft2.device
-        need = any(ctx.needs_input_grad[8:11])
+        # needs_input_grad follows requires_grad even under torch.no_grad():
+        # the caller's grad mode decides whether a backward can follow
+        need = grad_mode and any(ctx.needs_input_grad[8:11])
         a = w = None
         if dev.type == "cuda":
             out_ft = torch.empty(fwd.num_rows, F, dtype=torch.float32, device=dev)
@@ -1556,7 +1563,7 @@ class _GATAggregate(torch.autograd.Function):
                                      emap=_fwd_slot_of_bwd(adj))
             if need_er:
                 d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
-        return (None,) * 8 + (d_el, d_er, d_ft2, None)
+        return (None,) * 8 + (d_el, d_er, d_ft2, None, None)
 
 
 def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0,
@@ -1595,5 +1602,5 @@ def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0
             seed = int(torch.randint(0, 1 << 62, (1,)).item())
     ft_sum, z = _GATAggregate.apply(adj, float(alpha), float(clamp[0]), float(clamp[1]),
                                     bool(apply_exp), p, int(seed or 0), seed_off, el2, er2,
-                                    ft2, D)
+                                    ft2, D, torch.is_grad_enabled())
     return ft_sum.view(-1, H, D), z.view(-1, H, 1)

@@ -228,3 +228,19 @@ def test_source_blocked_gat_bits(H, D, p):
     assert torch.equal(fs1, fs0) and torch.equal(z1, z0)
     for a, b in zip(g1, g0):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_no_grad_stores_no_attention(device):
+    """Under torch.no_grad() the fused layer keeps no E x H attention even
+    when its inputs require grad (needs_input_grad alone does not say a
+    backward will follow); the outputs are the same bits."""
+    dev = _dev(device)
+    g = _graph(n=500, m=5000)
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(g.number_of_nodes(), 4, 8, dev)
+    with torch.no_grad():
+        fs, z = kernel.gat_aggregate(adj, ft, el, er)
+    fs2, z2 = kernel.gat_aggregate(adj, ft, el, er)
+    assert torch.equal(fs, fs2.detach()) and torch.equal(z, z2.detach())
+    assert fs.grad_fn is None and fs2.grad_fn is not None
