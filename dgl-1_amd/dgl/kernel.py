@@ -657,13 +657,15 @@ def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
 # same slice of H at a time, which their 4 MiB L2s serve, instead of from the
 # whole table through the Infinity Cache (Reddit-shaped graph, F = 128: 7.41
 # -> 4.21 ms at B = 16, tools/blocked_study.py). Used only where it keeps
-# every chain: when along each row's slots (edge-id order) the sources'
-# blocks never decrease — then block by block IS the row's order, and the
-# results are bit-identical (true of graphs whose edges are numbered
-# source-major, as the (src, dst)-sorted loaders, the synthetic generators and
-# the transposed CSR of any such graph give them). Other graphs, tables that
-# fit one L2 or exceed the Infinity Cache, and rows too short to split keep
-# the one-launch schedule.
+# every chain: along each row's slots (edge-id order) the sources' blocks
+# never decrease over a prefix of the row — then block by block IS the
+# prefix's order — and the slots after it (at most 1/16 of all) continue the
+# chain in one last launch, in order. The results are bit-identical. Graphs
+# whose edges are numbered source-major qualify whole (the (src, dst)-sorted
+# loaders, the synthetic generators, the transposed CSR of any such graph),
+# and so do such graphs with edges appended later (GCN's self-loops: one
+# suffix slot per row). Other graphs, tables that fit one L2 or exceed the
+# Infinity Cache, and rows too short to split keep the one-launch schedule.
 _BLOCKED = os.environ.get("DGLHIP_BLOCKED", "auto")
 _BLOCK_BYTES = int(os.environ.get("DGLHIP_BLOCK_BYTES", 6 << 20))  # 6 MiB per block
 _BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
@@ -720,45 +722,73 @@ def _block_plan(csr, ufeat2, feat_len):
     key = ("blocked", B)
     if key in csr._plans:
         return csr._plans[key]
-    dev = csr.device
-    blk, counts = _block_counts(csr, B, lo, hi)
+    split = _block_split(csr, B, lo, hi)
     plan = None
-    if counts is not None:
+    if split is not None:
+        blk, counts, pre, sfx = split
         plan = []
         for b in range(B):
-            sel = blk == b
-            ip = torch.zeros(csr.num_rows + 1, dtype=torch.int64, device=dev)
-            torch.cumsum(counts[:, b], 0, out=ip[1:])
-            host_ip = ip.cpu()
-            ro = torch.empty(csr.num_rows, dtype=torch.int32)
-            check_call(LIB.dglhip_rows_by_degree_host(csr.num_rows, ptr(host_ip), ptr(ro)))
-            # copy_u never reads edge ids: the segments carry none
-            seg = CSR(ip, csr.indices[sel], None, csr.num_cols, ro.to(dev), host_ip)
-            seg._plans["segment"] = True  # not blocked again
-            plan.append(seg)
+            sel = blk == b if pre is None else (blk == b) & pre
+            plan.append(_segment_csr(csr, counts[:, b], csr.indices[sel]))
             del sel
-    del blk
+        if pre is not None:  # each row's slots after its monotone prefix, run last
+            plan.append(_segment_csr(csr, sfx, csr.indices[~pre]))
+        del blk, counts, pre, sfx
     csr._plans[key] = plan
     return plan
 
 
-def _block_counts(csr, B, lo, hi):
-    """(block of each slot, per-row slot counts (num_rows, B)) for B even
-    blocks of columns [lo, hi), or (None, None) when some row's blocks
-    decrease along its slots (blocking would reorder its chain)."""
+def _segment_csr(csr, row_counts, indices):
+    """A CSR over ``csr``'s rows with ``row_counts`` slots each (``indices``
+    in order), degree-descending schedule, no edge ids (copy_u reads none),
+    never blocked again."""
+    ip = torch.zeros(csr.num_rows + 1, dtype=torch.int64, device=csr.device)
+    torch.cumsum(row_counts, 0, out=ip[1:])
+    host_ip = ip.cpu()
+    ro = torch.empty(csr.num_rows, dtype=torch.int32)
+    check_call(LIB.dglhip_rows_by_degree_host(csr.num_rows, ptr(host_ip), ptr(ro)))
+    seg = CSR(ip, indices, None, csr.num_cols, ro.to(csr.device), host_ip)
+    seg._plans["segment"] = True
+    return seg
+
+
+# at most this share of the slots may follow their row's monotone prefix
+# (GCN's self-loops, appended after the edges: one slot per row)
+_BLOCK_MAX_SUFFIX = 1.0 / 16
+
+
+def _block_split(csr, B, lo, hi):
+    """The blocked schedule of ``csr`` over B even blocks of columns [lo, hi):
+    (block of each slot, per-row counts (num_rows, B) of the slots in each
+    row's monotone prefix, prefix mask or None when every row is monotone,
+    per-row suffix counts or None). A row's prefix runs up to its first slot
+    whose block is lower than the previous slot's; blocks then keep the
+    prefix's chain, and the suffix continues it in one last launch. None when
+    the suffixes exceed _BLOCK_MAX_SUFFIX of the slots."""
     dev = csr.device
+    R = csr.num_rows
     bs = -(-(hi - lo) // B)
     blk = torch.div(csr.indices - lo, bs, rounding_mode="floor")  # block of each slot
-    first = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
-    first[csr.indptr[:-1][csr.degrees() > 0]] = True
-    monotone = not bool(((blk[1:] < blk[:-1]) & ~first[1:]).any())
-    del first
-    if not monotone:
-        return None, None
-    rid = torch.repeat_interleave(torch.arange(csr.num_rows, device=dev), csr.degrees(),
-                                  output_size=csr.nnz)
-    counts = torch.bincount(rid * B + blk.long(), minlength=csr.num_rows * B)
-    return blk, counts.view(csr.num_rows, B)
+    deg = csr.degrees()
+    dec = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
+    dec[1:] = blk[1:] < blk[:-1]
+    dec[csr.indptr[:-1][deg > 0]] = False  # a row's first slot starts its chain
+    rid = torch.repeat_interleave(torch.arange(R, device=dev), deg, output_size=csr.nnz)
+    pre = sfx = None
+    key = rid * B + blk
+    if bool(dec.any()):
+        cs = torch.cumsum(dec, 0)
+        # decreases before each row's first slot (not one itself): in-row count = cs - base
+        base = cs[csr.indptr[:-1].clamp(max=csr.nnz - 1)]
+        pre = (cs - base[rid]) == 0
+        del cs, base
+        if csr.nnz - int(pre.sum()) > csr.nnz * _BLOCK_MAX_SUFFIX:
+            return None
+        sfx = torch.bincount(rid[~pre], minlength=R)
+        key = key[pre]
+    del dec, rid
+    counts = torch.bincount(key, minlength=R * B).view(R, B)
+    return blk, counts, pre, sfx
 
 
 # the fused GAT kernels' blocks: their per-row work (the attention through LDS)
@@ -767,11 +797,12 @@ _GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11
 
 
 def _block_cuts(csr, row_bytes, block_bytes=None):
-    """The blocked schedule as row ranges (cached): B + 1 int64 arrays, row r's
-    slots of block b being [cuts[b][r], cuts[b + 1][r]) of the CSR itself
-    (cuts[0] = indptr[:-1], cuts[B] = indptr[1:]), for kernels that keep the
-    CSR's slot indices (the fused GAT layer). ``row_bytes``: bytes gathered
-    per source. None when the schedule does not apply."""
+    """The blocked schedule as row ranges (cached): B + 1 int64 arrays (B + 2
+    when some rows have a suffix, _block_split), row r's slots of range i being
+    [cuts[i][r], cuts[i + 1][r]) of the CSR itself (cuts[0] = indptr[:-1], the
+    last = indptr[1:]), for kernels that keep the CSR's slot indices (the
+    fused GAT layer). ``row_bytes``: bytes gathered per source. None when the
+    schedule does not apply."""
     if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
         return None
     lo, hi = _column_span(csr)
@@ -780,14 +811,16 @@ def _block_cuts(csr, row_bytes, block_bytes=None):
         return None
     key = ("cuts", B)
     if key not in csr._plans:
-        blk, counts = _block_counts(csr, B, lo, hi)
+        split = _block_split(csr, B, lo, hi)
         cuts = None
-        if counts is not None:
-            del blk
+        if split is not None:
+            _, counts, pre, _ = split
             start = csr.indptr[:-1]
             cum = torch.cumsum(counts, 1)
             cuts = [start.contiguous()] + [(start + cum[:, b]).contiguous() for b in range(B)]
-            del cum, counts
+            if pre is not None:  # the suffixes: one more range, run last
+                cuts.append(csr.indptr[1:].contiguous())
+            del cum, counts, split
         csr._plans[key] = cuts
     return csr._plans[key]
 

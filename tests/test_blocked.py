@@ -63,6 +63,35 @@ def test_plan_gate_and_host_bits(small_blocks):
         kernel.set_blocked(old)
 
 
+def test_suffix_after_monotone_prefix(small_blocks):
+    """Edges appended after a source-major list (GCN's self-loops): each row's
+    monotone prefix is blocked and the rest runs last, in order; the host
+    run of the plan equals the oracle's chain bit for bit. A random-order
+    graph's suffixes are too long: no plan."""
+    n, m = 2000, 200_000
+    src, dst = _graph(n, m, 0, True)
+    ar = np.arange(n)
+    src, dst = np.concatenate([src, ar]), np.concatenate([dst, ar])
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                           kernel.ORDER_EID, "cpu")
+    h = torch.randn(n, 128, generator=torch.Generator().manual_seed(1))
+    plan = kernel._block_plan(csr, h, 128)
+    assert plan is not None and len(plan) >= 3
+    assert sum(p.nnz for p in plan) == csr.nnz
+    assert 0 < plan[-1].nnz <= n  # at most each row's self-loop
+    ref = torch.from_numpy(O.spmm_coo(n, dst, src, h.numpy()))
+    out = torch.empty(n, 128)
+    kernel._run_gspmm(plan[0], kernel.MSG_COPY_U, kernel.RED_SUM, h, None, 0, 128, False,
+                      out=out)
+    for seg in plan[1:]:
+        kernel._run_gspmm(seg, kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, h, None, 0, 128,
+                          False, out=out)
+    assert torch.equal(out, ref)
+    cuts = kernel._block_cuts(csr, 128 * 4, 1 << 16)
+    assert cuts is not None and len(cuts) == len(plan) + 1
+    assert torch.equal(cuts[-1], csr.indptr[1:]) and torch.equal(cuts[0], csr.indptr[:-1])
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("F", [128, 41])
 @pytest.mark.parametrize("reduce", ["sum", "mean"])
@@ -168,3 +197,38 @@ def test_blocked_accumulate_over_a_column_span(dtype):
         o0, n0 = run("off", acc)
         assert n1 > n0
         assert torch.equal(o1, o0)
+
+
+@pytest.mark.gpu
+def test_gcn_self_loops_blocked_bits():
+    """The GCN example's graph (edges, then self-loops appended) takes the
+    blocked schedule with a suffix launch; forward and backward equal the
+    one-launch path and the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 12, True)
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+    g.add_edges(g.nodes(), g.nodes())
+    adj = g.sparse_adjacency(dev)
+    H = torch.randn(n, 128, generator=torch.Generator().manual_seed(2))
+    plan = kernel._block_plan(adj.fwd, H.to(dev), 128)
+    assert plan is not None and plan[-1].nnz > 0
+
+    def run(policy):
+        old = kernel.set_blocked(policy)
+        try:
+            h = H.to(dev).requires_grad_(True)
+            g.ndata["h"] = h
+            g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+            g.ndata["o"].backward(torch.ones(n, 128, device=dev))
+            return g.ndata["o"].detach().cpu(), h.grad.cpu()
+        finally:
+            kernel.set_blocked(old)
+    o1, g1 = run("auto")
+    o0, g0 = run("off")
+    assert torch.equal(o1, o0) and torch.equal(g1, g0)
+    s2 = np.concatenate([src, np.arange(n)])
+    d2 = np.concatenate([dst, np.arange(n)])
+    assert np.array_equal(o1.numpy(), O.spmm_coo(n, d2, s2, H.numpy()))
