@@ -542,9 +542,23 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
     if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
             red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)):
+        if _BLOCKED == "ranges" and _plain_rows(msg, red, ufeat2, feat_len):  # study knob
+            cuts = _block_cuts(csr, feat_len * 4, _BLOCK_BYTES)
+            if cuts is not None:
+                return _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, None, 0, feat_len, None,
+                                             red, out), None
         blocks = _block_plan(csr, ufeat2, feat_len)
         if blocks is not None:
             return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out), None
+    if (dev.type == "cuda" and msg == MSG_U_MUL_E and red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)
+            and ufeat2 is not None and ufeat2.dtype == torch.float32 and efeat2 is not None):
+        blocks = _block_plan(csr, ufeat2, feat_len)
+        if blocks is not None:
+            # the edge values in the segments' slot order, one gather per call
+            rows = _block_edge_rows(csr, blocks, emap)
+            e_blk = efeat2.index_select(0, rows)
+            return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out, e_blk,
+                                elen), None
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
@@ -675,9 +689,10 @@ _BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
 
 
 def set_blocked(policy):
-    """Source-blocked schedule for copy_u sum / mean: "auto" (default: where
-    it keeps the chains bit-identical and the table size pays) or "off";
-    returns the old policy."""
+    """Source-blocked schedule for copy_u / u_mul_e with sum / mean: "auto"
+    (default: where it keeps the chains bit-identical and the table size
+    pays) or "off"; "ranges" (study) runs copy_u over row ranges of the CSR
+    itself instead of segment CSRs. Returns the old policy."""
     global _BLOCKED
     old = _BLOCKED
     _BLOCKED = str(policy)
@@ -733,6 +748,7 @@ def _block_plan(csr, ufeat2, feat_len):
             del sel
         if pre is not None:  # each row's slots after its monotone prefix, run last
             plan.append(_segment_csr(csr, sfx, csr.indices[~pre]))
+            plan[-1]._plans["suffix"] = True
         del blk, counts, pre, sfx
     csr._plans[key] = plan
     return plan
@@ -825,17 +841,30 @@ def _block_cuts(csr, row_bytes, block_bytes=None):
     return csr._plans[key]
 
 
-def _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, eid):
-    """sum over ``csr`` (edge values at rows ``eid`` per slot) as one
-    dglhip_gspmm_ranges_device launch per source block, every row's chain
-    continued block by block (the rows' sub-ranges ``cuts``, _block_cuts):
-    the one-launch bits when the blocks never decrease along each row."""
-    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
+def _plain_rows(msg, red, ufeat2, feat_len):
+    """fp32 source rows the row-range kernel reads as they are (contiguous,
+    no padded-stride copy due)."""
+    return (ufeat2 is not None and ufeat2.dtype == torch.float32 and ufeat2.dim() == 2 and
+            ufeat2.is_contiguous() and ufeat2.shape[1] == feat_len and
+            not _pad_rows(msg, red, ufeat2, feat_len))
+
+
+def _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, eid, red=RED_SUM,
+                          out=None):
+    """sum (mean, sum_accum) over ``csr`` (edge values at rows ``eid`` per
+    slot, or by slot when None) as one dglhip_gspmm_ranges_device launch per
+    source block, every row's chain continued range by range (the rows'
+    sub-ranges ``cuts``, _block_cuts): the one-launch bits. Mean divides by
+    the degree last, as the kernel does."""
+    if out is None:
+        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
     for b in range(len(cuts) - 1):
         check_call(LIB.dglhip_gspmm_ranges_device(
-            msg, csr.num_rows, feat_len, ptr(cuts[b]), ptr(cuts[b + 1]), 1 if b else 0,
-            ptr(csr.indices), ptr(eid), ptr(ufeat2), ptr(efeat2), elen, ptr(out),
-            _stream_of(out.device)))
+            msg, csr.num_rows, feat_len, ptr(cuts[b]), ptr(cuts[b + 1]),
+            1 if (b or red == RED_SUM_ACCUM) else 0, ptr(csr.indices), ptr(eid), ptr(ufeat2),
+            ptr(efeat2), elen, ptr(out), _stream_of(out.device)))
+    if red == RED_MEAN:
+        out.div_(csr.mean_divisor())
     return out
 
 
@@ -850,7 +879,45 @@ def blocked_schedule(adj, ufeat):
     return 0 if plan is None else len(plan)
 
 
-def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None):
+def _block_slots(csr, plan):
+    """int64: for each slot of the blocked plan's segments, in order, the
+    slot of ``csr`` it came from (cached; built on the first edge-valued
+    call)."""
+    key = ("blocked_slots", len(plan))
+    if key not in csr._plans:
+        B = len(plan) - (1 if plan[-1]._plans.get("suffix") else 0)
+        lo, hi = _column_span(csr)
+        blk, _, pre, _ = _block_split(csr, B, lo, hi)
+        parts = []
+        for b in range(B):
+            sel = blk == b if pre is None else (blk == b) & pre
+            parts.append(torch.nonzero(sel).squeeze(1))
+        if pre is not None:
+            parts.append(torch.nonzero(~pre).squeeze(1))
+        csr._plans[key] = torch.cat(parts)
+        del blk, pre, parts
+    return csr._plans[key]
+
+
+def _block_edge_rows(csr, plan, emap):
+    """Rows of the edge-value tensor for the blocked plan's slots, for the
+    layout ``emap`` names (_run_gspmm): None = edge ids (cached), SLOT = the
+    CSR's slots, or a per-slot row tensor."""
+    nseg = len(plan)
+    slots = _block_slots(csr, plan)
+    if emap is SLOT:
+        return slots
+    if emap is not None:
+        return emap.index_select(0, slots)
+    if csr.slot_eid is None:
+        return slots
+    key = ("blocked_eid", nseg)
+    if key not in csr._plans:
+        csr._plans[key] = csr.slot_eid.index_select(0, slots)
+    return csr._plans[key]
+
+
+def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None, efeat=None, elen=0):
     """copy_u (fp32 or bf16 rows) + sum (mean) over the segment CSRs, each row's chain continued
     block by block: the first block writes every row (unless ``red`` is
     SUM_ACCUM: then every block adds to ``out``), the others add to rows that
@@ -864,10 +931,15 @@ def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None):
         ufeat2 = up[:, :feat_len]
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
-    first = RED_SUM_ACCUM if red == RED_SUM_ACCUM else RED_SUM
-    _run_gspmm(blocks[0], msg, first, ufeat2, None, 0, feat_len, False, out=out)
-    for seg in blocks[1:]:
-        _run_gspmm(seg, msg, RED_SUM_ACCUM, ufeat2, None, 0, feat_len, False, out=out)
+    off = 0
+    for i, seg in enumerate(blocks):
+        r = RED_SUM_ACCUM if (i or red == RED_SUM_ACCUM) else RED_SUM
+        # u_mul_e: each segment's edge values, in its slot order (efeat is
+        # the plan's slots' values, segment after segment)
+        e = None if efeat is None else efeat[off:off + seg.nnz]
+        _run_gspmm(seg, msg, r, ufeat2, e, elen, feat_len, False, out=out,
+                   emap=None if efeat is None else SLOT)
+        off += seg.nnz
     if red == RED_MEAN:
         out.div_(csr.mean_divisor())
     return out

@@ -232,3 +232,66 @@ def test_gcn_self_loops_blocked_bits():
     s2 = np.concatenate([src, np.arange(n)])
     d2 = np.concatenate([dst, np.arange(n)])
     assert np.array_equal(o1.numpy(), O.spmm_coo(n, d2, s2, H.numpy()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("order", ["eid", "slot"])
+@pytest.mark.parametrize("reduce", ["sum", "mean"])
+def test_blocked_u_mul_e_bits(order, reduce):
+    """u_mul_e (scalar and per-head edge values) over the blocks' row ranges:
+    forward and both gradients equal the one-launch kernels."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 13, True)
+    adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                          kernel.ORDER_EID, dev)
+    gen = torch.Generator().manual_seed(14)
+    H = torch.randn(n, 128, generator=gen).to(dev)
+    for w in (torch.rand(m, 1, generator=gen), torch.rand(m, 4, 1, generator=gen)):
+        w = w.to(dev)
+        h3 = H if w.dim() == 2 else H.view(n, 4, 32)
+
+        def run(policy):
+            old = kernel.set_blocked(policy)
+            try:
+                h = h3.clone().requires_grad_(True)
+                we = w.clone().requires_grad_(True)
+                kernel.timing_enable(True)
+                o = kernel.gspmm(adj, "u_mul_e", reduce, h, we, edge_order=order)
+                torch.cuda.synchronize()
+                _, launches = kernel.timing_read()
+                kernel.timing_enable(False)
+                o.backward(torch.ones_like(o))
+                return o.detach().cpu(), h.grad.cpu(), we.grad.cpu(), launches
+            finally:
+                kernel.set_blocked(old)
+        a = run("auto")
+        b = run("off")
+        assert a[3] > b[3]
+        for x, y in zip(a[:3], b[:3]):
+            assert torch.equal(x, y)
+
+
+def test_u_mul_e_plan_slot_map(small_blocks):
+    """The blocked plan's slot map (segments in order, suffix last) covers
+    every slot once, and the host run of u_mul_e over it with the gathered
+    edge values equals the one-launch host kernel bit for bit."""
+    n, m = 2000, 200_000
+    src, dst = _graph(n, m, 3, True)
+    ar = np.arange(n)
+    src, dst = np.concatenate([src, ar]), np.concatenate([dst, ar])
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                           kernel.ORDER_EID, "cpu")
+    gen = torch.Generator().manual_seed(5)
+    h = torch.randn(n, 128, generator=gen)
+    w = torch.rand(csr.nnz, 1, generator=gen)
+    plan = kernel._block_plan(csr, h, 128)
+    slots = kernel._block_slots(csr, plan)
+    assert torch.equal(torch.sort(slots)[0], torch.arange(csr.nnz))
+    rows = kernel._block_edge_rows(csr, plan, None)
+    out = kernel._run_blocked(csr, plan, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, 128, None,
+                              w.index_select(0, rows), 1)
+    ref, _ = kernel._run_gspmm(csr, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, w, 1, 128, False)
+    assert torch.equal(out, ref)
