@@ -292,6 +292,17 @@ def test_u_mul_e_plan_slot_map(small_blocks):
     assert torch.equal(torch.sort(slots)[0], torch.arange(csr.nnz))
     rows = kernel._block_edge_rows(csr, plan, None)
     out = kernel._run_blocked(csr, plan, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, 128, None,
+                              w, 1, rows)
+    pre = kernel._run_blocked(csr, plan, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, 128, None,
                               w.index_select(0, rows), 1)
+    assert torch.equal(out, pre)
     ref, _ = kernel._run_gspmm(csr, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, w, 1, 128, False)
     assert torch.equal(out, ref)
+    # a per-slot row map: composed once per tensor object, anew when it changes
+    emap = torch.randperm(csr.nnz)
+    r1 = kernel._block_edge_rows(csr, plan, emap)
+    assert kernel._block_edge_rows(csr, plan, emap) is r1
+    assert torch.equal(r1, emap[slots])
+    emap[:5] = emap[:5].flip(0)
+    r2 = kernel._block_edge_rows(csr, plan, emap)
+    assert r2 is not r1 and torch.equal(r2, emap[slots])
