@@ -3,7 +3,7 @@
 # line, its kernel trace + per-call sum, emulated N=2/4/8 ranks, GAT bench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-OUT=gpurun_out/r03m3
+OUT=${OUT:-gpurun_out/r03m3}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
