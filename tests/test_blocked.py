@@ -306,3 +306,35 @@ def test_u_mul_e_plan_slot_map(small_blocks):
     emap[:5] = emap[:5].flip(0)
     r2 = kernel._block_edge_rows(csr, plan, emap)
     assert r2 is not r1 and torch.equal(r2, emap[slots])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("halo", ["allgather", "alltoall"])
+def test_pipelined_segments_blocked_bits(halo):
+    """An emulated rank of a 2-rank partition (no communication: the halo
+    rows are the rank's own random landing buffer): its pipelined segments
+    (own rows, then each halo chunk, continued with SUM_ACCUM) take the
+    blocked schedule over their column spans, with the one-launch bits."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from dgl.distributed import PartitionedGraph, balanced_bounds
+    dev = torch.device("cuda", 0)
+    n, m, W = 200_000, 24_000_000, 2
+    src, dst = _graph(n, m, 15, True)
+    src, dst = torch.from_numpy(src).to(dev), torch.from_numpy(dst).to(dev)
+    bounds = balanced_bounds(torch.bincount(dst, minlength=n), W)
+    lo, hi = int(bounds[0]), int(bounds[1])
+    sel = (dst >= lo) & (dst < hi)
+    pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev, pipeline_chunks=4, rank=0,
+                          world=W, halo=halo)
+    h_local = torch.rand(hi - lo, 128, generator=torch.Generator().manual_seed(16)).to(dev)
+    pg.update_all(h_local)  # lands the emulated halo rows
+    assert kernel._block_plan(pg.seg_csrs[0], h_local, 128) is not None
+
+    def run(policy):
+        old = kernel.set_blocked(policy)
+        try:
+            return pg.update_all(h_local).cpu()
+        finally:
+            kernel.set_blocked(old)
+    assert torch.equal(run("auto"), run("off"))
