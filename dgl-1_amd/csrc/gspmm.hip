@@ -59,11 +59,13 @@ __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, in
 template <bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
     int64_t num_rows, int64_t F, int64_t H, const int64_t* __restrict__ row_beg,
-    const int64_t* __restrict__ row_end, const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const int64_t* __restrict__ row_end, const int32_t* __restrict__ row_order,
+    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs,
     float* __restrict__ out, GatEpi epi) {
-  const int64_t wave = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
-  if (wave >= num_rows) return;
+  const int64_t it = block_linear() * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (it >= num_rows) return;
+  const int64_t wave = row_order ? row_order[it] : it;
   const int lane = threadIdx.x & 63;
   const float* a = lhs + wave * F;
   const int64_t D = F / H;
@@ -159,7 +161,7 @@ __device__ __forceinline__ void slot_reduce_scatter(float* q, int j) {
 template <int NB, int UNROLL, int H, bool EPI = false>
 __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
     int64_t num_rows, const int64_t* __restrict__ row_beg, const int64_t* __restrict__ row_end,
-    const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
+    const int32_t* __restrict__ row_order, const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ lhs, const float* __restrict__ rhs, float* __restrict__ out,
     GatEpi epi) {
   constexpr int F = NB * 32;
@@ -167,9 +169,11 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   constexpr int LPH = D >= 32 ? 8 : D / 4;  // lanes sharing a head
   constexpr int DBLK = D >= 32 ? D / 32 : 1;  // blocks per head (D >= 32)
   static_assert(D >= 32 ? D % 32 == 0 : (D == 4 || D == 8 || D == 16), "head width");
-  const int64_t row = block_linear() * (blockDim.x >> 6) +
-                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  if (row >= num_rows) return;
+  const int64_t it = block_linear() * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_rows) return;
+  // rows in the given schedule (degree-descending: the longest rows first)
+  const int64_t row = row_order ? __builtin_amdgcn_readfirstlane(row_order[it]) : it;
   const int lane = threadIdx.x & 63;
   const int s = lane >> 3, j = lane & 7;
   const int64_t beg = row_beg[row], end = row_end[row];
@@ -533,7 +537,8 @@ namespace dglhip {
 template <bool EPI>
 static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_heads,
                              const int64_t* row_beg, const int64_t* row_end,
-                             const int32_t* indices, const int64_t* eid,
+                             const int32_t* row_order, const int32_t* indices,
+                             const int64_t* eid,
                              const float* lhs, const float* rhs, float* out, const GatEpi& epi,
                              hipStream_t stream) {
   const int64_t blocks = (num_rows + 3) / 4;
@@ -548,7 +553,8 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
   timed_launch(stream, [&] {
 #define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
   hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI>), grid_1d(blocks), dim3(256), \
-                     0, stream, num_rows, row_beg, row_end, indices, eid, lhs, rhs, out, epi)
+                     0, stream, num_rows, row_beg, row_end, row_order, indices, eid, lhs, rhs,  \
+                     out, epi)
 #define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
   if (num_heads == HH) {                                                                   \
     if (!g_sddmm_alt) DGLHIP_SDDMM_K(NB, U, HH);                                          \
@@ -578,8 +584,8 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
       DGLHIP_SDDMM_H(16, 1, 64) DGLHIP_SDDMM_H(16, 1, 128)
     }
     hipLaunchKernelGGL((gsddmm_dot_kernel<EPI>), grid_1d(blocks), dim3(256), 0, stream,
-                       num_rows, feat_len, num_heads, row_beg, row_end, indices, eid, lhs, rhs,
-                       out, epi);
+                       num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices, eid,
+                       lhs, rhs, out, epi);
 #undef DGLHIP_SDDMM_K
 #undef DGLHIP_SDDMM_H
   });
@@ -601,14 +607,15 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
                "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
-  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indptr + 1, indices, eid, lhs,
-                          rhs, out, GatEpi{}, stream);
+  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indptr + 1, nullptr, indices,
+                          eid, lhs, rhs, out, GatEpi{}, stream);
   API_END();
 }
 
 int dglhip_gat_attention_grad_ranges_device(
     int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
-    const int64_t* row_end, const int32_t* indices, const float* dout, const float* ft,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft,
     const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
     float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream_) {
   API_BEGIN();
@@ -620,8 +627,8 @@ int dglhip_gat_attention_grad_ranges_device(
   DGLHIP_CHECK(row_beg && row_end && indices && dout && ft && attn && grad,
                "null pointer argument");
   const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp};
-  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, indices, nullptr, dout,
-                         ft, grad, epi, stream);
+  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
+                         nullptr, dout, ft, grad, epi, stream);
   API_END();
 }
 
@@ -632,7 +639,8 @@ int dglhip_gat_attention_grad_device(int64_t num_rows, int64_t feat_len, int64_t
                                      float clamp_lo, float clamp_hi, int apply_exp,
                                      float drop_scale, float* grad, void* stream) {
   return dglhip_gat_attention_grad_ranges_device(
-      num_rows, feat_len, num_heads, indptr, indptr ? indptr + 1 : nullptr, indices, dout, ft,
+      num_rows, feat_len, num_heads, indptr, indptr ? indptr + 1 : nullptr, nullptr, indices,
+      dout, ft,
       attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, apply_exp, drop_scale, grad, stream);
 }
 

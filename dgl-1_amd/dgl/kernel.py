@@ -1660,7 +1660,8 @@ class _GATAggregate(torch.autograd.Function):
                 ft2c = ft2.contiguous()
                 for b in range(len(cuts) - 1):
                     check_call(LIB.dglhip_gat_attention_grad_ranges_device(
-                        fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]), ptr(fwd.indices),
+                        fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
+                        ptr(fwd.row_order), ptr(fwd.indices),
                         ptr(d_ft), ptr(ft2c), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
                         float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
                         ptr(g), _stream_of(ft2.device)))

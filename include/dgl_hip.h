@@ -439,12 +439,15 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
                                 float* attn_out, float* attn_drop_out, void* stream);
 
 /* dglhip_gat_attention_grad_device over row ranges: row r's slots are
- * [row_beg[r], row_end[r]) (slot indices stay the CSR's). Every slot's value
- * is independent, so launches over the source blocks' sub-ranges give the
- * one-launch bits (the GAT backward under the source-blocked schedule). */
+ * [row_beg[r], row_end[r]) (slot indices stay the CSR's), rows launched in
+ * row_order (NULL: 0..num_rows-1; a degree-descending schedule starts the
+ * longest rows first). Every slot's value is independent, so launches over
+ * the source blocks' sub-ranges give the one-launch bits (the GAT backward
+ * under the source-blocked schedule). */
 int dglhip_gat_attention_grad_ranges_device(
     int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
-    const int64_t* row_end, const int32_t* indices, const float* dout, const float* ft,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft,
     const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
     float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream);
 
