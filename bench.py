@@ -390,6 +390,17 @@ def per_rank(values, world, dev):
     return [t[i * k:(i + 1) * k] for i in range(world)]
 
 
+def pipelined_blocks(pg):
+    """Source-blocked launches of a pipelined partition's segments per step
+    (0: every segment one launch): the own rows in fp32, the halo's at its
+    wire type."""
+    if pg.chunks <= 0:
+        return kernel.blocked_schedule(pg.adj, torch.empty(2, FEAT, device=pg.device))
+    halo = torch.float32 if pg.halo_dtype is None else pg.halo_dtype
+    return kernel.segment_blocks(pg.seg_csrs, FEAT,
+                                 [torch.float32] + [halo] * (len(pg.seg_csrs) - 1))
+
+
 def gather_peak(table_bytes, blocks=0):
     """(peak GB/s, source) of a row gather from a ``table_bytes`` table: with
     the source-blocked schedule (``blocks`` > 0) the guide's L2 indexed-row
@@ -680,6 +691,7 @@ def main(argv=None):
 
             def step():
                 pg.update_all(h_local)
+            blocks = pipelined_blocks(pg)
             mode = ("pipelined segments (own + all-to-allv halo of %d rows in %d chunks)"
                     % (pg.num_halo, args.pipeline_chunks)
                     if pg.halo_mode == "alltoall" else
@@ -690,6 +702,7 @@ def main(argv=None):
 
             def step():
                 kernel.gspmm(adj, "copy_u", "sum", h)
+            blocks = kernel.blocked_schedule(adj, h)
             mode = "one g-SpMM"
         del sel
         parallelism = "emulated rank 0 of %d, %s, no communication (H = %.0f MB)" % (
@@ -734,6 +747,7 @@ def main(argv=None):
         def step():
             pg.update_all(h_local)
         parallelism = describe_partition(pg, world, args)
+        blocks = pipelined_blocks(pg)
     del src, dst
     _sync(dev)
     if dev.type == "cuda":

@@ -550,6 +550,11 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
   const int64_t nb = feat_len % 32 == 0 ? feat_len / 32 : 0;
   const bool sliced = aligned && head_ok && (nb == 1 || nb == 2 || nb == 4 || nb == 8 ||
                                              nb == 16);
+  // row sub-ranges (the source-blocked schedule) gather from L2: there the
+  // shallower depth wins at F = 128 (Reddit-shaped graph, 1 / 8 / 16 heads:
+  // 6.30 -> 4.89, 6.68 -> 5.69, 7.70 -> 7.07 ms per call, eid order,
+  // tools/reducer_bench.py); dglhip_set_sddmm_variant(1) swaps the two
+  const bool alt = (row_end != row_beg + 1) != (g_sddmm_alt != 0);
   timed_launch(stream, [&] {
 #define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
   hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI>), grid_1d(blocks), dim3(256), \
@@ -557,7 +562,7 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
                      out, epi)
 #define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
   if (num_heads == HH) {                                                                   \
-    if (!g_sddmm_alt) DGLHIP_SDDMM_K(NB, U, HH);                                          \
+    if (!alt) DGLHIP_SDDMM_K(NB, U, HH);                                                  \
     else DGLHIP_SDDMM_K(NB, (U == 4 ? 2 : 2 * U), HH);                                     \
     return;                                                                                \
   }
@@ -595,10 +600,11 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
 
 extern "C" {
 
-int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
-                         int64_t num_heads, const int64_t* indptr, const int32_t* indices,
-                         const int64_t* eid, const float* lhs,
-                         const float* rhs, float* out, void* stream_) {
+int dglhip_gsddmm_ranges_device(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
+                                const int64_t* row_beg, const int64_t* row_end,
+                                const int32_t* row_order, const int32_t* indices,
+                                const int64_t* eid, const float* lhs, const float* rhs,
+                                float* out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(op == DGLHIP_SDDMM_DOT, "unknown sddmm op " << op);
@@ -606,10 +612,19 @@ int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
   DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
                "num_heads " << num_heads << " must divide feat_len " << feat_len);
   if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && lhs && rhs && out, "null pointer argument");
-  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, indptr, indptr + 1, nullptr, indices,
+  DGLHIP_CHECK(row_beg && row_end && indices && lhs && rhs && out, "null pointer argument");
+  launch_sddmm_dot<false>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
                           eid, lhs, rhs, out, GatEpi{}, stream);
   API_END();
+}
+
+int dglhip_gsddmm_device(int op, int64_t num_rows, int64_t feat_len,
+                         int64_t num_heads, const int64_t* indptr, const int32_t* indices,
+                         const int64_t* eid, const float* lhs,
+                         const float* rhs, float* out, void* stream) {
+  return dglhip_gsddmm_ranges_device(op, num_rows, feat_len, num_heads, indptr,
+                                     indptr ? indptr + 1 : nullptr, nullptr, indices, eid, lhs,
+                                     rhs, out, stream);
 }
 
 int dglhip_gat_attention_grad_ranges_device(

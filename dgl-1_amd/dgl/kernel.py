@@ -932,6 +932,20 @@ def _block_edge_rows(csr, plan, emap):
     return rows
 
 
+def segment_blocks(csrs, feat_len, dtypes):
+    """Launches of the source-blocked schedule over CSRs gathered at
+    ``feat_len`` features of the given row dtypes (one per CSR; a pipelined
+    partition's own and halo segments), 0 for a CSR that keeps one launch."""
+    total = 0
+    for csr, dt in zip(csrs, dtypes):
+        if csr.device.type != "cuda":
+            continue
+        proxy = torch.empty(2, feat_len, dtype=dt, device=csr.device)
+        plan = _block_plan(csr, proxy, feat_len)
+        total += 0 if plan is None else len(plan)
+    return total
+
+
 def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None, efeat=None, elen=0,
                  erows=None):
     """copy_u (fp32 or bf16 rows) + sum (mean) over the segment CSRs, each row's chain continued
@@ -993,9 +1007,13 @@ def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1, slot=False):
     F = lhs2.shape[1]
     eid = None if slot else csr.eid
     if dev.type == "cuda":
-        check_call(LIB.dglhip_gsddmm_device(0, csr.num_rows, F, heads, ptr(csr.indptr),
-                                            ptr(csr.indices), ptr(eid), ptr(lhs2), ptr(rhs2),
-                                            ptr(out), _stream_of(dev)))
+        # rows longest-first; the gathered rows one source block at a time
+        # where the CSR has a blocked schedule (per-edge values: same bits)
+        cuts = _block_cuts(csr, F * 4, _BLOCK_BYTES) or [csr.indptr, csr.indptr[1:]]
+        for b in range(len(cuts) - 1):
+            check_call(LIB.dglhip_gsddmm_ranges_device(
+                0, csr.num_rows, F, heads, ptr(cuts[b]), ptr(cuts[b + 1]), ptr(csr.row_order),
+                ptr(csr.indices), ptr(eid), ptr(lhs2), ptr(rhs2), ptr(out), _stream_of(dev)))
     else:
         check_call(LIB.dglhip_gsddmm_host(0, csr.num_rows, F, heads, ptr(csr.indptr),
                                           ptr(csr.indices), ptr(eid), ptr(lhs2), ptr(rhs2),

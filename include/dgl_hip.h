@@ -438,6 +438,17 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
                                 const int64_t* seed_offset, float* out_ft, float* out_z,
                                 float* attn_out, float* attn_drop_out, void* stream);
 
+/* dglhip_gsddmm_device over row ranges: row r's slots are
+ * [row_beg[r], row_end[r]) (outputs still at eid[k], or slot k when eid is
+ * NULL), rows launched in row_order (NULL: natural order). Every value is
+ * independent of the others: launches over the rows' source-block
+ * sub-ranges give the one-launch bits. */
+int dglhip_gsddmm_ranges_device(int op, int64_t num_rows, int64_t feat_len, int64_t num_heads,
+                                const int64_t* row_beg, const int64_t* row_end,
+                                const int32_t* row_order, const int32_t* indices,
+                                const int64_t* eid, const float* lhs, const float* rhs,
+                                float* out, void* stream);
+
 /* dglhip_gat_attention_grad_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) (slot indices stay the CSR's), rows launched in
  * row_order (NULL: 0..num_rows-1; a degree-descending schedule starts the
