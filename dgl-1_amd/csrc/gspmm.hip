@@ -503,6 +503,31 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   API_END();
 }
 
+int dglhip_gspmm_max_ranges_device(int msg_op, int64_t num_rows, int64_t feat_len,
+                                   const int64_t* indptr, const int64_t* row_beg,
+                                   const int64_t* row_end, int accumulate,
+                                   const int32_t* indices, const int64_t* eid,
+                                   const float* ufeat, const float* efeat, int64_t efeat_len,
+                                   float* out, int64_t* arg_out, const int32_t* row_order,
+                                   void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  if (num_rows == 0 || feat_len == 0) return 0;
+  DGLHIP_CHECK(indptr && row_beg && row_end && out, "null indptr/ranges/out");
+  const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
+  const bool use_e = !copies_u(msg_op);
+  DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
+  MaxLaunch m{num_rows, feat_len, use_e ? efeat_len : 1, indptr, indices, eid, ufeat, efeat,
+              out, arg_out, row_order, row_beg, row_end, accumulate != 0 ? 1 : 0};
+  dispatch_max(msg_op, m, stream);
+  API_END();
+}
+
 int dglhip_gspmm_ranges_device(int msg_op, int64_t num_items, int64_t feat_len,
                                const int64_t* item_beg, const int64_t* item_end,
                                int accumulate, const int32_t* indices, const int64_t* eid,

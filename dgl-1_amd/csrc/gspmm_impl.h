@@ -361,7 +361,8 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
                                         const int64_t* __restrict__ eid,
                                         const float* __restrict__ ufeat,
                                         const float* __restrict__ efeat,
-                                        float* __restrict__ out, int64_t* __restrict__ arg_out) {
+                                        float* __restrict__ out, int64_t* __restrict__ arg_out,
+                                        bool prev = false) {
   typedef typename Vec<VEC>::T V;
   auto message = [](const SlotLoad<VEC, MSG, EM>& s) -> V {
     if (copies_u(MSG)) return s.u;
@@ -378,7 +379,11 @@ __device__ __forceinline__ void max_row(int64_t row, int gl, int group, int64_t 
 #pragma unroll
     for (int i = 0; i < VEC; ++i) arg[i] = -1;
     int64_t k = beg;
-    if (k < end) {
+    if (prev) {  // the row's earlier slots (a previous source block): continue from them
+      best = ldv<VEC>(out + row * F + f0);
+#pragma unroll
+      for (int i = 0; i < VEC; ++i) arg[i] = arg_out ? arg_out[row * F + f0 + i] : -1;
+    } else if (k < end) {
       SlotLoad<VEC, MSG, EM> s;
       s.load(ufeat, efeat, F, F, f0, elen, eoff, indices[k], edge(k));
       best = message(s);
@@ -435,7 +440,8 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
     const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
     const float* __restrict__ ufeat, const float* __restrict__ efeat,
     float* __restrict__ out, int64_t* __restrict__ arg_out,
-    const int32_t* __restrict__ row_order) {
+    const int32_t* __restrict__ row_order, const int64_t* __restrict__ row_beg,
+    const int64_t* __restrict__ row_end, int accumulate) {
   constexpr int ITEMS_PER_WAVE = 64 / GROUP;
   const int lane = threadIdx.x & 63;
   const int64_t wave =
@@ -446,13 +452,19 @@ __global__ __launch_bounds__(256) void gspmm_max_kernel(
   const int gl = GROUP == 64 ? lane : (lane % GROUP);
   int64_t row = row_order ? row_order[it] : it;
   if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
-  const int64_t beg = indptr[row], end = indptr[row + 1];
+  // row ranges (source-blocked schedule): the row's slots [row_beg, row_end)
+  // of this block; with accumulate, continue from the earlier blocks' max
+  const int64_t rs = indptr[row];
+  const int64_t beg = row_beg ? row_beg[row] : rs;
+  const int64_t end = row_end ? row_end[row] : indptr[row + 1];
+  if (accumulate && beg == end) return;  // nothing new: the row keeps its value
+  const bool prev = accumulate && beg > rs;
   if (copies_u(MSG) || eid != nullptr)  // uniform branch
     max_row<VEC, UNROLL, MSG, EM, true>(row, gl, GROUP, beg, end, F, elen, indices, eid, ufeat,
-                                        efeat, out, arg_out);
+                                        efeat, out, arg_out, prev);
   else
     max_row<VEC, UNROLL, MSG, EM, false>(row, gl, GROUP, beg, end, F, elen, indices, eid,
-                                         ufeat, efeat, out, arg_out);
+                                         ufeat, efeat, out, arg_out, prev);
 }
 
 // ---------------------------------------------------------------------------
@@ -684,6 +696,9 @@ struct MaxLaunch {
   float* out;
   int64_t* arg_out;
   const int32_t* row_order;
+  const int64_t* row_beg = nullptr;  // row ranges (NULL: whole rows)
+  const int64_t* row_end = nullptr;
+  int accumulate = 0;
 };
 
 
@@ -703,7 +718,8 @@ static inline void dispatch_max_shape(const MaxLaunch& a, hipStream_t stream) {
       hipLaunchKernelGGL((gspmm_max_kernel<V, G, 8, MSG, EM>),                       \
                          grid_1d(blocks), dim3(256), 0, stream,  \
                          a.num_rows, a.F, a.elen, a.indptr, a.indices, a.eid,        \
-                         a.ufeat, a.efeat, a.out, a.arg_out, a.row_order);           \
+                         a.ufeat, a.efeat, a.out, a.arg_out, a.row_order, a.row_beg, \
+                         a.row_end, a.accumulate);                                   \
     });                                                                              \
     return;                                                                          \
   }

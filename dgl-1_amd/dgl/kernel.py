@@ -568,6 +568,20 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
                                     efeat2.index_select(0, rows), elen), None
             return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out, efeat2, elen,
                                 rows), None
+    if (dev.type == "cuda" and red == RED_MAX and out is None and ufeat2 is not None and
+            (msg == MSG_COPY_U or (msg == MSG_U_MUL_E and (
+                emap is SLOT or (emap is None and csr.slot_eid is None)))) and
+            ufeat2.dtype == torch.float32 and ufeat2.dim() == 2 and ufeat2.is_contiguous() and
+            ufeat2.shape[1] == feat_len):
+        # max over the blocks' row ranges, continued block by block: the
+        # same values and (strict >, slot order) the same argmax. Edge
+        # values by edge id stay in one launch: a dependent 4-B load per
+        # slot makes the blocked launches slower (8.75 vs 8.50 ms, Reddit-
+        # shaped); copy_u max 7.42 -> 4.16 ms
+        cuts = _block_cuts(csr, feat_len * 4, _BLOCK_BYTES)
+        if cuts is not None:
+            return _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg,
+                                    emap)
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
@@ -875,6 +889,23 @@ def _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, eid, r
     if red == RED_MEAN:
         out.div_(csr.mean_divisor())
     return out
+
+
+def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, emap):
+    """The max reducer as one dglhip_gspmm_max_ranges_device launch per
+    source block (row sub-ranges ``cuts``), every row continued from the
+    earlier blocks' max; argmax slot ids as the one-launch kernel's."""
+    dev = ufeat2.device
+    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
+    arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev) if want_arg else None
+    eid = None if msg == MSG_COPY_U or emap is SLOT else (
+        csr.slot_eid if emap is None else emap)
+    for b in range(len(cuts) - 1):
+        check_call(LIB.dglhip_gspmm_max_ranges_device(
+            msg, csr.num_rows, feat_len, ptr(csr.indptr), ptr(cuts[b]), ptr(cuts[b + 1]),
+            1 if b else 0, ptr(csr.indices), ptr(eid), ptr(ufeat2), ptr(efeat2), elen, ptr(out),
+            ptr(arg), ptr(csr.row_order), _stream_of(dev)))
+    return out, arg
 
 
 def blocked_schedule(adj, ufeat):

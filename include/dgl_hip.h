@@ -438,6 +438,22 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
                                 const int64_t* seed_offset, float* out_ft, float* out_z,
                                 float* attn_out, float* attn_drop_out, void* stream);
 
+/* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are
+ * [row_beg[r], row_end[r]) of the CSR (argmax slot ids stay the CSR's: k,
+ * mapped as dglhip_gspmm_device's), rows in row_order. With accumulate != 0
+ * a row whose range starts past indptr[r] continues from out / arg_out (its
+ * earlier slots' max) and a row with an empty range is left as it is; the
+ * first range of a row starts it. Launches over the rows' source-block
+ * sub-ranges in block order give the one-launch values and, ties included,
+ * the one-launch argmax (strict > keeps the earliest slot). */
+int dglhip_gspmm_max_ranges_device(int msg_op, int64_t num_rows, int64_t feat_len,
+                                   const int64_t* indptr, const int64_t* row_beg,
+                                   const int64_t* row_end, int accumulate,
+                                   const int32_t* indices, const int64_t* eid,
+                                   const float* ufeat, const float* efeat, int64_t efeat_len,
+                                   float* out, int64_t* arg_out, const int32_t* row_order,
+                                   void* stream);
+
 /* dglhip_gsddmm_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) (outputs still at eid[k], or slot k when eid is
  * NULL), rows launched in row_order (NULL: natural order). Every value is

@@ -338,3 +338,43 @@ def test_pipelined_segments_blocked_bits(halo):
         finally:
             kernel.set_blocked(old)
     assert torch.equal(run("auto"), run("off"))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("msg", ["copy_u", "u_mul_e"])
+def test_blocked_max_bits_with_ties(msg):
+    """The max reducer over the blocks' row ranges: values, and (features
+    drawn from a few integers: ties everywhere) the argmax routing of the
+    gradient, equal the one-launch kernel's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 17, True)
+    adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                          kernel.ORDER_EID, dev)
+    gen = torch.Generator().manual_seed(18)
+    H = torch.randint(-3, 4, (n, 128), generator=gen).float().to(dev)
+    w = torch.randint(1, 3, (m, 1), generator=gen).float().to(dev)
+    assert kernel._block_cuts(adj.fwd, 128 * 4, kernel._BLOCK_BYTES) is not None
+
+    def run(policy):
+        old = kernel.set_blocked(policy)
+        try:
+            h = H.clone().requires_grad_(True)
+            kernel.timing_enable(True)
+            if msg == "copy_u":
+                o = kernel.gspmm(adj, "copy_u", "max", h)
+            else:  # weights in slot order (blocked); by edge id they keep one launch
+                o = kernel.gspmm(adj, "u_mul_e", "max", h, w, edge_order="slot")
+            torch.cuda.synchronize()
+            _, launches = kernel.timing_read()
+            kernel.timing_enable(False)
+            o.backward(torch.arange(n * 128, device=dev, dtype=torch.float32).view(n, 128))
+            return o.detach().cpu(), h.grad.cpu(), launches
+        finally:
+            kernel.set_blocked(old)
+    o1, g1, n1 = run("auto")
+    o0, g0, n0 = run("off")
+    assert n1 > n0
+    assert torch.equal(o1, o0) and torch.equal(g1, g0)
