@@ -503,6 +503,31 @@ int dglhip_gspmm_chunked_device(int msg_op, int reduce_op, int64_t feat_len,
   API_END();
 }
 
+int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
+                              const int32_t* item_rows, const int64_t* item_ptr, int accumulate,
+                              const int32_t* indices, const int64_t* eid, const float* ufeat,
+                              int64_t ufeat_ld, const float* efeat, int64_t efeat_len,
+                              float* out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(msg_op >= 0 && msg_op <= 3, "unknown msg op " << msg_op);
+  DGLHIP_CHECK(num_items >= 0 && feat_len >= 0, "negative size");
+  if (num_items == 0 || feat_len == 0) return 0;
+  const bool use_u = msg_op != DGLHIP_MSG_COPY_E;
+  const bool use_e = !copies_u(msg_op);
+  DGLHIP_CHECK(item_rows && item_ptr && indices && out, "null items/indices/out");
+  DGLHIP_CHECK(!use_u || ufeat, "ufeat is null");
+  DGLHIP_CHECK(!use_e || efeat, "efeat is null");
+  DGLHIP_CHECK(!use_e || (efeat_len >= 1 && feat_len % efeat_len == 0),
+               "edge feature length " << efeat_len << " must divide feat_len " << feat_len);
+  DGLHIP_CHECK(ufeat_ld == 0 || ufeat_ld == feat_len || (ufeat_ld > feat_len && ufeat_ld % 2 == 0),
+               "ufeat_ld " << ufeat_ld << ": 0, feat_len, or an even width > feat_len");
+  SumLaunch a{num_items, feat_len, use_e ? efeat_len : 1, nullptr, indices, eid, ufeat, efeat,
+              out, item_rows, item_ptr, item_ptr + 1, accumulate != 0, false, ufeat_ld};
+  dispatch_sum(msg_op, false, a, stream);
+  API_END();
+}
+
 int dglhip_gspmm_max_ranges_device(int msg_op, int64_t num_rows, int64_t feat_len,
                                    const int64_t* indptr, const int64_t* row_beg,
                                    const int64_t* row_end, int accumulate,

@@ -296,7 +296,11 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   const int gl = GROUP == 64 ? lane : (lane % GROUP);
   int64_t row, beg, end;
   if (CHUNKED) {
-    row = it;
+    // item it: slots [chunk_beg[it], chunk_end[it]) into row row_order[it]
+    // (the blocked schedule's items), or into partial row it (heavy-row
+    // chunks, row ranges); the three loads are independent
+    row = row_order ? row_order[it] : it;
+    if (GROUP == 64) row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
     beg = chunk_beg[it];
     end = chunk_end[it];
   } else {

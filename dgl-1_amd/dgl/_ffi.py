@@ -91,6 +91,8 @@ def _load():
                                                       _vp, _vp, _vp, ctypes.c_float,
                                                       ctypes.c_float, ctypes.c_float, _c_int,
                                                       ctypes.c_float, _vp, _vp]),
+        "dglhip_gspmm_items_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
+                                               _vp, _c_i64, _vp, _c_i64, _vp, _vp]),
         "dglhip_gspmm_max_ranges_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _c_int,
                                                     _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                                     _vp]),

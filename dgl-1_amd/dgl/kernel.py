@@ -543,11 +543,6 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
     if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
             red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)):
-        if _BLOCKED == "ranges" and _plain_rows(msg, red, ufeat2, feat_len):  # study knob
-            cuts = _block_cuts(csr, feat_len * 4, _BLOCK_BYTES)
-            if cuts is not None:
-                return _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, None, 0, feat_len, None,
-                                             red, out), None
         blocks = _block_plan(csr, ufeat2, feat_len)
         if blocks is not None:
             return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out), None
@@ -712,10 +707,10 @@ _BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
 
 
 def set_blocked(policy):
-    """Source-blocked schedule for copy_u / u_mul_e with sum / mean: "auto"
-    (default: where it keeps the chains bit-identical and the table size
-    pays) or "off"; "ranges" (study) runs copy_u over row ranges of the CSR
-    itself instead of segment CSRs. Returns the old policy."""
+    """Source-blocked schedule for copy_u / u_mul_e with sum / mean / max and
+    the fused GAT layer: "auto" (default: where it keeps the chains
+    bit-identical and the table size pays) or "off". Returns the old
+    policy."""
     global _BLOCKED
     old = _BLOCKED
     _BLOCKED = str(policy)
@@ -757,38 +752,63 @@ def _block_plan(csr, ufeat2, feat_len):
     B = _block_count(csr, (hi - lo) * max(ld, feat_len) * ufeat2.element_size())
     if not B:
         return None
+    if _split_threshold(csr):  # a row long enough to need the heavy-row split
+        return None
     key = ("blocked", B)
-    if key in csr._plans:
-        return csr._plans[key]
+    if key not in csr._plans:
+        csr._plans[key] = _block_items(csr, B, lo, hi)
+    return csr._plans[key]
+
+
+class _BlockItems:
+    """One source block (or the suffix) of the blocked schedule as items:
+    ``rows`` (int32) the rows with slots in the block, longest first (stable
+    by row id); item i's slots are [ptr[i], ptr[i+1]) of ``indices``, laid out
+    in item order, in each row's slot order; ``pos`` the CSR slot each came
+    from (int32 below 2^31 slots)."""
+    __slots__ = ("rows", "ptr", "indices", "pos", "nnz", "suffix")
+
+    def __init__(self, csr, row_counts, pos_csr_order, suffix=False):
+        dev = csr.device
+        c = row_counts
+        cnt_sorted, order = torch.sort(c, descending=True, stable=True)
+        n = int((cnt_sorted > 0).sum())
+        order, cnt = order[:n], cnt_sorted[:n]
+        ptr_ = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(cnt, 0, out=ptr_[1:])
+        # where each row's slots sit in pos_csr_order (rows ascending)
+        start = torch.zeros(csr.num_rows, dtype=torch.int64, device=dev)
+        torch.cumsum(c[:-1], 0, out=start[1:])
+        nnz = int(ptr_[-1])
+        item = torch.repeat_interleave(torch.arange(n, device=dev), cnt, output_size=nnz)
+        within = torch.arange(nnz, device=dev) - ptr_[item]
+        pos = pos_csr_order[start[order][item] + within]
+        del item, within, start
+        self.indices = csr.indices[pos]
+        # int32 where it fits: the plan's slot map (edge-valued messages)
+        self.pos = pos.to(torch.int32) if csr.nnz < (1 << 31) else pos
+        del pos
+        self.rows = order.to(torch.int32)
+        self.ptr = ptr_
+        self.nnz = nnz
+        self.suffix = suffix
+
+
+def _block_items(csr, B, lo, hi):
+    """The blocked schedule of ``csr`` as _BlockItems (B blocks, then the
+    suffix if any), or None (_block_split)."""
     split = _block_split(csr, B, lo, hi)
-    plan = None
-    if split is not None:
-        blk, counts, pre, sfx = split
-        plan = []
-        for b in range(B):
-            sel = blk == b if pre is None else (blk == b) & pre
-            plan.append(_segment_csr(csr, counts[:, b], csr.indices[sel]))
-            del sel
-        if pre is not None:  # each row's slots after its monotone prefix, run last
-            plan.append(_segment_csr(csr, sfx, csr.indices[~pre]))
-            plan[-1]._plans["suffix"] = True
-        del blk, counts, pre, sfx
-    csr._plans[key] = plan
+    if split is None:
+        return None
+    blk, counts, pre, sfx = split
+    plan = []
+    for b in range(B):
+        sel = blk == b if pre is None else (blk == b) & pre
+        plan.append(_BlockItems(csr, counts[:, b], torch.nonzero(sel).squeeze(1)))
+        del sel
+    if pre is not None:
+        plan.append(_BlockItems(csr, sfx, torch.nonzero(~pre).squeeze(1), suffix=True))
     return plan
-
-
-def _segment_csr(csr, row_counts, indices):
-    """A CSR over ``csr``'s rows with ``row_counts`` slots each (``indices``
-    in order), degree-descending schedule, no edge ids (copy_u reads none),
-    never blocked again."""
-    ip = torch.zeros(csr.num_rows + 1, dtype=torch.int64, device=csr.device)
-    torch.cumsum(row_counts, 0, out=ip[1:])
-    host_ip = ip.cpu()
-    ro = torch.empty(csr.num_rows, dtype=torch.int32)
-    check_call(LIB.dglhip_rows_by_degree_host(csr.num_rows, ptr(host_ip), ptr(ro)))
-    seg = CSR(ip, indices, None, csr.num_cols, ro.to(csr.device), host_ip)
-    seg._plans["segment"] = True
-    return seg
 
 
 # at most this share of the slots may follow their row's monotone prefix
@@ -864,33 +884,6 @@ def _block_cuts(csr, row_bytes, block_bytes=None):
     return csr._plans[key]
 
 
-def _plain_rows(msg, red, ufeat2, feat_len):
-    """fp32 source rows the row-range kernel reads as they are (contiguous,
-    no padded-stride copy due)."""
-    return (ufeat2 is not None and ufeat2.dtype == torch.float32 and ufeat2.dim() == 2 and
-            ufeat2.is_contiguous() and ufeat2.shape[1] == feat_len and
-            not _pad_rows(msg, red, ufeat2, feat_len))
-
-
-def _gspmm_ranges_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, eid, red=RED_SUM,
-                          out=None):
-    """sum (mean, sum_accum) over ``csr`` (edge values at rows ``eid`` per
-    slot, or by slot when None) as one dglhip_gspmm_ranges_device launch per
-    source block, every row's chain continued range by range (the rows'
-    sub-ranges ``cuts``, _block_cuts): the one-launch bits. Mean divides by
-    the degree last, as the kernel does."""
-    if out is None:
-        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
-    for b in range(len(cuts) - 1):
-        check_call(LIB.dglhip_gspmm_ranges_device(
-            msg, csr.num_rows, feat_len, ptr(cuts[b]), ptr(cuts[b + 1]),
-            1 if (b or red == RED_SUM_ACCUM) else 0, ptr(csr.indices), ptr(eid), ptr(ufeat2),
-            ptr(efeat2), elen, ptr(out), _stream_of(out.device)))
-    if red == RED_MEAN:
-        out.div_(csr.mean_divisor())
-    return out
-
-
 def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, emap):
     """The max reducer as one dglhip_gspmm_max_ranges_device launch per
     source block (row sub-ranges ``cuts``), every row continued from the
@@ -908,6 +901,34 @@ def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, e
     return out, arg
 
 
+def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, erows):
+    """The blocked schedule's items (_BlockItems), one dglhip_gspmm_items_device
+    launch per block, every launch adding to the rows it lists: ``out``
+    starts from zero (the chains' own start: identical bits) unless ``red``
+    is SUM_ACCUM."""
+    dev = ufeat2.device
+    ld = ufeat2.stride(0) if _row_strided(ufeat2, feat_len) else 0
+    if out is None:
+        out = torch.zeros(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
+    elif red != RED_SUM_ACCUM:
+        out.zero_()
+    off = 0
+    for it in plan:
+        if efeat is None:
+            e, eid = None, None
+        elif erows is None:  # values already in the plan's slot order
+            e, eid = efeat[off:off + it.nnz], None
+        else:
+            e, eid = efeat, erows[off:off + it.nnz]
+        check_call(LIB.dglhip_gspmm_items_device(
+            msg, it.rows.numel(), feat_len, ptr(it.rows), ptr(it.ptr), 1, ptr(it.indices),
+            ptr(eid), ptr(ufeat2), ld, ptr(e), elen, ptr(out), _stream_of(dev)))
+        off += it.nnz
+    if red == RED_MEAN:
+        out.div_(csr.mean_divisor())
+    return out
+
+
 def blocked_schedule(adj, ufeat):
     """The number of source blocks the copy_u sum / mean g-SpMM of ``ufeat``
     over ``adj`` runs in (0: one launch), e.g. for a roofline's regime."""
@@ -920,22 +941,11 @@ def blocked_schedule(adj, ufeat):
 
 
 def _block_slots(csr, plan):
-    """int64: for each slot of the blocked plan's segments, in order, the
-    slot of ``csr`` it came from (cached; built on the first edge-valued
-    call)."""
+    """int64: for each slot of the blocked plan, blocks in order, the slot of
+    ``csr`` it came from (cached; for edge-valued messages)."""
     key = ("blocked_slots", len(plan))
     if key not in csr._plans:
-        B = len(plan) - (1 if plan[-1]._plans.get("suffix") else 0)
-        lo, hi = _column_span(csr)
-        blk, _, pre, _ = _block_split(csr, B, lo, hi)
-        parts = []
-        for b in range(B):
-            sel = blk == b if pre is None else (blk == b) & pre
-            parts.append(torch.nonzero(sel).squeeze(1))
-        if pre is not None:
-            parts.append(torch.nonzero(~pre).squeeze(1))
-        csr._plans[key] = torch.cat(parts)
-        del blk, pre, parts
+        csr._plans[key] = torch.cat([it.pos.long() for it in plan])
     return csr._plans[key]
 
 
@@ -979,36 +989,18 @@ def segment_blocks(csrs, feat_len, dtypes):
 
 def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None, efeat=None, elen=0,
                  erows=None):
-    """copy_u (fp32 or bf16 rows) + sum (mean) over the segment CSRs, each row's chain continued
-    block by block: the first block writes every row (unless ``red`` is
-    SUM_ACCUM: then every block adds to ``out``), the others add to rows that
-    have slots in them; mean divides by the degree last (the kernel's own
-    division: IEEE, by max(deg, 1))."""
+    """copy_u (fp32 or bf16 rows) / u_mul_e + sum (mean, sum_accum) over the
+    blocked schedule's items, each row's chain continued block by block;
+    mean divides by the degree last (the kernel's own division: IEEE, by
+    max(deg, 1)). Edge values: ``efeat`` rows ``erows`` per plan slot, or
+    without ``erows`` already in the plan's slot order."""
     if not _row_strided(ufeat2, feat_len) and _pad_rows(msg, RED_SUM, ufeat2, feat_len):
         # line-straddling rows: one padded copy for every block's launch
         ld = padded_width(feat_len)
         up = ufeat2.new_empty(ufeat2.shape[0], ld)
         up[:, :feat_len] = ufeat2
         ufeat2 = up[:, :feat_len]
-    if out is None:
-        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=ufeat2.device)
-    off = 0
-    for i, seg in enumerate(blocks):
-        r = RED_SUM_ACCUM if (i or red == RED_SUM_ACCUM) else RED_SUM
-        # u_mul_e: segment slot k reads efeat row erows[off + k] (the plan's
-        # slot map, segment after segment), or, without erows, row off + k
-        # of efeat (values already in the plan's slot order)
-        if efeat is None:
-            e, emap = None, None
-        elif erows is None:
-            e, emap = efeat[off:off + seg.nnz], SLOT
-        else:
-            e, emap = efeat, erows[off:off + seg.nnz]
-        _run_gspmm(seg, msg, r, ufeat2, e, elen, feat_len, False, out=out, emap=emap)
-        off += seg.nnz
-    if red == RED_MEAN:
-        out.div_(csr.mean_divisor())
-    return out
+    return _run_block_items(csr, blocks, msg, red, ufeat2, feat_len, out, efeat, elen, erows)
 
 
 _PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")

@@ -438,6 +438,21 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
                                 const int64_t* seed_offset, float* out_ft, float* out_z,
                                 float* attn_out, float* attn_drop_out, void* stream);
 
+/* Sum over items: item i adds the messages of slots [item_ptr[i],
+ * item_ptr[i+1]) of indices (and eid / efeat by slot) to output row
+ * item_rows[i] — from zero, or with accumulate != 0 continuing the row's
+ * chain from the value in out. Rows not listed are not touched. The
+ * source-blocked schedule runs one call per source block, its items the rows
+ * with slots in the block, longest first, their slots laid out in item order
+ * (DESIGN.md §4.1): the three loads that start an item are independent and
+ * the slot stream is sequential across items. ufeat rows at stride ufeat_ld
+ * (0: feat_len). */
+int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
+                              const int32_t* item_rows, const int64_t* item_ptr, int accumulate,
+                              const int32_t* indices, const int64_t* eid, const float* ufeat,
+                              int64_t ufeat_ld, const float* efeat, int64_t efeat_len,
+                              float* out, void* stream);
+
 /* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of the CSR (argmax slot ids stay the CSR's: k,
  * mapped as dglhip_gspmm_device's), rows in row_order. With accumulate != 0

@@ -33,6 +33,23 @@ def small_blocks(monkeypatch):
     monkeypatch.setattr(kernel, "_BLOCK_BYTES", 1 << 16)
 
 
+def _chains_kept(csr, plan):
+    """Every row's slots, read block by block in plan order (each block's
+    items in their slot order), are the row's CSR slots in order; every
+    block's indices are the CSR's at its positions."""
+    rows, segs, pos = [], [], []
+    for i, it in enumerate(plan):
+        assert torch.equal(it.indices, csr.indices[it.pos])
+        cnt = it.ptr[1:] - it.ptr[:-1]
+        assert bool((cnt > 0).all()) and bool((cnt[:-1] >= cnt[1:]).all())  # longest first
+        rows.append(torch.repeat_interleave(it.rows.long(), cnt))
+        segs.append(torch.full((it.nnz,), i, dtype=torch.int64))
+        pos.append(it.pos)
+    rows, segs, pos = torch.cat(rows), torch.cat(segs), torch.cat(pos)
+    order = torch.sort(rows * len(plan) + segs, stable=True)[1]
+    return torch.equal(pos[order], torch.arange(csr.nnz))
+
+
 def test_plan_gate_and_host_bits(small_blocks):
     n, m = 2000, 200_000
     src, dst = _graph(n, m, 0, True)
@@ -40,14 +57,17 @@ def test_plan_gate_and_host_bits(small_blocks):
                            kernel.ORDER_EID, "cpu")
     h = torch.randn(n, 128, generator=torch.Generator().manual_seed(1))
     plan = kernel._block_plan(csr, h, 128)
-    assert plan is not None and len(plan) >= 2
+    assert plan is not None and len(plan) >= 2 and not plan[-1].suffix
     assert sum(p.nnz for p in plan) == csr.nnz
+    assert _chains_kept(csr, plan)
+    # the same chains through the host kernel, item by item: the oracle's bits
     ref = torch.from_numpy(O.spmm_coo(n, dst, src, h.numpy()))
-    out = torch.empty(n, 128)
-    kernel._run_gspmm(plan[0], kernel.MSG_COPY_U, kernel.RED_SUM, h, None, 0, 128, False,
-                      out=out)
-    for seg in plan[1:]:
-        kernel._run_gspmm(seg, kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, h, None, 0, 128,
+    out = torch.zeros(n, 128)
+    for it in plan:
+        part = kernel.build_csr(n, n, torch.repeat_interleave(it.rows.long(),
+                                                              it.ptr[1:] - it.ptr[:-1]),
+                                it.indices.long(), kernel.ORDER_EID, "cpu")
+        kernel._run_gspmm(part, kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, h, None, 0, 128,
                           False, out=out)
     assert torch.equal(out, ref)
     # edges in random order: some row's blocks decrease -> no plan
@@ -76,17 +96,10 @@ def test_suffix_after_monotone_prefix(small_blocks):
                            kernel.ORDER_EID, "cpu")
     h = torch.randn(n, 128, generator=torch.Generator().manual_seed(1))
     plan = kernel._block_plan(csr, h, 128)
-    assert plan is not None and len(plan) >= 3
+    assert plan is not None and len(plan) >= 3 and plan[-1].suffix
     assert sum(p.nnz for p in plan) == csr.nnz
     assert 0 < plan[-1].nnz <= n  # at most each row's self-loop
-    ref = torch.from_numpy(O.spmm_coo(n, dst, src, h.numpy()))
-    out = torch.empty(n, 128)
-    kernel._run_gspmm(plan[0], kernel.MSG_COPY_U, kernel.RED_SUM, h, None, 0, 128, False,
-                      out=out)
-    for seg in plan[1:]:
-        kernel._run_gspmm(seg, kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, h, None, 0, 128,
-                          False, out=out)
-    assert torch.equal(out, ref)
+    assert _chains_kept(csr, plan)
     cuts = kernel._block_cuts(csr, 128 * 4, 1 << 16)
     assert cuts is not None and len(cuts) == len(plan) + 1
     assert torch.equal(cuts[-1], csr.indptr[1:]) and torch.equal(cuts[0], csr.indptr[:-1])
@@ -275,9 +288,9 @@ def test_blocked_u_mul_e_bits(order, reduce):
 
 
 def test_u_mul_e_plan_slot_map(small_blocks):
-    """The blocked plan's slot map (segments in order, suffix last) covers
-    every slot once, and the host run of u_mul_e over it with the gathered
-    edge values equals the one-launch host kernel bit for bit."""
+    """The blocked plan's slot map (blocks in order, suffix last) covers
+    every slot once and maps through the edge ids; a per-slot row tensor is
+    composed once per object and anew after an in-place change."""
     n, m = 2000, 200_000
     src, dst = _graph(n, m, 3, True)
     ar = np.arange(n)
@@ -290,14 +303,10 @@ def test_u_mul_e_plan_slot_map(small_blocks):
     plan = kernel._block_plan(csr, h, 128)
     slots = kernel._block_slots(csr, plan)
     assert torch.equal(torch.sort(slots)[0], torch.arange(csr.nnz))
+    assert torch.equal(slots, torch.cat([it.pos for it in plan]))
     rows = kernel._block_edge_rows(csr, plan, None)
-    out = kernel._run_blocked(csr, plan, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, 128, None,
-                              w, 1, rows)
-    pre = kernel._run_blocked(csr, plan, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, 128, None,
-                              w.index_select(0, rows), 1)
-    assert torch.equal(out, pre)
-    ref, _ = kernel._run_gspmm(csr, kernel.MSG_U_MUL_E, kernel.RED_SUM, h, w, 1, 128, False)
-    assert torch.equal(out, ref)
+    eid = csr.slot_eid if csr.slot_eid is not None else torch.arange(csr.nnz)
+    assert torch.equal(rows, eid[slots])
     # a per-slot row map: composed once per tensor object, anew when it changes
     emap = torch.randperm(csr.nnz)
     r1 = kernel._block_edge_rows(csr, plan, emap)

@@ -1,6 +1,7 @@
-"""Interleaved A/B of the source-blocked copy_u + sum on the bench graph:
-segment CSRs (default: degree-descending schedule, short-row tiers) vs row
-ranges of the CSR itself (natural row order), vs one launch; bits checked.
+"""Interleaved A/B of the source-blocked schedule (items) against one launch
+on the bench graph: copy_u + sum, u_mul_e + sum with weights by edge id and
+in slot order; bits checked. (The r03 record's earlier columns, segment CSRs
+and row ranges, came from the forms this replaced.)
 
   python tools/blocked_ranges_ab.py [--rounds 7] [--iters 5]
 """
@@ -28,14 +29,12 @@ def main():
     h = torch.rand(n, 128, device=dev) * 2 - 1
     w = torch.rand(adj.fwd.nnz, device=dev)
     cases = [("copy_u", None, "eid"), ("u_mul_e", w, "eid"), ("u_mul_e", w, "slot")]
-    pols = ["off", "auto", "ranges"]
+    pols = ["off", "auto"]
     refs = {}
     times = {(c, p): [] for c in range(len(cases)) for p in pols}
     for _ in range(args.rounds):
         for ci, (msg, e, order) in enumerate(cases):
             for p in pols:
-                if msg != "copy_u" and p == "ranges":
-                    continue
                 old = kernel.set_blocked(p)
                 out = kernel.gspmm(adj, msg, "sum", h, e, edge_order=order)
                 if ci not in refs:
