@@ -718,7 +718,9 @@ def set_blocked(policy):
 
 
 def _block_count(csr, table_bytes, block_bytes=None):
-    if csr.num_rows == 0 or csr.nnz == 0:
+    # a plan holds about 12 B per slot and its build about 40 B per slot
+    # transiently: graphs past 2^31 slots keep one launch
+    if csr.num_rows == 0 or csr.nnz == 0 or csr.nnz >= (1 << 31):
         return 0
     if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
         return 0
