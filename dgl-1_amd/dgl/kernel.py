@@ -704,6 +704,10 @@ _BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
 _BLOCK_TABLE_MAX = 256 << 20    # above: out's per-block pass outweighs the L2 hits
 # slots per row and block, on average (the rows' per-block pass must pay)
 _BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
+# rows of at most one 128-B line keep one launch: the Reddit-shaped graph at
+# F = 32 runs 1.74 ms in one launch against 1.89 in 5 blocks (F = 41 padded
+# to 192 B: 3.39 -> 2.05; F = 64: 3.56 -> 2.24; tools/blocked_width_sweep.py)
+_BLOCK_MIN_ROW_BYTES = 128
 
 
 def set_blocked(policy):
@@ -750,8 +754,11 @@ def _block_plan(csr, ufeat2, feat_len):
     if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
         return None
     ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
+    row_bytes = max(ld, feat_len) * ufeat2.element_size()
+    if row_bytes <= _BLOCK_MIN_ROW_BYTES:
+        return None
     lo, hi = _column_span(csr)
-    B = _block_count(csr, (hi - lo) * max(ld, feat_len) * ufeat2.element_size())
+    B = _block_count(csr, (hi - lo) * row_bytes)
     if not B:
         return None
     if _split_threshold(csr):  # a row long enough to need the heavy-row split
@@ -864,7 +871,8 @@ def _block_cuts(csr, row_bytes, block_bytes=None):
     last = indptr[1:]), for kernels that keep the CSR's slot indices (the
     fused GAT layer). ``row_bytes``: bytes gathered per source. None when the
     schedule does not apply."""
-    if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
+    if (_BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0 or
+            row_bytes <= _BLOCK_MIN_ROW_BYTES):
         return None
     lo, hi = _column_span(csr)
     B = _block_count(csr, (hi - lo) * row_bytes, block_bytes or _GAT_BLOCK_BYTES)
