@@ -251,22 +251,30 @@ def test_heavy_row_split(cuda, msg, reduce):
     np.testing.assert_allclose(split1, exact, rtol=1e-5, atol=1e-5 * scale)
 
 
-def test_full_reddit_bench_graph_bit_exact(cuda):
+@pytest.mark.parametrize("F", [128, 41])
+def test_full_reddit_bench_graph_bit_exact(cuda, F):
     """The bench workload at full size (BASELINE configs[1] shape: 232,965 nodes,
-    114.8M edges, F=128) through update_all on the MI355X == the oracle's
-    multi-core restatement, bit for bit."""
+    114.8M edges; F=128, and GCN's 41-class layer) through update_all on the
+    MI355X == the oracle's multi-core restatement, bit for bit: the forward
+    and the backward dH = A^T dC (both on the source-blocked schedule)."""
     import dgl.function as fn
     from dgl import data
     src, dst, n = data.reddit_like(scale=1, seed=0, device=cuda)
     gen = torch.Generator(device=cuda).manual_seed(1)
-    h = torch.rand(n, 128, generator=gen, device=cuda) * 2 - 1
+    h = (torch.rand(n, F, generator=gen, device=cuda) * 2 - 1).requires_grad_(True)
+    dc = torch.rand(n, F, generator=gen, device=cuda) * 2 - 1
     g = dgl.DGLGraph((src.cpu(), dst.cpu()))
     g.ndata["h"] = h
     g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
-    out = g.ndata["o"].cpu().numpy()
-    ip, ix, pos = O.coo_to_csr(n, dst.cpu().numpy(), src.cpu().numpy())
-    ref = O.spmm_csr(ip, ix, pos, h.cpu().numpy(), num_threads=16)
+    g.ndata["o"].backward(dc)
+    out = g.ndata["o"].detach().cpu().numpy()
+    s_np, d_np = src.cpu().numpy(), dst.cpu().numpy()
+    ip, ix, pos = O.coo_to_csr(n, d_np, s_np)
+    ref = O.spmm_csr(ip, ix, pos, h.detach().cpu().numpy(), num_threads=16)
     assert np.array_equal(out, ref)
+    ip, ix, pos = O.coo_to_csr(n, s_np, d_np)  # the transpose, slots in edge-id order
+    ref_grad = O.spmm_csr(ip, ix, pos, dc.cpu().numpy(), num_threads=16)
+    assert np.array_equal(h.grad.cpu().numpy(), ref_grad)
 
 
 @pytest.mark.parametrize("F,H", [(32, 1), (64, 8), (128, 1), (128, 2), (128, 4), (128, 8),
