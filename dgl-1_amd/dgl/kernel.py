@@ -708,6 +708,8 @@ _BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
 # F = 32 runs 1.74 ms in one launch against 1.89 in 5 blocks (F = 41 padded
 # to 192 B: 3.39 -> 2.05; F = 64: 3.56 -> 2.24; tools/blocked_width_sweep.py)
 _BLOCK_MIN_ROW_BYTES = 128
+# how far the slot rule may stretch the slices past the target (_block_count)
+_BLOCK_MAX_STRETCH = float(os.environ.get("DGLHIP_BLOCK_MAX_STRETCH", 2))
 
 
 def set_blocked(policy):
@@ -728,8 +730,14 @@ def _block_count(csr, table_bytes, block_bytes=None):
         return 0
     if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
         return 0
-    B = -(-table_bytes // (block_bytes or _BLOCK_BYTES))
-    B = min(B, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
+    want = -(-table_bytes // (block_bytes or _BLOCK_BYTES))
+    B = min(want, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
+    # rows too short to cut the table into L2-sized slices: slices past twice
+    # the target gain less than the extra passes over out cost (an emulated
+    # rank of 8, its 4 halo chunks at 107 slots per row: 8 blocks of 15 MB,
+    # 8.13 ms against 7.86 unblocked)
+    if _BLOCK_MAX_STRETCH * B < want:
+        return 0
     return int(B) if B >= 2 else 0
 
 
