@@ -709,7 +709,7 @@ _BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
 # to 192 B: 3.39 -> 2.05; F = 64: 3.56 -> 2.24; tools/blocked_width_sweep.py)
 _BLOCK_MIN_ROW_BYTES = 128
 # how far the slot rule may stretch the slices past the target (_block_count)
-_BLOCK_MAX_STRETCH = float(os.environ.get("DGLHIP_BLOCK_MAX_STRETCH", 2))
+_BLOCK_MAX_STRETCH = float(os.environ.get("DGLHIP_BLOCK_MAX_STRETCH", 3))
 
 
 def set_blocked(policy):
@@ -732,10 +732,10 @@ def _block_count(csr, table_bytes, block_bytes=None):
         return 0
     want = -(-table_bytes // (block_bytes or _BLOCK_BYTES))
     B = min(want, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
-    # rows too short to cut the table into L2-sized slices: slices past twice
-    # the target gain less than the extra passes over out cost (an emulated
-    # rank of 8, its 4 halo chunks at 107 slots per row: 8 blocks of 15 MB,
-    # 8.13 ms against 7.86 unblocked)
+    # rows too short to cut the table into L2-sized slices: slices stretched
+    # past 3x the target gain nothing (tools/segment_block_study.py, emulated
+    # ranks: 12.8 MB slices 1.48 -> 1.26 ms; 24-26 MB slices 1.03 -> 1.04,
+    # 1.78 -> 1.78)
     if _BLOCK_MAX_STRETCH * B < want:
         return 0
     return int(B) if B >= 2 else 0
