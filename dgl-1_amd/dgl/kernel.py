@@ -543,9 +543,6 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
     if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
             red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)):
-        sweep = _sweep_slices(csr, ufeat2, feat_len)
-        if sweep is not None:
-            return _run_sweep(csr, sweep, msg, red, ufeat2, feat_len, out), None
         blocks = _block_plan(csr, ufeat2, feat_len)
         if blocks is not None:
             return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out), None
@@ -948,120 +945,6 @@ def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, er
     if red == RED_MEAN:
         out.div_(csr.mean_divisor())
     return out
-
-
-# Source-swept schedule (dglhip_gspmm_sweep_device): one
-# launch in which every wave keeps the partial sums of its rows in registers
-# and walks the source columns in L2-sized slices, so the partial rows never
-# make the per-block trip through memory that the blocked schedule's launches
-# do. Exact for any slot order (a row waits for the slice of its next slot).
-_SWEEP = os.environ.get("DGLHIP_SWEEP", "off")
-_SWEEP_SLICE_BYTES = int(os.environ.get("DGLHIP_SWEEP_SLICE_BYTES", 2 << 20))
-_SWEEP_ROWS = int(os.environ.get("DGLHIP_SWEEP_ROWS", 8))      # rows per wave: 4, 8, 16
-_SWEEP_HEAVY = int(os.environ.get("DGLHIP_SWEEP_HEAVY", 1024))  # rows of >= this many slots
-# rows per wave the bf16-row kernel is built for
-_SWEEP_ROWS_BF16 = 8
-
-
-def set_sweep(policy, slice_bytes=None, rows=None, heavy=None):
-    """Source-swept schedule for copy_u sum / mean: "on" (where it applies),
-    "off"; optional slice size in bytes, rows per wave (4, 8, 16) and the
-    slot count from which a row gets a wave of its own. Returns the old
-    settings as a tuple for a later set_sweep(*old)."""
-    global _SWEEP, _SWEEP_SLICE_BYTES, _SWEEP_ROWS, _SWEEP_HEAVY
-    if rows is not None and int(rows) not in (4, 8, 16):
-        raise DGLError("rows per wave must be 4, 8 or 16")
-    old = (_SWEEP, _SWEEP_SLICE_BYTES, _SWEEP_ROWS, _SWEEP_HEAVY)
-    _SWEEP = str(policy)
-    if slice_bytes is not None:
-        _SWEEP_SLICE_BYTES = int(slice_bytes)
-    if rows is not None:
-        _SWEEP_ROWS = int(rows)
-    if heavy is not None:
-        _SWEEP_HEAVY = int(heavy)
-    return old
-
-
-def _sweep_slices(csr, ufeat2, feat_len):
-    """(col_lo, slice_cols, num_slices) of the swept schedule for ``csr``
-    gathering ``ufeat2``, or None where it does not apply."""
-    if _SWEEP != "on" or csr.nnz == 0 or feat_len % 2 or ufeat2 is None:
-        return None
-    if ufeat2.dim() != 2 or ufeat2.stride(1) != 1:
-        return None
-    ld = ufeat2.stride(0) if ufeat2.shape[0] > 1 else feat_len
-    if ld < feat_len or ld % 2:
-        return None
-    if ufeat2.dtype not in (torch.float32, torch.bfloat16):
-        return None
-    lo, hi = _column_span(csr)
-    table = (hi - lo) * ld * ufeat2.element_size()
-    S = max(1, -(-table // max(_SWEEP_SLICE_BYTES, 1)))
-    return lo, -(-(hi - lo) // S), S
-
-
-def _sweep_plan(csr, rows, skip_empty):
-    """(heavy rows int32, wave rows int32 [W * rows], W) of the swept schedule
-    (cached): rows of at least _SWEEP_HEAVY slots alone, longest first; the
-    others dealt in a snake over the degree-descending order (round t of W
-    rows goes to waves 0..W-1, the next round back from W-1), so every wave's
-    slot total is about the mean. Rows without slots are left out when the
-    call adds to ``out`` (``skip_empty``)."""
-    key = ("sweep", rows, _SWEEP_HEAVY, skip_empty)
-    plan = csr._plans.get(key)
-    if plan is not None:
-        return plan
-    dev = csr.device
-    deg = csr.degrees()
-    if csr.row_order is not None:
-        order = csr.row_order.long()
-    else:
-        order = torch.sort(deg, descending=True, stable=True)[1]
-    n = int((deg > 0).sum()) if skip_empty else csr.num_rows
-    order = order[:n]
-    nh = int((deg[order] >= _SWEEP_HEAVY).sum())
-    heavy = order[:nh].to(torch.int32).contiguous()
-    rest = order[nh:]
-    m = rest.numel()
-    W = -(-m // rows) if m else 0
-    wr = torch.full((W * rows,), -1, dtype=torch.int32, device=dev)
-    if m:
-        p = torch.arange(m, device=dev)
-        rnd, j = torch.div(p, W, rounding_mode="floor"), p % W
-        wave = torch.where(rnd % 2 == 0, j, W - 1 - j)
-        wr[wave * rows + rnd] = rest.to(torch.int32)
-    plan = (heavy, wr, W)
-    csr._plans[key] = plan
-    return plan
-
-
-def _run_sweep(csr, slices, msg, red, ufeat2, feat_len, out):
-    """copy_u (fp32 or bf16 rows) + sum / mean / sum_accum in one swept launch."""
-    dev = ufeat2.device
-    if out is None:
-        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
-    rows = _SWEEP_ROWS_BF16 if msg == MSG_COPY_U_BF16 else _SWEEP_ROWS
-    heavy, wr, W = _sweep_plan(csr, rows, red == RED_SUM_ACCUM)
-    ld = ufeat2.stride(0) if ufeat2.shape[0] > 1 else feat_len
-    lo, cols, S = slices
-    # study knob: at most this many waves per launch (rounds of resident
-    # waves that start together); 0 = one launch
-    per = _SWEEP_LAUNCH_WAVES or (heavy.numel() + W)
-    nh, w0 = heavy.numel(), 0
-    while True:
-        nw = min(W - w0, max(per - nh, 0))
-        check_call(LIB.dglhip_gspmm_sweep_device(
-            msg, red, feat_len, nh, ptr(heavy), nw, ptr(wr[w0 * rows:]) if nw else None, rows,
-            ptr(csr.indptr), ptr(csr.indices), ptr(ufeat2), ld, ptr(out), lo, cols, S,
-            _stream_of(dev)))
-        w0 += nw
-        nh = 0
-        if w0 >= W:
-            break
-    return out
-
-
-_SWEEP_LAUNCH_WAVES = int(os.environ.get("DGLHIP_SWEEP_LAUNCH_WAVES", 0))
 
 
 def blocked_schedule(adj, ufeat):

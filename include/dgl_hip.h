@@ -453,24 +453,6 @@ int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
                               int64_t ufeat_ld, const float* efeat, int64_t efeat_len,
                               float* out, void* stream);
 
-/* Source-swept copy_u + sum / sum_accum / mean / mean_accum (msg_op
- * DGLHIP_MSG_COPY_U, or DGLHIP_MSG_COPY_U_BF16 over bf16 rows), one launch:
- * a wave owns rows_per_wave (4, 8 or 16; 8 for bf16) output rows
- * wave_rows[w * rows_per_wave ...] (-1 = none) and walks the source columns
- * in num_slices slices [col_lo + s * slice_cols, col_lo + (s+1) * slice_cols)
- * (the last slice open-ended), each row consuming its next slots in slot
- * order while their column is below the slice's end, the partial sums in
- * registers. The num_heavy rows heavy_rows get a wave each, launched first.
- * Every row's chain is the CSR's slot order, so the results equal
- * dglhip_gspmm_device's bit for bit for any slot order.
- * feat_len even; ufeat rows at stride ufeat_ld (0: feat_len, else even). */
-int dglhip_gspmm_sweep_device(int msg_op, int reduce_op, int64_t feat_len, int64_t num_heavy,
-                              const int32_t* heavy_rows, int64_t num_waves,
-                              const int32_t* wave_rows, int rows_per_wave,
-                              const int64_t* indptr, const int32_t* indices, const float* ufeat,
-                              int64_t ufeat_ld, float* out, int64_t col_lo, int64_t slice_cols,
-                              int64_t num_slices, void* stream);
-
 /* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of the CSR (argmax slot ids stay the CSR's: k,
  * mapped as dglhip_gspmm_device's), rows in row_order. With accumulate != 0
