@@ -346,28 +346,49 @@ def describe_partition(pg, world, args):
     return "%d-way 1-D dst-row partition, %s" % (world, halo)
 
 
-def timed_steps(step, steps, warmup, world, dev):
+def timed_steps(step, steps, warmup, world, dev, call_events=False):
     """W warm-up steps, then K steps bracketed by barrier + synchronize; returns
     (max-over-ranks seconds, this rank's g-SpMM kernel ms per step). On the
     host path (no device launches to time) the kernel ms is the rank's own
-    wall time per step."""
+    wall time per step.
+
+    Kernel ms: with ``call_events`` (one process, a ROCm device) the GPU span
+    of each step between two events on the stream the library launches on
+    (torch's current stream): every launch of the call and its output's zero
+    fill, nothing else. Otherwise an event pair around every launch
+    (dglhip timing), which at the blocked schedule's 19 launches per call adds
+    about 0.18 ms of markers to the timed region (3.84 ms per call without
+    them, tools/items_policy_ab.py)."""
+    use_ev = call_events and dev.type == "cuda" and not dist.is_initialized()
     for _ in range(warmup):
         step()
     _sync(dev)
     if dist.is_initialized():
         dist.barrier()
-    kernel.timing_enable(True)
+    if not use_ev:
+        kernel.timing_enable(True)
+    evs = []
     _sync(dev)
     t_start = time.perf_counter()
     for _ in range(steps):
+        if use_ev:
+            a = torch.cuda.Event(enable_timing=True)
+            a.record()
         step()
+        if use_ev:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            evs.append((a, b))
     _sync(dev)
     own = time.perf_counter() - t_start
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    kms, launches = kernel.timing_read()
-    kernel.timing_enable(False)
+    if use_ev:
+        kms, launches = sum(a.elapsed_time(b) for a, b in evs), steps
+    else:
+        kms, launches = kernel.timing_read()
+        kernel.timing_enable(False)
     if launches == 0:
         kms = own * 1e3
     if dist.is_initialized():
@@ -518,7 +539,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         _sync(dev)
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
-        elapsed, kms = timed_steps(step, steps, 2, world, dev)
+        elapsed, kms = timed_steps(step, steps, 2, world, dev, call_events=True)
         exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
         # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
         roof = roofline_block(
@@ -754,11 +775,15 @@ def main(argv=None):
         log("setup done in %.1fs; peak HBM %.1f GB" % (
             time.time() - t0, torch.cuda.max_memory_allocated(dev) / 1e9))
 
-    elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
+    elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev, call_events=True)
     value = num_edges_total * args.steps / elapsed
     roof = roofline_block(
         num_local_edges, num_rows, kernel_ms, world, dev, n * FEAT * 4, blocks,
         traffic=None if pmc is None else pmc["bytes"],
+        kernel_timing=("GPU span of each call between two events on the launch stream (every "
+                       "launch of the call and its output's zero fill)"
+                       if not dist.is_initialized() and dev.type == "cuda" else
+                       "event pair around every launch, summed per step"),
         kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
             ", every segment of the pipelined partition" if dist.is_initialized() else
             ", every block launch and short-row tier of one call" if blocks else ""),
