@@ -226,10 +226,17 @@ class PartitionedGraph(object):
                 (SURVEY.md §8e); the local reduction stays fp32. Opt-in: the
                 rows' results then carry bf16 rounding of the remote inputs.
                 Gradients travel in fp32 in every halo mode.
+    overlap   : pipelined path only: run the chunk exchanges on a side stream
+                that the segments' products wait on by event. None (default):
+                with RCCL on a ROCm device; True: also with gloo on a ROCm
+                device (gloo orders its device copies against the stream a
+                collective is issued on, so the same events and stream
+                bookkeeping run as under RCCL: the one-GPU test of that path);
+                False: inline on the current stream.
     """
 
     def __init__(self, num_nodes, src, dst, bounds, device, group=None, pipeline_chunks=0,
-                 rank=None, world=None, halo="auto", halo_dtype=None):
+                 rank=None, world=None, halo="auto", halo_dtype=None, overlap=None):
         if halo_dtype not in (None, torch.float32, torch.bfloat16):
             raise ValueError("halo_dtype must be None, torch.float32 or torch.bfloat16")
         self.halo_dtype = None if halo_dtype == torch.float32 else halo_dtype
@@ -285,10 +292,15 @@ class PartitionedGraph(object):
             self.adj = kernel.from_coo(self.num_local, self.world * self.max_rows,
                                        dst - self.lo, cols, kernel.ORDER_EID, device)
         if self.chunks > 0:
-            # overlap needs an asynchronous collective backend (RCCL); gloo runs inline
-            overlap = (not self._emulated and self.device.type == "cuda"
-                       and dist.get_backend(self.group) == "nccl")
+            if overlap is None:
+                # by default only with an asynchronous collective backend (RCCL)
+                overlap = (not self._emulated and self.device.type == "cuda"
+                           and dist.get_backend(self.group) == "nccl")
+            elif overlap and (self._emulated or self.device.type != "cuda"):
+                raise ValueError("overlap needs a ROCm device and real peers")
             self.comm_stream = torch.cuda.Stream(self.device) if overlap else None
+        elif overlap:
+            raise ValueError("overlap applies to the pipelined path (pipeline_chunks > 0)")
 
     def _coll_dev(self):
         """Device the process group's collectives take tensors on."""
