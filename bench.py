@@ -346,49 +346,36 @@ def describe_partition(pg, world, args):
     return "%d-way 1-D dst-row partition, %s" % (world, halo)
 
 
-def timed_steps(step, steps, warmup, world, dev, call_events=False):
+def timed_steps(step, steps, warmup, world, dev):
     """W warm-up steps, then K steps bracketed by barrier + synchronize; returns
     (max-over-ranks seconds, this rank's g-SpMM kernel ms per step). On the
     host path (no device launches to time) the kernel ms is the rank's own
     wall time per step.
 
-    Kernel ms: with ``call_events`` (one process, a ROCm device) the GPU span
-    of each step between two events on the stream the library launches on
-    (torch's current stream): every launch of the call and its output's zero
-    fill, nothing else. Otherwise an event pair around every launch
-    (dglhip timing), which at the blocked schedule's 19 launches per call adds
-    about 0.18 ms of markers to the timed region (3.84 ms per call without
-    them, tools/items_policy_ab.py)."""
-    use_ev = call_events and dev.type == "cuda" and not dist.is_initialized()
+    Kernel ms: the GPU span of every g-SpMM call of the step between two
+    events on the stream the library launches on (kernel.timing_enable
+    per_call: the call's launches and its output's zero fill; at N > 1 the
+    waits on the exchange precede a segment's first event, so they stay out).
+    An event pair around every launch instead (r01-r03) put 38 markers into
+    each blocked call of the timed region: 0.18 ms per N = 1 step (3.84 ms per
+    call without them, tools/items_policy_ab.py)."""
     for _ in range(warmup):
         step()
     _sync(dev)
     if dist.is_initialized():
         dist.barrier()
-    if not use_ev:
-        kernel.timing_enable(True)
-    evs = []
+    kernel.timing_enable(True, per_call=dev.type == "cuda")
     _sync(dev)
     t_start = time.perf_counter()
     for _ in range(steps):
-        if use_ev:
-            a = torch.cuda.Event(enable_timing=True)
-            a.record()
         step()
-        if use_ev:
-            b = torch.cuda.Event(enable_timing=True)
-            b.record()
-            evs.append((a, b))
     _sync(dev)
     own = time.perf_counter() - t_start
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
-    if use_ev:
-        kms, launches = sum(a.elapsed_time(b) for a, b in evs), steps
-    else:
-        kms, launches = kernel.timing_read()
-        kernel.timing_enable(False)
+    kms, launches = kernel.timing_read()
+    kernel.timing_enable(False)
     if launches == 0:
         kms = own * 1e3
     if dist.is_initialized():
@@ -539,7 +526,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
         _sync(dev)
         log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
         steps = min(args.steps, 5)
-        elapsed, kms = timed_steps(step, steps, 2, world, dev, call_events=True)
+        elapsed, kms = timed_steps(step, steps, 2, world, dev)
         exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
         # HBM-honest roofline: H (34 GB at scale 26) cannot stay in the caches
         roof = roofline_block(
@@ -775,15 +762,14 @@ def main(argv=None):
         log("setup done in %.1fs; peak HBM %.1f GB" % (
             time.time() - t0, torch.cuda.max_memory_allocated(dev) / 1e9))
 
-    elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev, call_events=True)
+    elapsed, kernel_ms = timed_steps(step, args.steps, args.warmup, world, dev)
     value = num_edges_total * args.steps / elapsed
     roof = roofline_block(
         num_local_edges, num_rows, kernel_ms, world, dev, n * FEAT * 4, blocks,
         traffic=None if pmc is None else pmc["bytes"],
-        kernel_timing=("GPU span of each call between two events on the launch stream (every "
-                       "launch of the call and its output's zero fill)"
-                       if not dist.is_initialized() and dev.type == "cuda" else
-                       "event pair around every launch, summed per step"),
+        kernel_timing=("GPU span of each g-SpMM call between two events on the launch stream "
+                       "(every launch of the call and its output's zero fill), summed per step"
+                       if dev.type == "cuda" else "host wall time per step"),
         kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
             ", every segment of the pipelined partition" if dist.is_initialized() else
             ", every block launch and short-row tier of one call" if blocks else ""),

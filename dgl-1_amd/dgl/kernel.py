@@ -539,6 +539,19 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
     order), SLOT = row k (efeat2 laid out in this CSR's slot order), or an
     int64 tensor of rows per slot."""
     dev = (ufeat2 if ufeat2 is not None else efeat2).device
+    if _CALL_EVENTS is None or dev.type != "cuda":
+        return _run_gspmm_call(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out,
+                               emap, dev)
+    start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    start.record(torch.cuda.current_stream(dev))
+    res = _run_gspmm_call(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out, emap,
+                          dev)
+    end.record(torch.cuda.current_stream(dev))
+    _CALL_EVENTS.append((start, end))
+    return res
+
+
+def _run_gspmm_call(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out, emap, dev):
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
     if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
@@ -1424,13 +1437,29 @@ def set_sddmm_variant(alternate):
     check_call(LIB.dglhip_set_sddmm_variant(1 if alternate else 0))
 
 
-def timing_enable(flag=True):
-    """Bracket every g-SpMM/g-SDDMM launch with hipEvents (bench support)."""
-    check_call(LIB.dglhip_timing_enable(1 if flag else 0))
+# per-call timing (timing_enable(per_call=True)): (start, end) event pairs
+_CALL_EVENTS = None
+
+
+def timing_enable(flag=True, per_call=False):
+    """Bracket every g-SpMM/g-SDDMM launch with hipEvents (bench support).
+    With ``per_call`` instead one event pair on the current stream around each
+    g-SpMM call on a ROCm device (all of the call's launches and its output's
+    zero fill, no markers between the launches: the blocked schedule's 19
+    launches per call had paid 0.18 ms for them); timing_read then counts
+    calls."""
+    global _CALL_EVENTS
+    _CALL_EVENTS = [] if (flag and per_call) else None
+    check_call(LIB.dglhip_timing_enable(1 if (flag and not per_call) else 0))
 
 
 def timing_read():
-    """(total kernel ms, launches) since the last timing_enable."""
+    """(total kernel ms, launches — calls under per-call timing) since the
+    last timing_enable."""
+    if _CALL_EVENTS is not None:
+        for _, end in _CALL_EVENTS:
+            end.synchronize()
+        return sum(a.elapsed_time(b) for a, b in _CALL_EVENTS), len(_CALL_EVENTS)
     ms = ctypes.c_double()
     n = ctypes.c_int64()
     check_call(LIB.dglhip_timing_read(ctypes.byref(ms), ctypes.byref(n)))

@@ -446,3 +446,30 @@ def test_short_row_tiers_accumulate_and_bf16(cuda):
             finally:
                 kernel.set_short_rows(old)
         assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
+def test_per_call_timing_counts_calls():
+    """kernel.timing_enable(per_call=True): one event pair per g-SpMM call on
+    the launch stream (bench.py's kernel ms), whatever the call's launch
+    count; the per-launch mode still counts launches."""
+    from dgl import kernel
+    dev = torch.device("cuda", 0)
+    n = 5000
+    g = torch.Generator().manual_seed(0)
+    src = torch.randint(0, n, (200_000,), generator=g)
+    dst = torch.randint(0, n, (200_000,), generator=g)
+    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    h = torch.rand(n, 64, device=dev)
+    kernel.gspmm(adj, "copy_u", "sum", h)
+    kernel.timing_enable(True, per_call=True)
+    for _ in range(3):
+        kernel.gspmm(adj, "copy_u", "sum", h)
+    ms, calls = kernel.timing_read()
+    kernel.timing_enable(False)
+    assert calls == 3 and ms > 0
+    kernel.timing_enable(True)
+    kernel.gspmm(adj, "copy_u", "sum", h)
+    ms1, launches = kernel.timing_read()
+    kernel.timing_enable(False)
+    assert launches >= 1 and ms1 > 0
