@@ -58,7 +58,9 @@ __host__ __device__ __forceinline__ bool gat_keep(uint64_t seed, int64_t idx, ui
 }
 
 // study knob (dglhip_set_gat_variant): 0 automatic, 1 the per-lane kernel,
-// 2 the LDS-shared attention kernel (head counts 1, 2, 4, 8, 16)
+// 2 the LDS-shared attention kernel (head counts 1, 2, 4, 8, 16) with each
+// batch's feature rows gathered after its attention, 3 the same kernel with
+// them gathered before it
 int g_gat_variant = 0;
 
 // keep iff hash >= threshold: P(keep) = 1 - p
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
 // One batch of the LDS kernel: slots [k, k + nb) of the row (FULL: nb == U,
 // no predication; the row's last partial batch runs with FULL = false, as
 // reduce_range's predicated tail).
-template <int H, int VEC, bool DROP, bool SMALL, bool FULL>
+template <int H, int VEC, bool DROP, bool SMALL, bool FULL, bool EARLY>
 __device__ __forceinline__ void gat_batch(
     int64_t k, int nb, int64_t F, uint32_t voff, int64_t h, int hc, int jc, float rc,
     const int32_t* __restrict__ indices, const float* __restrict__ el,
@@ -220,6 +222,14 @@ __device__ __forceinline__ void gat_batch(
   constexpr int U = 16;
   constexpr int SPP = 64 / H;               // slots covered per pass of the wave
   constexpr int PPL = (U + SPP - 1) / SPP;  // attention values per lane per batch
+  V u[U];
+  if (EARLY) {
+    // the feature rows first: their latency then overlaps the logit gathers
+    // and the attention (study variant dglhip_set_gat_variant(3))
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, indices[k + j], F, voff);
+  }
 #pragma unroll
   for (int i = 0; i < PPL; ++i) {
     const int j = jc + SPP * i;
@@ -239,16 +249,17 @@ __device__ __forceinline__ void gat_batch(
     }
   }
   // the batch's feature-row gathers (column ids through the scalar cache),
-  // issued after the attention so that its few registers and the 16 rows in
-  // flight are never live together (7 waves per SIMD); the other waves of the
-  // SIMD hide the logit gathers' latency
+  // after the attention unless EARLY: then they are in flight during the
+  // logit gathers and the attention (84 instead of 92 VGPRs at 8 x 16, five
+  // waves per SIMD either way; the default on two-float lanes)
   // row base from the scalar slot stream (SGPRs) + the lane's 32-bit byte
   // offset: the saddr load form, one offset VGPR for all 16 gathers instead
   // of a 64-bit address per gather (80 -> fewer VGPRs, more waves per SIMD)
-  V u[U];
+  if (!EARLY) {
 #pragma unroll
-  for (int j = 0; j < U; ++j)
-    if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, indices[k + j], F, voff);
+    for (int j = 0; j < U; ++j)
+      if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, indices[k + j], F, voff);
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -275,7 +286,7 @@ __device__ __forceinline__ void gat_batch(
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int H, int VEC, bool DROP, bool SMALL>
+template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false>
 __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     int64_t num_rows, int64_t D, const int64_t* __restrict__ row_beg,
     const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
@@ -319,12 +330,12 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     }
     int64_t k = beg;
     for (; k + U <= end; k += U)
-      gat_batch<H, VEC, DROP, SMALL, true>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab,
+      gat_batch<H, VEC, DROP, SMALL, true, EARLY>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab,
                                            alpha, lo, hi,
                                     apply_exp, seed, thr, scale, s_a[wi], s_w[wi], a_out, w_out,
                                     acc, zacc);
     if (k < end)
-      gat_batch<H, VEC, DROP, SMALL, false>(k, static_cast<int>(end - k), F, voff, h, hc, jc,
+      gat_batch<H, VEC, DROP, SMALL, false, EARLY>(k, static_cast<int>(end - k), F, voff, h, hc, jc,
                                             rc, indices, el, ft, tab, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
                                      s_w[wi], a_out, w_out, acc, zacc);
     if (active) {
@@ -383,14 +394,24 @@ int dglhip_gat_aggregate_ranges_device(
   const bool whole_rows = row_end == row_beg + 1;
   const bool lds_heads = num_heads == 1 || num_heads == 2 || num_heads == 4 ||
                          num_heads == 8 || num_heads == 16;
-  if (lds_heads && (g_gat_variant == 2 || (g_gat_variant == 0 && (!v2 || !whole_rows)))) {
+  if (lds_heads && (g_gat_variant == 2 || (g_gat_variant != 1 && (!v2 || !whole_rows)))) {
+    // the batch's feature rows issued before its attention on two-float lanes
+    // (Reddit-shaped 8 x 16, blocked: 6.25 -> 6.07 ms, with dropout 7.05 ->
+    // 6.49; one-float lanes level: Pubmed's 8 x 8 and 8 x 3;
+    // tools/gat_early_ab.py); variant 2 keeps them after it, 3 before it
+    const bool early = g_gat_variant == 3 || (g_gat_variant == 0 && v2);
     timed_launch(stream, [&] {
-#define DGLHIP_GATL(HH, VV, DD, SM)                                                        \
-  hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD, SM>), grid_1d(blocks), dim3(256), \
-                     0, stream, num_rows, head_dim, row_beg, row_end, accumulate, indices,   \
-                     row_order, el, er, ft,                                                  \
+#define DGLHIP_GATL_E(HH, VV, DD, SM, EE)                                                    \
+  hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD, SM, EE>), grid_1d(blocks),        \
+                     dim3(256), 0, stream, num_rows, head_dim, row_beg, row_end, accumulate, \
+                     indices, row_order, el, er, ft,                                         \
                      alpha, clamp_lo, clamp_hi, apply_exp, seed, seed_offset, thr, scale,    \
                      out_ft, out_z, attn_out, attn_drop_out, tbytes)
+#define DGLHIP_GATL(HH, VV, DD, SM)                                                          \
+  do {                                                                                       \
+    if (early) DGLHIP_GATL_E(HH, VV, DD, SM, true);                                          \
+    else DGLHIP_GATL_E(HH, VV, DD, SM, false);                                               \
+  } while (0)
 #define DGLHIP_GATS(HH, VV, DD) \
   if (small) DGLHIP_GATL(HH, VV, DD, true); else DGLHIP_GATL(HH, VV, DD, false);
 #define DGLHIP_GATH(HH)                                                                    \
@@ -403,6 +424,7 @@ int dglhip_gat_aggregate_ranges_device(
 #undef DGLHIP_GATH
 #undef DGLHIP_GATS
 #undef DGLHIP_GATL
+#undef DGLHIP_GATL_E
     });
     return 0;
   }
@@ -440,7 +462,7 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
 
 int dglhip_set_gat_variant(int variant) {
   API_BEGIN();
-  DGLHIP_CHECK(variant >= 0 && variant <= 2, "unknown GAT kernel variant " << variant);
+  DGLHIP_CHECK(variant >= 0 && variant <= 3, "unknown GAT kernel variant " << variant);
   g_gat_variant = variant;
   API_END();
 }

@@ -1635,7 +1635,9 @@ def _gat_seed_offset(dev):
 def set_gat_variant(variant):
     """Study knob for the fused GAT kernel: 0 automatic (default), 1 the
     attention computed in every lane that consumes it, 2 once per (slot,
-    head) through LDS (1/2/4/8/16 heads). Same bits."""
+    head) through LDS (1/2/4/8/16 heads) with each batch's feature rows
+    gathered after its attention, 3 the LDS kernel with them gathered before
+    it (what 0 picks on two-float lanes). Same bits."""
     check_call(LIB.dglhip_set_gat_variant(int(variant)))
 
 

@@ -244,3 +244,34 @@ def test_no_grad_stores_no_attention(device):
     fs2, z2 = kernel.gat_aggregate(adj, ft, el, er)
     assert torch.equal(fs, fs2.detach()) and torch.equal(z, z2.detach())
     assert fs.grad_fn is None and fs2.grad_fn is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("H,D", [(8, 16), (4, 32), (8, 8), (2, 3)])
+@pytest.mark.parametrize("blocked", ["auto", "off"])
+def test_kernel_variants_same_bits(H, D, blocked):
+    """Every fused-kernel variant (dglhip_set_gat_variant: per-lane
+    attention, LDS attention with the feature rows gathered after it, or
+    before it) gives the automatic choice's outputs, kept attention and
+    dropped attention bit for bit, blocked or in one launch."""
+    dev = _dev("cuda")
+    n, m = 60_000, 3_000_000
+    rng = np.random.default_rng(5)
+    src, dst = rng.integers(0, n, m), rng.integers(0, n, m)
+    o = np.lexsort((dst, src))
+    g = dgl.DGLGraph((torch.from_numpy(src[o]), torch.from_numpy(dst[o])))
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(n, H, D, dev)
+    old = kernel.set_blocked(blocked)
+    try:
+        outs = {}
+        for v in (0, 1, 2, 3):
+            kernel.set_gat_variant(v)
+            fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, attn_drop=0.25, seed=19)
+            outs[v] = (fs.detach(), z.detach()) + tuple(_grads((fs, z), (ft, el, er)))
+    finally:
+        kernel.set_gat_variant(0)
+        kernel.set_blocked(old)
+    for v in (1, 2, 3):
+        for a, b in zip(outs[v], outs[0]):
+            assert torch.equal(a, b), v
