@@ -52,6 +52,17 @@ __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, in
   return (a > e.lo && a < e.hi) ? g : 0.0f;
 }
 
+// gat_epi on operands loaded ahead (the slot's attention a and dropped copy
+// w, the row's normaliser gradient dz): the same arithmetic.
+__device__ __forceinline__ float gat_epi_pre(const GatEpi& e, float t, float a, float w,
+                                             float dz) {
+  if (e.w) t = w != 0.0f ? t * e.scale : 0.0f;
+  if (e.dz) t = t + dz;
+  const float g = e.apply_exp ? (t * a) * (a < 1.0f ? e.alpha : 1.0f)
+                              : t * (a < 0.0f ? e.alpha : 1.0f);
+  return (a > e.lo && a < e.hi) ? g : 0.0f;
+}
+
 // SDDMM dot: one wave per row. One head (H == 1): per slot a wave-wide fma
 // dot product of two feature rows reduced in a fixed butterfly order. Several
 // heads: lane h computes head h's dot over its D = F / H features as one
@@ -158,7 +169,7 @@ __device__ __forceinline__ void slot_reduce_scatter(float* q, int j) {
 //     of the slot's heads (8 heads at D = 16: one 32-B run per slot).
 // The pairing of lanes is the full xor butterfly's (4, 2, 1 / 2, 1 / 1), so
 // results are deterministic and equal the butterfly's bits.
-template <int NB, int UNROLL, int H, bool EPI = false>
+template <int NB, int UNROLL, int H, bool EPI = false, bool PRE = true>
 __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
     int64_t num_rows, const int64_t* __restrict__ row_beg, const int64_t* __restrict__ row_end,
     const int32_t* __restrict__ row_order, const int32_t* __restrict__ indices, const int64_t* __restrict__ eid,
@@ -178,11 +189,25 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   const int s = lane >> 3, j = lane & 7;
   const int64_t beg = row_beg[row], end = row_end[row];
   if (beg == end) return;
+  // the heads this lane stores per slot (the branches below): T of them
+  constexpr int T = LPH == 8 ? (H >= 8 ? H / 8 : 1) : (NB >= LPH ? NB / LPH : 1);
+  auto lane_head = [&](int t) -> int {
+    if (LPH == 8) return H >= 8 ? j * (H / 8) + t : j / (H >= 8 ? 1 : 8 / H);
+    constexpr int HPB = 8 / LPH;
+    const int g = j / LPH, r = j % LPH;
+    return NB >= LPH ? (r * (NB / LPH) + t) * HPB + g : (r / (NB >= LPH ? 1 : LPH / NB)) * HPB + g;
+  };
+  // the GAT epilogue's per-row operand, loaded once
+  float dzv[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+    dzv[t] = (EPI && PRE && epi.dz) ? epi.dz[row * H + lane_head(t)] : 0.0f;
   f32x4 a[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) a[i] = ldv<4>(lhs + row * F + 32 * i + 4 * j);
   for (int64_t k0 = beg; k0 < end; k0 += 8 * UNROLL) {
     f32x4 c[UNROLL][NB];
+    float ea[UNROLL][T], ew[UNROLL][T];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       int64_t k = k0 + 8 * u + s;
@@ -190,6 +215,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
       const float* r = rhs + int64_t(indices[k]) * F + 4 * j;
 #pragma unroll
       for (int i = 0; i < NB; ++i) c[u][i] = ldv<4>(r + 32 * i);
+      // the epilogue's per-slot operands in flight with the gathers, not
+      // behind the dot product (attention gradient: fewer serial latencies)
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        ea[u][t] = (EPI && PRE) ? epi.a[k * H + lane_head(t)] : 0.0f;
+        ew[u][t] = (EPI && PRE && epi.w) ? epi.w[k * H + lane_head(t)] : 0.0f;
+      }
     }
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -216,13 +248,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t) {
             const int hh = j * (H / 8) + t;
-            if (k < end) out[obase + hh] = EPI ? gat_epi(epi, q[t], k, H, hh, row) : q[t];
+            if (k < end) out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
           }
         } else {
           constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
           const int hh = j / DUP;
           if (k < end && j % DUP == 0)
-            out[obase + hh] = EPI ? gat_epi(epi, q[0], k, H, hh, row) : q[0];
+            out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
         }
       } else {
         constexpr int HPB = 8 / LPH;
@@ -232,13 +264,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t) {
             const int hh = (r * (NB / LPH) + t) * HPB + g;
-            if (k < end) out[obase + hh] = EPI ? gat_epi(epi, p[t], k, H, hh, row) : p[t];
+            if (k < end) out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
           }
         } else {
           constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
           const int hh = (r / DUP) * HPB + g;
           if (k < end && r % DUP == 0)
-            out[obase + hh] = EPI ? gat_epi(epi, p[0], k, H, hh, row) : p[0];
+            out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
         }
       }
     }
@@ -604,12 +636,24 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
   // shallower depth wins at F = 128 (Reddit-shaped graph, 1 / 8 / 16 heads:
   // 6.30 -> 4.89, 6.68 -> 5.69, 7.70 -> 7.07 ms per call, eid order,
   // tools/reducer_bench.py); dglhip_set_sddmm_variant(1) swaps the two
-  const bool alt = (row_end != row_beg + 1) != (g_sddmm_alt != 0);
+  const bool alt = (row_end != row_beg + 1) != ((g_sddmm_alt & 1) != 0);
+  // the GAT epilogue's per-slot operands: loaded with the slot's gathers
+  // (default), or after the dot product (dglhip_set_sddmm_variant bit 1)
+  const bool late = (g_sddmm_alt & 2) != 0;
   timed_launch(stream, [&] {
+#define DGLHIP_SDDMM_K2(NB, U, HH, PP)                                                     \
+  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI, PP>), grid_1d(blocks),        \
+                     dim3(256), 0, stream, num_rows, row_beg, row_end, row_order, indices, eid, \
+                     lhs, rhs, out, epi)
 #define DGLHIP_SDDMM_K(NB, U, HH)                                                          \
-  hipLaunchKernelGGL((gsddmm_dot_sliced_kernel<NB, U, HH, EPI>), grid_1d(blocks), dim3(256), \
-                     0, stream, num_rows, row_beg, row_end, row_order, indices, eid, lhs, rhs,  \
-                     out, epi)
+  do {                                                                                     \
+    if constexpr (EPI) {                                                                   \
+      if (late) DGLHIP_SDDMM_K2(NB, U, HH, false);                                         \
+      else DGLHIP_SDDMM_K2(NB, U, HH, true);                                               \
+    } else {                                                                               \
+      DGLHIP_SDDMM_K2(NB, U, HH, true);                                                    \
+    }                                                                                      \
+  } while (0)
 #define DGLHIP_SDDMM_H(NB, U, HH)                                                          \
   if (num_heads == HH) {                                                                   \
     if (!alt) DGLHIP_SDDMM_K(NB, U, HH);                                                  \
@@ -642,6 +686,7 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
                        num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices, eid,
                        lhs, rhs, out, epi);
 #undef DGLHIP_SDDMM_K
+#undef DGLHIP_SDDMM_K2
 #undef DGLHIP_SDDMM_H
   });
 }
@@ -724,7 +769,9 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined) {
 
 int dglhip_set_sddmm_variant(int alternate) {
   API_BEGIN();
-  DGLHIP_CHECK(alternate == 0 || alternate == 1, "unsupported g-SDDMM variant " << alternate);
+  // bit 0: the other depth of slots in flight; bit 1: the GAT epilogue's
+  // operands loaded after the dot product (the form before r03's prefetch)
+  DGLHIP_CHECK(alternate >= 0 && alternate <= 3, "unsupported g-SDDMM variant " << alternate);
   g_sddmm_alt = alternate;
   API_END();
 }

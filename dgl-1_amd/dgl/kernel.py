@@ -1432,9 +1432,11 @@ def set_gather_mode(buffer_descriptors):
 
 
 def set_sddmm_variant(alternate):
-    """Study knob: run the sliced g-SDDMM dot at its alternative depth of
-    slots in flight (1) or the default (0)."""
-    check_call(LIB.dglhip_set_sddmm_variant(1 if alternate else 0))
+    """Study knob for the sliced g-SDDMM dot: bit 0 runs it at its
+    alternative depth of slots in flight, bit 1 loads the GAT epilogue's
+    per-slot operands after the dot product instead of with the slot's
+    gathers; 0 (default) neither. Same bits."""
+    check_call(LIB.dglhip_set_sddmm_variant(int(alternate)))
 
 
 # per-call timing (timing_enable(per_call=True)): (start, end) event pairs
