@@ -40,6 +40,10 @@ struct GatEpi {
   const float* dz;    // normaliser gradient, [rows, H] (NULL: zero)
   float alpha, lo, hi, scale;
   int apply_exp;
+  // optional: each row's per-head sum of the values stored, added in slot
+  // order to what rsum holds ([rows, H]; GAT's er gradient, the copy_e sum
+  // of the stored values over the row's slots, fused; sliced kernel only)
+  float* rsum = nullptr;
 };
 
 __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, int64_t H,
@@ -202,6 +206,12 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
   for (int t = 0; t < T; ++t)
     dzv[t] = (EPI && PRE && epi.dz) ? epi.dz[row * H + lane_head(t)] : 0.0f;
+  // the fused row sums: lanes of slot group s each chain the values of every
+  // slot of the row in slot order (s = 0 stores them)
+  const bool rs = EPI && epi.rsum != nullptr;  // wave-uniform
+  float racc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) racc[t] = rs ? epi.rsum[row * H + lane_head(t)] : 0.0f;
   f32x4 a[NB];
 #pragma unroll
   for (int i = 0; i < NB; ++i) a[i] = ldv<4>(lhs + row * F + 32 * i + 4 * j);
@@ -235,6 +245,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
         p[i] = __builtin_fmaf(a[i].w, c[u][i].w, t);
       }
       const int64_t obase = (k < end ? (eid ? eid[k] : k) : 0) * H;
+      float sv[T];  // the values this lane's slot stores, by lane_head(t)
       if (LPH == 8) {
         float q[H];
 #pragma unroll
@@ -248,13 +259,14 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t) {
             const int hh = j * (H / 8) + t;
-            if (k < end) out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
+            if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
           const int hh = j / DUP;
-          if (k < end && j % DUP == 0)
-            out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
+          if (k < end && j % DUP == 0) out[obase + hh] = sv[0];
         }
       } else {
         constexpr int HPB = 8 / LPH;
@@ -264,16 +276,33 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t) {
             const int hh = (r * (NB / LPH) + t) * HPB + g;
-            if (k < end) out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
+            if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
           const int hh = (r / DUP) * HPB + g;
-          if (k < end && r % DUP == 0)
-            out[obase + hh] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
+          if (k < end && r % DUP == 0) out[obase + hh] = sv[0];
+        }
+      }
+      if (rs) {
+        // the 8 slots of group u in slot order: lane (s, j) adds slot s2's
+        // value of its head from lane (s2, j) (same j, same head)
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) {
+#pragma unroll
+          for (int t = 0; t < T; ++t) {
+            const float v = __shfl(sv[t], s2 * 8 + j, 64);
+            if (k0 + 8 * u + s2 < end) racc[t] = racc[t] + v;
+          }
         }
       }
     }
+  }
+  if (rs && s == 0) {
+#pragma unroll
+    for (int t = 0; t < T; ++t) epi.rsum[row * H + lane_head(t)] = racc[t];
   }
 }
 
@@ -682,6 +711,10 @@ static void launch_sddmm_dot(int64_t num_rows, int64_t feat_len, int64_t num_hea
       DGLHIP_SDDMM_H(16, 1, 8) DGLHIP_SDDMM_H(16, 1, 16) DGLHIP_SDDMM_H(16, 1, 32)
       DGLHIP_SDDMM_H(16, 1, 64) DGLHIP_SDDMM_H(16, 1, 128)
     }
+    DGLHIP_CHECK(!EPI || epi.rsum == nullptr,
+                 "fused row sums need the sliced g-SDDMM (F = 32 x {1,2,4,8,16}, power-of-two "
+                 "heads of >= 4 features, 16-B aligned rows): F = " << feat_len << ", H = "
+                 << num_heads);
     hipLaunchKernelGGL((gsddmm_dot_kernel<EPI>), grid_1d(blocks), dim3(256), 0, stream,
                        num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices, eid,
                        lhs, rhs, out, epi);
@@ -727,8 +760,30 @@ int dglhip_gat_attention_grad_ranges_device(
     const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
     const float* dout, const float* ft,
     const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
-    float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream_) {
+    float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream) {
+  return dglhip_gat_attention_grad_rowsum_ranges_device(
+      num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices, dout, ft, attn,
+      attn_drop, dz, alpha, clamp_lo, clamp_hi, apply_exp, drop_scale, grad, nullptr, stream);
+}
+
+int dglhip_gat_attention_grad_rowsum_ok(int64_t feat_len, int64_t num_heads) {
+  if (feat_len <= 0 || num_heads < 1 || feat_len % 32 != 0 || feat_len % num_heads != 0) return 0;
+  const int64_t nb = feat_len / 32, D = feat_len / num_heads;
+  const bool nb_ok = nb == 1 || nb == 2 || nb == 4 || nb == 8 || nb == 16;
+  const bool pow2 = (num_heads & (num_heads - 1)) == 0;
+  return nb_ok && pow2 && D >= 4 ? 1 : 0;
+}
+
+int dglhip_gat_attention_grad_rowsum_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft,
+    const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_scale, float* grad, float* grad_rowsum,
+    void* stream_) {
   API_BEGIN();
+  DGLHIP_CHECK(grad_rowsum == nullptr || dglhip_gat_attention_grad_rowsum_ok(feat_len, num_heads),
+               "fused row sums: unsupported shape F = " << feat_len << ", H = " << num_heads);
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
   DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
@@ -736,7 +791,8 @@ int dglhip_gat_attention_grad_ranges_device(
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(row_beg && row_end && indices && dout && ft && attn && grad,
                "null pointer argument");
-  const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp};
+  const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp,
+                   grad_rowsum};
   launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
                          nullptr, dout, ft, grad, epi, stream);
   API_END();

@@ -103,6 +103,11 @@ def _load():
                                                              ctypes.c_float, ctypes.c_float,
                                                              ctypes.c_float, _c_int,
                                                              ctypes.c_float, _vp, _vp]),
+        "dglhip_gat_attention_grad_rowsum_ok": (_c_int, [_c_i64, _c_i64]),
+        "dglhip_gat_attention_grad_rowsum_ranges_device": (
+            _c_int, [_c_i64, _c_i64, _c_i64] + [_vp] * 9 +
+            [ctypes.c_float, ctypes.c_float, ctypes.c_float, _c_int, ctypes.c_float, _vp, _vp,
+             _vp]),
         "dglhip_gat_dropout_mask_host": (_c_int, [_c_i64, _c_i64, ctypes.c_float, ctypes.c_uint64,
                                                   _vp]),
         "dglhip_degree_bucketing_host": (_c_int, [_c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp, _vp]),

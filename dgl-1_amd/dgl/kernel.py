@@ -1750,13 +1750,22 @@ class _GATAggregate(torch.autograd.Function):
                 # (ft rows of one block at a time) give the same bits
                 cuts = _block_cuts(fwd, F * 4) or [fwd.indptr, fwd.indptr[1:]]
                 ft2c = ft2.contiguous()
+                # er's gradient (the copy_edge sum of g over each row's slots)
+                # summed in the same pass, in slot order across the blocks:
+                # the same chain as the separate sum, one E x H read less
+                fuse_er = (need_er and LIB.dglhip_gat_attention_grad_rowsum_ok(F, H) == 1 and
+                           d_ft.data_ptr() % 16 == 0 and ft2c.data_ptr() % 16 == 0)
+                er_sum = (torch.zeros(fwd.num_rows, H, dtype=torch.float32, device=ft2.device)
+                          if fuse_er else None)
                 for b in range(len(cuts) - 1):
-                    check_call(LIB.dglhip_gat_attention_grad_ranges_device(
+                    check_call(LIB.dglhip_gat_attention_grad_rowsum_ranges_device(
                         fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
                         ptr(fwd.row_order), ptr(fwd.indices),
                         ptr(d_ft), ptr(ft2c), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
                         float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
-                        ptr(g), _stream_of(ft2.device)))
+                        ptr(g), ptr(er_sum), _stream_of(ft2.device)))
+                if fuse_er:
+                    d_er = er_sum
             else:
                 d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
                 if w is not None:  # dropout's backward: the kept pairs, scaled
@@ -1775,7 +1784,7 @@ class _GATAggregate(torch.autograd.Function):
             if need_el:
                 d_el, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
                                      emap=_fwd_slot_of_bwd(adj))
-            if need_er:
+            if need_er and d_er is None:
                 d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
         return (None,) * 8 + (d_el, d_er, d_ft2, None, None)
 

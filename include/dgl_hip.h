@@ -493,6 +493,22 @@ int dglhip_gat_attention_grad_ranges_device(
     const float* attn, const float* attn_drop, const float* dz, float alpha, float clamp_lo,
     float clamp_hi, int apply_exp, float drop_scale, float* grad, void* stream);
 
+/* dglhip_gat_attention_grad_ranges_device that also adds, per row and head,
+ * the values it stores (in slot order) to grad_rowsum[row, h] (float,
+ * [num_rows, num_heads], zero-filled by the caller before the first range):
+ * the attention logit's destination-side gradient (GAT's er), which the
+ * reference's layer gets from a second pass, a copy_edge sum over the same
+ * values (examples/pytorch/gat/train.py:74-96) — same chain, same bits. Needs
+ * the sliced kernel: dglhip_gat_attention_grad_rowsum_ok(feat_len, num_heads)
+ * and 16-B aligned dout / ft rows. */
+int dglhip_gat_attention_grad_rowsum_ok(int64_t feat_len, int64_t num_heads);
+int dglhip_gat_attention_grad_rowsum_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft, const float* attn, const float* attn_drop,
+    const float* dz, float alpha, float clamp_lo, float clamp_hi, int apply_exp,
+    float drop_scale, float* grad, float* grad_rowsum, void* stream);
+
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
  * attention positions stay the CSR's); with accumulate != 0 both chains
