@@ -1782,11 +1782,58 @@ class _GATAggregate(torch.autograd.Function):
                     g = d_a * slope
                 g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
             if need_el:
-                d_el, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
-                                     emap=_fwd_slot_of_bwd(adj))
+                d_el = _gat_el_grad(adj, g, H)
             if need_er and d_er is None:
                 d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
         return (None,) * 8 + (d_el, d_er, d_ft2, None, None)
+
+
+# el's gradient reads the E x H attention gradient (forward slot order)
+# through the transpose's slot map: 32-B values at random forward slots, a
+# 128-B line each. Cut by destination block, each launch's values come from
+# one contiguous forward-slot range of about this many bytes, which the
+# Infinity Cache holds (Reddit-shaped graph, 8 heads: one launch 3.72 ms;
+# 32 / 128 / 256 / 512 MiB blocks 3.34 / 3.19 / 3.13 / 3.20 ms, the same
+# bits; tools/el_grad_sweep.py)
+_EL_GRAD_BLOCK_BYTES = int(os.environ.get("DGLHIP_EL_GRAD_BLOCK_BYTES", 256 << 20))
+
+
+def _gat_el_grad(adj, g, H):
+    """d_el[u, h] = sum of g[forward slot of k, h] over the transpose's slots k
+    of source u, in slot order (the copy_edge sum of the attention gradient
+    along the transpose). On a ROCm device with a graph numbered source-major
+    it runs over destination blocks (row sub-ranges of the transpose, each
+    continuing the rows' chains: the same bits); else in one launch."""
+    bwd = adj.bwd
+    emap = _fwd_slot_of_bwd(adj)
+    cuts = None
+    if g.is_cuda and _BLOCKED != "off" and bwd.nnz and bwd.nnz < (1 << 31):
+        B = -(-(g.numel() * g.element_size()) // _EL_GRAD_BLOCK_BYTES)
+        B = min(B, bwd.nnz // (_BLOCK_MIN_SLOTS * max(bwd.num_nonempty, 1)))
+        if B >= 2:
+            key = ("el_grad_cuts", B)
+            if key not in bwd._plans:
+                lo, hi = _column_span(bwd)
+                split = _block_split(bwd, B, lo, hi)
+                cuts = None
+                if split is not None:
+                    _, counts, pre, _ = split
+                    start = bwd.indptr[:-1]
+                    cum = torch.cumsum(counts, 1)
+                    cuts = [start.contiguous()] + [(start + cum[:, b]).contiguous()
+                                                   for b in range(B)]
+                    if pre is not None:  # the suffixes: one more range, run last
+                        cuts.append(bwd.indptr[1:].contiguous())
+                    del cum, counts, split
+                bwd._plans[key] = cuts
+            cuts = bwd._plans[key]
+    if cuts is None:
+        return _run_gspmm(bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=emap)[0]
+    out = torch.empty(bwd.num_rows, H, dtype=torch.float32, device=g.device)
+    for b in range(len(cuts) - 1):
+        gspmm_ranges(MSG_COPY_E, cuts[b], cuts[b + 1], b > 0, bwd.indices, out, efeat=g,
+                     eid=emap)
+    return out
 
 
 def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0,
