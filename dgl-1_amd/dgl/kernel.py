@@ -934,17 +934,27 @@ def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, e
 
 def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, erows):
     """The blocked schedule's items (_BlockItems), one dglhip_gspmm_items_device
-    launch per block, every launch adding to the rows it lists: ``out``
-    starts from zero (the chains' own start: identical bits) unless ``red``
-    is SUM_ACCUM."""
+    launch per block, every later launch adding to the rows it lists. Unless
+    ``red`` is SUM_ACCUM the first block's launch writes its rows from zero
+    (the chains' own start: identical bits) and only the rows it does not
+    list are zero-filled (none on the Reddit-shaped graph: no 119 MB fill and
+    no read of it per call)."""
     dev = ufeat2.device
     ld = ufeat2.stride(0) if _row_strided(ufeat2, feat_len) else 0
+    first_writes = red != RED_SUM_ACCUM
     if out is None:
-        out = torch.zeros(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
-    elif red != RED_SUM_ACCUM:
-        out.zero_()
+        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
+    if first_writes:
+        key = ("blocked_absent", len(plan))
+        absent = csr._plans.get(key)
+        if absent is None:
+            listed = torch.zeros(csr.num_rows, dtype=torch.bool, device=dev)
+            listed[plan[0].rows.long()] = True
+            absent = csr._plans[key] = torch.nonzero(~listed).squeeze(1)
+        if absent.numel():
+            out.index_fill_(0, absent, 0.0)
     off = 0
-    for it in plan:
+    for i, it in enumerate(plan):
         if efeat is None:
             e, eid = None, None
         elif erows is None:  # values already in the plan's slot order
@@ -952,7 +962,8 @@ def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, er
         else:
             e, eid = efeat, erows[off:off + it.nnz]
         check_call(LIB.dglhip_gspmm_items_device(
-            msg, it.rows.numel(), feat_len, ptr(it.rows), ptr(it.ptr), 1, ptr(it.indices),
+            msg, it.rows.numel(), feat_len, ptr(it.rows), ptr(it.ptr),
+            0 if (i == 0 and first_writes) else 1, ptr(it.indices),
             ptr(eid), ptr(ufeat2), ld, ptr(e), elen, ptr(out), _stream_of(dev)))
         off += it.nnz
     if red == RED_MEAN:
