@@ -883,6 +883,8 @@ def _block_split(csr, B, lo, hi):
 # the fused GAT kernels' blocks: their per-row work (the attention through LDS)
 # makes a row's pass per block dearer than copy_u's, so fewer, larger blocks
 _GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11 MiB
+# the fused forward when no attention is stored (inference)
+_GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 9 << 20))
 
 
 def _block_cuts(csr, row_bytes, block_bytes=None):
@@ -1707,8 +1709,11 @@ class _GATAggregate(torch.autograd.Function):
                 a = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
                 w = torch.empty_like(a) if p > 0 else None
             # source-blocked (exact where the blocks never decrease along a
-            # row): one launch per block, both chains continued
-            cuts = _block_cuts(fwd, (F + H) * 4)
+            # row): one launch per block, both chains continued; with nothing
+            # stored, smaller blocks (Reddit-shaped 8 x 16: 5.78 ms at 9 MiB
+            # vs 6.04 at 11; with the attention stored 6.79 vs 6.78,
+            # tools/gat_block_percall.py)
+            cuts = _block_cuts(fwd, (F + H) * 4, None if need else _GAT_BLOCK_BYTES_NOGRAD)
             if cuts is None:
                 cuts = [fwd.indptr, fwd.indptr[1:]]
             for b in range(len(cuts) - 1):
