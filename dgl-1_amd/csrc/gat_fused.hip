@@ -86,7 +86,7 @@ __device__ __forceinline__ typename Vec<VEC>::T gather_rsrc(const float* row, in
   return *reinterpret_cast<const typename Vec<VEC>::T*>(&w);
 }
 
-// Tables under 4 GB: one descriptor over the whole table, the row's byte
+// Tables under 2 GB: one descriptor over the whole table, the row's byte
 // offset as the (wave-uniform, SGPR) soffset and the lane's as voffset: no
 // per-gather descriptor (4 SGPRs each, 16 in flight) and no per-gather VGPR.
 struct GatTable {

@@ -934,6 +934,15 @@ def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, e
     return out, arg
 
 
+def _plan_tag(plan):
+    """(source blocks, has a suffix launch): the key of caches derived from a
+    blocked plan. The plan's length alone is ambiguous: B blocks plus a suffix
+    and B + 1 blocks without one are both B + 1 launches, and one CSR gets
+    different B at different widths or dtypes."""
+    sfx = bool(plan[-1].suffix)
+    return (len(plan) - int(sfx), sfx)
+
+
 def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, erows):
     """The blocked schedule's items (_BlockItems), one dglhip_gspmm_items_device
     launch per block, every later launch adding to the rows it lists. Unless
@@ -947,7 +956,7 @@ def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, er
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     if first_writes:
-        key = ("blocked_absent", len(plan))
+        key = ("blocked_absent",) + _plan_tag(plan)
         absent = csr._plans.get(key)
         if absent is None:
             listed = torch.zeros(csr.num_rows, dtype=torch.bool, device=dev)
@@ -987,7 +996,7 @@ def blocked_schedule(adj, ufeat):
 def _block_slots(csr, plan):
     """int64: for each slot of the blocked plan, blocks in order, the slot of
     ``csr`` it came from (cached; for edge-valued messages)."""
-    key = ("blocked_slots", len(plan))
+    key = ("blocked_slots",) + _plan_tag(plan)
     if key not in csr._plans:
         csr._plans[key] = torch.cat([it.pos.long() for it in plan])
     return csr._plans[key]
@@ -999,16 +1008,16 @@ def _block_edge_rows(csr, plan, emap):
     slots, or a per-slot row tensor (e.g. the transpose's forward-slot map).
     Cached: per layout, and for a row tensor per tensor object (held weakly:
     a new tensor, or one changed in place, composes anew)."""
-    nseg = len(plan)
+    tag = _plan_tag(plan)
     slots = _block_slots(csr, plan)
     if emap is SLOT or (emap is None and csr.slot_eid is None):
         return slots
     if emap is None:
-        key = ("blocked_eid", nseg)
+        key = ("blocked_eid",) + tag
         if key not in csr._plans:
             csr._plans[key] = csr.slot_eid.index_select(0, slots)
         return csr._plans[key]
-    key = ("blocked_emap", nseg)
+    key = ("blocked_emap",) + tag
     hit = csr._plans.get(key)
     if hit is not None and hit[0]() is emap and hit[1] == emap._version:
         return hit[2]
@@ -1635,12 +1644,12 @@ _GAT_SEED = {}
 
 
 def _gat_seed_offset(dev):
-    """A per-device int64 counter the fused kernel adds to its dropout seed,
-    advanced on the device at every call: a captured HIP graph draws a new
-    mask at every replay, and no host round trip is needed."""
+    """For a call captured in a HIP graph: a per-device int64 counter the
+    fused kernel adds to its dropout seed, advanced on the device at every
+    call, so every replay draws a new mask with no host round trip."""
     key = str(dev)
     if key not in _GAT_SEED:
-        base = int(torch.randint(0, 1 << 62, (1,)).item())  # torch's generator: manual_seed
+        base = int(torch.randint(0, 1 << 62, (1,)).item())
         _GAT_SEED[key] = (base, torch.zeros(1, dtype=torch.int64, device=dev))
     base, off = _GAT_SEED[key]
     off.add_(1)
@@ -1867,8 +1876,8 @@ def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0
     edge_order="slot") followed by gspmm(u_mul_e, sum) and gspmm(copy_e, sum)
     bit for bit. The dropout mask is the kernel's counter hash of (seed,
     slot, head) (gat_dropout_mask), not torch's generator; ``seed`` None draws
-    the seed from torch's generator once per device and advances a device
-    counter per call."""
+    the seed from torch's generator at every call (inside a HIP graph capture:
+    once per device, plus a device counter advanced at every replay)."""
     p = float(attn_drop) if training else 0.0
     if not 0.0 <= p < 1.0:
         raise DGLError("attention dropout must be in [0, 1), got %r" % (attn_drop,))
@@ -1882,9 +1891,9 @@ def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0
         raise DGLError("gat_aggregate: feature rows do not match the adjacency")
     seed_off = None
     if p > 0 and seed is None:
-        if dev.type == "cuda":
+        if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
             seed, seed_off = _gat_seed_offset(dev)
-        else:
+        else:  # torch's generator, every call: torch.manual_seed repeats the masks
             seed = int(torch.randint(0, 1 << 62, (1,)).item())
     ft_sum, z = _GATAggregate.apply(adj, float(alpha), float(clamp[0]), float(clamp[1]),
                                     bool(apply_exp), p, int(seed or 0), seed_off, el2, er2,

@@ -387,3 +387,82 @@ def test_blocked_max_bits_with_ties(msg):
     o0, g0, n0 = run("off")
     assert n1 > n0
     assert torch.equal(o1, o0) and torch.equal(g1, g0)
+
+
+def _tagged_graph():
+    """A CSR whose blocked plan has a suffix at B = 2 but none at B = 3: most
+    rows are source-sorted below column 600; a few end with sources 1000
+    then 999 (blocks 1 then 0 at B = 2 — a decrease, so a suffix; both in
+    block 1 at B = 3); one row references column 1999 (the span)."""
+    rng = np.random.default_rng(21)
+    n = 2000
+    src, dst = [], []
+    for r in range(n):
+        s = np.sort(rng.integers(0, 600, 40))
+        src.append(s)
+        dst.append(np.full(40, r))
+    for r in range(0, n, 50):
+        src.append(np.array([1000, 999]))
+        dst.append(np.array([r, r]))
+    src.append(np.array([1999]))
+    dst.append(np.array([7]))
+    return n, np.concatenate(src), np.concatenate(dst)
+
+
+def test_plan_caches_keyed_on_blocks_not_length():
+    """Caches derived from a blocked plan (slot map, edge rows) are keyed on
+    its block count and suffix, not its length: B = 2 plus a suffix and B = 3
+    without one are both three launches (the slot map of one was
+    reused for the other)."""
+    n, src, dst = _tagged_graph()
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                           kernel.ORDER_EID, "cpu")
+    lo, hi = kernel._column_span(csr)
+    p2 = kernel._block_items(csr, 2, lo, hi)
+    p3 = kernel._block_items(csr, 3, lo, hi)
+    assert len(p2) == len(p3) == 3 and p2[-1].suffix and not p3[-1].suffix
+    assert _chains_kept(csr, p2) and _chains_kept(csr, p3)
+    s2 = kernel._block_slots(csr, p2)
+    s3 = kernel._block_slots(csr, p3)
+    assert torch.equal(s2, torch.cat([it.pos.long() for it in p2]))
+    assert torch.equal(s3, torch.cat([it.pos.long() for it in p3]))
+    assert not torch.equal(s2, s3)
+    emap = torch.randperm(csr.nnz)
+    assert torch.equal(kernel._block_edge_rows(csr, p2, emap), emap[s2])
+    assert torch.equal(kernel._block_edge_rows(csr, p3, emap), emap[s3])
+    eid = csr.slot_eid if csr.slot_eid is not None else torch.arange(csr.nnz)
+    assert torch.equal(kernel._block_edge_rows(csr, p2, None), eid[s2])
+    assert torch.equal(kernel._block_edge_rows(csr, p3, None), eid[s3])
+
+
+@pytest.mark.gpu
+def test_one_csr_two_block_counts_device():
+    """One CSR through the blocked u_mul_e at two widths whose plans are
+    B = 2 + suffix and B = 3 (three launches each): both equal the oracle's
+    chain bit for bit, in either order of first use."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, src, dst = _tagged_graph()
+    gen = torch.Generator().manual_seed(22)
+    w = torch.rand(len(src), 1, generator=gen)
+    old = (kernel._BLOCK_TABLE_MIN, kernel._BLOCK_BYTES, kernel._BLOCK_MIN_SLOTS)
+    try:
+        kernel._BLOCK_TABLE_MIN, kernel._BLOCK_MIN_SLOTS = 0, 1
+        for widths in ((64, 96), (96, 64)):
+            adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                                  kernel.ORDER_EID, dev)
+            for F in widths:
+                # F = 64: 512 KB table -> 2 blocks; F = 96: 768 KB -> 3 blocks
+                kernel._BLOCK_BYTES = 256_000
+                H = torch.randn(n, F, generator=gen)
+                plan = kernel._block_plan(adj.fwd, H.to(dev), F)
+                assert plan is not None and len(plan) == 3
+                assert plan[-1].suffix == (F == 64)
+                out = kernel.gspmm(adj, "u_mul_e", "sum", H.to(dev), w.to(dev)).cpu()
+                ref = O.spmm_coo(n, dst, src, H.numpy(), w.numpy().ravel())
+                assert np.array_equal(out.numpy(), ref)
+                out = kernel.gspmm(adj, "copy_u", "sum", H.to(dev)).cpu()
+                assert np.array_equal(out.numpy(), O.spmm_coo(n, dst, src, H.numpy()))
+    finally:
+        kernel._BLOCK_TABLE_MIN, kernel._BLOCK_BYTES, kernel._BLOCK_MIN_SLOTS = old

@@ -124,16 +124,48 @@ def test_dropout_mask_is_the_host_hash(device, p):
     assert torch.equal(fs3, fs4)
 
 
-@pytest.mark.gpu
-def test_device_counter_draws_fresh_masks():
-    dev = _dev("cuda")
+@pytest.mark.parametrize("device", DEVICES)
+def test_masks_fresh_per_call_and_repeat_with_manual_seed(device):
+    """seed None: every call draws its seed from torch's generator, so calls
+    get fresh masks and torch.manual_seed repeats them (a seed
+    cached per process did not)."""
+    dev = _dev(device)
     g = _graph(n=500, m=5000)
     adj = g.sparse_adjacency(dev)
     ft, el, er = _inputs(g.number_of_nodes(), 4, 8, dev)
     with torch.no_grad():
+        torch.manual_seed(7)
         a, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
         b, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
+        torch.manual_seed(7)
+        c, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
+        d, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
     assert not torch.equal(a, b)
+    assert torch.equal(a, c) and torch.equal(b, d)
+
+
+@pytest.mark.gpu
+def test_graph_replays_draw_fresh_masks():
+    """Inside a HIP graph capture the device counter advances at every
+    replay: each replay draws a new mask."""
+    dev = _dev("cuda")
+    g = _graph(n=500, m=5000)
+    adj = g.sparse_adjacency(dev)
+    ft, el, er = _inputs(g.number_of_nodes(), 4, 8, dev)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.no_grad(), torch.cuda.stream(side):
+        kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)  # warm (plans, buffers)
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.no_grad(), torch.cuda.graph(graph, stream=side):
+        out, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.5)
+    graph.replay()
+    torch.cuda.synchronize()
+    a = out.clone()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(a, out)
 
 
 def test_bad_dropout_rejected():
