@@ -22,14 +22,9 @@
 #include "../../include/dgl_hip.h"
 #include "common.h"
 #include "launch.h"
+#include "timing.h"
 
 namespace dglhip {
-
-#define HIP_CALL(expr)                                                        \
-  do {                                                                        \
-    hipError_t _e = (expr);                                                   \
-    DGLHIP_CHECK(_e == hipSuccess, #expr << " -> " << hipGetErrorString(_e)); \
-  } while (0)
 
 namespace {
 
@@ -169,17 +164,18 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t
   hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_rows, npass, \
                      num_blocks, in_block, out_block, indptr, indices, eid, etype, ufeat, \
                      weight, enorm, out)
-  switch (in_block) {
-    case 1: DGLHIP_TB(1); break;
-    case 2: DGLHIP_TB(2); break;
-    case 4: DGLHIP_TB(4); break;
-    case 5: DGLHIP_TB(5); break;
-    case 8: DGLHIP_TB(8); break;
-    case 16: DGLHIP_TB(16); break;
-    default: DGLHIP_TB(0); break;
-  }
+  timed_launch(stream, [&] {
+    switch (in_block) {
+      case 1: DGLHIP_TB(1); break;
+      case 2: DGLHIP_TB(2); break;
+      case 4: DGLHIP_TB(4); break;
+      case 5: DGLHIP_TB(5); break;
+      case 8: DGLHIP_TB(8); break;
+      case 16: DGLHIP_TB(16); break;
+      default: DGLHIP_TB(0); break;
+    }
+  });
 #undef DGLHIP_TB
-  HIP_CALL(hipGetLastError());
   API_END();
 }
 
@@ -198,10 +194,11 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks, int64_
   DGLHIP_CHECK(rel_ptr && rel_src && rel_eid && edge_dst && ufeat && dout && dweight,
                "null pointer argument");
   DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
-  hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256),
-                     dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
-                     rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);
-  HIP_CALL(hipGetLastError());
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256),
+                       dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
+                       rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);
+  });
   API_END();
 }
 

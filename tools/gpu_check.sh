@@ -79,6 +79,15 @@ for s in $STEPS; do
         rc=$?; tail -1 gpurun_out/emul_$tag.err; [ $rc -eq 0 ] || exit $rc
         python -c "import json; d=json.load(open('gpurun_out/emul_$tag.json')); print('$tag', d['ms_per_step'], d['roofline']['kernel_ms'])"
       done; done ;;
+    rgcn)
+      # configs[4] step phase by phase + each typed-block kernel alone (fused; then the UDF formulation)
+      timeout -k 10 300 python -u tools/rgcn_step.py --kernels --out gpurun_out/rgcn_step.json > gpurun_out/rgcn.log 2>&1 &&
+      timeout -k 10 300 python -u tools/rgcn_step.py --udf --steps 5 --out gpurun_out/rgcn_step_udf.json >> gpurun_out/rgcn.log 2>&1
+      rc=$?; tail -2 gpurun_out/rgcn.log; [ $rc -eq 0 ] || exit $rc ;;
+    rgcnprof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rgcnprof -o run \
+        --output-format csv -- python tools/rgcn_step.py --steps 20 > gpurun_out/rgcnprof.log 2>&1
+      rc=$?; tail -2 gpurun_out/rgcnprof.log; [ $rc -eq 0 ] || exit $rc ;;
     sageprof)
       # kernel statistics of GraphSAGE-mean full-graph epochs on RMAT-$RMAT_SCALE (configs[3])
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sageprof -o run \
