@@ -201,6 +201,33 @@ static int gspmm_host_bf16(int reduce_op, int64_t num_rows, int64_t feat_len,
                            nullptr, wide.data(), nullptr, 0, out, arg_out, num_threads);
 }
 
+// The chunked chains of the typed-block kernels (typed_block.hip): a row of
+// `ptr` is cut into chunks of DGLHIP_TYPED_CHUNK slots, each chunk's chain
+// chain(k0, k1, acc) runs from zero, and the partials are added in order.
+template <typename ChainFn>
+static void typed_chunked_rows(int64_t num_rows, int64_t F, const int64_t* ptr, float* out,
+                               int nt, ChainFn&& chain) {
+  const int64_t C = DGLHIP_TYPED_CHUNK;
+  dglhip::parallel_for(num_rows, nt, [&](int64_t b0, int64_t b1, int) {
+    std::vector<float> part(F);
+    for (int64_t r = b0; r < b1; ++r) {
+      float* o = out + r * F;
+      const int64_t beg = ptr[r], end = ptr[r + 1];
+      for (int64_t f = 0; f < F; ++f) o[f] = 0.0f;
+      if (end - beg <= C) {
+        chain(beg, end, o);
+        continue;
+      }
+      chain(beg, beg + C, o);
+      for (int64_t k = beg + C; k < end; k += C) {
+        for (int64_t f = 0; f < F; ++f) part[f] = 0.0f;
+        chain(k, std::min(k + C, end), part.data());
+        for (int64_t f = 0; f < F; ++f) o[f] = o[f] + part[f];
+      }
+    }
+  });
+}
+
 extern "C" {
 
 int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
@@ -320,30 +347,26 @@ int dglhip_gspmm_ranges_host(int msg_op, int64_t num_items, int64_t feat_len,
 
 int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks, int64_t in_block,
                                  int64_t out_block, const int64_t* indptr,
-                                 const int32_t* indices, const int64_t* eid,
-                                 const int64_t* etype, const float* ufeat,
-                                 const float* weight, const float* enorm, float* out,
-                                 int num_threads) {
+                                 const int32_t* indices, const int32_t* slot_rel,
+                                 const float* slot_norm, const float* ufeat,
+                                 const float* weight, float* out, int num_threads) {
   API_BEGIN();
   DGLHIP_CHECK(num_rows >= 0 && num_blocks > 0 && in_block > 0 && out_block > 0, "bad sizes");
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && indices && slot_rel && ufeat && weight && out, "null pointer argument");
   const int64_t nb = num_blocks, si = in_block, so = out_block;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
-  parallel_for(num_rows, nt, [&](int64_t b0, int64_t b1, int) {
-    for (int64_t row = b0; row < b1; ++row) {
-      float* o = out + row * Fo;
-      for (int64_t jg = 0; jg < Fo; ++jg) o[jg] = 0.0f;
-      for (int64_t k = indptr[row]; k < indptr[row + 1]; ++k) {
-        const int64_t e = eid[k];
-        const float* h = ufeat + int64_t(indices[k]) * Fi;
-        const float* w = weight + etype[e] * wr;
-        const float nrm = enorm ? enorm[e] : 1.0f;
-        for (int64_t jg = 0; jg < Fo; ++jg) {
-          const int64_t b = jg / so, j = jg - b * so;
-          float m = 0.0f;
-          for (int64_t i = 0; i < si; ++i) m = std::fma(h[b * si + i], w[b * si * so + i * so + j], m);
-          o[jg] = std::fma(nrm, m, o[jg]);
-        }
+  typed_chunked_rows(num_rows, Fo, indptr, out, nt, [&](int64_t k0, int64_t k1, float* o) {
+    for (int64_t k = k0; k < k1; ++k) {
+      const float* h = ufeat + int64_t(indices[k]) * Fi;
+      const float* w = weight + int64_t(slot_rel[k]) * wr;
+      const float nrm = slot_norm ? slot_norm[k] : 1.0f;
+      for (int64_t jg = 0; jg < Fo; ++jg) {
+        const int64_t b = jg / so, j = jg - b * so;
+        float m = 0.0f;
+        for (int64_t i = 0; i < si; ++i) m = std::fma(h[b * si + i], w[b * si * so + i * so + j], m);
+        o[jg] = std::fma(nrm, m, o[jg]);
       }
     }
   });
@@ -352,26 +375,26 @@ int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks, int64_t i
 
 int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks, int64_t in_block,
                                   int64_t out_block, const int64_t* rel_ptr,
-                                  const int32_t* rel_src, const int64_t* rel_eid,
-                                  const int64_t* edge_dst, const float* ufeat,
-                                  const float* dout, const float* enorm, float* dweight,
-                                  int num_threads) {
+                                  const int32_t* rel_src, const int32_t* rel_dst,
+                                  const float* rel_norm, const float* ufeat, const float* dout,
+                                  float* dweight, int num_threads) {
   API_BEGIN();
+  DGLHIP_CHECK(num_rels >= 0 && num_blocks >= 0 && in_block >= 0 && out_block >= 0,
+               "bad sizes");
   const int64_t nb = num_blocks, si = in_block, so = out_block;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
+  if (num_rels == 0 || wr == 0) return 0;
+  DGLHIP_CHECK(rel_ptr && ufeat && dout && dweight, "null pointer argument");
   const int nt = num_threads > 0 ? num_threads : default_num_threads();
-  parallel_for(num_rels * wr, nt, [&](int64_t b0, int64_t b1, int) {
-    for (int64_t idx = b0; idx < b1; ++idx) {
-      const int64_t r = idx / wr, rem = idx - r * wr;
-      const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
-      float acc = 0.0f;
-      for (int64_t k = rel_ptr[r]; k < rel_ptr[r + 1]; ++k) {
-        const int64_t e = rel_eid[k];
-        const float x = ufeat[int64_t(rel_src[k]) * Fi + b * si + i];
-        const float g = dout[edge_dst[e] * Fo + b * so + j];
-        acc = std::fma(enorm ? enorm[e] * x : x, g, acc);
+  typed_chunked_rows(num_rels, wr, rel_ptr, dweight, nt, [&](int64_t k0, int64_t k1, float* o) {
+    for (int64_t k = k0; k < k1; ++k) {
+      const float* x = ufeat + int64_t(rel_src[k]) * Fi;
+      const float* g = dout + int64_t(rel_dst[k]) * Fo;
+      for (int64_t rem = 0; rem < wr; ++rem) {
+        const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
+        const float xv = x[b * si + i];
+        o[rem] = std::fma(rel_norm ? rel_norm[k] * xv : xv, g[b * so + j], o[rem]);
       }
-      dweight[idx] = acc;
     }
   });
   API_END();

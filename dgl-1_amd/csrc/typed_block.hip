@@ -6,17 +6,27 @@
 // in_block x out_block), multiply with torch.bmm into an E x out message
 // tensor, then reduce by destination (builtin sum -> incidence SPMV /
 // degree bucketing). Here the three steps are one kernel over the
-// destination-major CSR: each wave owns a destination row; lanes own output
-// features; per in-edge the wave reads the source row and the relation's
-// weight block (hot in L2: the whole weight tensor of FB15k-237's 474
-// relations x 100 blocks x 5 x 5 is 4.7 MB) and accumulates
-//   out[v, b*so + j] += norm_e * sum_i h[u, b*si + i] * W[r, b, i, j]
-// in CSR-slot order. No E x out message tensor is materialised.
+// destination-major CSR and no E x out message tensor is materialised:
+//   out[v, b*so + j] = sum over v's slots of norm_e * sum_i h[u, b*si + i] * W[r, b, i, j]
+//
+// Work items (r04). A row is cut into chunks of DGLHIP_TYPED_CHUNK slots;
+// each chunk is one item whose wave(s) run the chain over its slots from
+// zero, and a row of several chunks gets out = ((p0 + p1) + p2) ... in chunk
+// order (typed_block_combine_kernel). R-GCN's sampled graphs have hub
+// entities of ~1,000 in-edges; walked by one wave (r03) such a row set the
+// kernel time (0.43 ms per call for a 30,000-edge sample, rocprof,
+// profiles/r04/rgcn_step_kernel_stats.csv). A row of at most one chunk is
+// the plain slot-order chain, as before. The relation and norm of every slot
+// come in slot order (typed_block_spmm gathers them per call), so a slot's
+// loads are one dependent step (column id, relation, norm), then the row and
+// the weight column; a wave keeps kEdges of them in flight, predicated
+// (no serial tail).
 //
 // The backward runs the same kernel over the transposed CSR with the blocks
-// transposed (dH), and a relation-grouped kernel for dW in which every
-// weight element is one sequential chain over that relation's edges
-// (deterministic; no atomics).
+// transposed (dH), and dW the same way over the relation-major grouping:
+// every weight element a chain over a chunk of its relation's edges
+// (relation-major, forward-slot order), the chunks' partials added in order.
+// Deterministic, no atomics; the host entry points run the same chains.
 #include <hip/hip_runtime.h>
 
 #include "../../include/dgl_hip.h"
@@ -28,28 +38,54 @@ namespace dglhip {
 
 namespace {
 
-constexpr int kEdgesInFlight = 4;
+constexpr int64_t kChunk = DGLHIP_TYPED_CHUNK;
 
-// One wave per (destination row, 64-wide slice of the output features): the
-// slices of a row run in parallel waves (8 for R-GCN's 500 features) instead
-// of one wave looping over them per edge, and each wave keeps
-// kEdgesInFlight edges' loads outstanding. For every output element the
-// arithmetic is unchanged:  m_e = fma chain over i of h[u, b*si+i] *
-// W[r, b, i, j];  acc = fma(norm_e, m_e, acc) in CSR-slot order.
-// SI > 0: the block width as a compile-time constant (all loads of an edge
-// group issued before its fma chains); SI == 0: runtime width.
+// slots in flight per wave at block width SI (their row and weight values
+// in VGPRs: 2 * SI * kEdges of them)
+template <int SI>
+struct EdgesInFlight {
+  static constexpr int value = SI == 0 ? 4 : (SI <= 5 ? 8 : (SI <= 8 ? 4 : 2));
+};
+
+// The slot range of item `it` of the chunked rows (item_ptr: a row's first
+// item; a row of deg slots has max(1, ceil(deg / kChunk)) items) and where
+// its chain goes: the row itself when the row is one item, else the item's
+// partial row.
+__device__ __forceinline__ void item_range(int64_t it, const int64_t* __restrict__ ptr,
+                                           const int64_t* __restrict__ item_ptr,
+                                           const int32_t* __restrict__ item_row, int64_t* row,
+                                           int64_t* beg, int64_t* end, bool* single) {
+  const int64_t r = item_row[it];
+  const int64_t first = item_ptr[r], nit = item_ptr[r + 1] - first;
+  const int64_t b = ptr[r] + (it - first) * kChunk;
+  *row = r;
+  *beg = b;
+  *end = nit == 1 ? ptr[r + 1] : (b + kChunk < ptr[r + 1] ? b + kChunk : ptr[r + 1]);
+  *single = nit == 1;
+}
+
+// One wave per (item, 64-wide slice of the output features): the slices of
+// an item run in parallel waves (8 for R-GCN's 500 features). For every
+// output element:  m_e = fma chain over i of h[u, b*si+i] * W[r, b, i, j];
+// acc = fma(norm_e, m_e, acc) over the item's slots in slot order.
+// SI > 0: the block width as a compile-time constant; SI == 0: runtime width.
 template <int SI>
 __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
-    int64_t num_rows, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
-    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
-    const int64_t* __restrict__ eid, const int64_t* __restrict__ etype,
+    int64_t num_items, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
+    const int64_t* __restrict__ indptr, const int64_t* __restrict__ item_ptr,
+    const int32_t* __restrict__ item_row, const int32_t* __restrict__ indices,
+    const int32_t* __restrict__ slot_rel, const float* __restrict__ slot_norm,
     const float* __restrict__ ufeat, const float* __restrict__ weight,
-    const float* __restrict__ enorm, float* __restrict__ out) {
+    float* __restrict__ out, float* __restrict__ partial) {
+  constexpr int G = EdgesInFlight<SI>::value;
   const int64_t si = SI > 0 ? SI : si_rt;
   const int64_t wave = block_linear() * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
-  const int64_t row = wave / npass, pass = wave - (wave / npass) * npass;
-  if (row >= num_rows) return;
+  const int64_t it = wave / npass, pass = wave - it * npass;
+  if (it >= num_items) return;
+  int64_t row, beg, end;
+  bool single;
+  item_range(it, indptr, item_ptr, item_row, &row, &beg, &end, &single);
   const int lane = threadIdx.x & 63;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
   const int64_t jg = pass * 64 + lane;
@@ -58,23 +94,22 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
   const int64_t b = active ? jg / so : 0, j = active ? jg - b * so : 0;
   const int64_t hoff = b * si, woff = b * si * so + j;
   float acc = 0.0f;
-  const int64_t beg = indptr[row], end = indptr[row + 1];
-  int64_t k = beg;
-  for (; k + kEdgesInFlight <= end; k += kEdgesInFlight) {
-    const float* hb[kEdgesInFlight];
-    const float* wb[kEdgesInFlight];
-    float nrm[kEdgesInFlight];
+  for (int64_t k = beg; k < end; k += G) {
+    const int64_t cnt = end - k;  // wave-uniform: slots q >= cnt are predicated off
+    const float* hb[G];
+    const float* wb[G];
+    float nrm[G];
 #pragma unroll
-    for (int q = 0; q < kEdgesInFlight; ++q) {
-      const int64_t e = eid[k + q];
-      hb[q] = ufeat + int64_t(indices[k + q]) * Fi + hoff;
-      wb[q] = weight + etype[e] * wr + woff;
-      nrm[q] = enorm ? enorm[e] : 1.0f;
+    for (int q = 0; q < G; ++q) {
+      const int64_t kk = q < cnt ? k + q : end - 1;  // a valid slot for idle q
+      hb[q] = ufeat + int64_t(indices[kk]) * Fi + hoff;
+      wb[q] = weight + int64_t(slot_rel[kk]) * wr + woff;
+      nrm[q] = slot_norm ? slot_norm[kk] : 1.0f;
     }
     if (SI > 0) {
-      float hv[kEdgesInFlight][SI > 0 ? SI : 1], wv[kEdgesInFlight][SI > 0 ? SI : 1];
+      float hv[G][SI > 0 ? SI : 1], wv[G][SI > 0 ? SI : 1];
 #pragma unroll
-      for (int q = 0; q < kEdgesInFlight; ++q) {
+      for (int q = 0; q < G; ++q) {
 #pragma unroll
         for (int i = 0; i < SI; ++i) {
           hv[q][i] = hb[q][i];
@@ -82,57 +117,80 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
         }
       }
 #pragma unroll
-      for (int q = 0; q < kEdgesInFlight; ++q) {
+      for (int q = 0; q < G; ++q) {
         float m = 0.0f;
 #pragma unroll
         for (int i = 0; i < SI; ++i) m = __builtin_fmaf(hv[q][i], wv[q][i], m);
-        acc = __builtin_fmaf(nrm[q], m, acc);
+        if (q < cnt) acc = __builtin_fmaf(nrm[q], m, acc);
       }
     } else {
-      float m[kEdgesInFlight];
+      float m[G];
 #pragma unroll
-      for (int q = 0; q < kEdgesInFlight; ++q) m[q] = 0.0f;
+      for (int q = 0; q < G; ++q) m[q] = 0.0f;
       for (int64_t i = 0; i < si; ++i) {
 #pragma unroll
-        for (int q = 0; q < kEdgesInFlight; ++q)
-          m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
+        for (int q = 0; q < G; ++q) m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
       }
 #pragma unroll
-      for (int q = 0; q < kEdgesInFlight; ++q) acc = __builtin_fmaf(nrm[q], m[q], acc);
+      for (int q = 0; q < G; ++q)
+        if (q < cnt) acc = __builtin_fmaf(nrm[q], m[q], acc);
     }
   }
-  for (; k < end; ++k) {
-    const int64_t e = eid[k];
-    const float* h = ufeat + int64_t(indices[k]) * Fi + hoff;
-    const float* w = weight + etype[e] * wr + woff;
-    float m = 0.0f;
-    for (int64_t i = 0; i < si; ++i) m = __builtin_fmaf(h[i], w[i * so], m);
-    acc = __builtin_fmaf(enorm ? enorm[e] : 1.0f, m, acc);
-  }
-  if (active) out[row * Fo + jg] = acc;
+  if (active) (single ? out + row * Fo : partial + it * Fo)[jg] = acc;
 }
 
-// dW[r, b, i, j] = sum over edges e of relation r (edge-id order) of
-//   norm_e * h[src_e, b*si + i] * dout[dst_e, b*so + j]
+// out[row] = ((p0 + p1) + p2) ... over the row's items in order, for the
+// rows (or relations) of several items: one thread per (row, element).
+__global__ __launch_bounds__(256) void typed_block_combine_kernel(
+    int64_t num_heavy, int64_t F, const int32_t* __restrict__ heavy_row,
+    const int64_t* __restrict__ item_ptr, const float* __restrict__ partial,
+    float* __restrict__ out) {
+  const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
+  if (idx >= num_heavy * F) return;
+  const int64_t h = idx / F, f = idx - h * F;
+  const int64_t r = heavy_row[h];
+  const int64_t i0 = item_ptr[r], i1 = item_ptr[r + 1];
+  float s = partial[i0 * F + f];
+  for (int64_t i = i0 + 1; i < i1; ++i) s = s + partial[i * F + f];
+  out[r * F + f] = s;
+}
+
+// dW[r, b, i, j] over item `it` (a chunk of relation r's edges, relation-major
+// order): sum of norm_e * h[src_e, b*si + i] * dout[dst_e, b*so + j]. One
+// thread per (item, weight element of the relation); kEdges edges in flight.
 __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
-    int64_t num_rels, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ rel_ptr,
-    const int32_t* __restrict__ rel_src, const int64_t* __restrict__ rel_eid,
-    const int64_t* __restrict__ edge_dst, const float* __restrict__ ufeat,
-    const float* __restrict__ dout, const float* __restrict__ enorm, float* __restrict__ dw) {
+    int64_t num_items, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ rel_ptr,
+    const int64_t* __restrict__ item_ptr, const int32_t* __restrict__ item_rel,
+    const int32_t* __restrict__ rel_src, const int32_t* __restrict__ rel_dst,
+    const float* __restrict__ rel_norm, const float* __restrict__ ufeat,
+    const float* __restrict__ dout, float* __restrict__ dw, float* __restrict__ partial) {
+  constexpr int G = 8;
   const int64_t wr = nb * si * so;
   const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
-  if (idx >= num_rels * wr) return;
-  const int64_t r = idx / wr, rem = idx - r * wr;
+  if (idx >= num_items * wr) return;
+  const int64_t it = idx / wr, rem = idx - it * wr;
+  int64_t r, beg, end;
+  bool single;
+  item_range(it, rel_ptr, item_ptr, item_rel, &r, &beg, &end, &single);
   const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
   const int64_t Fi = nb * si, Fo = nb * so;
+  const int64_t xoff = b * si + i, goff = b * so + j;
   float acc = 0.0f;
-  for (int64_t k = rel_ptr[r]; k < rel_ptr[r + 1]; ++k) {
-    const int64_t e = rel_eid[k];
-    const float x = ufeat[int64_t(rel_src[k]) * Fi + b * si + i];
-    const float g = dout[edge_dst[e] * Fo + b * so + j];
-    acc = __builtin_fmaf(enorm ? enorm[e] * x : x, g, acc);
+  for (int64_t k = beg; k < end; k += G) {
+    const int64_t cnt = end - k;
+    float x[G], g[G], nrm[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t kk = q < cnt ? k + q : end - 1;
+      x[q] = ufeat[int64_t(rel_src[kk]) * Fi + xoff];
+      g[q] = dout[int64_t(rel_dst[kk]) * Fo + goff];
+      nrm[q] = rel_norm ? rel_norm[kk] : 1.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      if (q < cnt) acc = __builtin_fmaf(rel_norm ? nrm[q] * x[q] : x[q], g[q], acc);
   }
-  dw[idx] = acc;
+  (single ? dw + r * wr : partial + it * wr)[rem] = acc;
 }
 
 }  // namespace
@@ -142,28 +200,31 @@ using namespace dglhip;
 
 extern "C" {
 
-int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t in_block,
-                                   int64_t out_block, const int64_t* indptr,
-                                   const int32_t* indices, const int64_t* eid,
-                                   const int64_t* etype, const float* ufeat,
-                                   const float* weight, const float* enorm, float* out,
+int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t num_blocks,
+                                   int64_t in_block, int64_t out_block, const int64_t* indptr,
+                                   const int64_t* item_ptr, const int32_t* item_row,
+                                   int64_t num_heavy, const int32_t* heavy_row,
+                                   const int32_t* indices, const int32_t* slot_rel,
+                                   const float* slot_norm, const float* ufeat,
+                                   const float* weight, float* out, float* partial,
                                    void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rows >= 0 && num_blocks > 0 && in_block > 0 && out_block > 0,
-               "bad sizes");
+  DGLHIP_CHECK(num_rows >= 0 && num_items >= num_rows && num_heavy >= 0 && num_blocks > 0 &&
+               in_block > 0 && out_block > 0, "bad sizes");
   const int64_t Fo = num_blocks * out_block;
   if (num_rows == 0) return 0;
-  DGLHIP_CHECK(indptr && indices && eid && etype && ufeat && weight && out,
+  DGLHIP_CHECK(indptr && item_ptr && item_row && indices && slot_rel && ufeat && weight && out,
                "null pointer argument");
+  DGLHIP_CHECK(num_heavy == 0 || (heavy_row && partial), "chunked rows need their partials");
   const int64_t npass = (Fo + 63) / 64;
-  const int64_t waves = num_rows * npass;
+  const int64_t waves = num_items * npass;
   DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
   const dim3 grid = grid_1d((waves + 3) / 4), block(256);
-#define DGLHIP_TB(S)                                                                   \
-  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_rows, npass, \
-                     num_blocks, in_block, out_block, indptr, indices, eid, etype, ufeat, \
-                     weight, enorm, out)
+#define DGLHIP_TB(S)                                                                       \
+  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_items, npass, \
+                     num_blocks, in_block, out_block, indptr, item_ptr, item_row, indices, \
+                     slot_rel, slot_norm, ufeat, weight, out, partial)
   timed_launch(stream, [&] {
     switch (in_block) {
       case 1: DGLHIP_TB(1); break;
@@ -176,29 +237,46 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks, int64_t
     }
   });
 #undef DGLHIP_TB
+  if (num_heavy > 0) {
+    const int64_t total = num_heavy * Fo;
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                         stream, num_heavy, Fo, heavy_row, item_ptr, partial, out);
+    });
+  }
   API_END();
 }
 
-int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks, int64_t in_block,
-                                    int64_t out_block, const int64_t* rel_ptr,
-                                    const int32_t* rel_src, const int64_t* rel_eid,
-                                    const int64_t* edge_dst, const float* ufeat,
-                                    const float* dout, const float* enorm, float* dweight,
-                                    void* stream_) {
+int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
+                                    int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
+                                    const int64_t* item_ptr, const int32_t* item_rel,
+                                    int64_t num_heavy, const int32_t* heavy_rel,
+                                    const int32_t* rel_src, const int32_t* rel_dst,
+                                    const float* rel_norm, const float* ufeat, const float* dout,
+                                    float* dweight, float* partial, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rels >= 0 && num_blocks >= 0 && in_block >= 0 && out_block >= 0,
-               "bad sizes");
-  const int64_t total = num_rels * num_blocks * in_block * out_block;
-  if (total == 0) return 0;
-  DGLHIP_CHECK(rel_ptr && rel_src && rel_eid && edge_dst && ufeat && dout && dweight,
+  DGLHIP_CHECK(num_rels >= 0 && num_items >= num_rels && num_heavy >= 0 && num_blocks >= 0 &&
+               in_block >= 0 && out_block >= 0, "bad sizes");
+  const int64_t wr = num_blocks * in_block * out_block;
+  if (num_rels == 0 || wr == 0) return 0;
+  DGLHIP_CHECK(rel_ptr && item_ptr && item_rel && ufeat && dout && dweight,
                "null pointer argument");
+  DGLHIP_CHECK(num_heavy == 0 || (heavy_rel && partial), "chunked relations need their partials");
+  const int64_t total = num_items * wr;
   DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256),
-                       dim3(256), 0, stream, num_rels, num_blocks, in_block, out_block, rel_ptr,
-                       rel_src, rel_eid, edge_dst, ufeat, dout, enorm, dweight);
+    hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                       stream, num_items, num_blocks, in_block, out_block, rel_ptr, item_ptr,
+                       item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight, partial);
   });
+  if (num_heavy > 0) {
+    const int64_t t2 = num_heavy * wr;
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((t2 + 255) / 256), dim3(256), 0,
+                         stream, num_heavy, wr, heavy_rel, item_ptr, partial, dweight);
+    });
+  }
   API_END();
 }
 

@@ -65,10 +65,12 @@ def _load():
                                                 _vp, _vp, _c_i64, _vp, _vp]),
         "dglhip_gspmm_ranges_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
                                               _vp, _vp, _c_i64, _vp, _c_int]),
-        "dglhip_typed_block_spmm_device": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_vp]),
-        "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_c_int]),
-        "dglhip_typed_block_wgrad_device": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_vp]),
-        "dglhip_typed_block_wgrad_host": (_c_int, [_c_i64] * 4 + [_vp] * 8 + [_c_int]),
+        "dglhip_typed_block_spmm_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
+                                           [_vp] * 9),
+        "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),
+        "dglhip_typed_block_wgrad_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
+                                            [_vp] * 9),
+        "dglhip_typed_block_wgrad_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),
         "dglhip_gsddmm_attention_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                     ctypes.c_float, ctypes.c_float,
                                                     ctypes.c_float, _c_int, _vp, _vp]),

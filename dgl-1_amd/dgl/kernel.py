@@ -1493,38 +1493,109 @@ def timing_read():
 # ---------------------------------------------------------------------------
 # Typed-edge block-diagonal g-SpMM (R-GCN block layer)
 # ---------------------------------------------------------------------------
-def _run_typed_block(csr, ufeat2, weight, etype, enorm, nb, si, so):
+class _GatherRows(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, idx):
+        ctx.num_rows = x.shape[0]
+        ctx.save_for_backward(idx)
+        return x.index_select(0, idx)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (idx,) = ctx.saved_tensors
+        m = idx.numel()
+        if m == 0:
+            return dy.new_zeros((ctx.num_rows,) + tuple(dy.shape[1:])), None
+        dy2 = dy.reshape(m, -1)
+        adj = from_coo(ctx.num_rows, m, idx, torch.arange(m, device=idx.device), ORDER_EID,
+                       idx.device)
+        dx = gspmm(adj, "copy_u", "sum", dy2.contiguous())
+        return dx.view((ctx.num_rows,) + tuple(dy.shape[1:])), None
+
+
+def gather_rows(x, idx):
+    """``x[idx]`` (rows) whose gradient is a g-SpMM: dx[r] = the sum of dy[i]
+    over the positions i with idx[i] == r, in increasing i — deterministic
+    (torch's index backward accumulates duplicates in an implementation-
+    defined order, and walked a hub row's duplicates serially: R-GCN's
+    DistMult decoder spent 3 ms of an 8 ms step there, tools/rgcn_step.py)."""
+    idx = idx.to(device=x.device, dtype=torch.int64).reshape(-1)
+    return _GatherRows.apply(x, idx)
+
+
+TYPED_CHUNK = 64  # DGLHIP_TYPED_CHUNK: slots per chain of the typed-block kernels
+
+
+def _typed_items(ptr):
+    """The typed-block kernels' work items over a CSR-like ``ptr`` (cached by
+    the caller): (item_ptr int64[R+1] — each row's first item, a row of deg
+    slots having max(1, ceil(deg / TYPED_CHUNK)) items —, item_row int32[I],
+    heavy int32[rows of more than one item])."""
+    deg = ptr[1:] - ptr[:-1]
+    nit = torch.clamp((deg + (TYPED_CHUNK - 1)) // TYPED_CHUNK, min=1)
+    item_ptr = torch.zeros(len(deg) + 1, dtype=torch.int64, device=ptr.device)
+    torch.cumsum(nit, 0, out=item_ptr[1:])
+    total = int(item_ptr[-1])
+    item_row = torch.repeat_interleave(torch.arange(len(deg), device=ptr.device,
+                                                    dtype=torch.int32), nit, output_size=total)
+    heavy = torch.nonzero(nit > 1).squeeze(1).to(torch.int32)
+    return item_ptr, item_row, heavy
+
+
+def _run_typed_block(csr, ufeat2, weight, slot_rel, slot_norm, nb, si, so):
     dev = ufeat2.device
     out = torch.empty(csr.num_rows, nb * so, dtype=torch.float32, device=dev)
-    args = (csr.num_rows, nb, si, so, ptr(csr.indptr), ptr(csr.indices), ptr(csr.eid),
-            ptr(etype), ptr(ufeat2), ptr(weight), ptr(enorm), ptr(out))
     if dev.type == "cuda":
-        check_call(LIB.dglhip_typed_block_spmm_device(*(args + (_stream_of(dev),))))
+        items = csr._plans.get("typed_items")
+        if items is None:
+            items = csr._plans["typed_items"] = _typed_items(csr.indptr)
+        item_ptr, item_row, heavy = items
+        nh = heavy.numel()
+        part = torch.empty(item_row.numel() if nh else 0, nb * so, dtype=torch.float32,
+                           device=dev)
+        check_call(LIB.dglhip_typed_block_spmm_device(
+            csr.num_rows, item_row.numel(), nb, si, so, ptr(csr.indptr), ptr(item_ptr),
+            ptr(item_row), nh, ptr(heavy), ptr(csr.indices), ptr(slot_rel), ptr(slot_norm),
+            ptr(ufeat2), ptr(weight), ptr(out), ptr(part), _stream_of(dev)))
     else:
-        check_call(LIB.dglhip_typed_block_spmm_host(*(args + (0,))))
+        check_call(LIB.dglhip_typed_block_spmm_host(
+            csr.num_rows, nb, si, so, ptr(csr.indptr), ptr(csr.indices), ptr(slot_rel),
+            ptr(slot_norm), ptr(ufeat2), ptr(weight), ptr(out), 0))
     return out
 
 
-class _RelationGroups(object):
-    """Relation-major grouping of an adjacency's edges for the weight gradient."""
+def _slot_values(csr, etype, enorm):
+    """The per-edge relation (int32) and norm in ``csr``'s slot order."""
+    rel = etype.index_select(0, csr.eid).to(torch.int32)
+    nrm = None if enorm is None else enorm.index_select(0, csr.eid)
+    return rel, nrm
 
-    def __init__(self, fwd, etype, num_rels, num_edges):
-        rows = fwd.row_ids()
-        rel_of_slot = etype[fwd.eid]
+
+class _RelationGroups(object):
+    """Relation-major grouping of an adjacency's edges for the weight
+    gradient: ptr[R+1], the source and destination of each edge (forward
+    slot order within a relation), ``slot`` the forward slot each came from,
+    and the chunked items (_typed_items)."""
+
+    def __init__(self, fwd, etype, num_rels):
+        rel_of_slot = etype.index_select(0, fwd.eid)
         rel = build_csr(num_rels, max(fwd.num_cols, 1), rel_of_slot, fwd.indices.long(),
                         ORDER_EID, fwd.device, schedule=False)
         self.ptr = rel.indptr
         self.src = rel.indices
-        self.eid = fwd.eid[rel.eid]
-        self.edge_dst = torch.zeros(num_edges, dtype=torch.int64, device=fwd.device)
-        self.edge_dst[fwd.eid] = rows
+        self.slot = rel.eid  # forward slot of each relation-major position
+        self.dst = fwd.row_ids().index_select(0, self.slot).to(torch.int32)
+        self.items = _typed_items(self.ptr) if fwd.device.type == "cuda" else None
+        self.etype = etype  # the relations it was built for (by identity and version)
+        self.version = etype._version
 
 
 class _TypedBlock(torch.autograd.Function):
     @staticmethod
     def forward(ctx, adj, etype, num_rels, ufeat2, weight, enorm):
         R, nb, si, so = weight.shape
-        out = _run_typed_block(adj.fwd, ufeat2, weight, etype, enorm, nb, si, so)
+        rel, nrm = _slot_values(adj.fwd, etype, enorm)
+        out = _run_typed_block(adj.fwd, ufeat2, weight, rel, nrm, nb, si, so)
         ctx.adj, ctx.num_rels = adj, num_rels
         ctx.save_for_backward(etype, ufeat2, weight, enorm)
         return out
@@ -1538,18 +1609,28 @@ class _TypedBlock(torch.autograd.Function):
         du = dw = None
         if ctx.needs_input_grad[3]:
             wt = weight.transpose(2, 3).contiguous()  # (R, nb, so, si)
-            du = _run_typed_block(adj.bwd, dout, wt, etype, enorm, nb, so, si)
+            rel, nrm = _slot_values(adj.bwd, etype, enorm)
+            du = _run_typed_block(adj.bwd, dout, wt, rel, nrm, nb, so, si)
         if ctx.needs_input_grad[4]:
-            if getattr(adj, "_rel_groups", None) is None:
-                adj._rel_groups = _RelationGroups(adj.fwd, etype, R, etype.numel())
-            g = adj._rel_groups
+            g = getattr(adj, "_rel_groups", None)
+            if g is None or g.etype is not etype or g.version != etype._version:
+                g = adj._rel_groups = _RelationGroups(adj.fwd, etype, R)
+            fwd_nrm = None if enorm is None else enorm.index_select(0, adj.fwd.eid)
+            nrm = None if fwd_nrm is None else fwd_nrm.index_select(0, g.slot)
             dw = torch.empty_like(weight)
-            args = (R, nb, si, so, ptr(g.ptr), ptr(g.src), ptr(g.eid), ptr(g.edge_dst),
-                    ptr(ufeat2), ptr(dout), ptr(enorm), ptr(dw))
             if dout.is_cuda:
-                check_call(LIB.dglhip_typed_block_wgrad_device(*(args + (_stream_of(dout.device),))))
+                item_ptr, item_rel, heavy = g.items
+                nh = heavy.numel()
+                part = torch.empty(item_rel.numel() if nh else 0, nb * si * so,
+                                   dtype=torch.float32, device=dout.device)
+                check_call(LIB.dglhip_typed_block_wgrad_device(
+                    R, item_rel.numel(), nb, si, so, ptr(g.ptr), ptr(item_ptr), ptr(item_rel),
+                    nh, ptr(heavy), ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2), ptr(dout),
+                    ptr(dw), ptr(part), _stream_of(dout.device)))
             else:
-                check_call(LIB.dglhip_typed_block_wgrad_host(*(args + (0,))))
+                check_call(LIB.dglhip_typed_block_wgrad_host(
+                    R, nb, si, so, ptr(g.ptr), ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2),
+                    ptr(dout), ptr(dw), 0))
         return None, None, None, du, dw, None
 
 
@@ -1643,17 +1724,29 @@ def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
 _GAT_SEED = {}
 
 
-def _gat_seed_offset(dev):
-    """For a call captured in a HIP graph: a per-device int64 counter the
-    fused kernel adds to its dropout seed, advanced on the device at every
-    call, so every replay draws a new mask with no host round trip."""
+def _gat_seed_counter(dev):
+    """The per-device int64 counter of captured calls. Made at the first call
+    on the device outside a capture (the warm-up a capture needs anyway), so
+    its zero fill is not part of any graph; made first inside a capture its
+    start value is arbitrary (torch.empty: a captured fill would reset it at
+    every replay)."""
     key = str(dev)
     if key not in _GAT_SEED:
-        base = int(torch.randint(0, 1 << 62, (1,)).item())
-        _GAT_SEED[key] = (base, torch.zeros(1, dtype=torch.int64, device=dev))
-    base, off = _GAT_SEED[key]
+        if torch.cuda.is_current_stream_capturing():
+            _GAT_SEED[key] = torch.empty(1, dtype=torch.int64, device=dev)
+        else:
+            _GAT_SEED[key] = torch.zeros(1, dtype=torch.int64, device=dev)
+    return _GAT_SEED[key]
+
+
+def _gat_seed_offset(dev):
+    """For a call captured in a HIP graph: a base seed from torch's generator
+    (drawn at capture) and the device counter the fused kernel adds to it,
+    advanced on the device at every replay: every replay draws a new mask
+    with no host round trip."""
+    off = _gat_seed_counter(dev)
     off.add_(1)
-    return base, off
+    return int(torch.randint(0, 1 << 62, (1,)).item()), off
 
 
 def set_gat_variant(variant):
@@ -1894,6 +1987,8 @@ def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0
         if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
             seed, seed_off = _gat_seed_offset(dev)
         else:  # torch's generator, every call: torch.manual_seed repeats the masks
+            if dev.type == "cuda":
+                _gat_seed_counter(dev)  # ready for a later capture
             seed = int(torch.randint(0, 1 << 62, (1,)).item())
     ft_sum, z = _GATAggregate.apply(adj, float(alpha), float(clamp[0]), float(clamp[1]),
                                     bool(apply_exp), p, int(seed or 0), seed_off, el2, er2,

@@ -537,40 +537,58 @@ int dglhip_gat_dropout_mask_host(int64_t num_slots, int64_t num_heads, float dro
                                  uint64_t seed, uint8_t* keep);
 
 /* ------------------------------------------------------------------------ */
-/* Typed-edge block-diagonal g-SpMM (R-GCN block layer, examples/pytorch/    */
-/* rgcn/layers.py:121-132): with Fi = nb*si, Fo = nb*so,                     */
-/*   out[r, b*so+j] = sum_{slot k of row r} norm[e] *                       */
-/*                    sum_i ufeat[indices[k], b*si+i] * weight[type[e],b,i,j]*/
-/* (e = eid[k]; norm may be NULL = 1). One sequential chain per output      */
-/* element in slot order. weight is float32[R, nb, si, so]; etype int64[E]. */
+/* Typed-edge block-diagonal g-SpMM (R-GCN block layer; replaces the        */
+/* reference's edge UDF + builtin sum, examples/pytorch/rgcn/layers.py:      */
+/* 121-132 and link_predict.py's RGCNBlockLayer): with Fi = nb*si,           */
+/* Fo = nb*so,                                                               */
+/*   out[r, b*so+j] = sum_{slot k of row r} norm[k] *                       */
+/*                    sum_i ufeat[indices[k], b*si+i] * weight[rel[k],b,i,j] */
+/* with rel / norm given per CSR slot (norm may be NULL = 1); weight is     */
+/* float32[R, nb, si, so]. Rows are cut into chunks of DGLHIP_TYPED_CHUNK   */
+/* slots: each chunk is one sequential fma chain in slot order, and a row   */
+/* of several chunks is their partial sums added in chunk order. The host   */
+/* entry points run the same chains (identical bits).                       */
 /* ------------------------------------------------------------------------ */
-int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_blocks,
+#define DGLHIP_TYPED_CHUNK 64
+/* Device form: the chunks as items. item_ptr[num_rows+1] = each row's first
+ * item (a row of deg slots has max(1, ceil(deg / DGLHIP_TYPED_CHUNK))
+ * items), item_row[num_items] = the row of each item, heavy_row[num_heavy] =
+ * the rows of more than one item; partial = num_items x Fo floats of
+ * workspace (only heavy rows' items are written). */
+int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t num_blocks,
                                    int64_t in_block, int64_t out_block,
-                                   const int64_t* indptr, const int32_t* indices,
-                                   const int64_t* eid, const int64_t* etype,
-                                   const float* ufeat, const float* weight,
-                                   const float* enorm, float* out, void* stream);
+                                   const int64_t* indptr, const int64_t* item_ptr,
+                                   const int32_t* item_row, int64_t num_heavy,
+                                   const int32_t* heavy_row, const int32_t* indices,
+                                   const int32_t* slot_rel, const float* slot_norm,
+                                   const float* ufeat, const float* weight, float* out,
+                                   float* partial, void* stream);
 int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks,
                                  int64_t in_block, int64_t out_block,
                                  const int64_t* indptr, const int32_t* indices,
-                                 const int64_t* eid, const int64_t* etype,
-                                 const float* ufeat, const float* weight,
-                                 const float* enorm, float* out, int num_threads);
-/* Weight gradient: dweight[r,b,i,j] = sum over the edges of relation r
- * (relation-major CSR rel_ptr[R+1] / rel_src / rel_eid, edge-id order) of
- * norm[e] * ufeat[src, b*si+i] * dout[edge_dst[e], b*so+j]. */
-int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_blocks,
+                                 const int32_t* slot_rel, const float* slot_norm,
+                                 const float* ufeat, const float* weight, float* out,
+                                 int num_threads);
+/* Weight gradient: dweight[r,b,i,j] = sum over the edges k of relation r
+ * (relation-major CSR rel_ptr[R+1] with per-edge rel_src / rel_dst /
+ * rel_norm, norm may be NULL) of norm[k] * ufeat[src, b*si+i] *
+ * dout[dst, b*so+j]; each relation's edge list chunked as the rows above
+ * (items item_ptr / item_rel, heavy_rel, partial = num_items x nb*si*so
+ * floats). */
+int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
                                     int64_t in_block, int64_t out_block,
-                                    const int64_t* rel_ptr, const int32_t* rel_src,
-                                    const int64_t* rel_eid, const int64_t* edge_dst,
-                                    const float* ufeat, const float* dout,
-                                    const float* enorm, float* dweight, void* stream);
+                                    const int64_t* rel_ptr, const int64_t* item_ptr,
+                                    const int32_t* item_rel, int64_t num_heavy,
+                                    const int32_t* heavy_rel, const int32_t* rel_src,
+                                    const int32_t* rel_dst, const float* rel_norm,
+                                    const float* ufeat, const float* dout, float* dweight,
+                                    float* partial, void* stream);
 int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
                                   int64_t in_block, int64_t out_block,
                                   const int64_t* rel_ptr, const int32_t* rel_src,
-                                  const int64_t* rel_eid, const int64_t* edge_dst,
-                                  const float* ufeat, const float* dout,
-                                  const float* enorm, float* dweight, int num_threads);
+                                  const int32_t* rel_dst, const float* rel_norm,
+                                  const float* ufeat, const float* dout, float* dweight,
+                                  int num_threads);
 
 /* ------------------------------------------------------------------------ */
 /* Kernel timing (measurement support for bench.py): when enabled, every     */

@@ -145,23 +145,39 @@ static void run_case(int64_t n, int64_t nnz, int64_t F, int hub, int nthreads) {
                                   dots, nthreads));
   OK(dglhip_gsddmm_attention_host(n, F, indptr, indices, NULL, H, H, 0.2f, -INFINITY,
                                   INFINITY, 0, dots, nthreads));
-  /* typed blocks: 3 relations, F = nb * 1 blocks of 1x1 */
+  /* typed blocks: 3 relations, F = nb * 1 blocks of 1x1; relation and norm
+     per slot; the relation-major grouping of the same edges for dW (rows past
+     one chunk of DGLHIP_TYPED_CHUNK slots take the chunked chains) */
   {
     const int64_t R = 3, nb = F, si = 1, so = 1;
     int64_t* et = xmalloc(sizeof(int64_t) * (nnz ? nnz : 1));
+    int32_t* srel = xmalloc(sizeof(int32_t) * (nnz ? nnz : 1));
+    float* snrm = xmalloc(sizeof(float) * (nnz ? nnz : 1));
     float* w = xmalloc(sizeof(float) * R * nb * si * so);
     float* dw = xmalloc(sizeof(float) * R * nb * si * so);
     for (int64_t e = 0; e < nnz; ++e) et[e] = (int64_t)(rnd() % 3);
+    for (int64_t k = 0; k < nnz; ++k) {
+      srel[k] = (int32_t)et[eid[k]];
+      snrm[k] = W[eid[k]];
+    }
     for (int64_t i = 0; i < R * nb * si * so; ++i) w[i] = frand();
-    OK(dglhip_typed_block_spmm_host(n, nb, si, so, indptr, indices, eid, et, H, w, W, out,
+    OK(dglhip_typed_block_spmm_host(n, nb, si, so, indptr, indices, srel, snrm, H, w, out,
                                     nthreads));
-    /* relation-major grouping of the same edges for the weight gradient */
+    OK(dglhip_typed_block_spmm_host(n, nb, si, so, indptr, indices, srel, NULL, H, w, out,
+                                    nthreads));
     int64_t* rp = xmalloc(sizeof(int64_t) * (R + 1));
     int32_t* rs = xmalloc(sizeof(int32_t) * (nnz ? nnz : 1));
     int64_t* re = xmalloc(sizeof(int64_t) * (nnz ? nnz : 1));
+    int32_t* rd = xmalloc(sizeof(int32_t) * (nnz ? nnz : 1));
+    float* rn = xmalloc(sizeof(float) * (nnz ? nnz : 1));
     OK(dglhip_coo_to_csr_host(R, n, nnz, et, col, DGLHIP_ORDER_EID, rp, rs, re));
-    OK(dglhip_typed_block_wgrad_host(R, nb, si, so, rp, rs, re, row, H, H, W, dw, nthreads));
-    free(et); free(w); free(dw); free(rp); free(rs); free(re);
+    for (int64_t k = 0; k < nnz; ++k) {
+      rd[k] = (int32_t)row[re[k]];
+      rn[k] = W[re[k]];
+    }
+    OK(dglhip_typed_block_wgrad_host(R, nb, si, so, rp, rs, rd, rn, H, H, dw, nthreads));
+    free(et); free(srel); free(snrm); free(w); free(dw); free(rp); free(rs); free(re);
+    free(rd); free(rn);
   }
   /* degree bucketing of the messages by destination */
   {

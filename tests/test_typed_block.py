@@ -57,16 +57,18 @@ def test_typed_block(device, shape):
 @pytest.mark.parametrize("shape", [(7, 3, 1, 2), (9, 10, 2, 7), (11, 4, 3, 5), (20, 100, 5, 5),
                                    (5, 8, 8, 3), (4, 2, 16, 40), (6, 3, 7, 9)])
 def test_typed_block_device_matches_host_bits(shape):
-    """The HIP kernel (templated block widths 1/2/4/5/8/16, runtime width
-    otherwise; slices of 64 outputs per wave, 4 edges in flight) runs the same
-    per-element fma chains as the host kernel: identical bits, forward and
-    the transposed-block backward. A power-law destination set gives rows far
-    longer than the edge group."""
+    """The HIP kernels (templated block widths 1/2/4/5/8/16, runtime width
+    otherwise; slices of 64 outputs per wave, edges in flight predicated)
+    run the same per-element fma chains as the host kernels: identical bits,
+    forward, the transposed-block backward and the weight gradient. A
+    power-law destination set gives rows far longer than one chunk of
+    kernel.TYPED_CHUNK slots (their partials added in chunk order), and the
+    relations hold more than one chunk of edges each."""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     R, nb, si, so = shape
     rng = np.random.default_rng(sum(shape))
-    n, m = 400, 8000
+    n, m = 400, 8000 * R // 4 + 8000
     p = 1.0 / np.arange(1, n + 1) ** 1.1
     dst = torch.from_numpy(rng.choice(n, size=m, p=p / p.sum()))
     src = torch.from_numpy(rng.integers(0, n, m))
@@ -75,16 +77,23 @@ def test_typed_block_device_matches_host_bits(shape):
     h = torch.randn(n, nb * si)
     W = torch.randn(R, nb, si, so) * 0.3
     G = torch.randn(n, nb * so)
-    outs, grads = [], []
-    for dev in ("cpu", "cuda"):
-        adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
-        h1 = h.detach().to(dev).clone().requires_grad_(True)
-        out = kernel.typed_block_spmm(adj, h1, W.to(dev), etype.to(dev), norm.to(dev))
-        out.backward(G.to(dev))
-        outs.append(out.detach().cpu())
-        grads.append(h1.grad.cpu())
-    assert torch.equal(outs[0], outs[1])
-    assert torch.equal(grads[0], grads[1])
+    assert int(torch.bincount(dst).max()) > 4 * kernel.TYPED_CHUNK
+    assert int(torch.bincount(etype).min()) > kernel.TYPED_CHUNK
+    for nm in (norm, None):
+        outs, grads, wgrads = [], [], []
+        for dev in ("cpu", "cuda"):
+            adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+            h1 = h.detach().to(dev).clone().requires_grad_(True)
+            W1 = W.detach().to(dev).clone().requires_grad_(True)
+            out = kernel.typed_block_spmm(adj, h1, W1, etype.to(dev),
+                                          None if nm is None else nm.to(dev))
+            out.backward(G.to(dev))
+            outs.append(out.detach().cpu())
+            grads.append(h1.grad.cpu())
+            wgrads.append(W1.grad.cpu())
+        assert torch.equal(outs[0], outs[1])
+        assert torch.equal(grads[0], grads[1])
+        assert torch.equal(wgrads[0], wgrads[1])
 
 
 def _example():
