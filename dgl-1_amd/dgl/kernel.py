@@ -1649,8 +1649,13 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
     R, nb, si, so = weight.shape
     if ufeat.shape[1] != nb * si:
         raise DGLError("ufeat width %d != num_blocks * in_block %d" % (ufeat.shape[1], nb * si))
-    etype = etype.to(device=dev, dtype=torch.int64).contiguous()
+    etype = etype.to(device=dev, dtype=torch.int64).contiguous().reshape(-1)
     en = None if enorm is None else _f32c(enorm.to(dev).reshape(-1).detach())
+    # one relation (and norm) per edge id: the kernels gather them by edge id
+    E = adj.fwd.nnz
+    if etype.numel() != E or (en is not None and en.numel() != E):
+        raise DGLError("typed_block_spmm: %d edges but etype has %d and enorm %s entries"
+                       % (E, etype.numel(), "no" if en is None else en.numel()))
     return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en)
 
 

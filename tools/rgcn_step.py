@@ -83,6 +83,7 @@ def kernel_times(model, s, dev, iters=20):
     """Each typed-block kernel of layer 0 alone: (ms per call, algorithmic
     bytes) for the forward g-SpMM, the transposed dH g-SpMM and dW."""
     uniq, src, dst, rel, norm, _, _ = s
+    norm = norm.index_select(0, dst.to(norm.device))  # per edge: 1 / in-degree of its dst
     g = DGLGraph((src, dst), multigraph=True)
     if g.number_of_nodes() < len(uniq):
         g.add_nodes(len(uniq) - g.number_of_nodes())
