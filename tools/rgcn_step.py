@@ -29,9 +29,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "dgl-1_amd")]
 from dgl import DGLGraph, kernel  # noqa: E402
-from tests.conftest import load_example  # noqa: E402
 
-lp = load_example("rgcn/link_predict.py", "rgcn_step_lp")
+
+def _load_example(relpath, name):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "examples", relpath))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+lp = _load_example("rgcn/link_predict.py", "rgcn_step_lp")
 
 
 def make_samples(args, steps):
