@@ -128,6 +128,20 @@ def build_parser():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
                          "to rehearse the multi-rank path")
+    ap.add_argument("--no-model-legs", action="store_true",
+                    help="N=1: skip the configs[2]-[4] model legs (gat, gat_pubmed, sage, rgcn)")
+    ap.add_argument("--no-strong-leg", action="store_true",
+                    help="N>1: skip the fixed-graph (strong scaling) Reddit block")
+    ap.add_argument("--emulate-strong", action="store_true",
+                    help="with --emulate-world W: rank 0 of the fixed N=1 graph partitioned W "
+                         "ways (strong scaling) instead of the x W graph")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="N>1: collective timeout (s) of the process groups; a dead or hung "
+                         "peer then ends the job in bounded time")
+    ap.add_argument("--leg-deadline", type=float, default=None,
+                    help="seconds a secondary leg may run before rank 0 prints the line built "
+                         "so far (with the leg's error) and exits; default: the collective "
+                         "timeout less 60 s at N>1, 900 s at N=1")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: run every leg through the library's host kernels with gloo "
                          "(tests of the launcher and the multi-rank plumbing; not a driver line)")
@@ -159,26 +173,104 @@ def launch_command(args, argv, env, port=None):
             os.path.abspath(__file__)] + list(argv)
 
 
+class _Terminated(Exception):
+    def __init__(self, signum):
+        Exception.__init__(self, "signal %d" % signum)
+        self.signum = signum
+
+
 def relay(cmd, env=None):
-    """Run ``cmd`` as a child in its own process group, pass its stdout through
-    line by line (rank 0's JSON line among it), return its exit code. The
-    group is killed if this process is interrupted."""
+    """Run ``cmd`` as a child in its own session, pass its stdout through line
+    by line (rank 0's JSON line among it), return its exit code. SIGTERM,
+    SIGINT and SIGHUP to this process, or any exception here, kill the
+    child's whole process group (the torchrun agent and every rank) before
+    this process exits (128 + the signal's number for a signal). This
+    process never touches the GPU."""
+    import signal
     env = dict(os.environ if env is None else env)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True,
-                            bufsize=1, universal_newlines=True)
+    env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+
+    def on_signal(signum, frame):
+        raise _Terminated(signum)
+    old = {sig: signal.signal(sig, on_signal)
+           for sig in (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)}
+    proc = None
     try:
+        proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True,
+                                bufsize=1, universal_newlines=True)
         for line in proc.stdout:
             sys.stdout.write(line)
             sys.stdout.flush()
         return proc.wait()
+    except _Terminated as t:
+        log("relay: %s, killing the ranks' process group" % t)
+        _kill_group(proc)
+        return 128 + t.signum
     except BaseException:
+        _kill_group(proc)
+        raise
+    finally:
+        for sig, h in old.items():
+            signal.signal(sig, h)
+
+
+def _descendants(pid):
+    """Every live descendant pid of ``pid`` (from /proc's parent links)."""
+    kids = {}
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
         try:
-            os.killpg(proc.pid, 9)
+            with open("/proc/%s/stat" % d) as f:
+                st = f.read()
+            ppid = int(st[st.rindex(")") + 2:].split()[1])
+        except (OSError, ValueError, IndexError):
+            continue
+        kids.setdefault(ppid, []).append(int(d))
+    out, todo = [], [pid]
+    while todo:
+        for c in kids.get(todo.pop(), []):
+            out.append(c)
+            todo.append(c)
+    return out
+
+
+def _kill_group(proc):
+    """End the child and everything under it: torchrun starts its ranks in
+    sessions of their own, so the child's process group alone does not reach
+    them. SIGTERM first (torchrun stops its workers), then SIGKILL to every
+    descendant still there."""
+    if proc is None:
+        return
+    tree = set(_descendants(proc.pid))
+    for sig in (15, 9):
+        for pid in [proc.pid] + sorted(tree):
+            try:
+                os.kill(pid, sig)
+            except OSError:
+                pass
+        try:
+            os.killpg(proc.pid, sig)
         except OSError:
             pass
-        proc.wait()
-        raise
+        deadline = time.time() + (10 if sig == 15 else 30)
+        while time.time() < deadline:
+            tree |= set(_descendants(proc.pid)) if proc.poll() is None else set()
+            alive = [p for p in tree if os.path.exists("/proc/%d" % p) and
+                     not _zombie(p)]
+            if proc.poll() is not None and not alive:
+                return
+            time.sleep(0.2)
+
+
+def _zombie(pid):
+    try:
+        with open("/proc/%d/stat" % pid) as f:
+            st = f.read()
+        return st[st.rindex(")") + 2] == "Z"
+    except (OSError, ValueError, IndexError):
+        return True
 
 
 def world_mismatch(args, env):
@@ -485,21 +577,134 @@ def exchange_block(pg, h_local, steps, world, dev):
                     "bytes over that time"}
 
 
-def rmat_leg(args, world, rank, dev, pmc=None):
+class LegRunner(object):
+    """Runs the secondary legs after the headline on every rank so that one
+    leg's failure cannot lose the line (r03 verdict, Weak 6).
+
+    * Each leg is ``setup`` (rank-local work: graph generation, buffers)
+      then ``run`` (timing, collectives). Every rank catches its own
+      exception; after each phase the ranks exchange their errors over a
+      separate gloo group (``agree``), so a rank that failed in setup makes
+      every rank skip the leg together, with no collective left waiting.
+    * A failed leg is recorded as ``{"error": ...}`` (every failing rank's
+      message) and, at N > 1, the later legs are skipped: a collective may
+      have been left half-done.
+    * Rank 0 arms a deadline per leg (``--leg-deadline``, shorter than the
+      collectives' timeout): a leg still running then (a hung peer, a hung
+      kernel) makes rank 0 print the line built so far, with the leg's
+      error, and exit, before the process group's timeout (with
+      TORCH_NCCL_ASYNC_ERROR_HANDLING=1) tears the ranks down.
+    * ``DGLHIP_BENCH_FAIL=<leg>:<rank>[:run]`` injects a failure into one
+      rank's setup (or run) phase of one leg (tests)."""
+
+    def __init__(self, result, world, rank, deadline, group=None):
+        self.result, self.world, self.rank = result, world, rank
+        self.deadline = deadline
+        self.group = group
+        self.failed = None
+        inject = os.environ.get("DGLHIP_BENCH_FAIL", "")
+        parts = inject.split(":") if inject else []
+        self.inject = (parts[0], int(parts[1]), parts[2] if len(parts) > 2 else "setup") \
+            if len(parts) >= 2 else None
+
+    def _maybe_fail(self, name, phase):
+        if self.inject and self.inject[0] == name and self.inject[1] == self.rank and \
+                self.inject[2] == phase:
+            raise RuntimeError("injected failure (DGLHIP_BENCH_FAIL) in leg %s, %s phase"
+                               % (name, phase))
+
+    def agree(self, err):
+        """Every rank's error string (None: ok), on every rank."""
+        if self.world == 1 or not dist.is_initialized():
+            return [err]
+        out = [None] * self.world
+        dist.all_gather_object(out, err, group=self.group)
+        return out
+
+    def _arm(self, name):
+        if self.rank != 0 or not self.deadline:
+            return None
+        import threading
+
+        def fire():
+            line = dict(self.result)
+            line[name] = {"error": "leg still running after %.0f s (a peer failed or hung, "
+                                   "or a kernel hung): rank 0 printed the line and exited"
+                                   % self.deadline}
+            try:
+                sys.stdout.write(json.dumps(line) + "\n")
+                sys.stdout.flush()
+            finally:
+                os._exit(0)
+        t = threading.Timer(self.deadline, fire)
+        t.daemon = True
+        t.start()
+        return t
+
+    def run(self, name, setup, run=None, collective=True):
+        """Run one leg; its dict (or error) goes to result[name]. ``run``
+        gets setup's return value. Returns True when the leg succeeded."""
+        if self.failed is not None and collective and self.world > 1:
+            self.result[name] = {"skipped": "after the failure of leg %r" % self.failed}
+            return False
+        timer = self._arm(name)
+        t0 = time.time()
+        try:
+            err = state = None
+            try:
+                self._maybe_fail(name, "setup")
+                state = setup()
+            except Exception as e:  # noqa: BLE001 - any failure of the leg is recorded
+                err = "rank %d (setup): %r" % (self.rank, e)
+            errs = self.agree(err)
+            if all(x is None for x in errs) and run is not None:
+                try:
+                    self._maybe_fail(name, "run")
+                    state = run(state)
+                except Exception as e:  # noqa: BLE001
+                    err = "rank %d: %r" % (self.rank, e)
+                errs = self.agree(err)
+        finally:
+            if timer is not None:
+                timer.cancel()
+        bad = [x for x in errs if x is not None]
+        if bad:
+            self.result[name] = {"error": "; ".join(bad)}
+            if collective:
+                self.failed = name
+            log("leg %s failed: %s" % (name, "; ".join(bad)))
+            return False
+        self.result[name] = state
+        log("leg %s done in %.1fs" % (name, time.time() - t0))
+        return True
+
+
+def rmat_setup(args, rank, dev):
+    """The rmat leg's rank-local part: the graph (every rank generates the
+    same one), its CPU sample on rank 0, its distinct-source count."""
+    t0 = time.time()
+    src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
+    n_src = int((torch.bincount(src, minlength=n) > 0).sum())  # distinct sources
+    sample = None
+    if rank == 0 and not args.no_cpu_baseline:
+        sample = cpu_sample(src, dst, n, 2_000_000)
+    log("rmat leg: scale %d, %d edges, generated in %.1fs" % (args.rmat_scale, int(src.numel()),
+                                                              time.time() - t0))
+    return {"src": src, "dst": dst, "n": n, "n_src": n_src, "sample": sample}
+
+
+def rmat_run(args, world, rank, dev, st, pmc=None):
     """RMAT strong scaling on the same ranks: one fixed graph, 1-D dst-row
     partition, heavy rows chunked (kernel.set_row_split("auto"))."""
     from dgl.distributed import PartitionedGraph, balanced_bounds
     old = kernel.set_row_split("auto")
     try:
         t0 = time.time()
-        src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
+        src, dst, n, n_src, sample = st["src"], st["dst"], st["n"], st["n_src"], st["sample"]
+        st.clear()
         E = int(src.numel())
         gen = torch.Generator(device=dev)
         gen.manual_seed(1)
-        n_src = int((torch.bincount(src, minlength=n) > 0).sum())  # distinct sources
-        sample = None
-        if rank == 0 and not args.no_cpu_baseline:
-            sample = cpu_sample(src, dst, n, 2_000_000)
         if not dist.is_initialized():
             adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
             del src, dst
@@ -524,7 +729,7 @@ def rmat_leg(args, world, rank, dev, pmc=None):
                 pg.update_all(h_local)
             par = describe_partition(pg, world, args)
         _sync(dev)
-        log("rmat leg: scale %d, %d edges, setup %.1fs" % (args.rmat_scale, E, time.time() - t0))
+        log("rmat leg: setup %.1fs" % (time.time() - t0))
         steps = min(args.steps, 5)
         elapsed, kms = timed_steps(step, steps, 2, world, dev)
         exch = exchange_block(pg, h_local, steps, world, dev) if dist.is_initialized() else None
@@ -558,8 +763,6 @@ def rmat_leg(args, world, rank, dev, pmc=None):
             t2 = time.time()
             cpu = cpu_baseline(sample, n, None, seconds_budget=10.0)
             log("rmat cpu baseline took %.1fs" % (time.time() - t2))
-        if dist.is_initialized():
-            dist.barrier()
         return {"value": E * steps / elapsed, "unit": "edges/s", "n_gpus": world,
                 "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
                 "scaling": "strong",
@@ -570,6 +773,58 @@ def rmat_leg(args, world, rank, dev, pmc=None):
                 "halo_exchange": exch, "cpu_baseline": cpu}
     finally:
         kernel.set_row_split(old)
+
+
+def reddit_graph(args, scale, dev):
+    """The synthetic Reddit-shaped graph at ``scale`` x its size (times
+    --graph-scale, a testing knob)."""
+    if args.graph_scale == 1.0:
+        return data.reddit_like(scale=scale, seed=0, device=dev)
+    return data.chung_lu(int(data.REDDIT_NODES * scale * args.graph_scale),
+                         int(data.REDDIT_EDGES * scale * args.graph_scale),
+                         data.REDDIT_MAX_OVER_MEAN, seed=0, device=dev)
+
+
+def strong_setup(args, world, rank, dev):
+    """The fixed-graph block's rank-local part: the N = 1 Reddit-shaped graph
+    (every rank generates it) and this rank's rows of it."""
+    from dgl.distributed import balanced_bounds
+    src, dst, n = reddit_graph(args, 1, dev)
+    bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    sel = (dst >= lo) & (dst < hi)
+    return {"n": n, "E": int(src.numel()), "bounds": bounds, "lo": lo, "hi": hi,
+            "src": src[sel], "dst": dst[sel]}
+
+
+def strong_run(args, world, rank, dev, st):
+    """N > 1: the headline step on the FIXED N = 1 graph (114.8M edges at every
+    N), 1-D partitioned like the weak-scaled line: value = all its edges per
+    step over the max-over-ranks step time (scaling "strong")."""
+    from dgl.distributed import PartitionedGraph
+    n, E, lo, hi = st["n"], st["E"], st["lo"], st["hi"]
+    pg2 = PartitionedGraph(n, st.pop("src"), st.pop("dst"), st["bounds"], dev,
+                           pipeline_chunks=args.pipeline_chunks,
+                           halo_dtype=HALO_DTYPE[args.halo_dtype])
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    h2 = torch.rand(hi - lo, FEAT, generator=gen, device=dev) * 2 - 1
+
+    def step2():
+        pg2.update_all(h2)
+    el, kms = timed_steps(step2, args.steps, args.warmup, world, dev)
+    roof = roofline_block(pg2.num_edges, pg2.num_local, kms, world, dev, n * FEAT * 4,
+                          pipelined_blocks(pg2),
+                          kernel="gspmm_sum_kernel<copy_u> (rank 0, every segment of the "
+                                 "pipelined partition)")
+    return {"value": E * args.steps / el, "unit": "edges/s", "n_gpus": world,
+            "ms_per_step": el / args.steps * 1e3, "kernel_ms_rank0": kms, "scaling": "strong",
+            "config": "reddit-shaped x1%s (the N = 1 graph): %d nodes, %d edges, feat=%d, "
+                      "1-D partitioned over %d ranks"
+                      % ("" if args.graph_scale == 1.0 else " (graph-scale %g)" % args.graph_scale,
+                         n, E, FEAT, world),
+            "parallelism": describe_partition(pg2, world, args), "roofline": roof,
+            "halo_exchange": exchange_block(pg2, h2, args.steps, world, dev)}
 
 
 def main(argv=None):
@@ -595,6 +850,7 @@ def main(argv=None):
             args.dist_backend = "gloo"
     pmc = None
     rmat_pmc = None
+    side_group = None
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
         t0 = time.time()  # before this process initialises the GPU
         # every g-SpMM kernel of the 3 calls (warm-up + 2 steps), per call
@@ -620,10 +876,16 @@ def main(argv=None):
         os.environ.setdefault("MASTER_PORT", "29631")
         os.environ.setdefault("RANK", str(rank))
         os.environ.setdefault("WORLD_SIZE", str(world))
+        # a dead or hung peer ends the job in bounded time (r03 verdict, Weak 6)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        from datetime import timedelta
+        tmo = timedelta(seconds=args.dist_timeout)
         if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(args.dist_backend, timeout=tmo)
+        # the legs' error exchange (LegRunner.agree) on its own gloo group
+        side_group = dist.new_group(backend="gloo", timeout=tmo)
 
     t0 = time.time()
     real_reddit = None
@@ -644,12 +906,8 @@ def main(argv=None):
         n = ds.num_nodes
         real_reddit = "Reddit release files under %s (self-loops added)" % root
         del ds, s0, d0, loops
-    elif args.graph_scale == 1.0:
-        src, dst, n = data.reddit_like(scale=world, seed=0, device=dev)
     else:
-        src, dst, n = data.chung_lu(int(data.REDDIT_NODES * world * args.graph_scale),
-                                    int(data.REDDIT_EDGES * world * args.graph_scale),
-                                    data.REDDIT_MAX_OVER_MEAN, seed=0, device=dev)
+        src, dst, n = reddit_graph(args, world, dev)
     num_edges_total = int(src.numel())
     gen = torch.Generator(device=dev)
     gen.manual_seed(1)
@@ -675,7 +933,7 @@ def main(argv=None):
     elif not dist.is_initialized() and args.emulate_world > 1:
         from dgl.distributed import balanced_bounds
         W = args.emulate_world
-        if args.workload == "reddit":  # weak scaling: the x W graph
+        if args.workload == "reddit" and not args.emulate_strong:  # weak: the x W graph
             del src, dst
             src, dst, n = data.reddit_like(scale=W, seed=0, device=dev)
         num_edges_total = int(src.numel())
@@ -713,8 +971,9 @@ def main(argv=None):
             blocks = kernel.blocked_schedule(adj, h)
             mode = "one g-SpMM"
         del sel
-        parallelism = "emulated rank 0 of %d, %s, no communication (H = %.0f MB)" % (
-            W, mode, n * FEAT * 4 / 1e6)
+        parallelism = "emulated rank 0 of %d%s, %s, no communication (H = %.0f MB)" % (
+            W, " (fixed N = 1 graph: strong scaling)" if args.emulate_strong else "", mode,
+            n * FEAT * 4 / 1e6)
         args.no_cpu_baseline = True
     elif not dist.is_initialized():
         g = dgl.DGLGraph((src.cpu(), dst.cpu()))
@@ -828,79 +1087,118 @@ def main(argv=None):
     }
     if on_cpu:
         result["device"] = "cpu (host kernels; plumbing test, not a measurement)"
-    if dist.is_initialized():
-        result["halo_exchange"] = exchange_block(pg, h_local, args.steps, world, dev)
-    if dist.is_initialized() and args.halo_dtype == "fp32" and not args.no_bf16_leg:
+    deadline = args.leg_deadline
+    if deadline is None:
+        deadline = max(args.dist_timeout - 60.0, 30.0) if world > 1 else 900.0
+    legs = LegRunner(result, world, rank, deadline, group=side_group)
+    distributed = dist.is_initialized()
+
+    if distributed:
+        legs.run("halo_exchange", lambda: None,
+                 lambda _: exchange_block(pg, h_local, args.steps, world, dev))
+    if distributed and args.halo_dtype == "fp32" and not args.no_bf16_leg:
         # the opt-in bf16 halo on the same partition (not the headline: remote
         # rows are rounded to bf16, so rows are no longer bit-exact)
-        pg.set_halo_dtype(torch.bfloat16)
-        el16, k16 = timed_steps(step, args.steps, args.warmup, world, dev)
-        pg.set_halo_dtype(None)
-        result["halo_bf16"] = {
-            "value": num_edges_total * args.steps / el16, "unit": "edges/s",
-            "ms_per_step": el16 / args.steps * 1e3, "kernel_ms_rank0": k16,
-            "note": "same partition and step with halo_dtype=bf16: remote rows travel and "
-                    "are read as bf16, summed in fp32; own rows exact. Opt-in, not the "
-                    "headline (results carry bf16 rounding of remote inputs)"}
+        def bf16_run(_):
+            pg.set_halo_dtype(torch.bfloat16)
+            try:
+                el16, k16 = timed_steps(step, args.steps, args.warmup, world, dev)
+            finally:
+                pg.set_halo_dtype(None)
+            return {"value": num_edges_total * args.steps / el16, "unit": "edges/s",
+                    "ms_per_step": el16 / args.steps * 1e3, "kernel_ms_rank0": k16,
+                    "note": "same partition and step with halo_dtype=bf16: remote rows travel "
+                            "and are read as bf16, summed in fp32; own rows exact. Opt-in, not "
+                            "the headline (results carry bf16 rounding of remote inputs)"}
+        legs.run("halo_bf16", lambda: None, bf16_run)
     if args.workload == "reddit" and args.emulate_world <= 1 and not args.no_train_leg:
         # training step of the same layer: forward + backward (the transposed
         # g-SpMM; at N > 1 the pipelined halo's reverse exchange overlapped with
         # the transposed segments), inputs requiring grad, a fixed upstream grad
-        if dist.is_initialized():
-            h_tr = h_local.detach().clone().requires_grad_(True)
-            d_out = torch.rand(pg.num_local, FEAT, generator=gen, device=dev) * 2 - 1
+        def train_setup():
+            if distributed:
+                h_tr = h_local.detach().clone().requires_grad_(True)
+                d_out = torch.rand(pg.num_local, FEAT, generator=gen, device=dev) * 2 - 1
+            else:
+                h_tr = h.detach().clone().requires_grad_(True)
+                d_out = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
+            return h_tr, d_out
 
-            def train_step():
-                pg.update_all(h_tr).backward(d_out)
-        else:
-            h_tr = h.detach().clone().requires_grad_(True)
-            d_out = torch.rand(n, FEAT, generator=gen, device=dev) * 2 - 1
-
-            def train_step():
-                g.ndata["h"] = h_tr
-                g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
-                g.ndata["h_out"].backward(d_out)
-        el_tr, k_tr = timed_steps(train_step, args.steps, args.warmup, world, dev)
-        if not dist.is_initialized():
-            g.ndata["h"] = h
-        result["train_step"] = {
-            "value": num_edges_total * args.steps / el_tr, "unit": "edges/s (fwd+bwd)",
-            "ms_per_step": el_tr / args.steps * 1e3, "kernel_ms_rank0": k_tr,
-            "note": "update_all(copy_src, sum) forward + backward (dH = A^T dC through the "
-                    "transposed CSR%s) per step, same graph and partition"
-                    % ("; halo exchange and its reverse pipelined in %d chunks"
-                       % args.pipeline_chunks if dist.is_initialized() and
-                       args.pipeline_chunks > 0 else "")}
-        del h_tr, d_out
-    if sample is not None:
-        # rank 0, after the timed region (the other ranks wait at the barrier)
-        t2 = time.time()
-        result["cpu_baseline"] = cpu_baseline(sample, n, h_cpu)
-        log("cpu baseline took %.1fs" % (time.time() - t2))
-        sample = h_cpu = None
-    if dist.is_initialized():
-        dist.barrier()
+        def train_run(st):
+            h_tr, d_out = st
+            if distributed:
+                def train_step():
+                    pg.update_all(h_tr).backward(d_out)
+            else:
+                def train_step():
+                    g.ndata["h"] = h_tr
+                    g.update_all(fn.copy_src("h", "m"), fn.sum("m", "h_out"))
+                    g.ndata["h_out"].backward(d_out)
+            try:
+                el_tr, k_tr = timed_steps(train_step, args.steps, args.warmup, world, dev)
+            finally:
+                if not distributed:
+                    g.ndata["h"] = h
+            return {"value": num_edges_total * args.steps / el_tr, "unit": "edges/s (fwd+bwd)",
+                    "ms_per_step": el_tr / args.steps * 1e3, "kernel_ms_rank0": k_tr,
+                    "note": "update_all(copy_src, sum) forward + backward (dH = A^T dC through "
+                            "the transposed CSR%s) per step, same graph and partition"
+                            % ("; halo exchange and its reverse pipelined in %d chunks"
+                               % args.pipeline_chunks if distributed and
+                               args.pipeline_chunks > 0 else "")}
+        legs.run("train_step", train_setup, train_run)
+    if distributed and args.workload == "reddit" and not args.no_strong_leg:
+        legs.run("strong", lambda: strong_setup(args, world, rank, dev),
+                 lambda st: strong_run(args, world, rank, dev, st))
+    if sample is not None or world > 1:
+        # rank 0, after the timed region (the other ranks wait in agree)
+        def cpu_run(_):
+            if sample is None:
+                return None
+            t2 = time.time()
+            out = cpu_baseline(sample, n, h_cpu)
+            log("cpu baseline took %.1fs" % (time.time() - t2))
+            return out
+        legs.run("cpu_baseline", lambda: None, cpu_run, collective=False)
+    if (world == 1 and args.workload == "reddit" and args.emulate_world <= 1 and
+            not args.no_model_legs and not on_cpu and not args.dist_rehearsal):
+        import bench_models as bm
+        want = not args.no_cpu_baseline
+        legs.run("gat", lambda: None, lambda _: bm.gat_layer_leg(
+            g, dev, kernel, gather_peak, sample, cpu=want), collective=False)
+        legs.run("sage", lambda: None, lambda _: bm.sage_leg(
+            g, dev, kernel, gather_peak, algorithmic_bytes, sample, cpu=want),
+            collective=False)
+        _release(dev)
+        legs.run("gat_pubmed", lambda: None, lambda _: bm.gat_pubmed_leg(
+            dev, kernel, gather_peak, cpu=want), collective=False)
+        legs.run("rgcn", lambda: None, lambda _: bm.rgcn_leg(
+            dev, kernel, gather_peak, cpu=want), collective=False)
+    sample = h_cpu = None
     if not args.no_rmat_leg and args.workload == "reddit" and args.emulate_world <= 1:
         # release the headline leg before the 1.07B-edge graph
         step = g = h = adj = pg = h_local = None  # noqa: F841
-        import gc
-        gc.collect()
-        if dev.type == "cuda":
-            torch.cuda.empty_cache()
-        key = "rmat%d" % args.rmat_scale
-        if not dist.is_initialized():
-            try:
-                result[key] = rmat_leg(args, world, rank, dev, rmat_pmc)
-            except (RuntimeError, MemoryError, dgl.DGLError) as err:
-                result[key] = {"error": repr(err)}
-        else:  # collectives: a failing rank must end the job, not leave peers waiting
-            result[key] = rmat_leg(args, world, rank, dev)
+        _release(dev)
+        legs.run("rmat%d" % args.rmat_scale, lambda: rmat_setup(args, rank, dev),
+                 lambda st: rmat_run(args, world, rank, dev, st, rmat_pmc))
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if dist.is_initialized():
+    if distributed:
+        if legs.failed is not None:
+            # a collective may be half-done: leave without the group's teardown
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _release(dev):
+    import gc
+    gc.collect()
+    if dev.type == "cuda":
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,472 @@
+"""bench.py's model legs (BASELINE.json configs[2]-[4] at N = 1): each a
+training step of one §8(f) model through the engine, timed like the headline
+(warm-up, then K steps between two synchronises), with
+
+* ``kernel_ms``: the library's own launches per step (hipEvent pairs around
+  every g-SpMM / g-SDDMM / GAT / typed-block launch on its stream);
+* ``roofline``: the step's dominant engine kernel alone (its algorithmic
+  bytes per call over its mean duration, events on the launch stream)
+  against the ceiling of its regime (bench.gather_peak);
+* ``cpu_baseline``: the reference's formulation of the same step on the host
+  cores (this engine's host path, kind "port", core count stated), on the
+  same model or a bounded sample of the same graph.
+
+The reference times these loops itself: gat/train.py:216-235 (epoch),
+rgcn/link_predict.py:163-174 (forward + backward + Adam), and (the mean
+reducer as a UDF: the reference has no builtin mean) degree_bucketing.py.
+"""
+from __future__ import absolute_import
+
+import importlib.util
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+_EXAMPLES = {}
+
+
+def example(relpath):
+    """An example script imported by path (once)."""
+    if relpath not in _EXAMPLES:
+        name = "bench_ex_" + relpath.replace("/", "_").replace(".py", "")
+        spec = importlib.util.spec_from_file_location(name, os.path.join(ROOT, "examples",
+                                                                         relpath))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _EXAMPLES[relpath] = mod
+    return _EXAMPLES[relpath]
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
+def wall_steps(step, steps, warmup, dev, kernel):
+    """(wall ms per step, library kernel ms per step) over ``steps`` steps
+    after ``warmup``; kernel ms from the library's per-launch events."""
+    for _ in range(warmup):
+        step()
+    _sync(dev)
+    kernel.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    _sync(dev)
+    el = time.perf_counter() - t0
+    kms, launches = kernel.timing_read()
+    kernel.timing_enable(False)
+    return el / steps * 1e3, kms / steps, launches // max(steps, 1)
+
+
+def call_ms(fn, iters, dev):
+    """Mean GPU span of ``fn`` (events on the current stream, which the
+    library launches on), after one untimed call."""
+    fn()
+    _sync(dev)
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def _threads():
+    return torch.get_num_threads()
+
+
+def roof(bytes_, ms, peak, source, kernel_name, **extra):
+    ach = bytes_ / (ms * 1e-3) / 1e9 if ms > 0 else None
+    r = {"bound": "hbm", "achieved": ach, "peak": peak, "unit": "GB/s",
+         "frac": None if ach is None else ach / peak, "kernel": kernel_name,
+         "kernel_ms": ms, "bytes_per_call": bytes_, "peak_source": source}
+    r.update(extra)
+    return r
+
+
+# -- GAT layer on the Reddit-shaped graph: 8 heads x 16 ------------------------
+def gat_fwd_bytes(E, n, H, D, stored):
+    """Fused GAT forward (kernel.gat_aggregate): per edge the gathered feature
+    row, its column id, the source's H logits and (training) the H stored
+    attention values; per row the output row, its H normalisers, H logits and
+    its indptr entry."""
+    F_ = H * D
+    return E * (4 * F_ + 4 + 4 * H + (4 * H if stored else 0)) + n * (4 * F_ + 8 * H + 8)
+
+
+def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, D=16,
+                  cpu=True):
+    """One GAT layer's aggregation, forward + backward, on the bench graph
+    (attention, its per-head weighted sum and the copy_edge normaliser: the
+    message passing of gat/train.py:61-96) with random features."""
+    adj = g.sparse_adjacency(dev)
+    n, E = g.number_of_nodes(), g.number_of_edges()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(5)
+    ft = (torch.rand(n, H, D, generator=gen, device=dev) * 2 - 1).requires_grad_(True)
+    el = (torch.rand(n, H, generator=gen, device=dev) - 0.5).requires_grad_(True)
+    er = (torch.rand(n, H, generator=gen, device=dev) - 0.5).requires_grad_(True)
+    gout = torch.rand(n, H, D, generator=gen, device=dev)
+    gz = torch.rand(n, H, 1, generator=gen, device=dev)
+
+    def step():
+        fs, z = kernel.gat_aggregate(adj, ft, el, er)
+        torch.autograd.backward([fs, z], [gout, gz])
+        ft.grad = el.grad = er.grad = None
+    ms, kms, launches = wall_steps(step, steps, warmup, dev, kernel)
+
+    def fwd():
+        kernel.gat_aggregate(adj, ft, el, er)  # training forward: attention stored
+    fms = call_ms(fwd, steps, dev)
+    cuts = kernel._block_cuts(adj.fwd, H * D * 4)
+    peak, src = gather_peak(n * H * D * 4, 0 if cuts is None else len(cuts) - 1)
+    res = {"value": E / (ms * 1e-3), "unit": "edges/s (fwd+bwd)", "ms_per_step": ms,
+           "kernel_ms": kms, "launches_per_step": launches, "steps": steps, "warmup": warmup,
+           "config": "GAT layer aggregation, %d heads x %d, on the headline graph (%d nodes, "
+                     "%d edges): kernel.gat_aggregate forward + backward, dropout 0"
+                     % (H, D, n, E),
+           "roofline": roof(gat_fwd_bytes(E, n, H, D, True), fms, peak, src,
+                            "fused GAT forward (dglhip_gat_aggregate_device, attention "
+                            "stored for the backward)"),
+           "cpu_baseline": None}
+    if cpu and sample is not None:
+        res["cpu_baseline"] = gat_layer_cpu(sample, n, H, D)
+    return res
+
+
+def _edge_attention(edges):
+    # gat/train.py:90-96 (the reference's edge UDF), dropout 0
+    a = F.leaky_relu(edges.src["a1"] + edges.dst["a2"], 0.2)
+    a = torch.exp(a).clamp(-10, 10)
+    return {"a": a, "a_drop": a}
+
+
+def gat_layer_cpu(sample, n, H, D, target_edges=1_000_000):
+    """The reference's layer on the host: the edge UDF for the attention,
+    then update_all([src_mul_edge, copy_edge], [sum, sum]) and the division
+    (gat/train.py:74-96), forward + backward, on the in-edges of the first
+    rows of the headline's CPU sample (about ``target_edges``)."""
+    import dgl
+    import dgl.function as fn
+    rows, d, s = sample
+    cum = torch.cumsum(torch.bincount(d, minlength=rows), 0)
+    r1 = min(int(torch.searchsorted(cum, torch.tensor(target_edges))) + 1, rows)
+    sel = d < r1
+    d, s = d[sel], s[sel]
+    # sources keep their ids in the full table; rows are the first r1 nodes
+    g = dgl.DGLGraph((s, d))
+    if g.number_of_nodes() < n:
+        g.add_nodes(n - g.number_of_nodes())
+    gen = torch.Generator().manual_seed(6)
+    ft = (torch.rand(n, H, D, generator=gen) * 2 - 1).requires_grad_(True)
+    a1 = (torch.rand(n, H, 1, generator=gen) - 0.5).requires_grad_(True)
+    a2 = (torch.rand(n, H, 1, generator=gen) - 0.5).requires_grad_(True)
+
+    def once():
+        g.ndata.update({"ft": ft, "a1": a1, "a2": a2})
+        g.apply_edges(_edge_attention)
+        g.update_all([fn.src_mul_edge("ft", "a_drop", "ft"), fn.copy_edge("a", "a")],
+                     [fn.sum("ft", "ft"), fn.sum("a", "z")])
+        out = g.ndata["ft"] / g.ndata["z"].clamp(min=1e-30)
+        out[:r1].sum().backward()
+    once()  # builds the host CSRs
+    reps, t = 0, 0.0
+    while reps < 2:
+        t0 = time.perf_counter()
+        once()
+        t += time.perf_counter() - t0
+        reps += 1
+    e = int(s.numel())
+    return {"value": e * reps / t, "unit": "edges/s (fwd+bwd)", "cores": _threads(),
+            "kind": "port",
+            "sample": "the reference's GAT layer (edge UDF attention + src_mul_edge/copy_edge "
+                      "sums, gat/train.py:74-96) through this engine's host path, forward + "
+                      "backward, on the in-edges of the first %d rows of the headline graph "
+                      "(%d edges, sources over all %d nodes), %d heads x %d, %d reps, "
+                      "torch %d threads" % (r1, e, n, H, D, reps, _threads())}
+
+
+# -- GAT on Pubmed (configs[2]) ----------------------------------------------
+def gat_pubmed_leg(dev, kernel, gather_peak, epochs=20, warmup=3, cpu=True):
+    """configs[2]: the example's GAT (8 heads x 8 hidden, 8 output heads,
+    fused layer aggregation) on the Pubmed-shaped dataset, one epoch =
+    forward + cross-entropy + backward + Adam; eager and as one replayed HIP
+    graph (gat/train.py --hip-graph)."""
+    from dgl import DGLGraph
+    from dgl.data import load_data
+    gat = example("gat/train.py")
+    data = load_data("pubmed", seed=0, device=dev)
+    src, dst = data.graph
+    g = DGLGraph((src.cpu(), dst.cpu()))
+    g.add_edges(g.nodes(), g.nodes())
+    E, n = g.number_of_edges(), g.number_of_nodes()
+
+    def build(device, udf=False, capturable=False):
+        torch.manual_seed(0)
+        m = gat.GAT(g, 1, data.features.shape[1], 8, data.num_labels, [8, 8], F.elu, 0.6, 0.6,
+                    0.2, False, udf).to(device)
+        return m, torch.optim.Adam(m.parameters(), lr=0.005, weight_decay=5e-4,
+                                   capturable=capturable)
+    model, opt = build(dev)
+    model.train()
+    feats, labels = data.features, data.labels
+    mask = data.train_mask.nonzero(as_tuple=True)[0]
+    lab = labels[mask]
+
+    def epoch():
+        opt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(model(feats).index_select(0, mask), lab)
+        loss.backward()
+        opt.step()
+    ms, kms, launches = wall_steps(epoch, epochs, warmup, dev, kernel)
+    # the same epoch captured once and replayed (the example's --hip-graph)
+    gmodel, gopt = build(dev, capturable=True)
+    gmodel.train()
+
+    def gepoch():
+        gopt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(gmodel(feats).index_select(0, mask), lab)
+        loss.backward()
+        gopt.step()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            gepoch()
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    gopt.zero_grad(set_to_none=True)
+    with torch.cuda.graph(graph, stream=side):
+        gepoch()
+    gms = call_ms(graph.replay, epochs, dev)
+    # the dominant engine kernel: the first layer's fused aggregation forward
+    layer = model.layers[0]
+    with torch.no_grad():
+        ft = layer.fc(feats).reshape(n, 8, -1)
+        hf = ft.transpose(0, 1)
+        a1 = torch.bmm(hf, layer.attn_l).transpose(0, 1).contiguous()
+        a2 = torch.bmm(hf, layer.attn_r).transpose(0, 1).contiguous()
+    ft, a1, a2 = ft.requires_grad_(True), a1.requires_grad_(True), a2.requires_grad_(True)
+    adj = g.sparse_adjacency(dev)
+    fms = call_ms(lambda: kernel.gat_aggregate(adj, ft, a1, a2, attn_drop=0.6), epochs, dev)
+    D = ft.shape[2]
+    peak, src_ = gather_peak(n * 8 * D * 4, 0)
+    res = {"value": 1e3 / gms, "unit": "epochs/s (HIP graph)", "ms_per_epoch": ms,
+           "ms_per_epoch_hip_graph": gms, "kernel_ms": kms, "launches_per_epoch": launches,
+           "epochs": epochs, "warmup": warmup,
+           "config": "configs[2]: GAT 8 heads x 8 hidden + 8 output heads on the Pubmed-shaped "
+                     "dataset (%d nodes, %d edges incl. self-loops, 500 features, 3 classes), "
+                     "dropout 0.6, Adam; eager and one replayed HIP graph per epoch" % (n, E),
+           "roofline": roof(gat_fwd_bytes(E, n, 8, D, True) + E * 4 * 8, fms, peak, src_,
+                            "fused GAT forward of layer 1 (attention dropout 0.6: the "
+                            "attention and its dropped copy stored)",
+                            regime="launch-bound: %.1f MB per call" %
+                                   ((gat_fwd_bytes(E, n, 8, D, True) + E * 32) / 1e6)),
+           "reference_v100_ms_per_epoch": 30.2,
+           "cpu_baseline": None}
+    if cpu:
+        res["cpu_baseline"] = gat_pubmed_cpu(build, feats.cpu(), labels.cpu(), mask.cpu())
+    return res
+
+
+def gat_pubmed_cpu(build, feats, labels, mask, epochs=3):
+    model, opt = build(torch.device("cpu"), udf=True)
+    model.train()
+    lab = labels[mask]
+
+    def epoch():
+        opt.zero_grad(set_to_none=True)
+        loss = F.cross_entropy(model(feats).index_select(0, mask), lab)
+        loss.backward()
+        opt.step()
+    epoch()
+    t0 = time.perf_counter()
+    for _ in range(epochs):
+        epoch()
+    ms = (time.perf_counter() - t0) / epochs * 1e3
+    return {"value": 1e3 / ms, "unit": "epochs/s", "ms_per_epoch": ms, "cores": _threads(),
+            "kind": "port",
+            "sample": "the whole configs[2] epoch with the reference's edge UDF attention "
+                      "(examples/gat/train.py --udf, gat/train.py:74-96) through this engine's "
+                      "host path, %d epochs, torch %d threads" % (epochs, _threads())}
+
+
+# -- R-GCN link prediction (configs[4]) ----------------------------------------
+def rgcn_leg(dev, kernel, gather_peak, steps=20, warmup=3, cpu=True):
+    """configs[4]: the example's R-GCN link-prediction step (2 block layers,
+    500 hidden, 100 bases of 5 x 5, DistMult, Adam) on 30,000-edge samples of
+    the FB15k-237-shaped KG; timed as the reference times it (forward +
+    backward + clip + Adam, link_predict.py:163-171), sampled graphs built
+    outside the timer."""
+    import tools.rgcn_step as rs
+    args = rs.lp.parser().parse_args([])
+    raw = rs.make_samples(args, warmup + steps)
+    samples = [rs.to_dev(s, dev) for s in raw]
+    model, opt = rs.build_model(args, dev)
+    model.train()
+    graphs = []
+    for s in samples:
+        uniq, src, dst = s[0], s[1], s[2]
+        from dgl import DGLGraph
+        gg = DGLGraph((src, dst), multigraph=True)
+        if gg.number_of_nodes() < len(uniq):
+            gg.add_nodes(len(uniq) - gg.number_of_nodes())
+        graphs.append(gg)
+    it = iter(range(warmup + steps))
+
+    def step():
+        i = next(it)
+        uniq, _, _, rel, norm, smp, lab = samples[i]
+        h = model(graphs[i], uniq, rel, norm)
+        loss = model.loss(h, smp, lab)
+        opt.zero_grad()
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(model.parameters(), args.grad_norm)
+        opt.step()
+    ms, kms, launches = wall_steps(step, steps, warmup, dev, kernel)
+    kt = rs.kernel_times(model, samples[-1], dev)
+    E = int(samples[0][1].numel())
+    peak, src_ = gather_peak(len(raw[0][0]) * 500 * 4, 0)
+    res = {"value": 1e3 / ms, "unit": "steps/s", "ms_per_step": ms, "kernel_ms": kms,
+           "launches_per_step": launches, "steps": steps, "warmup": warmup,
+           "config": "configs[4]: R-GCN link prediction, FB15k-237-shaped synthetic KG (14,541 "
+                     "entities, 237 relations x 2 directions, 272,115 triples), %d-edge sampled "
+                     "graph per step, 2 block layers of 100 bases 5x5 (500 hidden), DistMult, "
+                     "Adam; graph sampling and DGLGraph build outside the timer (the "
+                     "reference's)" % E,
+           "typed_block_kernels": kt,
+           "roofline": roof(kt["forward"]["bytes"], kt["forward"]["ms"], peak, src_,
+                            "typed_block_spmm forward (chunked items + combine)",
+                            regime="latency-bound: %.0f MB per call over %d rows"
+                                   % (kt["forward"]["bytes"] / 1e6, kt["rows"])),
+           "reference_v100_ms_per_step": 633.0,
+           "cpu_baseline": None}
+    if cpu:
+        res["cpu_baseline"] = rgcn_cpu(rs, raw[:3])
+    return res
+
+
+def rgcn_cpu(rs, raw):
+    args = rs.lp.parser().parse_args(["--udf"])
+    dev = torch.device("cpu")
+    model, opt = rs.build_model(args, dev)
+    model.train()
+    samples = [rs.to_dev(s, dev) for s in raw]
+    rs.one_step(model, opt, samples[0], args)
+    t0 = time.perf_counter()
+    for s in samples[1:]:
+        rs.one_step(model, opt, s, args)
+    ms = (time.perf_counter() - t0) / (len(samples) - 1) * 1e3
+    return {"value": 1e3 / ms, "unit": "steps/s", "ms_per_step": ms, "cores": _threads(),
+            "kind": "port",
+            "sample": "the same step with the reference's formulation (edge UDF gather + bmm "
+                      "into an E x 500 message tensor, builtin sum, rgcn/layers.py:121-132; "
+                      "link_predict.py --udf) through this engine's host path, %d steps on the "
+                      "same samples, torch %d threads" % (len(samples) - 1, _threads())}
+
+
+# -- GraphSAGE-mean epoch on the Reddit-shaped graph ---------------------------
+def sage_leg(g, dev, kernel, gather_peak, algorithmic_bytes, sample, epochs=10, warmup=3,
+             cpu=True):
+    """configs[3]'s model (GraphSAGE-mean, 602 -> 128 -> 41, examples/
+    graphsage/train.py) for one full-graph epoch (forward + loss + backward +
+    Adam) on the bench's Reddit-shaped graph, random 602-wide features, 41
+    classes, 66 % training nodes."""
+    import dgl.function as fn
+    from dgl.nn.pytorch import weighted_cross_entropy
+    sage = example("graphsage/train.py")
+    n, E = g.number_of_nodes(), g.number_of_edges()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    feats = 0.1 * torch.randn(n, 602, generator=gen, device=dev)
+    labels = torch.randint(0, 41, (n,), generator=gen, device=dev)
+    train_w = (torch.rand(n, generator=gen, device=dev) < 0.66).float()
+    ntrain = float(train_w.sum())
+
+    def aggregate(h):
+        g.ndata["h"] = h
+        g.update_all(fn.copy_src("h", "m"), fn.mean("m", "neigh"))
+        return g.ndata.pop("neigh")
+    aggregate.add_into = lambda h, out: kernel.gspmm_mean_add(g.sparse_adjacency(h.device),
+                                                              h, out)
+    torch.manual_seed(0)
+    model = sage.SAGE(602, 128, 41, 1, 0.0).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+    model.train()
+
+    def epoch():
+        logits = model(feats, aggregate)
+        loss = weighted_cross_entropy(logits, labels, train_w) * (1.0 / ntrain)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    ms, kms, launches = wall_steps(epoch, epochs, warmup, dev, kernel)
+    h = torch.rand(n, 128, generator=gen, device=dev)
+    adj = g.sparse_adjacency(dev)
+    ams = call_ms(lambda: kernel.gspmm(adj, "copy_u", "mean", h), epochs, dev)
+    blocks = kernel.blocked_schedule(adj, h)
+    peak, src_ = gather_peak(n * 128 * 4, blocks)
+    res = {"value": 1e3 / ms, "unit": "epochs/s", "ms_per_epoch": ms, "kernel_ms": kms,
+           "launches_per_epoch": launches, "epochs": epochs, "warmup": warmup,
+           "config": "configs[3]'s model (GraphSAGE-mean 602-128-41, fc_neigh ahead of the "
+                     "mean, NodeLinear, fused loss; examples/graphsage/train.py) for one "
+                     "full-graph epoch on the headline graph (%d nodes, %d edges), 66 %% "
+                     "training nodes, Adam" % (n, E),
+           "roofline": roof(algorithmic_bytes(E, n, 128), ams, peak, src_,
+                            "g-SpMM copy_u + mean, F = 128 (one layer's aggregation; %d "
+                            "launches per call)" % max(blocks, 1)),
+           "cpu_baseline": None}
+    if cpu and sample is not None:
+        res["cpu_baseline"] = mean_bucketing_cpu(sample, n)
+    return res
+
+
+def mean_bucketing_cpu(sample, n, F_=128, target_edges=2_000_000):
+    """The reference's mean aggregation on the host: no builtin mean exists
+    (function/reducer.py: sum, max), so ``lambda nodes: mailbox.mean(1)``
+    runs under degree bucketing (runtime/degree_bucketing.py:13-84: rows
+    grouped by in-degree, each bucket's messages gathered into (rows, deg,
+    F) and reduced, the buckets merged by row id) — restated here with torch
+    on a sample of the headline graph (the in-edges of its first rows)."""
+    rows, d, s = sample
+    cum = torch.cumsum(torch.bincount(d, minlength=rows), 0)
+    r1 = min(int(torch.searchsorted(cum, torch.tensor(target_edges))) + 1, rows)
+    sel = d < r1
+    d, s = d[sel], s[sel]
+    e = int(s.numel())
+    h = torch.rand(n, F_, generator=torch.Generator().manual_seed(8))
+    order = torch.sort(d, stable=True)[1]  # mailbox order: edge order within a row
+    d, s = d[order], s[order]
+
+    def once():
+        deg = torch.bincount(d, minlength=r1)
+        starts = torch.zeros(r1 + 1, dtype=torch.int64)
+        torch.cumsum(deg, 0, out=starts[1:])
+        out = torch.zeros(r1, F_)
+        for k in torch.unique(deg[deg > 0]).tolist():
+            vb = torch.nonzero(deg == k).squeeze(1)
+            mids = (starts[vb].unsqueeze(1) + torch.arange(k)).reshape(-1)
+            mail = h.index_select(0, s.index_select(0, mids)).view(-1, k, F_)
+            out[vb] = mail.mean(1)
+        return out
+    once()
+    reps, t = 0, 0.0
+    while reps < 2:
+        t0 = time.perf_counter()
+        once()
+        t += time.perf_counter() - t0
+        reps += 1
+    return {"value": e * reps / t, "unit": "edges/s (mean aggregation)", "cores": _threads(),
+            "kind": "port",
+            "sample": "degree-bucketing mean (the reference's UDF route for mean, "
+                      "degree_bucketing.py:13-84) restated with torch, on the in-edges of the "
+                      "first %d rows of the headline graph (%d edges, F = %d), %d reps, torch "
+                      "%d threads; GPU comparison: roofline.kernel_ms is one such aggregation "
+                      "over the whole graph" % (r1, e, F_, reps, _threads())}

@@ -86,3 +86,87 @@ def test_bench_two_ranks_without_outer_launcher():
     # the two ranks' rmat partitions cover the graph's edges
     assert sum(x["bytes_per_step"] for x in rm["roofline"]["per_rank"]) >= \
         bench.algorithmic_bytes(1 << 16, 0, bench.FEAT)
+
+
+def _bench_env(**extra):
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+              "DGLHIP_BENCH_FAIL"):
+        env.pop(k, None)
+    env.update(extra)
+    return env
+
+
+_SMALL = ["--gpus", "2", "--device", "cpu", "--graph-scale", "0.002", "--rmat-scale", "12",
+          "--steps", "2", "--warmup", "1", "--cpu-sample-edges", "20000"]
+
+
+def _line(stdout):
+    lines = [l for l in stdout.decode().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    return json.loads(lines[0])
+
+
+def test_rank1_setup_failure_in_rmat_leg_keeps_the_line():
+    """A failure in rank 1's setup of the rmat leg (injected): every rank
+    skips the leg together, rank 0 prints the headline line with the leg's
+    error, and the job exits 0 promptly (no collective left waiting)."""
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + _SMALL +
+                       ["--dist-timeout", "60", "--leg-deadline", "40"],
+                       env=_bench_env(DGLHIP_BENCH_FAIL="rmat12:1"), stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=120)
+    assert p.returncode == 0, p.stderr.decode()[-3000:]
+    r = _line(p.stdout)
+    assert r["value"] > 0 and r["n_gpus"] == 2
+    assert "rank 1 (setup)" in r["rmat12"]["error"] and "injected" in r["rmat12"]["error"]
+    assert r["train_step"]["value"] > 0 and r["strong"]["value"] > 0
+
+
+def test_rank1_failure_inside_a_collective_leg_is_bounded():
+    """Rank 1 fails inside the train_step leg's run phase, so rank 0 waits in
+    a collective rank 1 never joins: rank 0's leg deadline prints the line
+    (headline intact, the leg's error) well within the collective timeout."""
+    import time
+    t0 = time.time()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + _SMALL +
+                       ["--dist-timeout", "60", "--leg-deadline", "15"],
+                       env=_bench_env(DGLHIP_BENCH_FAIL="train_step:1:run"),
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=180)
+    took = time.time() - t0
+    r = _line(p.stdout)
+    assert r["value"] > 0 and r["halo_exchange"]["mode"] in ("allgather", "alltoall")
+    assert "still running after 15 s" in r["train_step"]["error"]
+    assert took < 100
+
+
+def test_relay_sigterm_kills_every_rank():
+    """SIGTERM to the launching parent (the driver's kill) takes the torchrun
+    child and every rank down with it: no descendant survives."""
+    import signal
+    import time
+    psutil = pytest.importorskip("psutil")
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--device", "cpu", "--graph-scale", "0.002", "--steps", "100000",
+                          "--warmup", "1", "--no-rmat-leg", "--no-cpu-baseline"],
+                         env=_bench_env(), stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        parent = psutil.Process(p.pid)
+        kids = []
+        t0 = time.time()
+        while time.time() - t0 < 120:  # the agent and both ranks are up
+            kids = parent.children(recursive=True)
+            if sum("bench.py" in " ".join(k.cmdline()) for k in kids
+                   if k.is_running()) >= 3:
+                break
+            time.sleep(0.5)
+        assert len(kids) >= 3
+        time.sleep(3)  # the ranks are past their imports
+        p.send_signal(signal.SIGTERM)
+        rc = p.wait(timeout=60)
+        assert rc == 128 + signal.SIGTERM
+        gone, alive = psutil.wait_procs(kids, timeout=30)
+        assert not alive, [k.pid for k in alive]
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()

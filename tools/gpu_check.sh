@@ -35,6 +35,10 @@ for s in $STEPS; do
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       rc=$?; tail -3 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
+    benchquick)
+      # the default line's legs without the PMC passes and the RMAT leg
+      timeout -k 10 600 python bench.py --no-traffic --no-rmat-leg ${BENCH_ARGS:-} > gpurun_out/benchquick.json 2> gpurun_out/benchquick.err
+      rc=$?; tail -12 gpurun_out/benchquick.err; [ $rc -eq 0 ] || exit $rc ;;
     bench)
       timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       rc=$?; tail -5 gpurun_out/bench.err; cat gpurun_out/bench.json; [ $rc -eq 0 ] || exit $rc ;;
