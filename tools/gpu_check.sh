@@ -92,6 +92,24 @@ for s in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/rgcnprof -o run \
         --output-format csv -- python tools/rgcn_step.py --steps 20 > gpurun_out/rgcnprof.log 2>&1
       rc=$?; tail -2 gpurun_out/rgcnprof.log; [ $rc -eq 0 ] || exit $rc ;;
+    l2split)
+      # the headline's L2 hits / misses and EA requests per block launch (tools/l2_split.py)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -s KILL 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/l2a -o run \
+        --output-format csv -- python tools/l2_split.py run --out gpurun_out/l2_plan.json > gpurun_out/l2a.log 2>&1 &&
+      timeout -s KILL 180 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d gpurun_out/l2b -o run \
+        --output-format csv -- python tools/l2_split.py run --out gpurun_out/l2_plan.json > gpurun_out/l2b.log 2>&1 &&
+      python tools/l2_split.py parse gpurun_out/l2_plan.json gpurun_out/l2a/run_counter_collection.csv \
+        --out gpurun_out/l2_split_hits.json > /dev/null &&
+      python tools/l2_split.py parse gpurun_out/l2_plan.json gpurun_out/l2b/run_counter_collection.csv \
+        --out gpurun_out/l2_split_ea.json > /dev/null
+      rc=$?; tail -2 gpurun_out/l2b.log; [ $rc -eq 0 ] || exit $rc ;;
+    gatprof)
+      # GAT 8 x 16 forward + backward on the Reddit-shaped graph: kernel statistics
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/gatprof -o run \
+        --output-format csv -- python tools/gat_bench.py --fwd-bwd-only --iters 10 > gpurun_out/gatprof.log 2>&1
+      rc=$?; tail -2 gpurun_out/gatprof.log; [ $rc -eq 0 ] || exit $rc ;;
     sageprof)
       # kernel statistics of GraphSAGE-mean full-graph epochs on RMAT-$RMAT_SCALE (configs[3])
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/sageprof -o run \
