@@ -345,6 +345,153 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused GAT backward over the transpose (r04), 8 heads x 16 features.
+//
+// The backward of gat_aggregate needs, per edge u -> v (a forward slot kf of
+// row v, a transposed slot of row u):
+//   a  = clamp(exp(leaky_relu(el[u] + er[v])))        (the forward's attention)
+//   w  = keep(kf) ? a * scale : 0                      (its dropped copy)
+//   d_ft[u] += w * dout[v]                            (u_mul_e over the transpose)
+//   t  = <dout[v, h], ft[u, h]>                        (the g-SDDMM dot)
+//   g  = epilogue(t, a, keep, dz[v])                   (gat_epi_pre's operations)
+//   d_el[u] += g  (copy_e over the transpose)    d_er[v] += g  (copy_e over the CSR)
+// r03 ran it as three passes: the attention gradient over the CSR (storing g),
+// d_ft over the transpose (reading w through the slot map: a 128-B line per
+// 32-B value) and d_el over the transpose (g through the slot map), with a
+// and w stored by the forward. Here ONE pass over the transpose, one wave per
+// row u, computes d_ft and d_el (their chains in the transpose's slot order,
+// as before) and every g, stored at its forward slot for d_er's sum (a
+// sequential copy_e pass over the CSR). a and w are recomputed from el, er
+// and the dropout hash of the forward slot (the forward's expressions, so
+// the same bits), so the forward stores no E x H tensor.
+//
+// The dot keeps the sliced g-SDDMM's association (gsddmm_dot_sliced_kernel,
+// D = 16: four lanes of 4 features per head, partials p_r = fma chains over
+// features 4r..4r+3 starting with a product, total (p0 + p2) + (p1 + p3)):
+// here lane 2m holds features 4m, 4m+1 and lane 2m+1 features 4m+2, 4m+3; the
+// even lane's half chain continues on the odd lane (DPP), and the partials of
+// lanes 8h+1, 8h+3, 8h+5, 8h+7 combine by xor 4 then xor 2. The per-(slot,
+// head) attention and keep bit are computed once per batch of 16 slots (two
+// pairs per lane) and shared through LDS, as the forward's LDS kernel does.
+//
+// Items: as dglhip_gspmm_items_device (the transposed CSR's source-blocked
+// plan: item i = row item_row[i], slots [item_beg[i], item_end[i]) of cols /
+// fslot, accumulate continuing both chains), or whole rows (by_row: item i is
+// row item_row[i] with slots [item_beg[row], item_end[row])).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float dpp_even_to_odd(float v) {
+  // quad_perm [0, 0, 2, 2]: lane 2m+1 reads lane 2m
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xA0, 0xF, 0xF, false));
+}
+
+template <bool DROP, bool SMALL>
+__global__ __launch_bounds__(256) void gat_backward_t_kernel(
+    int64_t num_items, const int32_t* __restrict__ item_row, const int64_t* __restrict__ item_beg,
+    const int64_t* __restrict__ item_end, int by_row, int accumulate,
+    const int32_t* __restrict__ cols, const int64_t* __restrict__ fslot,
+    const float* __restrict__ ft, const float* __restrict__ el, const float* __restrict__ er,
+    const float* __restrict__ dz, const float* __restrict__ dout, float alpha, float lo,
+    float hi, int apply_exp, uint64_t seed0, const int64_t* __restrict__ seed_off, uint32_t thr,
+    float scale, float* __restrict__ d_ft, float* __restrict__ d_el, float* __restrict__ g_out,
+    int64_t table_bytes) {
+  constexpr int H = 8, F = 128, U = 16;
+  typedef Vec<2>::T V;
+  __shared__ float s_a[4][H * U];
+  __shared__ float s_w[4][H * U];
+  __shared__ float s_k[4][DROP ? H * U : 1];
+  __shared__ float s_z[4][H * U];
+  const int lane = threadIdx.x & 63;
+  const int wi = threadIdx.x >> 6;
+  const int64_t it = block_linear() * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_items) return;
+  int64_t row = item_row ? item_row[it] : it;
+  row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+  const int64_t ix = by_row ? row : it;
+  const int64_t beg = item_beg[ix], end = item_end[ix];
+  if (accumulate && beg == end) return;
+  const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
+  const GatTable tab = gat_table(dout, SMALL ? table_bytes : 0);
+  const int64_t f0 = int64_t(lane) * 2;
+  const int h = lane >> 3;              // this lane's head (16 features = 8 lanes)
+  const bool odd = (lane & 1) != 0;
+  const bool head_lane = (lane & 7) == 1;  // holds the head's dot: lane 8h + 1
+  const uint32_t voff = static_cast<uint32_t>(f0 * int64_t(sizeof(float)));
+  // the pairs this lane computes: head hc of slots jc and jc + 8
+  const int hc = lane & 7, jc = lane >> 3;
+  const float elc = el[row * H + hc];
+  const V ftv = ldv<2>(ft + row * F + f0);
+  V acc = accumulate ? ldv<2>(d_ft + row * F + f0) : Vec<2>::zero();
+  float elacc = (accumulate && head_lane) ? d_el[row * H + h] : 0.0f;
+  float* la = s_a[wi];
+  float* lw = s_w[wi];
+  float* lk = s_k[wi];
+  float* lz = s_z[wi];
+  for (int64_t k = beg; k < end; k += U) {
+    const int nb = end - k < U ? static_cast<int>(end - k) : U;
+    V u[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (j < nb) u[j] = gat_gather<2, SMALL>(dout, tab, cols[k + j], F, voff);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = jc + 8 * i;
+      if (j < nb) {
+        const int64_t v = cols[k + j];
+        float x = elc + er[v * H + hc];
+        x = x > 0.0f ? x : alpha * x;
+        if (apply_exp) x = __expf(x);
+        const float a = fminf(fmaxf(x, lo), hi);
+        la[hc * U + j] = a;
+        float w = a;
+        if (DROP) {
+          const bool keep = gat_keep(seed, fslot[k + j] * H + hc, thr);
+          w = keep ? a * scale : 0.0f;
+          lk[hc * U + j] = keep ? 1.0f : 0.0f;
+        }
+        lw[hc * U + j] = w;
+        lz[hc * U + j] = dz ? dz[v * H + hc] : 0.0f;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (j < nb) {
+        const float w = lw[h * U + j];
+        acc = Vec<2>::fma(Vec<2>::splat(w), u[j], acc);
+        // the head's dot in the sliced kernel's association
+        float t = u[j].x * ftv.x;
+        t = __builtin_fmaf(u[j].y, ftv.y, t);
+        const float tin = dpp_even_to_odd(t);
+        float p = __builtin_fmaf(u[j].x, ftv.x, tin);
+        p = __builtin_fmaf(u[j].y, ftv.y, p);
+        p = odd ? p : 0.0f;
+        const float s2 = p + __shfl_xor(p, 4, 64);
+        const float dot = s2 + __shfl_xor(s2, 2, 64);
+        if (head_lane) {
+          const float a = la[h * U + j];
+          float tt = dot;
+          if (DROP) tt = lk[h * U + j] != 0.0f ? tt * scale : 0.0f;
+          if (dz) tt = tt + lz[h * U + j];
+          float g = apply_exp ? (tt * a) * (a < 1.0f ? alpha : 1.0f)
+                              : tt * (a < 0.0f ? alpha : 1.0f);
+          g = (a > lo && a < hi) ? g : 0.0f;
+          elacc = elacc + g;
+          g_out[fslot[k + j] * H + h] = g;
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  stv<2>(d_ft + row * F + f0, acc);
+  if (head_lane) d_el[row * H + h] = elacc;
+}
+
 }  // namespace dglhip
 
 using namespace dglhip;
@@ -458,6 +605,54 @@ int dglhip_gat_aggregate_device(int64_t num_rows, int64_t num_src, int64_t num_h
       num_rows, num_src, num_heads, head_dim, indptr, indptr ? indptr + 1 : nullptr, 0, indices,
       row_order, el, er, ft, alpha, clamp_lo, clamp_hi, apply_exp, drop_p, seed, seed_offset,
       out_ft, out_z, attn_out, attn_drop_out, stream);
+}
+
+int dglhip_gat_backward_t_ok(int64_t num_heads, int64_t head_dim) {
+  return num_heads == 8 && head_dim == 16 ? 1 : 0;
+}
+
+int dglhip_gat_backward_t_device(
+    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+    int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
+    int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
+    const float* er, const float* dz, const float* dout, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
+    float* d_ft, float* d_el, float* grad, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(dglhip_gat_backward_t_ok(num_heads, head_dim) == 1,
+               "the transposed GAT backward runs 8 heads x 16 features, got " << num_heads
+               << " x " << head_dim);
+  DGLHIP_CHECK(num_items >= 0 && num_rows >= 0 && num_src >= 0, "bad sizes");
+  DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
+  if (num_items == 0) return 0;
+  DGLHIP_CHECK(item_beg && item_end && cols && fslot && ft && el && er && dout && d_ft && d_el &&
+               grad, "null pointer argument");
+  DGLHIP_CHECK(reinterpret_cast<uintptr_t>(ft) % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(dout) % 8 == 0 &&
+               reinterpret_cast<uintptr_t>(d_ft) % 8 == 0, "rows must be 8-B aligned");
+  const int64_t blocks = (num_items + 3) / 4;
+  DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large");
+  const bool drop = drop_p > 0.0f;
+  const uint32_t thr = drop ? gat_drop_threshold(drop_p) : 0u;
+  const float scale = drop ? 1.0f / (1.0f - drop_p) : 1.0f;
+  // dout is gathered by destination v: num_rows rows of the forward CSR
+  const int64_t tbytes = num_rows * num_heads * head_dim * int64_t(sizeof(float));
+  const bool small = tbytes < (int64_t(1) << 31);
+  timed_launch(stream, [&] {
+#define DGLHIP_GBT(DD, SM)                                                                    \
+  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM>), grid_1d(blocks), dim3(256), 0, stream,   \
+                     num_items, item_row, item_beg, item_end, by_row, accumulate, cols, fslot, \
+                     ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp, seed,         \
+                     seed_offset, thr, scale, d_ft, d_el, grad, tbytes)
+    if (drop) {
+      if (small) DGLHIP_GBT(true, true); else DGLHIP_GBT(true, false);
+    } else {
+      if (small) DGLHIP_GBT(false, true); else DGLHIP_GBT(false, false);
+    }
+#undef DGLHIP_GBT
+  });
+  API_END();
 }
 
 int dglhip_set_gat_variant(int variant) {

@@ -43,6 +43,8 @@ def lib_path():
 _c_i64 = ctypes.c_int64
 _c_int = ctypes.c_int
 _vp = ctypes.c_void_p
+_c_float = ctypes.c_float
+_c_u64 = ctypes.c_uint64
 
 
 def _load():
@@ -65,6 +67,11 @@ def _load():
                                                 _vp, _vp, _c_i64, _vp, _vp]),
         "dglhip_gspmm_ranges_host": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
                                               _vp, _vp, _c_i64, _vp, _c_int]),
+        "dglhip_gat_backward_t_ok": (_c_int, [_c_i64, _c_i64]),
+        "dglhip_gat_backward_t_device": (_c_int, [_c_i64, _vp, _vp, _vp, _c_int, _c_int] +
+                                         [_c_i64] * 4 + [_vp] * 7 +
+                                         [_c_float, _c_float, _c_float, _c_int, _c_float,
+                                          _c_u64, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_typed_block_spmm_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
                                            [_vp] * 9),
         "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),

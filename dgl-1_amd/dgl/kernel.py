@@ -1727,6 +1727,18 @@ def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
 # Fused GAT aggregation: attention + dropout + normaliser + head-broadcast sum
 # ---------------------------------------------------------------------------
 _GAT_SEED = {}
+# the GAT backward: "auto" (the one-pass transposed kernel where it applies,
+# 8 heads x 16) or "three" (r03's three passes, the attention stored)
+_GAT_BWD = os.environ.get("DGLHIP_GAT_BWD", "auto")
+
+
+def set_gat_backward(policy):
+    """Study / test knob for the fused GAT layer's backward: "auto" or
+    "three"; returns the old policy. Same bits either way."""
+    global _GAT_BWD
+    old = _GAT_BWD
+    _GAT_BWD = str(policy)
+    return old
 
 
 def _gat_seed_counter(dev):
@@ -1809,10 +1821,14 @@ class _GATAggregate(torch.autograd.Function):
         # the caller's grad mode decides whether a backward can follow
         need = grad_mode and any(ctx.needs_input_grad[8:11])
         a = w = None
+        # the one-pass backward over the transpose recomputes the attention:
+        # nothing per edge is stored (8 heads x 16, _gat_backward_t)
+        ctx.use_t = (need and dev.type == "cuda" and _GAT_BWD == "auto" and
+                     LIB.dglhip_gat_backward_t_ok(H, D) == 1 and ft2.data_ptr() % 8 == 0)
         if dev.type == "cuda":
             out_ft = torch.empty(fwd.num_rows, F, dtype=torch.float32, device=dev)
             out_z = torch.empty(fwd.num_rows, H, dtype=torch.float32, device=dev)
-            if need:
+            if need and not ctx.use_t:
                 a = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
                 w = torch.empty_like(a) if p > 0 else None
             # source-blocked (exact where the blocks never decrease along a
@@ -1820,7 +1836,8 @@ class _GATAggregate(torch.autograd.Function):
             # stored, smaller blocks (Reddit-shaped 8 x 16: 5.78 ms at 9 MiB
             # vs 6.04 at 11; with the attention stored 6.79 vs 6.78,
             # tools/gat_block_percall.py)
-            cuts = _block_cuts(fwd, (F + H) * 4, None if need else _GAT_BLOCK_BYTES_NOGRAD)
+            cuts = _block_cuts(fwd, (F + H) * 4,
+                               None if a is not None else _GAT_BLOCK_BYTES_NOGRAD)
             if cuts is None:
                 cuts = [fwd.indptr, fwd.indptr[1:]]
             for b in range(len(cuts) - 1):
@@ -1843,11 +1860,21 @@ class _GATAggregate(torch.autograd.Function):
                 a = w = None
         ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp, ctx.p = adj, alpha, lo, hi, \
             apply_exp, p
-        ctx.save_for_backward(ft2, a, w)
+        if ctx.use_t:
+            # the dropout seed as this call used it (a captured call's device
+            # counter moves on at the next call)
+            ctx.seed = int(seed)
+            ctx.seed_off = None if (seed_off is None or p == 0) else seed_off.clone()
+            ctx.D = D
+            ctx.save_for_backward(ft2, el, er)
+        else:
+            ctx.save_for_backward(ft2, a, w)
         return out_ft, out_z
 
     @staticmethod
     def backward(ctx, d_ft, d_z):
+        if ctx.use_t:
+            return _gat_backward_t(ctx, d_ft, d_z)
         ft2, a, w = ctx.saved_tensors
         adj = ctx.adj
         fwd = adj.fwd
@@ -1909,6 +1936,62 @@ class _GATAggregate(torch.autograd.Function):
             if need_er and d_er is None:
                 d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
         return (None,) * 8 + (d_el, d_er, d_ft2, None, None)
+
+
+def _gat_backward_t(ctx, d_ft, d_z):
+    """The GAT layer's backward as ONE pass over the transpose
+    (dglhip_gat_backward_t_device): d_ft and d_el chained in the transpose's
+    slot order — over its source-blocked plan when it has one, each block's
+    launch continuing the chains — and the attention gradient g stored at its
+    forward slot; d_er is the copy_e sum of g over the forward CSR. The
+    attention and the dropout keep bits are recomputed from el, er and the
+    seed, so the forward stored nothing per edge. Same bits as the r03
+    three-pass backward (attention gradient over the CSR, d_ft and d_el over
+    the transpose through the slot map)."""
+    ft2, el, er = ctx.saved_tensors
+    adj = ctx.adj
+    fwd, bwd = adj.fwd, adj.bwd
+    H, F, D = el.shape[1], ft2.shape[1], ctx.D
+    need_el, need_er, need_ft = ctx.needs_input_grad[8:11]
+    dev = ft2.device
+    dout = (torch.zeros(fwd.num_rows, F, dtype=torch.float32, device=dev) if d_ft is None
+            else _f32c(d_ft))
+    dz = None if d_z is None else _f32c(d_z)
+    emap = _fwd_slot_of_bwd(adj)
+    d_ft2 = torch.empty(bwd.num_rows, F, dtype=torch.float32, device=dev)
+    d_el = torch.empty(bwd.num_rows, H, dtype=torch.float32, device=dev)
+    g = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
+    common = (fwd.num_rows, ft2.shape[0], H, D)
+    tail = (ptr(ft2), ptr(el), ptr(er), ptr(dz), ptr(dout), float(ctx.alpha), float(ctx.lo),
+            float(ctx.hi), 1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,
+            ptr(ctx.seed_off), ptr(d_ft2), ptr(d_el), ptr(g), _stream_of(dev))
+    plan = _block_plan(bwd, dout, F) if bwd.nnz else None
+    if plan is None:
+        check_call(LIB.dglhip_gat_backward_t_device(
+            bwd.num_rows, ptr(bwd.row_order), ptr(bwd.indptr), ptr(bwd.indptr[1:]), 1, 0,
+            *(common + (ptr(bwd.indices), ptr(emap)) + tail)))
+    else:
+        erows = _block_edge_rows(bwd, plan, emap)
+        key = ("blocked_absent",) + _plan_tag(plan)
+        absent = bwd._plans.get(key)
+        if absent is None:
+            listed = torch.zeros(bwd.num_rows, dtype=torch.bool, device=dev)
+            listed[plan[0].rows.long()] = True
+            absent = bwd._plans[key] = torch.nonzero(~listed).squeeze(1)
+        if absent.numel():
+            d_ft2.index_fill_(0, absent, 0.0)
+            d_el.index_fill_(0, absent, 0.0)
+        off = 0
+        for i, it in enumerate(plan):
+            check_call(LIB.dglhip_gat_backward_t_device(
+                it.rows.numel(), ptr(it.rows), ptr(it.ptr), ptr(it.ptr[1:]), 0, 1 if i else 0,
+                *(common + (ptr(it.indices), ptr(erows[off:off + it.nnz])) + tail)))
+            off += it.nnz
+    d_er = None
+    if need_er:
+        d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
+    return ((None,) * 8 + (d_el if need_el else None, d_er, d_ft2 if need_ft else None, None,
+                           None))
 
 
 # el's gradient reads the E x H attention gradient (forward slot order)

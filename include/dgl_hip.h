@@ -509,6 +509,30 @@ int dglhip_gat_attention_grad_rowsum_ranges_device(
     const float* dz, float alpha, float clamp_lo, float clamp_hi, int apply_exp,
     float drop_scale, float* grad, float* grad_rowsum, void* stream);
 
+/* The backward of dglhip_gat_aggregate_device in one pass over the
+ * TRANSPOSED CSR (rows u = sources, columns v = destinations), 8 heads x 16
+ * features (dglhip_gat_backward_t_ok). Per transposed slot (u -> v, forward
+ * slot kf = fslot[slot]) it recomputes the forward's attention a and dropped
+ * weight w from el[u], er[v] and the dropout hash of kf (seed as the forward's,
+ * seed + *seed_offset), and
+ *   d_ft[u] = sum w * dout[v]            (fma chain in the transpose's slot order)
+ *   d_el[u] = sum g                      (add chain, same order)
+ *   grad[kf, h] = g = epilogue of <dout[v, h], ft[u, h]> (the attention gradient
+ *                 of dglhip_gat_attention_grad_device, same bits; d_er is then
+ *                 the copy_e sum of grad over the forward CSR)
+ * Items as dglhip_gspmm_items_device: item i is row item_row[i] (NULL: i) with
+ * slots [item_beg[i], item_end[i]) of cols / fslot, or with by_row != 0 slots
+ * [item_beg[row], item_end[row]); accumulate != 0 continues both chains from
+ * d_ft / d_el (source blocks of the transpose in order). dz may be NULL. */
+int dglhip_gat_backward_t_ok(int64_t num_heads, int64_t head_dim);
+int dglhip_gat_backward_t_device(
+    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+    int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
+    int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
+    const float* er, const float* dz, const float* dout, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
+    float* d_ft, float* d_el, float* grad, void* stream);
+
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
  * attention positions stay the CSR's); with accumulate != 0 both chains
