@@ -385,6 +385,13 @@ __device__ __forceinline__ float dpp_even_to_odd(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xA0, 0xF, 0xF, false));
 }
 
+// row_shl:N (within a 16-lane row): lane i reads lane i + N
+template <int N>
+__device__ __forceinline__ float dpp_shl(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x100 + N, 0xF, 0xF,
+                                                    false));
+}
+
 template <bool DROP, bool SMALL>
 __global__ __launch_bounds__(256) void gat_backward_t_kernel(
     int64_t num_items, const int32_t* __restrict__ item_row, const int64_t* __restrict__ item_beg,
@@ -397,10 +404,8 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
     int64_t table_bytes) {
   constexpr int H = 8, F = 128, U = 16;
   typedef Vec<2>::T V;
-  __shared__ float s_a[4][H * U];
-  __shared__ float s_w[4][H * U];
-  __shared__ float s_k[4][DROP ? H * U : 1];
-  __shared__ float s_z[4][H * U];
+  __shared__ float s_w[4][H * U];  // the batch's dropped attention, by head
+  __shared__ float s_d[4][H * U];  // its dots, then its attention gradients
   const int lane = threadIdx.x & 63;
   const int wi = threadIdx.x >> 6;
   const int64_t it = block_linear() * (blockDim.x >> 6) +
@@ -414,74 +419,107 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
   const uint64_t seed = DROP ? seed0 + (seed_off ? static_cast<uint64_t>(*seed_off) : 0) : 0;
   const GatTable tab = gat_table(dout, SMALL ? table_bytes : 0);
   const int64_t f0 = int64_t(lane) * 2;
-  const int h = lane >> 3;              // this lane's head (16 features = 8 lanes)
-  const bool odd = (lane & 1) != 0;
+  const int h = lane >> 3;                 // this lane's head (16 features = 8 lanes)
   const bool head_lane = (lane & 7) == 1;  // holds the head's dot: lane 8h + 1
   const uint32_t voff = static_cast<uint32_t>(f0 * int64_t(sizeof(float)));
-  // the pairs this lane computes: head hc of slots jc and jc + 8
+  // the (slot, head) pairs this lane computes: head hc of slots jc and jc + 8
   const int hc = lane & 7, jc = lane >> 3;
   const float elc = el[row * H + hc];
   const V ftv = ldv<2>(ft + row * F + f0);
   V acc = accumulate ? ldv<2>(d_ft + row * F + f0) : Vec<2>::zero();
   float elacc = (accumulate && head_lane) ? d_el[row * H + h] : 0.0f;
-  float* la = s_a[wi];
   float* lw = s_w[wi];
-  float* lk = s_k[wi];
-  float* lz = s_z[wi];
+  float* ld = s_d[wi];
   for (int64_t k = beg; k < end; k += U) {
     const int nb = end - k < U ? static_cast<int>(end - k) : U;
     V u[U];
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (j < nb) u[j] = gat_gather<2, SMALL>(dout, tab, cols[k + j], F, voff);
+    // the pairs: attention, keep bit, dropped weight (the forward's
+    // expressions), the normaliser gradient and the forward slot
+    float pa[2], pz[2];
+    bool pk[2];
+    int64_t pf[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = jc + 8 * i;
+      pa[i] = pz[i] = 0.0f;
+      pk[i] = true;
+      pf[i] = 0;
       if (j < nb) {
         const int64_t v = cols[k + j];
         float x = elc + er[v * H + hc];
         x = x > 0.0f ? x : alpha * x;
         if (apply_exp) x = __expf(x);
         const float a = fminf(fmaxf(x, lo), hi);
-        la[hc * U + j] = a;
+        pf[i] = fslot[k + j];
         float w = a;
         if (DROP) {
-          const bool keep = gat_keep(seed, fslot[k + j] * H + hc, thr);
-          w = keep ? a * scale : 0.0f;
-          lk[hc * U + j] = keep ? 1.0f : 0.0f;
+          pk[i] = gat_keep(seed, pf[i] * H + hc, thr);
+          w = pk[i] ? a * scale : 0.0f;
         }
+        pa[i] = a;
+        pz[i] = dz ? dz[v * H + hc] : 0.0f;
         lw[hc * U + j] = w;
-        lz[hc * U + j] = dz ? dz[v * H + hc] : 0.0f;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // per slot: d_ft's chain and the head's dot in the sliced g-SDDMM's
+    // association (partials of lanes 8h+1, 8h+3, 8h+5, 8h+7 = p0..p3;
+    // (p0 + p2) + (p1 + p3) on lane 8h+1)
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (j < nb) {
-        const float w = lw[h * U + j];
-        acc = Vec<2>::fma(Vec<2>::splat(w), u[j], acc);
-        // the head's dot in the sliced kernel's association
-        float t = u[j].x * ftv.x;
-        t = __builtin_fmaf(u[j].y, ftv.y, t);
-        const float tin = dpp_even_to_odd(t);
-        float p = __builtin_fmaf(u[j].x, ftv.x, tin);
-        p = __builtin_fmaf(u[j].y, ftv.y, p);
-        p = odd ? p : 0.0f;
-        const float s2 = p + __shfl_xor(p, 4, 64);
-        const float dot = s2 + __shfl_xor(s2, 2, 64);
-        if (head_lane) {
-          const float a = la[h * U + j];
-          float tt = dot;
-          if (DROP) tt = lk[h * U + j] != 0.0f ? tt * scale : 0.0f;
-          if (dz) tt = tt + lz[h * U + j];
-          float g = apply_exp ? (tt * a) * (a < 1.0f ? alpha : 1.0f)
-                              : tt * (a < 0.0f ? alpha : 1.0f);
-          g = (a > lo && a < hi) ? g : 0.0f;
-          elacc = elacc + g;
-          g_out[fslot[k + j] * H + h] = g;
+    for (int q = 0; q < U / 4; ++q) {
+      const f32x4 w4 = *reinterpret_cast<const f32x4*>(lw + h * U + 4 * q);
+      const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int j = 4 * q + i;
+        if (j < nb) {
+          acc = Vec<2>::fma(Vec<2>::splat(wv[i]), u[j], acc);
+          float t = u[j].x * ftv.x;
+          t = __builtin_fmaf(u[j].y, ftv.y, t);
+          float p = __builtin_fmaf(u[j].x, ftv.x, dpp_even_to_odd(t));
+          p = __builtin_fmaf(u[j].y, ftv.y, p);
+          const float s2 = p + dpp_shl<4>(p);
+          const float dot = s2 + dpp_shl<2>(s2);
+          if (head_lane) ld[h * U + j] = dot;
         }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the epilogue per pair (gat_epi_pre's operations), g stored at its
+    // forward slot and, by head, back into the LDS row for d_el's chain
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = jc + 8 * i;
+      if (j < nb) {
+        const float a = pa[i];
+        float tt = ld[hc * U + j];
+        if (DROP) tt = pk[i] ? tt * scale : 0.0f;
+        if (dz) tt = tt + pz[i];
+        float g = apply_exp ? (tt * a) * (a < 1.0f ? alpha : 1.0f)
+                            : tt * (a < 0.0f ? alpha : 1.0f);
+        g = (a > lo && a < hi) ? g : 0.0f;
+        g_out[pf[i] * H + hc] = g;
+        ld[hc * U + j] = g;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (head_lane) {
+#pragma unroll
+      for (int q = 0; q < U / 4; ++q) {
+        const f32x4 g4 = *reinterpret_cast<const f32x4*>(ld + h * U + 4 * q);
+        const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * q + i < nb) elacc = elacc + gv[i];
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -51,17 +51,22 @@ struct EdgesInFlight {
 // item; a row of deg slots has max(1, ceil(deg / kChunk)) items) and where
 // its chain goes: the row itself when the row is one item, else the item's
 // partial row.
-__device__ __forceinline__ void item_range(int64_t it, const int64_t* __restrict__ ptr,
+// Items past the last row's (item_row[it] >= num_rows: the caller sized the
+// item list by its bound num_rows + nnz / kChunk, no host sync) do nothing.
+__device__ __forceinline__ bool item_range(int64_t it, int64_t num_rows,
+                                           const int64_t* __restrict__ ptr,
                                            const int64_t* __restrict__ item_ptr,
                                            const int32_t* __restrict__ item_row, int64_t* row,
                                            int64_t* beg, int64_t* end, bool* single) {
   const int64_t r = item_row[it];
+  if (r >= num_rows) return false;
   const int64_t first = item_ptr[r], nit = item_ptr[r + 1] - first;
   const int64_t b = ptr[r] + (it - first) * kChunk;
   *row = r;
   *beg = b;
   *end = nit == 1 ? ptr[r + 1] : (b + kChunk < ptr[r + 1] ? b + kChunk : ptr[r + 1]);
   *single = nit == 1;
+  return true;
 }
 
 // One wave per (item, 64-wide slice of the output features): the slices of
@@ -71,7 +76,7 @@ __device__ __forceinline__ void item_range(int64_t it, const int64_t* __restrict
 // SI > 0: the block width as a compile-time constant; SI == 0: runtime width.
 template <int SI>
 __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
-    int64_t num_items, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
+    int64_t num_items, int64_t num_rows, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
     const int64_t* __restrict__ indptr, const int64_t* __restrict__ item_ptr,
     const int32_t* __restrict__ item_row, const int32_t* __restrict__ indices,
     const int32_t* __restrict__ slot_rel, const float* __restrict__ slot_norm,
@@ -85,7 +90,7 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
   if (it >= num_items) return;
   int64_t row, beg, end;
   bool single;
-  item_range(it, indptr, item_ptr, item_row, &row, &beg, &end, &single);
+  if (!item_range(it, num_rows, indptr, item_ptr, item_row, &row, &beg, &end, &single)) return;
   const int lane = threadIdx.x & 63;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
   const int64_t jg = pass * 64 + lane;
@@ -141,6 +146,7 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
 
 // out[row] = ((p0 + p1) + p2) ... over the row's items in order, for the
 // rows (or relations) of several items: one thread per (row, element).
+// heavy_row NULL: every row, those of one item skipped.
 __global__ __launch_bounds__(256) void typed_block_combine_kernel(
     int64_t num_heavy, int64_t F, const int32_t* __restrict__ heavy_row,
     const int64_t* __restrict__ item_ptr, const float* __restrict__ partial,
@@ -148,8 +154,9 @@ __global__ __launch_bounds__(256) void typed_block_combine_kernel(
   const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
   if (idx >= num_heavy * F) return;
   const int64_t h = idx / F, f = idx - h * F;
-  const int64_t r = heavy_row[h];
+  const int64_t r = heavy_row ? heavy_row[h] : h;
   const int64_t i0 = item_ptr[r], i1 = item_ptr[r + 1];
+  if (i1 - i0 <= 1) return;
   float s = partial[i0 * F + f];
   for (int64_t i = i0 + 1; i < i1; ++i) s = s + partial[i * F + f];
   out[r * F + f] = s;
@@ -159,7 +166,8 @@ __global__ __launch_bounds__(256) void typed_block_combine_kernel(
 // order): sum of norm_e * h[src_e, b*si + i] * dout[dst_e, b*so + j]. One
 // thread per (item, weight element of the relation); kEdges edges in flight.
 __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
-    int64_t num_items, int64_t nb, int64_t si, int64_t so, const int64_t* __restrict__ rel_ptr,
+    int64_t num_items, int64_t num_rels, int64_t nb, int64_t si, int64_t so,
+    const int64_t* __restrict__ rel_ptr,
     const int64_t* __restrict__ item_ptr, const int32_t* __restrict__ item_rel,
     const int32_t* __restrict__ rel_src, const int32_t* __restrict__ rel_dst,
     const float* __restrict__ rel_norm, const float* __restrict__ ufeat,
@@ -171,7 +179,7 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
   const int64_t it = idx / wr, rem = idx - it * wr;
   int64_t r, beg, end;
   bool single;
-  item_range(it, rel_ptr, item_ptr, item_rel, &r, &beg, &end, &single);
+  if (!item_range(it, num_rels, rel_ptr, item_ptr, item_rel, &r, &beg, &end, &single)) return;
   const int64_t b = rem / (si * so), i = (rem / so) % si, j = rem % so;
   const int64_t Fi = nb * si, Fo = nb * so;
   const int64_t xoff = b * si + i, goff = b * so + j;
@@ -210,20 +218,20 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t 
                                    void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rows >= 0 && num_items >= num_rows && num_heavy >= 0 && num_blocks > 0 &&
+  DGLHIP_CHECK(num_rows >= 0 && num_items >= 0 && num_heavy >= 0 && num_blocks > 0 &&
                in_block > 0 && out_block > 0, "bad sizes");
   const int64_t Fo = num_blocks * out_block;
   if (num_rows == 0) return 0;
   DGLHIP_CHECK(indptr && item_ptr && item_row && indices && slot_rel && ufeat && weight && out,
                "null pointer argument");
-  DGLHIP_CHECK(num_heavy == 0 || (heavy_row && partial), "chunked rows need their partials");
+  DGLHIP_CHECK(num_heavy == 0 || partial, "chunked rows need their partials");
   const int64_t npass = (Fo + 63) / 64;
   const int64_t waves = num_items * npass;
   DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
   const dim3 grid = grid_1d((waves + 3) / 4), block(256);
 #define DGLHIP_TB(S)                                                                       \
-  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_items, npass, \
-                     num_blocks, in_block, out_block, indptr, item_ptr, item_row, indices, \
+  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_items,       \
+                     num_rows, npass, num_blocks, in_block, out_block, indptr, item_ptr, item_row, indices, \
                      slot_rel, slot_norm, ufeat, weight, out, partial)
   timed_launch(stream, [&] {
     switch (in_block) {
@@ -256,18 +264,19 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
                                     float* dweight, float* partial, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(num_rels >= 0 && num_items >= num_rels && num_heavy >= 0 && num_blocks >= 0 &&
+  DGLHIP_CHECK(num_rels >= 0 && num_items >= 0 && num_heavy >= 0 && num_blocks >= 0 &&
                in_block >= 0 && out_block >= 0, "bad sizes");
   const int64_t wr = num_blocks * in_block * out_block;
   if (num_rels == 0 || wr == 0) return 0;
   DGLHIP_CHECK(rel_ptr && item_ptr && item_rel && ufeat && dout && dweight,
                "null pointer argument");
-  DGLHIP_CHECK(num_heavy == 0 || (heavy_rel && partial), "chunked relations need their partials");
+  DGLHIP_CHECK(num_heavy == 0 || partial, "chunked relations need their partials");
   const int64_t total = num_items * wr;
   DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
   timed_launch(stream, [&] {
     hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
-                       stream, num_items, num_blocks, in_block, out_block, rel_ptr, item_ptr,
+                       stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr,
+                       item_ptr,
                        item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight, partial);
   });
   if (num_heavy > 0) {

@@ -1526,20 +1526,22 @@ def gather_rows(x, idx):
 TYPED_CHUNK = 64  # DGLHIP_TYPED_CHUNK: slots per chain of the typed-block kernels
 
 
-def _typed_items(ptr):
-    """The typed-block kernels' work items over a CSR-like ``ptr`` (cached by
-    the caller): (item_ptr int64[R+1] — each row's first item, a row of deg
-    slots having max(1, ceil(deg / TYPED_CHUNK)) items —, item_row int32[I],
-    heavy int32[rows of more than one item])."""
+def _typed_items(ptr, nnz):
+    """The typed-block kernels' work items over a CSR-like ``ptr`` with
+    ``nnz`` slots, built on the device with no host sync (cached by the
+    caller): (item_ptr int64[R+1] — each row's first item, a row of deg slots
+    having max(1, ceil(deg / TYPED_CHUNK)) items —, item_row int32[I_max],
+    I_max = R + ceil(nnz / TYPED_CHUNK) >= the item count, the entries past
+    the last item = R (padding the kernels skip))."""
+    R = ptr.numel() - 1
     deg = ptr[1:] - ptr[:-1]
     nit = torch.clamp((deg + (TYPED_CHUNK - 1)) // TYPED_CHUNK, min=1)
-    item_ptr = torch.zeros(len(deg) + 1, dtype=torch.int64, device=ptr.device)
+    item_ptr = torch.zeros(R + 1, dtype=torch.int64, device=ptr.device)
     torch.cumsum(nit, 0, out=item_ptr[1:])
-    total = int(item_ptr[-1])
-    item_row = torch.repeat_interleave(torch.arange(len(deg), device=ptr.device,
-                                                    dtype=torch.int32), nit, output_size=total)
-    heavy = torch.nonzero(nit > 1).squeeze(1).to(torch.int32)
-    return item_ptr, item_row, heavy
+    bound = R + -(-nnz // TYPED_CHUNK)
+    item_row = torch.searchsorted(item_ptr[1:], torch.arange(bound, device=ptr.device),
+                                  right=True).to(torch.int32)
+    return item_ptr, item_row
 
 
 def _run_typed_block(csr, ufeat2, weight, slot_rel, slot_norm, nb, si, so):
@@ -1548,15 +1550,13 @@ def _run_typed_block(csr, ufeat2, weight, slot_rel, slot_norm, nb, si, so):
     if dev.type == "cuda":
         items = csr._plans.get("typed_items")
         if items is None:
-            items = csr._plans["typed_items"] = _typed_items(csr.indptr)
-        item_ptr, item_row, heavy = items
-        nh = heavy.numel()
-        part = torch.empty(item_row.numel() if nh else 0, nb * so, dtype=torch.float32,
-                           device=dev)
+            items = csr._plans["typed_items"] = _typed_items(csr.indptr, csr.nnz)
+        item_ptr, item_row = items
+        part = torch.empty(item_row.numel(), nb * so, dtype=torch.float32, device=dev)
         check_call(LIB.dglhip_typed_block_spmm_device(
             csr.num_rows, item_row.numel(), nb, si, so, ptr(csr.indptr), ptr(item_ptr),
-            ptr(item_row), nh, ptr(heavy), ptr(csr.indices), ptr(slot_rel), ptr(slot_norm),
-            ptr(ufeat2), ptr(weight), ptr(out), ptr(part), _stream_of(dev)))
+            ptr(item_row), csr.num_rows, None, ptr(csr.indices), ptr(slot_rel),
+            ptr(slot_norm), ptr(ufeat2), ptr(weight), ptr(out), ptr(part), _stream_of(dev)))
     else:
         check_call(LIB.dglhip_typed_block_spmm_host(
             csr.num_rows, nb, si, so, ptr(csr.indptr), ptr(csr.indices), ptr(slot_rel),
@@ -1585,7 +1585,7 @@ class _RelationGroups(object):
         self.src = rel.indices
         self.slot = rel.eid  # forward slot of each relation-major position
         self.dst = fwd.row_ids().index_select(0, self.slot).to(torch.int32)
-        self.items = _typed_items(self.ptr) if fwd.device.type == "cuda" else None
+        self.items = _typed_items(self.ptr, fwd.nnz) if fwd.device.type == "cuda" else None
         self.etype = etype  # the relations it was built for (by identity and version)
         self.version = etype._version
 
@@ -1619,13 +1619,12 @@ class _TypedBlock(torch.autograd.Function):
             nrm = None if fwd_nrm is None else fwd_nrm.index_select(0, g.slot)
             dw = torch.empty_like(weight)
             if dout.is_cuda:
-                item_ptr, item_rel, heavy = g.items
-                nh = heavy.numel()
-                part = torch.empty(item_rel.numel() if nh else 0, nb * si * so,
-                                   dtype=torch.float32, device=dout.device)
+                item_ptr, item_rel = g.items
+                part = torch.empty(item_rel.numel(), nb * si * so, dtype=torch.float32,
+                                   device=dout.device)
                 check_call(LIB.dglhip_typed_block_wgrad_device(
                     R, item_rel.numel(), nb, si, so, ptr(g.ptr), ptr(item_ptr), ptr(item_rel),
-                    nh, ptr(heavy), ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2), ptr(dout),
+                    R, None, ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2), ptr(dout),
                     ptr(dw), ptr(part), _stream_of(dout.device)))
             else:
                 check_call(LIB.dglhip_typed_block_wgrad_host(

@@ -576,9 +576,12 @@ int dglhip_gat_dropout_mask_host(int64_t num_slots, int64_t num_heads, float dro
 #define DGLHIP_TYPED_CHUNK 64
 /* Device form: the chunks as items. item_ptr[num_rows+1] = each row's first
  * item (a row of deg slots has max(1, ceil(deg / DGLHIP_TYPED_CHUNK))
- * items), item_row[num_items] = the row of each item, heavy_row[num_heavy] =
- * the rows of more than one item; partial = num_items x Fo floats of
- * workspace (only heavy rows' items are written). */
+ * items), item_row[num_items] = the row of each item (entries >= num_rows:
+ * padding, skipped — an item list sized by its bound num_rows + nnz /
+ * DGLHIP_TYPED_CHUNK needs no host sync), heavy_row[num_heavy] = the rows of
+ * more than one item (NULL with num_heavy = num_rows: every row checked);
+ * partial = num_items x Fo floats of workspace (only heavy rows' items are
+ * written). */
 int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t num_blocks,
                                    int64_t in_block, int64_t out_block,
                                    const int64_t* indptr, const int64_t* item_ptr,
