@@ -123,8 +123,10 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
     ms, kms, launches = wall_steps(step, steps, warmup, dev, kernel)
 
     def fwd():
-        kernel.gat_aggregate(adj, ft, el, er)  # training forward: attention stored
+        kernel.gat_aggregate(adj, ft, el, er)  # training forward
     fms = call_ms(fwd, steps, dev)
+    # the one-pass transposed backward recomputes the attention: nothing stored
+    stored = kernel.LIB.dglhip_gat_backward_t_ok(H, D) != 1
     cuts = kernel._block_cuts(adj.fwd, H * D * 4)
     peak, src = gather_peak(n * H * D * 4, 0 if cuts is None else len(cuts) - 1)
     res = {"value": E / (ms * 1e-3), "unit": "edges/s (fwd+bwd)", "ms_per_step": ms,
@@ -132,9 +134,10 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
            "config": "GAT layer aggregation, %d heads x %d, on the headline graph (%d nodes, "
                      "%d edges): kernel.gat_aggregate forward + backward, dropout 0"
                      % (H, D, n, E),
-           "roofline": roof(gat_fwd_bytes(E, n, H, D, True), fms, peak, src,
-                            "fused GAT forward (dglhip_gat_aggregate_device, attention "
-                            "stored for the backward)"),
+           "roofline": roof(gat_fwd_bytes(E, n, H, D, stored), fms, peak, src,
+                            "fused GAT forward (dglhip_gat_aggregate_device%s)"
+                            % (", attention stored for the backward" if stored else
+                               "; the backward recomputes the attention")),
            "cpu_baseline": None}
     if cpu and sample is not None:
         res["cpu_baseline"] = gat_layer_cpu(sample, n, H, D)

@@ -1493,6 +1493,17 @@ def timing_read():
 # ---------------------------------------------------------------------------
 # Typed-edge block-diagonal g-SpMM (R-GCN block layer)
 # ---------------------------------------------------------------------------
+class _Segments(object):
+    """A CSR-like view for the typed-block kernels: rows with slot ranges
+    ``indptr`` over column ids ``indices`` (int32)."""
+
+    def __init__(self, indptr, indices):
+        self.indptr, self.indices = indptr, indices
+        self.num_rows = indptr.numel() - 1
+        self.nnz = indices.numel()
+        self._plans = {}
+
+
 class _GatherRows(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, idx):
@@ -1503,22 +1514,37 @@ class _GatherRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         (idx,) = ctx.saved_tensors
-        m = idx.numel()
+        m, n = idx.numel(), ctx.num_rows
         if m == 0:
-            return dy.new_zeros((ctx.num_rows,) + tuple(dy.shape[1:])), None
-        dy2 = dy.reshape(m, -1)
-        adj = from_coo(ctx.num_rows, m, idx, torch.arange(m, device=idx.device), ORDER_EID,
-                       idx.device)
-        dx = gspmm(adj, "copy_u", "sum", dy2.contiguous())
-        return dx.view((ctx.num_rows,) + tuple(dy.shape[1:])), None
+            return dy.new_zeros((n,) + tuple(dy.shape[1:])), None
+        dy2 = _f32c(dy.reshape(m, -1))
+        F = dy2.shape[1]
+        dev = dy2.device
+        # positions grouped by row, in increasing position (a stable sort; the
+        # counts by an integer scatter-add): no host sync
+        order = torch.sort(idx, stable=True)[1].to(torch.int32)
+        counts = torch.zeros(n, dtype=torch.int64, device=dev).scatter_add_(
+            0, idx, torch.ones_like(idx))
+        ptr_ = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        torch.cumsum(counts, 0, out=ptr_[1:])
+        # the sum per row as the typed-block kernel over F blocks of 1 x 1
+        # ones (fma(1, x, acc) == acc + x): chains of TYPED_CHUNK positions,
+        # the chunks of a long row added in order
+        seg = _Segments(ptr_, order)
+        ones = torch.ones(1, F, 1, 1, dtype=torch.float32, device=dev)
+        rel = torch.zeros(m, dtype=torch.int32, device=dev)
+        dx = _run_typed_block(seg, dy2, ones, rel, None, F, 1, 1)
+        return dx.view((n,) + tuple(dy.shape[1:])), None
 
 
 def gather_rows(x, idx):
-    """``x[idx]`` (rows) whose gradient is a g-SpMM: dx[r] = the sum of dy[i]
-    over the positions i with idx[i] == r, in increasing i — deterministic
-    (torch's index backward accumulates duplicates in an implementation-
-    defined order, and walked a hub row's duplicates serially: R-GCN's
-    DistMult decoder spent 3 ms of an 8 ms step there, tools/rgcn_step.py)."""
+    """``x[idx]`` (rows) whose gradient sums each row's duplicates
+    deterministically: dx[r] = the dy[i] with idx[i] == r in increasing i, as
+    chains of TYPED_CHUNK positions whose partials are added in order (the
+    typed-block kernel with unit weights; no atomics, no host sync). torch's
+    index backward accumulates duplicates in an implementation-defined order
+    and walks a hub row's duplicates serially (R-GCN's DistMult decoder: 3 of
+    the 8 ms step, tools/rgcn_step.py)."""
     idx = idx.to(device=x.device, dtype=torch.int64).reshape(-1)
     return _GatherRows.apply(x, idx)
 

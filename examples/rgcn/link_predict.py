@@ -124,7 +124,14 @@ class LinkPredict(nn.Module):
         return h
 
     def loss(self, h, samples, labels):
-        s = h[samples[:, 0]] * self.w_relation[samples[:, 1]] * h[samples[:, 2]]
+        # DistMult (the reference's calc_score); the fused model gathers the
+        # rows with a deterministic chunked backward (kernel.gather_rows)
+        if self.udf:
+            s = h[samples[:, 0]] * self.w_relation[samples[:, 1]] * h[samples[:, 2]]
+        else:
+            n = samples.shape[0]
+            ho = kernel.gather_rows(h, torch.cat([samples[:, 0], samples[:, 2]]))
+            s = ho[:n] * kernel.gather_rows(self.w_relation, samples[:, 1]) * ho[n:]
         score = s.sum(1)
         reg = h.pow(2).mean() + self.w_relation.pow(2).mean()
         return F.binary_cross_entropy_with_logits(score, labels) + self.reg * reg
