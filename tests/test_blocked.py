@@ -285,6 +285,35 @@ def test_blocked_u_mul_e_bits(order, reduce):
         assert a[3] > b[3]
         for x, y in zip(a[:3], b[:3]):
             assert torch.equal(x, y)
+        # pinned to the oracle directly (r03 verdict, "Next" 7): per head the
+        # forward is the reference's fma chain over COO (dst, src) in edge
+        # order with that head's weights (mean: that chain over max(deg, 1),
+        # IEEE division); dH the same chain over the transpose with dC's
+        # rows; the weight gradient within 1e-5 of the float64 dot
+        wc = w.cpu().reshape(m, -1).numpy()
+        # edge_order "slot": the values are in the CSR's slot order (edges
+        # grouped by destination in edge order); map them to edge ids
+        inv = np.argsort(np.argsort(dst, kind="stable"), kind="stable")
+        if order == "slot":
+            wc = wc[inv]
+        Hh = wc.shape[1]
+        Hc = H.cpu().numpy().reshape(n, Hh, -1)
+        deg = np.maximum(np.bincount(dst, minlength=n), 1).astype(np.float32)
+        dC = np.ones((n, Hh, Hc.shape[2]), np.float32)
+        if reduce == "mean":
+            dC = dC / deg[:, None, None]
+        for hh in range(Hh):
+            ref = O.spmm_coo(n, dst, src, Hc[:, hh], wc[:, hh])
+            if reduce == "mean":
+                ref = ref / deg[:, None]
+            assert np.array_equal(a[0].reshape(n, Hh, -1)[:, hh].numpy(), ref)
+            dref = O.spmm_coo(n, src, dst, dC[:, hh], wc[:, hh])
+            assert np.array_equal(a[1].reshape(n, Hh, -1)[:, hh].numpy(), dref)
+            dw = O.sddmm_dot(dst, src, dC[:, hh], Hc[:, hh])
+            gw = a[2].reshape(m, Hh)[:, hh].numpy()
+            if order == "slot":
+                gw = gw[inv]
+            assert np.allclose(gw, dw, rtol=1e-5, atol=1e-5 * float(np.abs(dw).max()))
 
 
 def test_u_mul_e_plan_slot_map(small_blocks):
@@ -387,6 +416,46 @@ def test_blocked_max_bits_with_ties(msg):
     o0, g0, n0 = run("off")
     assert n1 > n0
     assert torch.equal(o1, o0) and torch.equal(g1, g0)
+    # pinned to the oracle directly (r03 verdict, "Next" 7): the values are
+    # the degree-bucketing max over each row's mailbox (messages in edge
+    # order; empty rows 0); with the upstream gradient zero past row R0, each
+    # (row, feature)'s value routes to the source of its first maximal message
+    # in edge order (strict >): integers throughout, exact
+    inv = np.argsort(np.argsort(dst, kind="stable"), kind="stable")
+    w_edge = w.cpu().numpy()[inv]  # slot-ordered weights, per edge id
+    Hn = H.cpu().numpy()
+    full = Hn[src] if msg == "copy_u" else Hn[src] * w_edge
+    assert np.array_equal(o1.numpy(), O.max_mailbox(n, dst, full))
+    R0 = 3000
+    G = np.zeros((n, 128), np.float32)
+    G[:R0] = np.arange(R0 * 128, dtype=np.float32).reshape(R0, 128)
+    old = kernel.set_blocked("auto")
+    try:
+        h = H.clone().requires_grad_(True)
+        if msg == "copy_u":
+            o = kernel.gspmm(adj, "copy_u", "max", h)
+        else:
+            o = kernel.gspmm(adj, "u_mul_e", "max", h, w, edge_order="slot")
+        o.backward(torch.from_numpy(G).to(dev))
+        got = h.grad.cpu().numpy()
+    finally:
+        kernel.set_blocked(old)
+    expect = np.zeros((n, 128), np.float64)
+    es = np.nonzero(dst < R0)[0]  # edge order
+    rows = dst[es]
+    srt = np.argsort(rows, kind="stable")
+    es, rows = es[srt], rows[srt]
+    starts = np.searchsorted(rows, np.arange(R0))
+    ends = np.searchsorted(rows, np.arange(R0), side="right")
+    for r in range(R0):
+        if starts[r] == ends[r]:
+            continue
+        e = es[starts[r]:ends[r]]
+        block = full[e]
+        first = np.argmax(block == block.max(0), axis=0)  # first maximal message
+        wgt = 1.0 if msg == "copy_u" else w_edge[e[first], 0]
+        np.add.at(expect, (src[e[first]], np.arange(128)), G[r] * wgt)
+    assert np.array_equal(got, expect.astype(np.float32))
 
 
 def _tagged_graph():
