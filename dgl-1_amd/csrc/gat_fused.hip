@@ -530,6 +530,60 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
   if (head_lane) d_el[row * H + h] = elacc;
 }
 
+// Per row and head, the sum of an [nnz, 8] slot-ordered tensor over the row's
+// slots, as the copy_e sum's chain ((0 + v0) + v1) + ... in slot order (GAT's
+// d_er from the attention gradient). gspmm_sum_kernel gives each row 4 lanes
+// and walks it slot by slot, so a hub row of ~20,000 slots (Reddit-shaped
+// graph) is ~1,300 serial load latencies (1.32 ms per call). Here a wave owns
+// a row: 64 slots per step arrive as 8 coalesced 256-B loads (lane = slot %
+// 8 x 8 + head), pass through LDS transposed to head-major, and the head's
+// lane adds its 64 values in slot order.
+__global__ __launch_bounds__(256) void rowsum_heads8_kernel(
+    int64_t num_rows, const int64_t* __restrict__ indptr, const int32_t* __restrict__ row_order,
+    const float* __restrict__ vals, float* __restrict__ out) {
+  constexpr int H = 8, S = 64;
+  __shared__ float s_v[4][H * S];
+  const int lane = threadIdx.x & 63;
+  const int wi = threadIdx.x >> 6;
+  const int64_t it = block_linear() * (blockDim.x >> 6) +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_rows) return;
+  int64_t row = row_order ? row_order[it] : it;
+  row = __builtin_amdgcn_readfirstlane(static_cast<int>(row));
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const int s = lane >> 3, hh = lane & 7;
+  float* lv = s_v[wi];
+  float acc = 0.0f;
+  for (int64_t k = beg; k < end; k += S) {
+    const int nb = end - k < S ? static_cast<int>(end - k) : S;
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = 8 * q + s;
+      v[q] = j < nb ? vals[(k + j) * H + hh] : 0.0f;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) lv[hh * S + 8 * q + s] = v[q];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane < H) {
+#pragma unroll
+      for (int q = 0; q < S / 4; ++q) {
+        const f32x4 t = *reinterpret_cast<const f32x4*>(lv + lane * S + 4 * q);
+        const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (4 * q + i < nb) acc = acc + tv[i];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  if (lane < H) out[row * H + lane] = acc;
+}
+
 }  // namespace dglhip
 
 using namespace dglhip;
@@ -689,6 +743,23 @@ int dglhip_gat_backward_t_device(
       if (small) DGLHIP_GBT(false, true); else DGLHIP_GBT(false, false);
     }
 #undef DGLHIP_GBT
+  });
+  API_END();
+}
+
+int dglhip_rowsum_heads8_device(int64_t num_rows, const int64_t* indptr,
+                                const int32_t* row_order, const float* vals, float* out,
+                                void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0, "bad sizes");
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && vals && out, "null pointer argument");
+  const int64_t blocks = (num_rows + 3) / 4;
+  DGLHIP_CHECK(blocks <= 0x7fffffff, "grid too large");
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(rowsum_heads8_kernel, grid_1d(blocks), dim3(256), 0, stream, num_rows,
+                       indptr, row_order, vals, out);
   });
   API_END();
 }

@@ -2013,8 +2013,11 @@ def _gat_backward_t(ctx, d_ft, d_z):
                 *(common + (ptr(it.indices), ptr(erows[off:off + it.nnz])) + tail)))
             off += it.nnz
     d_er = None
-    if need_er:
-        d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
+    if need_er:  # the copy_e sum of g over the CSR, one wave per row (same chain)
+        d_er = torch.empty(fwd.num_rows, H, dtype=torch.float32, device=dev)
+        check_call(LIB.dglhip_rowsum_heads8_device(fwd.num_rows, ptr(fwd.indptr),
+                                                   ptr(fwd.row_order), ptr(g), ptr(d_er),
+                                                   _stream_of(dev)))
     return ((None,) * 8 + (d_el if need_el else None, d_er, d_ft2 if need_ft else None, None,
                            None))
 

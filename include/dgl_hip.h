@@ -533,6 +533,14 @@ int dglhip_gat_backward_t_device(
     float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
     float* d_ft, float* d_el, float* grad, void* stream);
 
+/* out[r, h] = sum over the slots k of row r of vals[k, h], 8 heads, as the
+ * copy_e sum's chain ((0 + v0) + v1) + ... in slot order (the same bits as
+ * dglhip_gspmm_device(COPY_E, SUM) with slot-ordered values), one wave per
+ * row: the GAT backward's d_er. row_order may be NULL. */
+int dglhip_rowsum_heads8_device(int64_t num_rows, const int64_t* indptr,
+                                const int32_t* row_order, const float* vals, float* out,
+                                void* stream);
+
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
  * attention positions stay the CSR's); with accumulate != 0 both chains
