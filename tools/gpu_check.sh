@@ -76,9 +76,10 @@ for s in $STEPS; do
     emul)
       wl=${WORKLOAD:-reddit}
       for w in ${EMUL_WORLDS:-2 8}; do for c in ${CHUNKS:-0 4}; do
-        tag=${wl}_${w}_$c${HALO_DTYPE:+_$HALO_DTYPE}
+        tag=${wl}_${w}_$c${HALO_DTYPE:+_$HALO_DTYPE}${STRONG:+_strong}
         timeout -k 10 600 python bench.py --workload $wl --emulate-world $w --pipeline-chunks $c \
           --steps 10 --warmup 3 --no-traffic ${HALO_DTYPE:+--halo-dtype $HALO_DTYPE} \
+          ${STRONG:+--emulate-strong} \
           > gpurun_out/emul_$tag.json 2> gpurun_out/emul_$tag.err
         rc=$?; tail -1 gpurun_out/emul_$tag.err; [ $rc -eq 0 ] || exit $rc
         python -c "import json; d=json.load(open('gpurun_out/emul_$tag.json')); print('$tag', d['ms_per_step'], d['roofline']['kernel_ms'])"
