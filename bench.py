@@ -855,7 +855,8 @@ def main(argv=None):
         t0 = time.time()  # before this process initialises the GPU
         # every g-SpMM kernel of the 3 calls (warm-up + 2 steps), per call
         pmc = pmc_traffic(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
-                           "--no-rmat-leg", "--no-train-leg"], per_call_calls=3)
+                           "--no-rmat-leg", "--no-train-leg", "--no-model-legs"],
+                          per_call_calls=3)
         if not args.no_rmat_leg and args.emulate_world <= 1:
             # the rmat leg's kernels: every g-SpMM kernel of a call, per call
             rmat_pmc = pmc_traffic(["--workload", "rmat", "--rmat-scale", str(args.rmat_scale),

@@ -46,7 +46,7 @@ for s in $STEPS; do
       # the bench line and the kernel statistics of the SAME process (headline leg only)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
-        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-train-leg --no-cpu-baseline \
+        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-train-leg --no-cpu-baseline --no-model-legs \
         > gpurun_out/prof.json 2> gpurun_out/prof.log
       rc=$?; tail -1 gpurun_out/prof.log; cat gpurun_out/prof.json; [ $rc -eq 0 ] || exit $rc ;;
     dist)
@@ -148,7 +148,7 @@ for s in $STEPS; do
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
-          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-rmat-leg --no-train-leg > gpurun_out/pmc_$c.log 2>&1
+          -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-traffic --no-rmat-leg --no-train-leg --no-model-legs > gpurun_out/pmc_$c.log 2>&1
         rc=$?; tail -2 gpurun_out/pmc_$c.log; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac
