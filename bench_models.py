@@ -139,6 +139,19 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
                             % (", attention stored for the backward" if stored else
                                "; the backward recomputes the attention")),
            "cpu_baseline": None}
+    if not stored:
+        # the backward's kernels (the transposed pass and d_er's row sums): the
+        # step's library launches less the forward's
+        bms = max(kms - fms, 1e-6)
+        F_ = H * D
+        bbytes = (E * (4 * F_ + 12 + 12 * H) + n * (8 * F_ + 8 * H + 8) +
+                  E * 4 * H + n * 4 * H)
+        res["roofline_backward"] = roof(
+            bbytes, bms, peak, src,
+            "GAT backward: dglhip_gat_backward_t_device (per edge the gathered dout row, "
+            "column id, forward slot, er and dz values, the stored gradient; per source row "
+            "ft, el, d_ft, d_el) + dglhip_rowsum_heads8_device (d_er)",
+            timing="library launches per step less the forward call")
     if cpu and sample is not None:
         res["cpu_baseline"] = gat_layer_cpu(sample, n, H, D)
     return res
