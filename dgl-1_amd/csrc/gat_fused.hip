@@ -32,42 +32,18 @@
 // indices (dropout hash, attention positions) stay the CSR's.
 //
 // Dropout mask: keep(k, h) = hash(seed, k * H + h) >= threshold, a stateless
-// counter hash (gat_keep below, host and device), so the backward and the host
+// counter hash (gat_keep, gspmm_impl.h: host and device), so the backward and the host
 // path reproduce it from (seed, slot, head) alone.
 
 #include "gspmm_impl.h"
 
 namespace dglhip {
 
-// lowbias32 (a 32-bit integer finaliser); two rounds over the 64-bit index
-__host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
-  x ^= x >> 16;
-  x *= 0x7feb352du;
-  x ^= x >> 15;
-  x *= 0x846ca68bu;
-  x ^= x >> 16;
-  return x;
-}
-
-__host__ __device__ __forceinline__ bool gat_keep(uint64_t seed, int64_t idx, uint32_t thr) {
-  const uint64_t i = static_cast<uint64_t>(idx);
-  const uint32_t r = gat_mix32(gat_mix32(static_cast<uint32_t>(i) ^ static_cast<uint32_t>(seed)) ^
-                               (static_cast<uint32_t>(i >> 32) + static_cast<uint32_t>(seed >> 32) +
-                                0x9e3779b9u));
-  return r >= thr;
-}
-
 // study knob (dglhip_set_gat_variant): 0 automatic, 1 the per-lane kernel,
 // 2 the LDS-shared attention kernel (head counts 1, 2, 4, 8, 16) with each
 // batch's feature rows gathered after its attention, 3 the same kernel with
 // them gathered before it
 int g_gat_variant = 0;
-
-// keep iff hash >= threshold: P(keep) = 1 - p
-static inline uint32_t gat_drop_threshold(float p) {
-  const double t = static_cast<double>(p) * 4294967296.0;
-  return t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
-}
 
 // One row of VEC floats per lane through a buffer descriptor built from the
 // wave-uniform row address: a 32-bit per-lane byte offset instead of a 64-bit
@@ -502,8 +478,8 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
         float tt = ld[hc * U + j];
         if (DROP) tt = pk[i] ? tt * scale : 0.0f;
         if (dz) tt = tt + pz[i];
-        float g = apply_exp ? (tt * a) * (a < 1.0f ? alpha : 1.0f)
-                            : tt * (a < 0.0f ? alpha : 1.0f);
+        float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
+                            : tt * (a <= 0.0f ? alpha : 1.0f);
         g = (a > lo && a < hi) ? g : 0.0f;
         g_out[pf[i] * H + hc] = g;
         ld[hc * U + j] = g;

@@ -28,9 +28,11 @@ namespace dglhip {
 // GAT attention-gradient epilogue of the SDDMM dot (EPI = true): the dot
 // d_w[k, h] = <dC[row, h, :], ft[u, h, :]> becomes the gradient of the
 // attention's pre-activation, stored in slot order:
-//   t = d_w; t = keep ? t * scale : 0 (dropout: keep = w[k, h] != 0);
+//   t = d_w; t = keep ? t * scale : 0 (dropout: keep from the forward's hash
+//   of (seed, k * H + h) with hash_keep, else w[k, h] != 0);
 //   t = t + dz[row, h] (the normaliser's gradient);
-//   g = (t * a) * (a < 1 ? alpha : 1) (exp; else t * (a < 0 ? alpha : 1));
+//   g = (t * a) * (a <= 1 ? alpha : 1) (exp; else t * (a <= 0 ? alpha : 1): the
+//       slope alpha where the logit x <= 0, as torch's leaky_relu backward);
 //   g = lo < a < hi ? g : 0
 // the float operations, and their order, of kernel._GATAggregate's torch
 // backward, so both give the same bits.
@@ -44,26 +46,38 @@ struct GatEpi {
   // order to what rsum holds ([rows, H]; GAT's er gradient, the copy_e sum
   // of the stored values over the row's slots, fused; sliced kernel only)
   float* rsum = nullptr;
+  // dropout keep bits from the forward's hash (seed + *seed_off, threshold
+  // thr) instead of w != 0: a kept pair whose attention is exactly 0 keeps
+  // its gradient (r03 ADVICE); w is then not read
+  int hash_keep = 0;
+  uint64_t seed = 0;
+  const int64_t* seed_off = nullptr;
+  uint32_t thr = 0;
 };
+
+__device__ __forceinline__ uint64_t gat_epi_seed(const GatEpi& e) {
+  return e.seed + (e.seed_off ? static_cast<uint64_t>(*e.seed_off) : 0);
+}
 
 __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, int64_t H,
                                          int64_t h, int64_t row) {
   const float a = e.a[k * H + h];
-  if (e.w) t = e.w[k * H + h] != 0.0f ? t * e.scale : 0.0f;
+  if (e.hash_keep) t = gat_keep(gat_epi_seed(e), k * H + h, e.thr) ? t * e.scale : 0.0f;
+  else if (e.w) t = e.w[k * H + h] != 0.0f ? t * e.scale : 0.0f;
   if (e.dz) t = t + e.dz[row * H + h];
-  const float g = e.apply_exp ? (t * a) * (a < 1.0f ? e.alpha : 1.0f)
-                              : t * (a < 0.0f ? e.alpha : 1.0f);
+  const float g = e.apply_exp ? (t * a) * (a <= 1.0f ? e.alpha : 1.0f)
+                              : t * (a <= 0.0f ? e.alpha : 1.0f);
   return (a > e.lo && a < e.hi) ? g : 0.0f;
 }
 
-// gat_epi on operands loaded ahead (the slot's attention a and dropped copy
-// w, the row's normaliser gradient dz): the same arithmetic.
-__device__ __forceinline__ float gat_epi_pre(const GatEpi& e, float t, float a, float w,
+// gat_epi on operands loaded ahead (the slot's attention a and keep bit,
+// the row's normaliser gradient dz): the same arithmetic.
+__device__ __forceinline__ float gat_epi_pre(const GatEpi& e, float t, float a, bool keep,
                                              float dz) {
-  if (e.w) t = w != 0.0f ? t * e.scale : 0.0f;
+  if (e.w || e.hash_keep) t = keep ? t * e.scale : 0.0f;
   if (e.dz) t = t + dz;
-  const float g = e.apply_exp ? (t * a) * (a < 1.0f ? e.alpha : 1.0f)
-                              : t * (a < 0.0f ? e.alpha : 1.0f);
+  const float g = e.apply_exp ? (t * a) * (a <= 1.0f ? e.alpha : 1.0f)
+                              : t * (a <= 0.0f ? e.alpha : 1.0f);
   return (a > e.lo && a < e.hi) ? g : 0.0f;
 }
 
@@ -201,7 +215,11 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
     const int g = j / LPH, r = j % LPH;
     return NB >= LPH ? (r * (NB / LPH) + t) * HPB + g : (r / (NB >= LPH ? 1 : LPH / NB)) * HPB + g;
   };
-  // the GAT epilogue's per-row operand, loaded once
+  // the GAT epilogue's per-row operand, loaded once; the dropout hash's seed
+  const uint64_t hseed = (EPI && epi.hash_keep) ? gat_epi_seed(epi) : 0;
+  auto keep_of = [&](int64_t k, int hh, float w) -> bool {
+    return (EPI && epi.hash_keep) ? gat_keep(hseed, k * H + hh, epi.thr) : w != 0.0f;
+  };
   float dzv[T];
 #pragma unroll
   for (int t = 0; t < T; ++t)
@@ -259,13 +277,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t) {
             const int hh = j * (H / 8) + t;
-            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
             if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
           const int hh = j / DUP;
-          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
           if (k < end && j % DUP == 0) out[obase + hh] = sv[0];
         }
       } else {
@@ -276,13 +294,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t) {
             const int hh = (r * (NB / LPH) + t) * HPB + g;
-            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], ew[u][t], dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
             if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
           const int hh = (r / DUP) * HPB + g;
-          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], ew[u][0], dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
           if (k < end && r % DUP == 0) out[obase + hh] = sv[0];
         }
       }
@@ -793,6 +811,35 @@ int dglhip_gat_attention_grad_rowsum_ranges_device(
                "null pointer argument");
   const GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi, drop_scale, apply_exp,
                    grad_rowsum};
+  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
+                         nullptr, dout, ft, grad, epi, stream);
+  API_END();
+}
+
+int dglhip_gat_attention_grad_keep_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft, const float* attn, const float* dz, float alpha,
+    float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream_) {
+  API_BEGIN();
+  DGLHIP_CHECK(grad_rowsum == nullptr || dglhip_gat_attention_grad_rowsum_ok(feat_len, num_heads),
+               "fused row sums: unsupported shape F = " << feat_len << ", H = " << num_heads);
+  DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(row_beg && row_end && indices && dout && ft && attn && grad,
+               "null pointer argument");
+  const bool drop = drop_p > 0.0f;
+  GatEpi epi{attn, nullptr, dz, alpha, clamp_lo, clamp_hi, drop ? 1.0f / (1.0f - drop_p) : 1.0f,
+             apply_exp, grad_rowsum};
+  epi.hash_keep = drop ? 1 : 0;
+  epi.seed = seed;
+  epi.seed_off = seed_offset;
+  epi.thr = drop ? gat_drop_threshold(drop_p) : 0u;
   launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
                          nullptr, dout, ft, grad, epi, stream);
   API_END();

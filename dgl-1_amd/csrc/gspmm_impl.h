@@ -21,6 +21,33 @@
 
 namespace dglhip {
 
+// GAT attention dropout: keep(k, h) = hash(seed, k * H + h) >= threshold, a
+// stateless counter hash shared by the fused forward (gat_fused.hip), the
+// backward epilogues (gspmm.hip) and the host mask.
+// lowbias32 (a 32-bit integer finaliser); two rounds over the 64-bit index
+__host__ __device__ __forceinline__ uint32_t gat_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+
+__host__ __device__ __forceinline__ bool gat_keep(uint64_t seed, int64_t idx, uint32_t thr) {
+  const uint64_t i = static_cast<uint64_t>(idx);
+  const uint32_t r = gat_mix32(gat_mix32(static_cast<uint32_t>(i) ^ static_cast<uint32_t>(seed)) ^
+                               (static_cast<uint32_t>(i >> 32) + static_cast<uint32_t>(seed >> 32) +
+                                0x9e3779b9u));
+  return r >= thr;
+}
+
+// keep iff hash >= threshold: P(keep) = 1 - p
+static inline uint32_t gat_drop_threshold(float p) {
+  const double t = static_cast<double>(p) * 4294967296.0;
+  return t >= 4294967295.0 ? 0xffffffffu : static_cast<uint32_t>(t);
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 

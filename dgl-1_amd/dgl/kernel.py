@@ -1715,11 +1715,12 @@ class _EdgeAttention(torch.autograd.Function):
         # d/dx clamp(exp(lrelu(x))): out * lrelu'(x) where not clamped
         inside = (out > ctx.lo) & (out < ctx.hi)
         if ctx.apply_exp:
-            # lrelu(x) = log(out); slope alpha where lrelu(x) < 0  <=>  out < 1
-            slope = torch.where(out < 1, torch.full_like(out, ctx.alpha), torch.ones_like(out))
+            # lrelu(x) = log(out); torch's leaky_relu backward takes the slope
+            # alpha where x <= 0 (x == 0 included)  <=>  out <= 1
+            slope = torch.where(out <= 1, torch.full_like(out, ctx.alpha), torch.ones_like(out))
             g = dout * out * slope
         else:
-            slope = torch.where(out < 0, torch.full_like(out, ctx.alpha), torch.ones_like(out))
+            slope = torch.where(out <= 0, torch.full_like(out, ctx.alpha), torch.ones_like(out))
             g = dout * slope
         g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
         adj = ctx.adj
@@ -1885,11 +1886,11 @@ class _GATAggregate(torch.autograd.Function):
                 a = w = None
         ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp, ctx.p = adj, alpha, lo, hi, \
             apply_exp, p
+        # the dropout seed as this call used it (a captured call's device
+        # counter moves on at the next call): the backward recomputes keep bits
+        ctx.seed = int(seed)
+        ctx.seed_off = None if (seed_off is None or p == 0 or not need) else seed_off.clone()
         if ctx.use_t:
-            # the dropout seed as this call used it (a captured call's device
-            # counter moves on at the next call)
-            ctx.seed = int(seed)
-            ctx.seed_off = None if (seed_off is None or p == 0) else seed_off.clone()
             ctx.D = D
             ctx.save_for_backward(ft2, el, er)
         else:
@@ -1933,6 +1934,14 @@ class _GATAggregate(torch.autograd.Function):
                 er_sum = (torch.zeros(fwd.num_rows, H, dtype=torch.float32, device=ft2.device)
                           if fuse_er else None)
                 for b in range(len(cuts) - 1):
+                    if w is not None:  # keep bits from the forward's hash, not w != 0
+                        check_call(LIB.dglhip_gat_attention_grad_keep_ranges_device(
+                            fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
+                            ptr(fwd.row_order), ptr(fwd.indices), ptr(d_ft), ptr(ft2c), ptr(a),
+                            ptr(dz), float(ctx.alpha), float(ctx.lo), float(ctx.hi),
+                            1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,
+                            ptr(ctx.seed_off), ptr(g), ptr(er_sum), _stream_of(ft2.device)))
+                        continue
                     check_call(LIB.dglhip_gat_attention_grad_rowsum_ranges_device(
                         fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
                         ptr(fwd.row_order), ptr(fwd.indices),
@@ -1943,17 +1952,18 @@ class _GATAggregate(torch.autograd.Function):
                     d_er = er_sum
             else:
                 d_a = _run_sddmm_dot(fwd, d_ft, ft2.contiguous(), fwd.nnz, H, slot=True)
-                if w is not None:  # dropout's backward: the kept pairs, scaled
-                    d_a = torch.where(w != 0, d_a * scale, torch.zeros_like(d_a))
+                if w is not None:  # dropout's backward: the kept pairs (the hash), scaled
+                    keep = gat_dropout_mask(fwd.nnz, H, ctx.p, ctx.seed).to(d_a.device)
+                    d_a = torch.where(keep, d_a * scale, torch.zeros_like(d_a))
                 if d_z is not None:
                     d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
                 # the attention's backward (_EdgeAttention.backward, slot order)
                 inside = (a > ctx.lo) & (a < ctx.hi)
                 if ctx.apply_exp:
-                    slope = torch.where(a < 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                    slope = torch.where(a <= 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
                     g = d_a * a * slope
                 else:
-                    slope = torch.where(a < 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                    slope = torch.where(a <= 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
                     g = d_a * slope
                 g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
             if need_el:

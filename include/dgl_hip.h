@@ -381,7 +381,8 @@ int dglhip_gsddmm_host(int op, int64_t num_rows, int64_t feat_len,
  *   t = attn_drop ? (attn_drop[k, h] != 0 ? t * drop_scale : 0) : t
  *   t = dz ? t + dz[r, h] : t                (the normaliser's gradient)
  *   grad[k, h] = lo < a < hi ? (apply_exp ? (t * a) * s : t * s) : 0,
- *   a = attn[k, h], s = alpha where a < 1 (exp) / a < 0, else 1
+ *   a = attn[k, h], s = alpha where a <= 1 (exp) / a <= 0 (the logit <= 0, as
+ *   torch's leaky_relu backward), else 1
  * attn, attn_drop, grad: [nnz, H] slot order; dout: [num_rows, F]; ft:
  * [num_src, F]; dz: [num_rows, H] or NULL; attn_drop NULL without dropout. */
 int dglhip_gat_attention_grad_device(int64_t num_rows, int64_t feat_len, int64_t num_heads,
@@ -540,6 +541,17 @@ int dglhip_gat_backward_t_device(
 int dglhip_rowsum_heads8_device(int64_t num_rows, const int64_t* indptr,
                                 const int32_t* row_order, const float* vals, float* out,
                                 void* stream);
+
+/* dglhip_gat_attention_grad_rowsum_ranges_device with the dropout's keep
+ * bits recomputed from the forward's hash (seed + *seed_offset, drop_p) instead
+ * of read as attn_drop != 0: a kept pair whose attention is exactly 0 keeps
+ * its gradient. grad_rowsum may be NULL. */
+int dglhip_gat_attention_grad_keep_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft, const float* attn, const float* dz, float alpha,
+    float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream);
 
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the

@@ -379,3 +379,43 @@ def test_rowsum_heads8_is_the_copy_e_chain():
         n, kernel.ptr(adj.fwd.indptr), kernel.ptr(adj.fwd.row_order), kernel.ptr(vals),
         kernel.ptr(out), kernel._stream_of(dev)))
     assert torch.equal(out, ref.reshape(n, 8))
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("H,D", [(8, 8), (8, 16)])
+def test_dropout_keeps_pairs_with_zero_attention(device, H, D):
+    """A kept (slot, head) pair whose attention is exactly 0 (no exp, a zero
+    logit) keeps its gradient: the backward's keep bits come from the
+    forward's hash, not from the dropped copy being nonzero (r03 ADVICE).
+    Checked against torch autograd through the same mask (1e-5)."""
+    dev = _dev(device)
+    g = _graph(n=400, m=6000, seed=9)
+    adj = g.sparse_adjacency(dev)
+    n, E = g.number_of_nodes(), g.number_of_edges()
+    gen = torch.Generator().manual_seed(10)
+    ft0 = torch.randn(n, H, D, generator=gen)
+    el0 = torch.randn(n, H, generator=gen)
+    er0 = torch.randn(n, H, generator=gen)
+    el0[: n // 2] = 0.0
+    er0[: n // 2] = 0.0  # edges among the first half: logit exactly 0
+    p, seed = 0.5, 4242
+    gout = torch.randn(n, H, D, generator=gen)
+    gz = torch.randn(n, H, 1, generator=gen)
+    ft, el, er = (x.clone().to(dev).requires_grad_(True) for x in (ft0, el0, er0))
+    fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, clamp=(-10.0, 10.0), attn_drop=p,
+                                 apply_exp=False, seed=seed)
+    torch.autograd.backward([fs, z], [gout.to(dev), gz.to(dev)])
+    # reference: torch autograd over the slot-ordered attention, same mask
+    fwd = adj.fwd
+    u = fwd.indices.long().cpu()
+    v = fwd.row_ids().cpu()
+    keep = kernel.gat_dropout_mask(E, H, p, seed)
+    elr, err, ftr = (x.double().requires_grad_(True) for x in (el0, er0, ft0))
+    a = F.leaky_relu(elr[u] + err[v], 0.2).clamp(-10.0, 10.0)
+    w = torch.where(keep, a * (1.0 / (1.0 - p)), torch.zeros_like(a))
+    fsr = torch.zeros(n, H, D, dtype=torch.float64).index_add(0, v, w.unsqueeze(-1) * ftr[u])
+    zr = torch.zeros(n, H, dtype=torch.float64).index_add(0, v, a)
+    torch.autograd.backward([fsr, zr], [gout.double(), gz.double().squeeze(-1)])
+    assert bool(((a == 0) & keep).any())  # the case is present
+    for got, ref in ((el.grad, elr.grad), (er.grad, err.grad), (ft.grad, ftr.grad)):
+        torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-5, atol=1e-4)
