@@ -402,6 +402,7 @@ Timing g_timing;
 int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
 int g_cache_policy = -1;
 int g_gather_buf = 0;
+int g_row_pol = 0;
 int g_sddmm_alt = 0;
 
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
@@ -884,6 +885,13 @@ int dglhip_set_gather_mode(int buffer_descriptors) {
   DGLHIP_CHECK(buffer_descriptors == 0 || buffer_descriptors == 1,
                "unknown gather mode " << buffer_descriptors);
   g_gather_buf = buffer_descriptors;
+  API_END();
+}
+
+int dglhip_set_row_policy(int policy) {
+  API_BEGIN();
+  DGLHIP_CHECK(policy >= 0 && policy <= 3, "unknown running-row policy " << policy);
+  g_row_pol = policy;
   API_END();
 }
 

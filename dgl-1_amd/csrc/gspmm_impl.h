@@ -290,6 +290,49 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
   return acc;
 }
 
+// Cache policy of the running output row of accumulating items (the
+// blocked schedule's launches after the first read and rewrite each item's
+// row: 30 % of the fabric bytes, streaming through the L2s that hold the
+// gathered source block). RP (dglhip_set_row_policy, a study knob):
+//   0  plain load and store;
+//   1  non-temporal load and store;
+//   2  non-temporal load, store with sc1 (the line leaves the XCD's L2);
+//   3  load with sc0 sc1 and store with sc1 (system scope both ways).
+// Same values in every variant.
+template <int VEC, int RP>
+__device__ __forceinline__ typename Vec<VEC>::T load_out(const float* row, int64_t f0) {
+  typedef typename Vec<VEC>::T V;
+  if (RP == 1 || RP == 2) return __builtin_nontemporal_load(reinterpret_cast<const V*>(row + f0));
+  if (RP == 3 && VEC == 2) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(row), 0, 0x7fffffff, 0x00020000);
+    const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(
+        r, static_cast<uint32_t>(f0 * int64_t(sizeof(float))), 0, 1 | 16);
+    return *reinterpret_cast<const V*>(&w);
+  }
+  return ldv<VEC>(row + f0);
+}
+
+template <int VEC, int RP>
+__device__ __forceinline__ void store_out(float* row, int64_t f0, typename Vec<VEC>::T v) {
+  typedef typename Vec<VEC>::T V;
+  if (RP == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<V*>(row + f0));
+    return;
+  }
+  if ((RP == 2 || RP == 3) && VEC == 2) {
+    typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff,
+                                                                       0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b64(*reinterpret_cast<const u32x2*>(&v), r,
+                                          static_cast<uint32_t>(f0 * int64_t(sizeof(float))),
+                                          0, 16);
+    return;
+  }
+  stv<VEC>(row + f0, v);
+}
+
 // Sum-reduce kernel (also MEAN). GROUP lanes per work item, VEC floats per
 // lane. A work item is a whole row (CHUNKED = false: item i = row_order[i]),
 // or a slot range [chunk_beg[i], chunk_end[i]) whose sum goes to out[i, :]
@@ -298,7 +341,7 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 // MEAN and ACCUM on whole rows the row's mean is added to the value in
 // out[i, :] (out + mean: a sum of two terms, the same bits either way round).
 template <int VEC, int GROUP, int UNROLL, int MSG, int EM, bool MEAN, bool CHUNKED,
-          bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT, bool BUF = false>
+          bool ACCUM, bool PIPE = false, int POL = POL_DEFAULT, bool BUF = false, int RP = 0>
 __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     int64_t num_items, int64_t F, int64_t elen, int64_t ldu,
     const int64_t* __restrict__ indptr,
@@ -334,7 +377,7 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
   for (int64_t f0 = int64_t(gl) * VEC; f0 < F; f0 += int64_t(GROUP) * VEC) {
     const int64_t eoff = EM == EM_HEAD ? f0 / (F / elen) : (EM == EM_FULL ? f0 : 0);
     constexpr bool ADD_MEAN = MEAN && ACCUM && !CHUNKED;
-    V acc = (ACCUM && !ADD_MEAN) ? ldv<VEC>(out + row * F + f0) : Vec<VEC>::zero();
+    V acc = (ACCUM && !ADD_MEAN) ? load_out<VEC, RP>(out + row * F, f0) : Vec<VEC>::zero();
     if (PIPE && MSG == DGLHIP_MSG_COPY_U)
       acc = reduce_range_pipelined<VEC, UNROLL>(acc, beg, end, ldu, f0, indices, ufeat);
     else if (copies_u(MSG) || eid != nullptr)  // uniform branch
@@ -346,7 +389,8 @@ __global__ __launch_bounds__(256) void gspmm_sum_kernel(
     if (!CHUNKED && MEAN && end - beg > 1)
       acc = acc / Vec<VEC>::splat(static_cast<float>(end - beg));
     if (ADD_MEAN) acc = ldv<VEC>(out + row * F + f0) + acc;
-    store_row<VEC, POL>(out + row * F + f0, acc);
+    if (RP) store_out<VEC, RP>(out + row * F, f0, acc);
+    else store_row<VEC, POL>(out + row * F + f0, acc);
   }
 }
 
@@ -562,6 +606,9 @@ extern int g_cache_policy;
 // Row gathers of copy_u + sum at VEC 2 x 64 lanes through buffer descriptors
 // (dglhip_set_gather_mode): 1 on, 0 global loads.
 extern int g_gather_buf;
+// Running-row cache policy of accumulating copy_u + sum items (load_out /
+// store_out; dglhip_set_row_policy): 0 default.
+extern int g_row_pol;
 
 template <int VEC, int GROUP, int MSG, int EM, bool MEAN, int UNROLL_OVERRIDE = 0,
           bool PIPE = false>
@@ -595,6 +642,17 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
       if (pol == POL_NT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT); else DGLHIP_POL_LAUNCH(false, POL_NT); }
       else if (pol == POL_HOT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_HOT); else DGLHIP_POL_LAUNCH(false, POL_HOT); }
       else { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT_OUT); else DGLHIP_POL_LAUNCH(false, POL_NT_OUT); }
+    } else if (POL_OK && a.chunk_beg && a.accumulate && g_row_pol > 0) {
+#define DGLHIP_RP_LAUNCH(RPV)                                                                   \
+  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true, false,    \
+                                       POL_DEFAULT, false, RPV>),                               \
+                     grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,           \
+                     a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,  \
+                     a.row_order, a.chunk_beg, a.chunk_end)
+      if (g_row_pol == 1) DGLHIP_RP_LAUNCH(1);
+      else if (g_row_pol == 2) DGLHIP_RP_LAUNCH(2);
+      else DGLHIP_RP_LAUNCH(3);
+#undef DGLHIP_RP_LAUNCH
     } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
                          grid_1d(blocks), dim3(256), 0, stream,

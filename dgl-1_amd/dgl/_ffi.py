@@ -134,6 +134,7 @@ def _load():
         "dglhip_gspmm_resident_waves": (_c_int, [_c_int, ctypes.POINTER(_c_i64)]),
         "dglhip_set_spmm_variant": (_c_int, [_c_int, _c_int, _c_int, _c_int]),
         "dglhip_set_cache_policy": (_c_int, [_c_int]),
+        "dglhip_set_row_policy": (_c_int, [_c_int]),
         "dglhip_set_gather_mode": (_c_int, [_c_int]),
         "dglhip_set_sddmm_variant": (_c_int, [_c_int]),
         "dglhip_gspmm_short_rows_device": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64,

@@ -655,6 +655,11 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined);
  *   set by the caller, on a CSR copy no other kernel reads) default and the
  *   rest non-temporal; 3 non-temporal output stores only. */
 int dglhip_set_cache_policy(int policy);
+/* Study knob: the cache policy of the running output rows that accumulating
+ * copy_u + sum items (the source-blocked schedule's later launches) read and
+ * rewrite: 0 plain (default), 1 non-temporal load and store, 2 non-temporal
+ * load + sc1 store, 3 sc0 sc1 load + sc1 store. Same values. */
+int dglhip_set_row_policy(int policy);
 /* Synchronises on the recorded events and returns the summed kernel time
  * (ms) and launch count since the last enable/reset. */
 int dglhip_timing_read(double* total_ms, int64_t* launches);
