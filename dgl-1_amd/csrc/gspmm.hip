@@ -890,7 +890,7 @@ int dglhip_set_gather_mode(int buffer_descriptors) {
 
 int dglhip_set_row_policy(int policy) {
   API_BEGIN();
-  DGLHIP_CHECK(policy >= 0 && policy <= 3, "unknown running-row policy " << policy);
+  DGLHIP_CHECK(policy >= 0 && policy <= 4, "unknown running-row policy " << policy);
   g_row_pol = policy;
   API_END();
 }

@@ -297,7 +297,9 @@ __device__ __forceinline__ typename Vec<VEC>::T reduce_range_pipelined(
 //   0  plain load and store;
 //   1  non-temporal load and store;
 //   2  non-temporal load, store with sc1 (the line leaves the XCD's L2);
-//   3  load with sc0 sc1 and store with sc1 (system scope both ways).
+//   3  load with sc0 sc1 and store with sc1 (system scope both ways);
+//   4  plain load, store with sc1.
+// With 2-4 the first launch (which only writes its rows) stores with sc1 too.
 // Same values in every variant.
 template <int VEC, int RP>
 __device__ __forceinline__ typename Vec<VEC>::T load_out(const float* row, int64_t f0) {
@@ -321,7 +323,7 @@ __device__ __forceinline__ void store_out(float* row, int64_t f0, typename Vec<V
     __builtin_nontemporal_store(v, reinterpret_cast<V*>(row + f0));
     return;
   }
-  if ((RP == 2 || RP == 3) && VEC == 2) {
+  if ((RP == 2 || RP == 3 || RP == 4) && VEC == 2) {
     typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff,
                                                                        0x00020000);
@@ -651,8 +653,16 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                      a.row_order, a.chunk_beg, a.chunk_end)
       if (g_row_pol == 1) DGLHIP_RP_LAUNCH(1);
       else if (g_row_pol == 2) DGLHIP_RP_LAUNCH(2);
-      else DGLHIP_RP_LAUNCH(3);
+      else if (g_row_pol == 3) DGLHIP_RP_LAUNCH(3);
+      else DGLHIP_RP_LAUNCH(4);
 #undef DGLHIP_RP_LAUNCH
+    } else if (POL_OK && a.chunk_beg && !a.accumulate && g_row_pol >= 2) {
+      // the first launch writes its rows: the same store policy
+      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false, false,
+                                           POL_DEFAULT, false, 4>),
+                         grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,
+                         a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,
+                         a.row_order, a.chunk_beg, a.chunk_end);
     } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
                          grid_1d(blocks), dim3(256), 0, stream,

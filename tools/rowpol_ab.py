@@ -30,10 +30,10 @@ def main():
     del src, dst
     h = torch.rand(n, 128, device=dev) * 2 - 1
     ref = kernel.gspmm(adj, "copy_u", "sum", h)
-    res = {p: [] for p in range(4)}
+    res = {p: [] for p in range(5)}
     same = {}
     for _ in range(args.rounds):
-        for p in range(4):
+        for p in range(5):
             kernel.check_call(kernel.LIB.dglhip_set_row_policy(p))
             out = kernel.gspmm(adj, "copy_u", "sum", h)
             torch.cuda.synchronize()
