@@ -628,6 +628,25 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                   : g_cache_policy >= 0 ? g_cache_policy
                   : a.nt_out ? POL_NT_OUT : POL_DEFAULT;
   timed_launch(stream, [&] {
+    // the running-row cache policy study (dglhip_set_row_policy): only the
+    // shapes POL_OK covers are instantiated
+    if constexpr (POL_OK) {
+      if (a.chunk_beg && g_row_pol > 0 && (a.accumulate || g_row_pol >= 2)) {
+#define DGLHIP_RP_LAUNCH(ACC, RPV)                                                              \
+  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, ACC, false,     \
+                                       POL_DEFAULT, false, RPV>),                               \
+                     grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,           \
+                     a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,  \
+                     a.row_order, a.chunk_beg, a.chunk_end)
+        if (!a.accumulate) DGLHIP_RP_LAUNCH(false, 4);  // the first launch: stores only
+        else if (g_row_pol == 1) DGLHIP_RP_LAUNCH(true, 1);
+        else if (g_row_pol == 2) DGLHIP_RP_LAUNCH(true, 2);
+        else if (g_row_pol == 3) DGLHIP_RP_LAUNCH(true, 3);
+        else DGLHIP_RP_LAUNCH(true, 4);
+#undef DGLHIP_RP_LAUNCH
+        return;
+      }
+    }
 #define DGLHIP_POL_LAUNCH_B(CH, P, B)                                                      \
   hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, false, CH, false, false, P, B>), \
                      grid_1d(blocks), dim3(256), 0, stream, a.num_items,   \
@@ -644,25 +663,6 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
       if (pol == POL_NT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT); else DGLHIP_POL_LAUNCH(false, POL_NT); }
       else if (pol == POL_HOT) { if (ch) DGLHIP_POL_LAUNCH(true, POL_HOT); else DGLHIP_POL_LAUNCH(false, POL_HOT); }
       else { if (ch) DGLHIP_POL_LAUNCH(true, POL_NT_OUT); else DGLHIP_POL_LAUNCH(false, POL_NT_OUT); }
-    } else if (POL_OK && a.chunk_beg && a.accumulate && g_row_pol > 0) {
-#define DGLHIP_RP_LAUNCH(RPV)                                                                   \
-  hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true, false,    \
-                                       POL_DEFAULT, false, RPV>),                               \
-                     grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,           \
-                     a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,  \
-                     a.row_order, a.chunk_beg, a.chunk_end)
-      if (g_row_pol == 1) DGLHIP_RP_LAUNCH(1);
-      else if (g_row_pol == 2) DGLHIP_RP_LAUNCH(2);
-      else if (g_row_pol == 3) DGLHIP_RP_LAUNCH(3);
-      else DGLHIP_RP_LAUNCH(4);
-#undef DGLHIP_RP_LAUNCH
-    } else if (POL_OK && a.chunk_beg && !a.accumulate && g_row_pol >= 2) {
-      // the first launch writes its rows: the same store policy
-      hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, false, false,
-                                           POL_DEFAULT, false, 4>),
-                         grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,
-                         a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,
-                         a.row_order, a.chunk_beg, a.chunk_end);
     } else if (a.chunk_beg && a.accumulate)
       hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, true>),
                          grid_1d(blocks), dim3(256), 0, stream,
