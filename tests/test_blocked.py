@@ -535,3 +535,26 @@ def test_one_csr_two_block_counts_device():
                 assert np.array_equal(out.numpy(), O.spmm_coo(n, dst, src, H.numpy()))
     finally:
         kernel._BLOCK_TABLE_MIN, kernel._BLOCK_BYTES, kernel._BLOCK_MIN_SLOTS = old
+
+
+@pytest.mark.gpu
+def test_row_policies_same_bits():
+    """The running-row cache policies of the blocked launches
+    (dglhip_set_row_policy: non-temporal / sc1 loads and stores) change where
+    lines live, not values: every policy gives the default's bits."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 19, True)
+    adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                          kernel.ORDER_EID, dev)
+    H = torch.randn(n, 128, generator=torch.Generator().manual_seed(20)).to(dev)
+    assert kernel.blocked_schedule(adj, H) >= 2
+    ref = kernel.gspmm(adj, "copy_u", "sum", H)
+    try:
+        for pol in range(5):
+            kernel.check_call(kernel.LIB.dglhip_set_row_policy(pol))
+            assert torch.equal(kernel.gspmm(adj, "copy_u", "sum", H), ref)
+    finally:
+        kernel.check_call(kernel.LIB.dglhip_set_row_policy(0))
