@@ -262,7 +262,7 @@ __device__ __forceinline__ void gat_batch(
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false>
+template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false, int RP = 0>
 __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     int64_t num_rows, int64_t D, const int64_t* __restrict__ row_beg,
     const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     V acc = Vec<VEC>::zero();
     float zacc = 0.0f;
     if (accumulate && active) {
-      acc = ldv<VEC>(out_ft + row * F + f0);
+      acc = load_out<VEC, RP>(out_ft + row * F, f0);
       if (f0 - h * D == 0) zacc = out_z[row * H + h];
     }
     int64_t k = beg;
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
                                             rc, indices, el, ft, tab, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
                                      s_w[wi], a_out, w_out, acc, zacc);
     if (active) {
-      stv<VEC>(out_ft + row * F + f0, acc);
+      store_out<VEC, RP>(out_ft + row * F, f0, acc);
       if (f0 - h * D == 0) out_z[row * H + h] = zacc;
     }
   }
@@ -368,7 +368,7 @@ __device__ __forceinline__ float dpp_shl(float v) {
                                                     false));
 }
 
-template <bool DROP, bool SMALL>
+template <bool DROP, bool SMALL, int RP = 0>
 __global__ __launch_bounds__(256) void gat_backward_t_kernel(
     int64_t num_items, const int32_t* __restrict__ item_row, const int64_t* __restrict__ item_beg,
     const int64_t* __restrict__ item_end, int by_row, int accumulate,
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
   const int hc = lane & 7, jc = lane >> 3;
   const float elc = el[row * H + hc];
   const V ftv = ldv<2>(ft + row * F + f0);
-  V acc = accumulate ? ldv<2>(d_ft + row * F + f0) : Vec<2>::zero();
+  V acc = accumulate ? load_out<2, RP>(d_ft + row * F, f0) : Vec<2>::zero();
   float elacc = (accumulate && head_lane) ? d_el[row * H + h] : 0.0f;
   float* lw = s_w[wi];
   float* ld = s_d[wi];
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
-  stv<2>(d_ft + row * F + f0, acc);
+  store_out<2, RP>(d_ft + row * F, f0, acc);
   if (head_lane) d_el[row * H + h] = elacc;
 }
 
@@ -615,6 +615,26 @@ int dglhip_gat_aggregate_ranges_device(
     // 6.49; one-float lanes level: Pubmed's 8 x 8 and 8 x 3;
     // tools/gat_early_ab.py); variant 2 keeps them after it, 3 before it
     const bool early = g_gat_variant == 3 || (g_gat_variant == 0 && v2);
+    if (num_heads == 8 && v2 && early && (g_row_pol == 2 || g_row_pol == 4)) {
+      // the running rows' cache policy (dglhip_set_row_policy) on the 8-head
+      // two-float shape (the Reddit-shaped 8 x 16 layer)
+      timed_launch(stream, [&] {
+#define DGLHIP_GATRP(DD, SM, RPV)                                                              \
+  hipLaunchKernelGGL((gat_aggregate_lds_kernel<8, 2, DD, SM, true, RPV>), grid_1d(blocks),       \
+                     dim3(256), 0, stream, num_rows, head_dim, row_beg, row_end, accumulate,    \
+                     indices, row_order, el, er, ft, alpha, clamp_lo, clamp_hi, apply_exp, seed, \
+                     seed_offset, thr, scale, out_ft, out_z, attn_out, attn_drop_out, tbytes)
+        if (g_row_pol == 2) {
+          if (drop) { if (small) DGLHIP_GATRP(true, true, 2); else DGLHIP_GATRP(true, false, 2); }
+          else { if (small) DGLHIP_GATRP(false, true, 2); else DGLHIP_GATRP(false, false, 2); }
+        } else {
+          if (drop) { if (small) DGLHIP_GATRP(true, true, 4); else DGLHIP_GATRP(true, false, 4); }
+          else { if (small) DGLHIP_GATRP(false, true, 4); else DGLHIP_GATRP(false, false, 4); }
+        }
+#undef DGLHIP_GATRP
+      });
+      return 0;
+    }
     timed_launch(stream, [&] {
 #define DGLHIP_GATL_E(HH, VV, DD, SM, EE)                                                    \
   hipLaunchKernelGGL((gat_aggregate_lds_kernel<HH, VV, DD, SM, EE>), grid_1d(blocks),        \
@@ -708,17 +728,24 @@ int dglhip_gat_backward_t_device(
   const int64_t tbytes = num_rows * num_heads * head_dim * int64_t(sizeof(float));
   const bool small = tbytes < (int64_t(1) << 31);
   timed_launch(stream, [&] {
-#define DGLHIP_GBT(DD, SM)                                                                    \
-  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM>), grid_1d(blocks), dim3(256), 0, stream,   \
-                     num_items, item_row, item_beg, item_end, by_row, accumulate, cols, fslot, \
-                     ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp, seed,         \
+#define DGLHIP_GBT_R(DD, SM, RPV)                                                             \
+  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM, RPV>), grid_1d(blocks), dim3(256), 0,      \
+                     stream, num_items, item_row, item_beg, item_end, by_row, accumulate, cols, \
+                     fslot, ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp, seed,   \
                      seed_offset, thr, scale, d_ft, d_el, grad, tbytes)
+#define DGLHIP_GBT(DD, SM)                                                                    \
+  do {                                                                                        \
+    if (g_row_pol == 2) DGLHIP_GBT_R(DD, SM, 2);                                              \
+    else if (g_row_pol == 4) DGLHIP_GBT_R(DD, SM, 4);                                         \
+    else DGLHIP_GBT_R(DD, SM, 0);                                                             \
+  } while (0)
     if (drop) {
       if (small) DGLHIP_GBT(true, true); else DGLHIP_GBT(true, false);
     } else {
       if (small) DGLHIP_GBT(false, true); else DGLHIP_GBT(false, false);
     }
 #undef DGLHIP_GBT
+#undef DGLHIP_GBT_R
   });
   API_END();
 }
