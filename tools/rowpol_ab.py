@@ -18,6 +18,37 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dgl-1_amd")]
 from dgl import data, kernel  # noqa: E402
 
 
+def block_sweep(adj, h, ref, args):
+    """ms per call at 5 / 6 / 7 / 8 / 9 MiB source blocks under row policies 0, 2 and
+    4 (interleaved), and whether each keeps the bits."""
+    old_bytes = kernel._BLOCK_BYTES
+    res, same = {}, {}
+    try:
+        for _ in range(args.rounds):
+            for mib in (5, 6, 7, 8, 9):
+                kernel._BLOCK_BYTES = mib << 20
+                for p in (0, 2, 4):
+                    kernel.check_call(kernel.LIB.dglhip_set_row_policy(p))
+                    o = kernel.gspmm(adj, "copy_u", "sum", h)
+                    torch.cuda.synchronize()
+                    key = "%d MiB / policy %d (%d launches)" % (
+                        mib, p, kernel.blocked_schedule(adj, h))
+                    same[key] = bool(torch.equal(o, ref))
+                    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(
+                        enable_timing=True)
+                    s.record()
+                    for _ in range(args.calls):
+                        kernel.gspmm(adj, "copy_u", "sum", h)
+                    e.record()
+                    e.synchronize()
+                    res.setdefault(key, []).append(s.elapsed_time(e) / args.calls)
+    finally:
+        kernel._BLOCK_BYTES = old_bytes
+        kernel.check_call(kernel.LIB.dglhip_set_row_policy(0))
+    return {"ms_per_call": res, "min": {k: min(v) for k, v in res.items()},
+            "bit_identical": same}
+
+
 def gat_ab(adj, n, dev, args):
     """The GAT layer 8 x 16 on the same graph: forward (training) and forward +
     backward wall ms per policy 0 / 2 / 4, outputs and gradients vs policy 0."""
@@ -66,6 +97,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--gat", action="store_true")
+    ap.add_argument("--sweep", action="store_true")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     src, dst, n = data.reddit_like(scale=1, seed=0, device=dev)
@@ -91,6 +123,8 @@ def main():
     kernel.check_call(kernel.LIB.dglhip_set_row_policy(0))
     out = {"ms_per_call": res, "min": {p: min(v) for p, v in res.items()},
            "bit_identical": same, "launches": kernel.blocked_schedule(adj, h)}
+    if args.sweep:
+        out["block_sweep"] = block_sweep(adj, h, ref, args)
     if args.gat:
         out["gat"] = gat_ab(adj, n, dev, args)
     line = json.dumps(out)
