@@ -402,7 +402,10 @@ Timing g_timing;
 int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
 int g_cache_policy = -1;
 int g_gather_buf = 0;
-int g_row_pol = 0;
+// running rows of the blocked launches: non-temporal loads, sc1 stores (the
+// line leaves the XCD's L2): Reddit-shaped headline 3.83 -> 3.74 ms, GAT 8 x 16
+// forward + backward 17.01 -> 16.94 (tools/rowpol_ab.py, profiles/r04/rowpol_ab.json)
+int g_row_pol = 2;
 int g_sddmm_alt = 0;
 
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {

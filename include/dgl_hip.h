@@ -657,9 +657,10 @@ int dglhip_set_spmm_variant(int vec, int group, int unroll, int pipelined);
 int dglhip_set_cache_policy(int policy);
 /* Study knob: the cache policy of the running output rows that accumulating
  * copy_u + sum items (the source-blocked schedule's later launches) read and
- * rewrite: 0 plain (default), 1 non-temporal load and store, 2 non-temporal
- * load + sc1 store, 3 sc0 sc1 load + sc1 store, 4 plain load + sc1 store
- * (2-4: the first launch's stores with sc1 too). Same values. */
+ * rewrite (and the fused GAT layer's 8-head rows): 0 plain, 1 non-temporal
+ * load and store, 2 non-temporal load + sc1 store (the default), 3 sc0 sc1
+ * load + sc1 store, 4 plain load + sc1 store (2-4: the first launch's stores
+ * with sc1 too). Same values. */
 int dglhip_set_row_policy(int policy);
 /* Synchronises on the recorded events and returns the summed kernel time
  * (ms) and launch count since the last enable/reset. */
