@@ -78,6 +78,12 @@ def test_bench_two_ranks_without_outer_launcher():
     cb = r["cpu_baseline"]
     assert cb["kind"] == "reference" and cb["value"] > 0
     assert cb["build_kernel"]["bit_identical_to_reference"]
+    # the fixed-graph block beside the weak-scaled line (r03 verdict "Next" 6)
+    st = r["strong"]
+    assert st["scaling"] == "strong" and st["n_gpus"] == 2 and st["value"] > 0
+    assert "the N = 1 graph" in st["config"]
+    assert [x["rank"] for x in st["roofline"]["per_rank"]] == [0, 1]
+    assert st["halo_exchange"]["mode"] in ("allgather", "alltoall")
     rm = r["rmat12"]
     assert rm["n_gpus"] == 2 and rm["scaling"] == "strong"
     assert [x["rank"] for x in rm["roofline"]["per_rank"]] == [0, 1]
