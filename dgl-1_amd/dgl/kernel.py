@@ -768,10 +768,11 @@ def _column_span(csr):
     return span
 
 
-def _block_plan(csr, ufeat2, feat_len):
+def _block_plan(csr, ufeat2, feat_len, block_bytes=None):
     """The segment CSRs of the blocked schedule for ``csr`` (cached), or None
     when the schedule does not apply or would reorder some row's chain. The
-    blocks cut the referenced column range evenly."""
+    blocks cut the referenced column range evenly (``block_bytes`` of source
+    rows each, default _BLOCK_BYTES)."""
     if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
         return None
     ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
@@ -779,7 +780,7 @@ def _block_plan(csr, ufeat2, feat_len):
     if row_bytes <= _BLOCK_MIN_ROW_BYTES:
         return None
     lo, hi = _column_span(csr)
-    B = _block_count(csr, (hi - lo) * row_bytes)
+    B = _block_count(csr, (hi - lo) * row_bytes, block_bytes)
     if not B:
         return None
     if _split_threshold(csr):  # a row long enough to need the heavy-row split
@@ -885,6 +886,9 @@ def _block_split(csr, B, lo, hi):
 _GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11 MiB
 # the fused forward when no attention is stored (inference)
 _GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 9 << 20))
+# the one-pass GAT backward over the transpose (its own per-row work: the
+# attention recomputed per pair, the dot's exchanges, the epilogue)
+_GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 6 << 20))
 
 
 def _block_cuts(csr, row_bytes, block_bytes=None):
@@ -2000,7 +2004,7 @@ def _gat_backward_t(ctx, d_ft, d_z):
     tail = (ptr(ft2), ptr(el), ptr(er), ptr(dz), ptr(dout), float(ctx.alpha), float(ctx.lo),
             float(ctx.hi), 1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,
             ptr(ctx.seed_off), ptr(d_ft2), ptr(d_el), ptr(g), _stream_of(dev))
-    plan = _block_plan(bwd, dout, F) if bwd.nnz else None
+    plan = _block_plan(bwd, dout, F, _GAT_BWD_BLOCK_BYTES) if bwd.nnz else None
     if plan is None:
         check_call(LIB.dglhip_gat_backward_t_device(
             bwd.num_rows, ptr(bwd.row_order), ptr(bwd.indptr), ptr(bwd.indptr[1:]), 1, 0,
