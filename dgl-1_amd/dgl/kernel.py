@@ -887,8 +887,11 @@ _GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11
 # the fused forward when no attention is stored (inference)
 _GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 9 << 20))
 # the one-pass GAT backward over the transpose (its own per-row work: the
-# attention recomputed per pair, the dot's exchanges, the epilogue)
-_GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 6 << 20))
+# attention recomputed per pair, the dot's exchanges, the epilogue): larger
+# slices, as the forward's (Reddit-shaped 8 x 16, forward + backward: 4 / 6 /
+# 8 / 11 / 14 / 18 MiB 17.97 / 16.86 / 16.48 / 16.18 / 16.25 / 16.39 ms, the
+# same bits; tools/gat_bwd_sweep.py, profiles/r04/gat_bwd_sweep.json)
+_GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 11 << 20))
 
 
 def _block_cuts(csr, row_bytes, block_bytes=None):
