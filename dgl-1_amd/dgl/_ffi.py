@@ -100,6 +100,7 @@ def _load():
                                                         ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp,
                                                         _vp]),
         "dglhip_set_gat_variant": (_c_int, [_c_int]),
+        "dglhip_set_gat_bwd_variant": (_c_int, [_c_int]),
         "dglhip_gat_attention_grad_device": (_c_int, [_c_i64, _c_i64, _c_i64, _vp, _vp, _vp, _vp,
                                                       _vp, _vp, _vp, ctypes.c_float,
                                                       ctypes.c_float, ctypes.c_float, _c_int,

@@ -575,6 +575,13 @@ int dglhip_gat_aggregate_ranges_device(
  * head), shared through LDS (H in {1, 2, 4, 8, 16}). Same bits. */
 int dglhip_set_gat_variant(int variant);
 
+/* Study knob for dglhip_gat_backward_t_device: bits 0-1 the attention
+ * gradient's store (0 default, 1 non-temporal, 2 none — the gradient buffer is
+ * then left unwritten, so d_er is not valid: timing only); bit 2 the first
+ * form of the kernel (each batch's loads in program order). Values 0-2 and
+ * 4-6. Same bits. */
+int dglhip_set_gat_bwd_variant(int variant);
+
 /* The attention-dropout mask of dglhip_gat_aggregate_device: keep[i] = 1 for
  * the kept (slot, head) pairs i = k * H + h, a stateless hash of (seed, i). */
 int dglhip_gat_dropout_mask_host(int64_t num_slots, int64_t num_heads, float drop_p,
