@@ -214,19 +214,34 @@ __device__ __forceinline__ void gat_batch(
   constexpr int SPP = 64 / H;               // slots covered per pass of the wave
   constexpr int PPL = (U + SPP - 1) / SPP;  // attention values per lane per batch
   V u[U];
+  float lg[PPL];  // EARLY: the pairs' logits, loaded ahead of the row gathers
   if (EARLY) {
-    // the feature rows first: their latency then overlaps the logit gathers
-    // and the attention (study variant dglhip_set_gat_variant(3))
+    // the batch's column ids through the scalar cache (one wide load when
+    // FULL); each lane's pair columns selected from them, so the pairs' logit
+    // loads go out first and the 16 feature-row gathers right behind them:
+    // the attention is computed while the rows are in flight
+    int cj[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) cj[j] = indices[k + (FULL || j < nb ? j : 0)];
+#pragma unroll
+    for (int i = 0; i < PPL; ++i) {
+      const int j = jc + SPP * i;
+      int c = cj[SPP * i < U ? SPP * i : 0];
+#pragma unroll
+      for (int t = 1; t < SPP; ++t)
+        if (SPP * i + t < U) c = jc == t ? cj[SPP * i + t] : c;
+      if (!((SPP * PPL == U || j < U) && (FULL || j < nb))) c = cj[0];
+      lg[i] = el[int64_t(c) * H + hc];
+    }
 #pragma unroll
     for (int j = 0; j < U; ++j)
-      if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, indices[k + j], F, voff);
+      if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, cj[j], F, voff);
   }
 #pragma unroll
   for (int i = 0; i < PPL; ++i) {
     const int j = jc + SPP * i;
     if ((SPP * PPL == U || j < U) && (FULL || j < nb)) {
-      const int64_t src = indices[k + j];
-      float x = el[src * H + hc] + rc;
+      float x = (EARLY ? lg[i] : el[int64_t(indices[k + j]) * H + hc]) + rc;
       x = x > 0.0f ? x : alpha * x;
       if (apply_exp) x = __expf(x);
       const float a = fminf(fmaxf(x, lo), hi);
