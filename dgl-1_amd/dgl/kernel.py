@@ -884,8 +884,12 @@ def _block_split(csr, B, lo, hi):
 # the fused GAT kernels' blocks: their per-row work (the attention through LDS)
 # makes a row's pass per block dearer than copy_u's, so fewer, larger blocks
 _GAT_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES", 11 << 20))  # 11 MiB
-# the fused forward when no attention is stored (inference)
-_GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 9 << 20))
+# the fused forward when no attention is stored (inference, and training with
+# the one-pass backward, which recomputes it): with the batch's logits loaded
+# ahead of its row gathers the per-row pass got cheaper, so smaller blocks pay
+# (Reddit-shaped 8 x 16: 4.96 ms at 7 MiB, 4.98 at 8, 5.22 at 9, 5.81 at 11;
+# tools/gat_block_percall.py, profiles/r04/gat_bwd/fwd_block_sweep.log)
+_GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 7 << 20))
 # the one-pass GAT backward over the transpose (its own per-row work: the
 # attention recomputed per pair, the dot's exchanges, the epilogue): larger
 # slices, as the forward's (Reddit-shaped 8 x 16, forward + backward: 4 / 6 /
@@ -1866,9 +1870,7 @@ class _GATAggregate(torch.autograd.Function):
                 w = torch.empty_like(a) if p > 0 else None
             # source-blocked (exact where the blocks never decrease along a
             # row): one launch per block, both chains continued; with nothing
-            # stored, smaller blocks (Reddit-shaped 8 x 16: 5.78 ms at 9 MiB
-            # vs 6.04 at 11; with the attention stored 6.79 vs 6.78,
-            # tools/gat_block_percall.py)
+            # stored, smaller blocks (_GAT_BLOCK_BYTES_NOGRAD)
             cuts = _block_cuts(fwd, (F + H) * 4,
                                None if a is not None else _GAT_BLOCK_BYTES_NOGRAD)
             if cuts is None:
