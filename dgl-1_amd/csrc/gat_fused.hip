@@ -911,8 +911,8 @@ int dglhip_gat_backward_t_device(
   DGLHIP_CHECK(num_items >= 0 && num_rows >= 0 && num_src >= 0, "bad sizes");
   DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
   if (num_items == 0) return 0;
-  DGLHIP_CHECK(item_beg && item_end && cols && fslot && ft && el && er && dout && d_ft && d_el &&
-               grad, "null pointer argument");
+  DGLHIP_CHECK(item_beg && item_end && cols && fslot && ft && el && er && dout && d_ft && d_el,
+               "null pointer argument");
   DGLHIP_CHECK(reinterpret_cast<uintptr_t>(ft) % 8 == 0 &&
                reinterpret_cast<uintptr_t>(dout) % 8 == 0 &&
                reinterpret_cast<uintptr_t>(d_ft) % 8 == 0, "rows must be 8-B aligned");
@@ -924,7 +924,7 @@ int dglhip_gat_backward_t_device(
   // dout is gathered by destination v: num_rows rows of the forward CSR
   const int64_t tbytes = num_rows * num_heads * head_dim * int64_t(sizeof(float));
   const bool small = tbytes < (int64_t(1) << 31);
-  const int gpol = g_gat_bwd_variant & 3;
+  const int gpol = grad ? (g_gat_bwd_variant & 3) : 2;  // no grad buffer: nothing stored
   const bool v1 = (g_gat_bwd_variant & 4) != 0;
   timed_launch(stream, [&] {
 #define DGLHIP_GBT_W(DD, SM, RPV, W)                                                          \

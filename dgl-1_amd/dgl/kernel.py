@@ -2004,7 +2004,9 @@ def _gat_backward_t(ctx, d_ft, d_z):
     emap = _fwd_slot_of_bwd(adj)
     d_ft2 = torch.empty(bwd.num_rows, F, dtype=torch.float32, device=dev)
     d_el = torch.empty(bwd.num_rows, H, dtype=torch.float32, device=dev)
-    g = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev)
+    # the attention gradient at its forward slot, for d_er's sum (none when
+    # er needs no gradient: the kernel then stores nothing)
+    g = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev) if need_er else None
     common = (fwd.num_rows, ft2.shape[0], H, D)
     tail = (ptr(ft2), ptr(el), ptr(er), ptr(dz), ptr(dout), float(ctx.alpha), float(ctx.lo),
             float(ctx.hi), 1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,

@@ -524,7 +524,8 @@ int dglhip_gat_attention_grad_rowsum_ranges_device(
  * Items as dglhip_gspmm_items_device: item i is row item_row[i] (NULL: i) with
  * slots [item_beg[i], item_end[i]) of cols / fslot, or with by_row != 0 slots
  * [item_beg[row], item_end[row]); accumulate != 0 continues both chains from
- * d_ft / d_el (source blocks of the transpose in order). dz may be NULL. */
+ * d_ft / d_el (source blocks of the transpose in order). dz may be NULL;
+ * grad may be NULL when d_er is not wanted (nothing stored). */
 int dglhip_gat_backward_t_ok(int64_t num_heads, int64_t head_dim);
 int dglhip_gat_backward_t_device(
     int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,

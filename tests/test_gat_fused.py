@@ -419,3 +419,28 @@ def test_dropout_keeps_pairs_with_zero_attention(device, H, D):
     assert bool(((a == 0) & keep).any())  # the case is present
     for got, ref in ((el.grad, elr.grad), (er.grad, err.grad), (ft.grad, ftr.grad)):
         torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_transposed_backward_without_er_grad():
+    """er not requiring grad: the one-pass backward stores no attention
+    gradient (NULL buffer) and d_ft / d_el keep the bits of the full
+    backward."""
+    dev = _dev("cuda")
+    n, m = 40_000, 1_500_000
+    rng = np.random.default_rng(43)
+    g = dgl.DGLGraph((torch.from_numpy(rng.integers(0, n, m)),
+                      torch.from_numpy(rng.integers(0, n, m))))
+    adj = g.sparse_adjacency(dev)
+    ft0, el0, er0 = (x.detach() for x in _inputs(n, 8, 16, dev))
+    gout = torch.randn(n, 8, 16, device=dev)
+    outs = []
+    for er_grad in (True, False):
+        ft, el = ft0.clone().requires_grad_(True), el0.clone().requires_grad_(True)
+        er = er0.clone().requires_grad_(er_grad)
+        fs, _ = kernel.gat_aggregate(adj, ft, el, er, attn_drop=0.3, seed=5)
+        fs.backward(gout)
+        outs.append((ft.grad, el.grad))
+        assert (er.grad is not None) == er_grad
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
