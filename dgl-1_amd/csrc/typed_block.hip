@@ -29,6 +29,8 @@
 // Deterministic, no atomics; the host entry points run the same chains.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "../../include/dgl_hip.h"
 #include "common.h"
 #include "launch.h"
@@ -99,22 +101,25 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
   const int64_t b = active ? jg / so : 0, j = active ? jg - b * so : 0;
   const int64_t hoff = b * si, woff = b * si * so + j;
   float acc = 0.0f;
-  for (int64_t k = beg; k < end; k += G) {
-    const int64_t cnt = end - k;  // wave-uniform: slots q >= cnt are predicated off
-    const float* hb[G];
-    const float* wb[G];
-    float nrm[G];
+  // one batch of up to GB slots from k (slots q >= cnt predicated off: their
+  // loads read a valid slot, their products are dropped)
+  auto batch = [&](int64_t k, auto gb_tag) {
+    constexpr int GB = decltype(gb_tag)::value;
+    const int64_t cnt = end - k;  // wave-uniform
+    const float* hb[GB];
+    const float* wb[GB];
+    float nrm[GB];
 #pragma unroll
-    for (int q = 0; q < G; ++q) {
+    for (int q = 0; q < GB; ++q) {
       const int64_t kk = q < cnt ? k + q : end - 1;  // a valid slot for idle q
       hb[q] = ufeat + int64_t(indices[kk]) * Fi + hoff;
       wb[q] = weight + int64_t(slot_rel[kk]) * wr + woff;
       nrm[q] = slot_norm ? slot_norm[kk] : 1.0f;
     }
     if (SI > 0) {
-      float hv[G][SI > 0 ? SI : 1], wv[G][SI > 0 ? SI : 1];
+      float hv[GB][SI > 0 ? SI : 1], wv[GB][SI > 0 ? SI : 1];
 #pragma unroll
-      for (int q = 0; q < G; ++q) {
+      for (int q = 0; q < GB; ++q) {
 #pragma unroll
         for (int i = 0; i < SI; ++i) {
           hv[q][i] = hb[q][i];
@@ -122,24 +127,39 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
         }
       }
 #pragma unroll
-      for (int q = 0; q < G; ++q) {
+      for (int q = 0; q < GB; ++q) {
         float m = 0.0f;
 #pragma unroll
         for (int i = 0; i < SI; ++i) m = __builtin_fmaf(hv[q][i], wv[q][i], m);
         if (q < cnt) acc = __builtin_fmaf(nrm[q], m, acc);
       }
     } else {
-      float m[G];
+      float m[GB];
 #pragma unroll
-      for (int q = 0; q < G; ++q) m[q] = 0.0f;
+      for (int q = 0; q < GB; ++q) m[q] = 0.0f;
       for (int64_t i = 0; i < si; ++i) {
 #pragma unroll
-        for (int q = 0; q < G; ++q) m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
+        for (int q = 0; q < GB; ++q) m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
       }
 #pragma unroll
-      for (int q = 0; q < G; ++q)
+      for (int q = 0; q < GB; ++q)
         if (q < cnt) acc = __builtin_fmaf(nrm[q], m[q], acc);
     }
+  };
+  // short batches (most items of a sampled KG hold 1-4 slots) at a quarter
+  // or half of the width: a G-wide batch issues its loads for every q, idle
+  // or not
+  constexpr int G4 = G >= 8 ? G / 4 : G, G2 = G >= 8 ? G / 2 : G;
+  for (int64_t k = beg; k < end; k += G) {
+    if (end - k <= G4) {
+      batch(k, std::integral_constant<int, G4>());
+      break;
+    }
+    if (end - k <= G2) {
+      batch(k, std::integral_constant<int, G2>());
+      break;
+    }
+    batch(k, std::integral_constant<int, G>());
   }
   if (active) (single ? out + row * Fo : partial + it * Fo)[jg] = acc;
 }
