@@ -127,8 +127,14 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
     fms = call_ms(fwd, steps, dev)
     # the one-pass transposed backward recomputes the attention: nothing stored
     stored = kernel.LIB.dglhip_gat_backward_t_ok(H, D) != 1
-    cuts = kernel._block_cuts(adj.fwd, H * D * 4)
+    # the forward's row ranges as gat_aggregate cuts them (nothing stored:
+    # _GAT_BLOCK_BYTES_NOGRAD), the backward's plan over the transpose
+    cuts = kernel._block_cuts(adj.fwd, (H * D + H) * 4,
+                              None if stored else kernel._GAT_BLOCK_BYTES_NOGRAD)
     peak, src = gather_peak(n * H * D * 4, 0 if cuts is None else len(cuts) - 1)
+    bplan = kernel._block_plan(adj.bwd, gout.view(n, H * D), H * D,
+                               kernel._GAT_BWD_BLOCK_BYTES)
+    bpeak, bsrc = gather_peak(n * H * D * 4, 0 if bplan is None else len(bplan))
     res = {"value": E / (ms * 1e-3), "unit": "edges/s (fwd+bwd)", "ms_per_step": ms,
            "kernel_ms": kms, "launches_per_step": launches, "steps": steps, "warmup": warmup,
            "config": "GAT layer aggregation, %d heads x %d, on the headline graph (%d nodes, "
@@ -147,7 +153,7 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
         bbytes = (E * (4 * F_ + 12 + 12 * H) + n * (8 * F_ + 8 * H + 8) +
                   E * 4 * H + n * 4 * H)
         res["roofline_backward"] = roof(
-            bbytes, bms, peak, src,
+            bbytes, bms, bpeak, bsrc,
             "GAT backward: dglhip_gat_backward_t_device (per edge the gathered dout row, "
             "column id, forward slot, er and dz values, the stored gradient; per source row "
             "ft, el, d_ft, d_el) + dglhip_rowsum_heads8_device (d_er)",
