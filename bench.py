@@ -180,8 +180,9 @@ class _Terminated(Exception):
 
 
 def relay(cmd, env=None):
-    """Run ``cmd`` as a child in its own session, pass its stdout through line
-    by line (rank 0's JSON line among it), return its exit code. SIGTERM,
+    """Run ``cmd`` as a child in its own session, pass rank 0's JSON line
+    through to stdout (every other line of the child's stdout to stderr),
+    return its exit code. SIGTERM,
     SIGINT and SIGHUP to this process, or any exception here, kill the
     child's whole process group (the torchrun agent and every rank) before
     this process exits (128 + the signal's number for a signal). This
@@ -200,8 +201,10 @@ def relay(cmd, env=None):
         proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True,
                                 bufsize=1, universal_newlines=True)
         for line in proc.stdout:
-            sys.stdout.write(line)
-            sys.stdout.flush()
+            # the JSON line to stdout, anything a library printed there to stderr
+            out = sys.stdout if line.lstrip().startswith("{") else sys.stderr
+            out.write(line)
+            out.flush()
         return proc.wait()
     except _Terminated as t:
         log("relay: %s, killing the ranks' process group" % t)
@@ -830,6 +833,17 @@ def strong_run(args, world, rank, dev, st):
             "halo_exchange": exchange_block(pg2, h2, args.steps, world, dev)}
 
 
+def _claim_stdout():
+    """Keep the process's stdout for the one JSON line. Libraries write to
+    file descriptor 1 themselves (gloo's "[Gloo] Rank r is connected to ..."
+    for every group it builds, RCCL and ROCm notices): point descriptor 1 at
+    stderr and give Python a stream on a duplicate of the original stdout."""
+    sys.stdout.flush()
+    keep = os.dup(1)
+    os.dup2(2, 1)
+    sys.stdout = os.fdopen(keep, "w", buffering=1)
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     args = build_parser().parse_args(argv)
@@ -843,6 +857,7 @@ def main(argv=None):
     if err is not None:
         log("error: " + err)
         return 2
+    _claim_stdout()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

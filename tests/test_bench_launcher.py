@@ -52,11 +52,15 @@ def test_world_mismatch_is_an_error():
 
 
 def test_relay_passes_output_and_exit_code(capfd):
+    """The child's JSON line reaches stdout, anything else it printed there
+    (e.g. gloo's connection notices) goes to stderr; the exit code is the
+    child's."""
     rc = bench.relay([sys.executable, "-c",
                       "import sys; print('line one'); print('{\"k\": 1}'); sys.exit(3)"])
     assert rc == 3
-    out = capfd.readouterr().out
-    assert "line one" in out and '{"k": 1}' in out
+    cap = capfd.readouterr()
+    assert cap.out.strip() == '{"k": 1}'
+    assert "line one" in cap.err
 
 
 def test_bench_two_ranks_without_outer_launcher():
@@ -68,8 +72,10 @@ def test_bench_two_ranks_without_outer_launcher():
                         "--steps", "2", "--warmup", "1", "--cpu-sample-edges", "20000"],
                        env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
     assert p.returncode == 0, p.stderr.decode()[-3000:]
-    lines = [l for l in p.stdout.decode().splitlines() if l.startswith("{")]
-    assert len(lines) == 1  # rank 0 only
+    # stdout holds rank 0's JSON line and nothing else (the gloo groups'
+    # connection notices go to stderr)
+    lines = [l for l in p.stdout.decode().splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), lines[:3]
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["scaling"] == "weak"
     assert "2-way 1-D dst-row partition" in r["config"]["parallelism"]
@@ -108,8 +114,8 @@ _SMALL = ["--gpus", "2", "--device", "cpu", "--graph-scale", "0.002", "--rmat-sc
 
 
 def _line(stdout):
-    lines = [l for l in stdout.decode().splitlines() if l.startswith("{")]
-    assert len(lines) == 1
+    lines = [l for l in stdout.decode().splitlines() if l.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), lines[:3]  # the line, nothing else
     return json.loads(lines[0])
 
 
