@@ -47,12 +47,8 @@ namespace dglhip {
 // them gathered before it
 int g_gat_variant = 0;
 // study knob of the transposed backward (dglhip_set_gat_bwd_variant): bits 0-1
-// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid),
-// bit 2 the r04 first form of the kernel (each batch's loads in program order)
+// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid)
 int g_gat_bwd_variant = 0;
-#ifndef GBT_WPE
-#define GBT_WPE 1
-#endif
 
 // One row of VEC floats per lane through a buffer descriptor built from the
 // wave-uniform row address: a 32-bit per-lane byte offset instead of a 64-bit
@@ -399,8 +395,8 @@ __device__ __forceinline__ float dpp_shl(float v) {
                                                     false));
 }
 
-template <bool DROP, bool SMALL, int RP = 0, bool V1 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V1 ? 1 : GBT_WPE))) void gat_backward_t_kernel(
+template <bool DROP, bool SMALL, int RP = 0>
+__global__ __launch_bounds__(256) void gat_backward_t_kernel(
     int64_t num_items, const int32_t* __restrict__ item_row, const int64_t* __restrict__ item_beg,
     const int64_t* __restrict__ item_end, int by_row, int accumulate,
     const int32_t* __restrict__ cols, const int64_t* __restrict__ fslot,
@@ -439,189 +435,78 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V1 ? 1 : GB
   float elacc = (accumulate && head_lane) ? d_el[row * H + h] : 0.0f;
   float* lw = s_w[wi];
   float* ld = s_d[wi];
-  if (!V1) {
-    const int rbytes = SMALL ? static_cast<int>(table_bytes / (F / H)) : 0;
-    const __amdgpu_buffer_rsrc_t er_r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(er), 0, rbytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t dz_r =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dz ? dz : er), 0, rbytes, 0x00020000);
-    // One batch of U slots [k, k + nb) (FULL: nb == U, no predication). The
-    // column ids come through the scalar cache first; the pairs' operands
-    // (er, dz, the forward slot) are loaded before the 16 row gathers, so the
-    // attention is computed while the rows are in flight; the attention
-    // gradients are stored at the end of the batch, so no wait on their
-    // write acknowledgements sits inside it.
-    auto batch = [&](int64_t k, int nb, auto full_tag) {
-      constexpr bool FULL = decltype(full_tag)::value;
-      int cj[U];
+  const int rbytes = SMALL ? static_cast<int>(table_bytes / (F / H)) : 0;
+  const __amdgpu_buffer_rsrc_t er_r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(er), 0, rbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dz_r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(dz ? dz : er), 0, rbytes, 0x00020000);
+  // One batch of U slots [k, k + nb) (FULL: nb == U, no predication). The
+  // column ids come through the scalar cache first; the pairs' operands
+  // (er, dz, the forward slot) are loaded before the 16 row gathers, so the
+  // attention is computed while the rows are in flight; the attention
+  // gradients are stored at the end of the batch, so no wait on their
+  // write acknowledgements sits inside it.
+  auto batch = [&](int64_t k, int nb, auto full_tag) {
+    constexpr bool FULL = decltype(full_tag)::value;
+    int cj[U];
 #pragma unroll
-      for (int j = 0; j < U; ++j) cj[j] = cols[k + (FULL || j < nb ? j : 0)];
-      // this lane's pairs: slots jc and jc + 8 (clamped into the batch when
-      // partial; the values of slots past nb are never used)
-      int pc[2];
-      int64_t pj[2];
+    for (int j = 0; j < U; ++j) cj[j] = cols[k + (FULL || j < nb ? j : 0)];
+    // this lane's pairs: slots jc and jc + 8 (clamped into the batch when
+    // partial; the values of slots past nb are never used)
+    int pc[2];
+    int64_t pj[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        int c = cj[8 * i];
+    for (int i = 0; i < 2; ++i) {
+      int c = cj[8 * i];
 #pragma unroll
-        for (int t = 1; t < 8; ++t) c = jc == t ? cj[8 * i + t] : c;
-        const int j = jc + 8 * i;
-        pj[i] = FULL || j < nb ? j : 0;
-        pc[i] = FULL || j < nb ? c : cj[0];
-      }
-      float per[2], pz[2];
-      int64_t pf[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (SMALL) {  // er and dz are 32 B per row of dout's: 32-bit offsets
-          const uint32_t o = static_cast<uint32_t>(pc[i]) * (H * 4u) + hc * 4u;
-          per[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(er_r, o, 0, 0));
-          pz[i] = dz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dz_r, o, 0, 0))
-                     : 0.0f;
-        } else {
-          per[i] = er[int64_t(pc[i]) * H + hc];
-          pz[i] = dz ? dz[int64_t(pc[i]) * H + hc] : 0.0f;
-        }
-        pf[i] = fslot[k + pj[i]];
-      }
-      V u[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (FULL || j < nb) u[j] = gat_gather<2, SMALL>(dout, tab, cj[j], F, voff);
-      // the pairs: attention, keep bit, dropped weight (the forward's
-      // expressions)
-      float pa[2];
-      bool pk[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int j = jc + 8 * i;
-        float x = elc + per[i];
-        x = x > 0.0f ? x : alpha * x;
-        if (apply_exp) x = __expf(x);
-        const float a = fminf(fmaxf(x, lo), hi);
-        float w = a;
-        pk[i] = true;
-        if (DROP) {
-          pk[i] = gat_keep(seed, pf[i] * H + hc, thr);
-          w = pk[i] ? a * scale : 0.0f;
-        }
-        pa[i] = a;
-        lw[hc * LU + j] = w;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // per slot: d_ft's chain and the head's dot (as below)
-#pragma unroll
-      for (int q = 0; q < U / 4; ++q) {
-        const f32x4 w4 = *reinterpret_cast<const f32x4*>(lw + h * LU + 4 * q);
-        const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int j = 4 * q + i;
-          if (FULL || j < nb) {
-            acc = Vec<2>::fma(Vec<2>::splat(wv[i]), u[j], acc);
-            float t = u[j].x * ftv.x;
-            t = __builtin_fmaf(u[j].y, ftv.y, t);
-            float p = __builtin_fmaf(u[j].x, ftv.x, dpp_even_to_odd(t));
-            p = __builtin_fmaf(u[j].y, ftv.y, p);
-            const float s2 = p + dpp_shl<4>(p);
-            const float dot = s2 + dpp_shl<2>(s2);
-            if (head_lane) ld[h * LU + j] = dot;
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // the epilogue per pair (gat_epi_pre's operations), g back into the
-      // LDS row by head for d_el's chain
-      float pg[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int j = jc + 8 * i;
-        const float a = pa[i];
-        float tt = ld[hc * LU + j];
-        if (DROP) tt = pk[i] ? tt * scale : 0.0f;
-        if (dz) tt = tt + pz[i];
-        float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
-                            : tt * (a <= 0.0f ? alpha : 1.0f);
-        g = (a > lo && a < hi) ? g : 0.0f;
-        pg[i] = g;
-        ld[hc * LU + j] = g;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (head_lane) {
-#pragma unroll
-        for (int q = 0; q < U / 4; ++q) {
-          const f32x4 g4 = *reinterpret_cast<const f32x4*>(ld + h * LU + 4 * q);
-          const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (FULL || 4 * q + i < nb) elacc = elacc + gv[i];
-        }
-      }
-      // g at its forward slot, for d_er's sum over the CSR
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        if (FULL || jc + 8 * i < nb) {
-          if (gpol == 0) g_out[pf[i] * H + hc] = pg[i];
-          else if (gpol == 1) __builtin_nontemporal_store(pg[i], g_out + pf[i] * H + hc);
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    };
-    int64_t k = beg;
-    for (; k + U <= end; k += U) batch(k, U, std::true_type());
-    if (k < end) batch(k, static_cast<int>(end - k), std::false_type());
-    store_out<2, RP>(d_ft + row * F, f0, acc);
-    if (head_lane) d_el[row * H + h] = elacc;
-    return;
-  }
-  for (int64_t k = beg; k < end; k += U) {
-    const int nb = end - k < U ? static_cast<int>(end - k) : U;
-    V u[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (j < nb) u[j] = gat_gather<2, SMALL>(dout, tab, cols[k + j], F, voff);
-    // the pairs: attention, keep bit, dropped weight (the forward's
-    // expressions), the normaliser gradient and the forward slot
-    float pa[2], pz[2];
-    bool pk[2];
+      for (int t = 1; t < 8; ++t) c = jc == t ? cj[8 * i + t] : c;
+      const int j = jc + 8 * i;
+      pj[i] = FULL || j < nb ? j : 0;
+      pc[i] = FULL || j < nb ? c : cj[0];
+    }
+    float per[2], pz[2];
     int64_t pf[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int j = jc + 8 * i;
-      pa[i] = pz[i] = 0.0f;
-      pk[i] = true;
-      pf[i] = 0;
-      if (j < nb) {
-        const int64_t v = cols[k + j];
-        float x = elc + er[v * H + hc];
-        x = x > 0.0f ? x : alpha * x;
-        if (apply_exp) x = __expf(x);
-        const float a = fminf(fmaxf(x, lo), hi);
-        pf[i] = fslot[k + j];
-        float w = a;
-        if (DROP) {
-          pk[i] = gat_keep(seed, pf[i] * H + hc, thr);
-          w = pk[i] ? a * scale : 0.0f;
-        }
-        pa[i] = a;
-        pz[i] = dz ? dz[v * H + hc] : 0.0f;
-        lw[hc * LU + j] = w;
+      if (SMALL) {  // er and dz are 32 B per row of dout's: 32-bit offsets
+        const uint32_t o = static_cast<uint32_t>(pc[i]) * (H * 4u) + hc * 4u;
+        per[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(er_r, o, 0, 0));
+        pz[i] = dz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dz_r, o, 0, 0))
+                   : 0.0f;
+      } else {
+        per[i] = er[int64_t(pc[i]) * H + hc];
+        pz[i] = dz ? dz[int64_t(pc[i]) * H + hc] : 0.0f;
       }
+      pf[i] = fslot[k + pj[i]];
+    }
+    V u[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (FULL || j < nb) u[j] = gat_gather<2, SMALL>(dout, tab, cj[j], F, voff);
+    // the pairs: attention, keep bit, dropped weight (the forward's
+    // expressions)
+    float pa[2];
+    bool pk[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int j = jc + 8 * i;
+      float x = elc + per[i];
+      x = x > 0.0f ? x : alpha * x;
+      if (apply_exp) x = __expf(x);
+      const float a = fminf(fmaxf(x, lo), hi);
+      float w = a;
+      pk[i] = true;
+      if (DROP) {
+        pk[i] = gat_keep(seed, pf[i] * H + hc, thr);
+        w = pk[i] ? a * scale : 0.0f;
+      }
+      pa[i] = a;
+      lw[hc * LU + j] = w;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // per slot: d_ft's chain and the head's dot in the sliced g-SDDMM's
-    // association (partials of lanes 8h+1, 8h+3, 8h+5, 8h+7 = p0..p3;
-    // (p0 + p2) + (p1 + p3) on lane 8h+1)
+    // per slot: d_ft's chain and the head's dot (as below)
 #pragma unroll
     for (int q = 0; q < U / 4; ++q) {
       const f32x4 w4 = *reinterpret_cast<const f32x4*>(lw + h * LU + 4 * q);
@@ -629,7 +514,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V1 ? 1 : GB
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int j = 4 * q + i;
-        if (j < nb) {
+        if (FULL || j < nb) {
           acc = Vec<2>::fma(Vec<2>::splat(wv[i]), u[j], acc);
           float t = u[j].x * ftv.x;
           t = __builtin_fmaf(u[j].y, ftv.y, t);
@@ -644,23 +529,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V1 ? 1 : GB
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // the epilogue per pair (gat_epi_pre's operations), g stored at its
-    // forward slot and, by head, back into the LDS row for d_el's chain
+    // the epilogue per pair (gat_epi_pre's operations), g back into the
+    // LDS row by head for d_el's chain
+    float pg[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = jc + 8 * i;
-      if (j < nb) {
-        const float a = pa[i];
-        float tt = ld[hc * LU + j];
-        if (DROP) tt = pk[i] ? tt * scale : 0.0f;
-        if (dz) tt = tt + pz[i];
-        float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
-                            : tt * (a <= 0.0f ? alpha : 1.0f);
-        g = (a > lo && a < hi) ? g : 0.0f;
-        if (gpol == 0) g_out[pf[i] * H + hc] = g;
-        else if (gpol == 1) __builtin_nontemporal_store(g, g_out + pf[i] * H + hc);
-        ld[hc * LU + j] = g;
-      }
+      const float a = pa[i];
+      float tt = ld[hc * LU + j];
+      if (DROP) tt = pk[i] ? tt * scale : 0.0f;
+      if (dz) tt = tt + pz[i];
+      float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
+                          : tt * (a <= 0.0f ? alpha : 1.0f);
+      g = (a > lo && a < hi) ? g : 0.0f;
+      pg[i] = g;
+      ld[hc * LU + j] = g;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -672,13 +555,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(V1 ? 1 : GB
         const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          if (4 * q + i < nb) elacc = elacc + gv[i];
+          if (FULL || 4 * q + i < nb) elacc = elacc + gv[i];
+      }
+    }
+    // g at its forward slot, for d_er's sum over the CSR
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (FULL || jc + 8 * i < nb) {
+        if (gpol == 0) g_out[pf[i] * H + hc] = pg[i];
+        else if (gpol == 1) __builtin_nontemporal_store(pg[i], g_out + pf[i] * H + hc);
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  }
+  };
+  int64_t k = beg;
+  for (; k + U <= end; k += U) batch(k, U, std::true_type());
+  if (k < end) batch(k, static_cast<int>(end - k), std::false_type());
   store_out<2, RP>(d_ft + row * F, f0, acc);
   if (head_lane) d_el[row * H + h] = elacc;
 }
@@ -925,18 +819,15 @@ int dglhip_gat_backward_t_device(
   const int64_t tbytes = num_rows * num_heads * head_dim * int64_t(sizeof(float));
   const bool small = tbytes < (int64_t(1) << 31);
   const int gpol = grad ? (g_gat_bwd_variant & 3) : 2;  // no grad buffer: nothing stored
-  const bool v1 = (g_gat_bwd_variant & 4) != 0;
   timed_launch(stream, [&] {
-#define DGLHIP_GBT_W(DD, SM, RPV, W)                                                          \
-  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM, RPV, W>), grid_1d(blocks), dim3(256), 0,   \
+#define DGLHIP_GBT_R(DD, SM, RPV)                                                             \
+  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM, RPV>), grid_1d(blocks), dim3(256), 0,      \
                      stream, num_items, item_row, item_beg, item_end, by_row, accumulate, cols, \
                      fslot, ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp, seed,   \
                      seed_offset, thr, scale, d_ft, d_el, grad, tbytes, gpol)
-#define DGLHIP_GBT_R(DD, SM, RPV) DGLHIP_GBT_W(DD, SM, RPV, false)
 #define DGLHIP_GBT(DD, SM)                                                                    \
   do {                                                                                        \
-    if (v1) DGLHIP_GBT_W(DD, SM, 2, true);                                                     \
-    else if (g_row_pol == 2) DGLHIP_GBT_R(DD, SM, 2);                                         \
+    if (g_row_pol == 2) DGLHIP_GBT_R(DD, SM, 2);                                              \
     else if (g_row_pol == 4) DGLHIP_GBT_R(DD, SM, 4);                                         \
     else DGLHIP_GBT_R(DD, SM, 0);                                                             \
   } while (0)
@@ -947,7 +838,6 @@ int dglhip_gat_backward_t_device(
     }
 #undef DGLHIP_GBT
 #undef DGLHIP_GBT_R
-#undef DGLHIP_GBT_W
   });
   API_END();
 }
@@ -978,8 +868,7 @@ int dglhip_set_gat_variant(int variant) {
 
 int dglhip_set_gat_bwd_variant(int variant) {
   API_BEGIN();
-  DGLHIP_CHECK(variant >= 0 && variant <= 6 && (variant & 3) != 3,
-               "unknown GAT backward variant " << variant);
+  DGLHIP_CHECK(variant >= 0 && variant <= 2, "unknown GAT backward variant " << variant);
   g_gat_bwd_variant = variant;
   API_END();
 }

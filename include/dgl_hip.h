@@ -576,11 +576,9 @@ int dglhip_gat_aggregate_ranges_device(
  * head), shared through LDS (H in {1, 2, 4, 8, 16}). Same bits. */
 int dglhip_set_gat_variant(int variant);
 
-/* Study knob for dglhip_gat_backward_t_device: bits 0-1 the attention
- * gradient's store (0 default, 1 non-temporal, 2 none — the gradient buffer is
- * then left unwritten, so d_er is not valid: timing only); bit 2 the first
- * form of the kernel (each batch's loads in program order). Values 0-2 and
- * 4-6. Same bits. */
+/* Study knob for dglhip_gat_backward_t_device: the attention gradient's store
+ * (0 default, 1 non-temporal, 2 none — the gradient buffer is then left
+ * unwritten, so d_er is not valid: timing only). */
 int dglhip_set_gat_bwd_variant(int variant);
 
 /* The attention-dropout mask of dglhip_gat_aggregate_device: keep[i] = 1 for
