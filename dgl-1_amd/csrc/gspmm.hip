@@ -401,7 +401,7 @@ __global__ __launch_bounds__(256) void gsddmm_attention_vec_kernel(
 Timing g_timing;
 int g_var_vec = 0, g_var_group = 0, g_var_unroll = 0, g_var_pipe = 0;
 int g_cache_policy = -1;
-int g_gather_buf = 0;
+int g_gather_buf = 2;
 // running rows of the blocked launches: non-temporal loads, sc1 stores (the
 // line leaves the XCD's L2): Reddit-shaped headline 3.83 -> 3.74 ms, GAT 8 x 16
 // forward + backward 17.01 -> 16.94 (tools/rowpol_ab.py, profiles/r04/rowpol_ab.json)
@@ -885,7 +885,7 @@ int dglhip_set_sddmm_variant(int alternate) {
 
 int dglhip_set_gather_mode(int buffer_descriptors) {
   API_BEGIN();
-  DGLHIP_CHECK(buffer_descriptors == 0 || buffer_descriptors == 1,
+  DGLHIP_CHECK(buffer_descriptors >= 0 && buffer_descriptors <= 3,
                "unknown gather mode " << buffer_descriptors);
   g_gather_buf = buffer_descriptors;
   API_END();

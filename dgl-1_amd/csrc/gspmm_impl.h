@@ -608,7 +608,9 @@ extern int g_var_vec, g_var_group, g_var_unroll, g_var_pipe;
 // -1: automatic (non-temporal output past 512 MiB, default otherwise).
 extern int g_cache_policy;
 // Row gathers of copy_u + sum at VEC 2 x 64 lanes through buffer descriptors
-// (dglhip_set_gather_mode): 1 on, 0 global loads.
+// (dglhip_set_gather_mode), a bit mask: bit 0 one-launch (and first-block)
+// launches, bit 1 the blocked schedule's launches (the default, 2); 0 global
+// loads everywhere.
 extern int g_gather_buf;
 // Running-row cache policy of accumulating copy_u + sum items (load_out /
 // store_out; dglhip_set_row_policy): 2 by default.
@@ -634,18 +636,29 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
     // shapes POL_OK covers are instantiated
     if constexpr (POL_OK) {
       if (a.chunk_beg && g_row_pol > 0 && (a.accumulate || g_row_pol >= 2)) {
-#define DGLHIP_RP_LAUNCH(ACC, RPV)                                                              \
+#define DGLHIP_RP_LAUNCH_B(ACC, RPV, B)                                                         \
   hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, ACC, false,     \
-                                       POL_DEFAULT, false, RPV>),                               \
+                                       POL_DEFAULT, B, RPV>),                                   \
                      grid_1d(blocks), dim3(256), 0, stream, a.num_items, a.F, a.elen,           \
                      a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,  \
                      a.row_order, a.chunk_beg, a.chunk_end)
+#define DGLHIP_RP_LAUNCH(ACC, RPV) DGLHIP_RP_LAUNCH_B(ACC, RPV, false)
+        if ((g_gather_buf & 2) && g_row_pol == 2) {
+          // the default: row gathers through per-row buffer descriptors (the
+          // row base in SGPRs, one lane offset for all 16: 42 instead of 70
+          // VGPRs, 8 waves per SIMD instead of 7; Reddit-shaped headline
+          // 3.74 -> 3.61 ms, same bits, tools/gather_mode_ab.py)
+          if (!a.accumulate) DGLHIP_RP_LAUNCH_B(false, 4, true);
+          else DGLHIP_RP_LAUNCH_B(true, 2, true);
+          return;
+        }
         if (!a.accumulate) DGLHIP_RP_LAUNCH(false, 4);  // the first launch: stores only
         else if (g_row_pol == 1) DGLHIP_RP_LAUNCH(true, 1);
         else if (g_row_pol == 2) DGLHIP_RP_LAUNCH(true, 2);
         else if (g_row_pol == 3) DGLHIP_RP_LAUNCH(true, 3);
         else DGLHIP_RP_LAUNCH(true, 4);
 #undef DGLHIP_RP_LAUNCH
+#undef DGLHIP_RP_LAUNCH_B
         return;
       }
     }
@@ -655,7 +668,7 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
                      a.F, a.elen, a.ldu ? a.ldu : a.F, a.indptr, a.indices, a.eid, a.ufeat, a.efeat, a.out,         \
                      a.row_order, a.chunk_beg, a.chunk_end)
 #define DGLHIP_POL_LAUNCH(CH, P) DGLHIP_POL_LAUNCH_B(CH, P, false)
-    if (POL_OK && g_gather_buf && !a.accumulate && (pol == POL_DEFAULT || pol == POL_NT_OUT)) {
+    if (POL_OK && (g_gather_buf & 1) && !a.accumulate && (pol == POL_DEFAULT || pol == POL_NT_OUT)) {
       // row gathers through buffer descriptors (gather_row_buf)
       const bool ch = a.chunk_beg != nullptr;
       if (pol == POL_DEFAULT) { if (ch) DGLHIP_POL_LAUNCH_B(true, POL_DEFAULT, true); else DGLHIP_POL_LAUNCH_B(false, POL_DEFAULT, true); }

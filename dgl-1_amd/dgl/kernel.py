@@ -1458,10 +1458,14 @@ def gspmm_ranges(msg, beg, end, accumulate, indices, out, ufeat=None, efeat=None
     return out
 
 
-def set_gather_mode(buffer_descriptors):
-    """Study knob: the copy_u + sum kernel's row gathers through buffer
-    descriptors (True) or global loads (False); same values."""
-    check_call(LIB.dglhip_set_gather_mode(1 if buffer_descriptors else 0))
+def set_gather_mode(mode):
+    """Study knob: where the copy_u + sum kernel's row gathers go through
+    buffer descriptors instead of global loads, a bit mask (bit 0 one-launch
+    calls, bit 1 the blocked schedule's launches: the default, 2); True = 3,
+    False = 0. Same values."""
+    if isinstance(mode, bool):
+        mode = 3 if mode else 0
+    check_call(LIB.dglhip_set_gather_mode(int(mode)))
 
 
 def set_sddmm_variant(alternate):

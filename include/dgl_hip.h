@@ -343,10 +343,12 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
                       int64_t efeat_len, float* out, int64_t* arg_out,
                       int num_threads);
 
-/* Study knob: 1 = the copy_u + sum kernel's row gathers (two floats per lane,
- * a wave per row) go through buffer descriptors built from the wave-uniform
- * row address (one 32-bit lane offset for every gather in flight instead of a
- * 64-bit address each); 0 = global loads. Same values. */
+/* Knob: where the copy_u + sum kernel's row gathers (two floats per lane, a
+ * wave per row) go through buffer descriptors built from the wave-uniform row
+ * address (one 32-bit lane offset for every gather in flight instead of a
+ * 64-bit address each) rather than global loads, as a bit mask: bit 0 the
+ * one-launch calls, bit 1 the source-blocked schedule's launches (the default,
+ * 2: 42 instead of 70 VGPRs there). Same values. */
 int dglhip_set_gather_mode(int buffer_descriptors);
 
 /* Resident waves of the headline g-SpMM kernel (F = 128 copy_u + sum) on

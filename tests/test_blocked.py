@@ -557,4 +557,36 @@ def test_row_policies_same_bits():
             kernel.check_call(kernel.LIB.dglhip_set_row_policy(pol))
             assert torch.equal(kernel.gspmm(adj, "copy_u", "sum", H), ref)
     finally:
-        kernel.check_call(kernel.LIB.dglhip_set_row_policy(0))
+        kernel.check_call(kernel.LIB.dglhip_set_row_policy(2))  # the default
+
+
+@pytest.mark.gpu
+def test_gather_modes_same_bits():
+    """Row gathers through buffer descriptors (dglhip_set_gather_mode: bit 0
+    one-launch calls, bit 1 the blocked launches, the default 2) or global
+    loads load the same rows: every mode gives the default's bits, blocked and
+    in one launch, under the row policies the blocked launches pair them with."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 23, True)
+    adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
+                          kernel.ORDER_EID, dev)
+    H = torch.randn(n, 128, generator=torch.Generator().manual_seed(24)).to(dev)
+    assert kernel.blocked_schedule(adj, H) >= 2
+    refs = {}
+    try:
+        for blocked in ("auto", "off"):
+            kernel.set_blocked(blocked)
+            refs[blocked] = kernel.gspmm(adj, "copy_u", "sum", H)
+            for mode in range(4):
+                kernel.set_gather_mode(mode)
+                for pol in (2, 4):
+                    kernel.check_call(kernel.LIB.dglhip_set_row_policy(pol))
+                    assert torch.equal(kernel.gspmm(adj, "copy_u", "sum", H), refs[blocked])
+        assert torch.equal(refs["auto"], refs["off"])
+    finally:
+        kernel.set_blocked("auto")
+        kernel.set_gather_mode(2)
+        kernel.check_call(kernel.LIB.dglhip_set_row_policy(2))

@@ -1,11 +1,12 @@
-"""A/B of the copy_u + sum kernel's row gathers: global loads (a 64-bit
-address per gather in flight, 72 VGPRs, 7 waves per SIMD) vs buffer
-descriptors built from the wave-uniform row address (one 32-bit offset, 42
-VGPRs, 8 waves per SIMD). Interleaved rounds in one process on the
-Reddit-shaped graph and RMAT (heavy rows chunked); outputs compared bit for
-bit.
+"""A/B of the headline's row gathers under the blocked schedule
+(dglhip_set_gather_mode): 0 = global loads with a 64-bit address per gather
+(70 VGPRs, 7 waves per SIMD), 2 = per-row buffer descriptors (the row base in
+SGPRs, one shared 32-bit lane offset: 42 VGPRs, 8 waves). Per mode the mean
+GPU span of a copy_u + sum call on the Reddit-shaped graph (events around the
+calls on the launch stream), interleaved over rounds, output bits vs mode 0;
+also at 5 and 8 MiB blocks (more waves may move the slice optimum).
 
-  python tools/gather_mode_ab.py [--rmat-scale 26] [--rounds 5]
+  python tools/gather_mode_ab.py [--calls 20 --rounds 3] [--out file.json]
 """
 import argparse
 import json
@@ -19,48 +20,48 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dgl-1_amd")]
 from dgl import data, kernel  # noqa: E402
 
 
-def ab(name, adj, h, rounds, iters=10):
-    res = {0: [], 1: []}
-    outs = {}
-    for _ in range(rounds):
-        for mode in (0, 1):
-            kernel.set_gather_mode(mode)
-            outs[mode] = kernel.gspmm(adj, "copy_u", "sum", h)
-            torch.cuda.synchronize()
-            kernel.timing_enable(True)
-            for _ in range(iters):
-                kernel.gspmm(adj, "copy_u", "sum", h)
-            ms, n = kernel.timing_read()
-            kernel.timing_enable(False)
-            res[mode].append(ms / iters)
-    kernel.set_gather_mode(0)
-    same = bool(torch.equal(outs[0], outs[1]))
-    return {"graph": name, "global_loads_ms": res[0], "buffer_descriptors_ms": res[1],
-            "best_global": min(res[0]), "best_buffer": min(res[1]), "bit_identical": same}
-
-
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--rmat-scale", type=int, default=26)
-    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--calls", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--mib", type=int, nargs="+", default=[5, 6, 8])
+    ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    out = []
-    src, dst, n = data.reddit_like(device=dev)
+    src, dst, n = data.reddit_like(scale=1, seed=0, device=dev)
     adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
     del src, dst
     h = torch.rand(n, 128, device=dev) * 2 - 1
-    out.append(ab("reddit_like", adj, h, args.rounds))
-    print(json.dumps(out[-1]), flush=True)
-    del adj, h
-    torch.cuda.empty_cache()
-    kernel.set_row_split("auto")
-    src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
-    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
-    del src, dst
-    h = torch.rand(n, 128, device=dev) * 2 - 1
-    out.append(ab("rmat-%d" % args.rmat_scale, adj, h, args.rounds, iters=3))
-    print(json.dumps(out[-1]), flush=True)
+    ref = kernel.gspmm(adj, "copy_u", "sum", h)
+    old_bytes = kernel._BLOCK_BYTES
+    res, same = {}, {}
+    try:
+        for _ in range(args.rounds):
+            for mib in args.mib:
+                kernel._BLOCK_BYTES = mib << 20
+                for mode in (0, 2):
+                    kernel.check_call(kernel.LIB.dglhip_set_gather_mode(mode))
+                    key = "%d MiB / mode %d" % (mib, mode)
+                    out = kernel.gspmm(adj, "copy_u", "sum", h)
+                    same[key] = bool(torch.equal(out, ref))
+                    torch.cuda.synchronize()
+                    s = torch.cuda.Event(enable_timing=True)
+                    e = torch.cuda.Event(enable_timing=True)
+                    s.record()
+                    for _ in range(args.calls):
+                        kernel.gspmm(adj, "copy_u", "sum", h)
+                    e.record()
+                    e.synchronize()
+                    res.setdefault(key, []).append(s.elapsed_time(e) / args.calls)
+    finally:
+        kernel._BLOCK_BYTES = old_bytes
+        kernel.check_call(kernel.LIB.dglhip_set_gather_mode(0))
+    line = json.dumps({"ms_per_call": res, "min": {k: min(v) for k, v in res.items()},
+                       "bit_identical": same})
+    print(line)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(line + "\n")
 
 
 if __name__ == "__main__":
