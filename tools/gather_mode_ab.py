@@ -24,7 +24,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=20)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--mib", type=int, nargs="+", default=[5, 6, 8])
+    ap.add_argument("--mib", type=float, nargs="+", default=[5, 6, 8])
+    ap.add_argument("--modes", type=int, nargs="+", default=[0, 2])
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -38,10 +39,10 @@ def main():
     try:
         for _ in range(args.rounds):
             for mib in args.mib:
-                kernel._BLOCK_BYTES = mib << 20
-                for mode in (0, 2):
+                kernel._BLOCK_BYTES = int(mib * (1 << 20))
+                for mode in args.modes:
                     kernel.check_call(kernel.LIB.dglhip_set_gather_mode(mode))
-                    key = "%d MiB / mode %d" % (mib, mode)
+                    key = "%g MiB / mode %d" % (mib, mode)
                     out = kernel.gspmm(adj, "copy_u", "sum", h)
                     same[key] = bool(torch.equal(out, ref))
                     torch.cuda.synchronize()
@@ -55,7 +56,7 @@ def main():
                     res.setdefault(key, []).append(s.elapsed_time(e) / args.calls)
     finally:
         kernel._BLOCK_BYTES = old_bytes
-        kernel.check_call(kernel.LIB.dglhip_set_gather_mode(0))
+        kernel.check_call(kernel.LIB.dglhip_set_gather_mode(2))  # the default
     line = json.dumps({"ms_per_call": res, "min": {k: min(v) for k, v in res.items()},
                        "bit_identical": same})
     print(line)
