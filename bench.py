@@ -1096,7 +1096,7 @@ def main(argv=None):
                             " (graph-scale %g)" % args.graph_scale, n, num_edges_total, FEAT))
                         if args.workload == "reddit" else
                         ("rmat-%d: %d nodes, %d edges, feat=%d, row split %s"
-                         % (args.rmat_scale, n, num_edges_total, FEAT, kernel._ROW_SPLIT)),
+                         % (args.rmat_scale, n, num_edges_total, FEAT, kernel.get_row_split())),
             "global_batch": n,
             "feat": FEAT,
             "parallelism": parallelism,

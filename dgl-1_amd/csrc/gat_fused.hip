@@ -47,7 +47,8 @@ namespace dglhip {
 // them gathered before it
 int g_gat_variant = 0;
 // study knob of the transposed backward (dglhip_set_gat_bwd_variant): bits 0-1
-// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid)
+// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid);
+// bit 2 the kernel built for 5 waves per SIMD (96 VGPRs) instead of 4 (97)
 int g_gat_bwd_variant = 0;
 
 // One row of VEC floats per lane through a buffer descriptor built from the
@@ -395,8 +396,12 @@ __device__ __forceinline__ float dpp_shl(float v) {
                                                     false));
 }
 
-template <bool DROP, bool SMALL, int RP = 0>
-__global__ __launch_bounds__(256) void gat_backward_t_kernel(
+// PACK: er and dz arrive as one [rows, 2H] table (er then dz per row, the
+// caller's packing): the pair's two operands sit in one 64-B run, one line
+// per slot instead of two (r05: 230M of the backward's 873M L2 requests per
+// call were these two 32-B reads)
+template <bool DROP, bool SMALL, int RP = 0, int WPE = 4, bool PACK = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void gat_backward_t_kernel(
     int64_t num_items, const int32_t* __restrict__ item_row, const int64_t* __restrict__ item_beg,
     const int64_t* __restrict__ item_end, int by_row, int accumulate,
     const int32_t* __restrict__ cols, const int64_t* __restrict__ fslot,
@@ -435,7 +440,8 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
   float elacc = (accumulate && head_lane) ? d_el[row * H + h] : 0.0f;
   float* lw = s_w[wi];
   float* ld = s_d[wi];
-  const int rbytes = SMALL ? static_cast<int>(table_bytes / (F / H)) : 0;
+  const int rbytes = SMALL ? static_cast<int>(table_bytes / (F / H)) * (PACK ? 2 : 1) : 0;
+  constexpr uint32_t ERS = PACK ? 2 * H : H;  // er / dz row stride (floats)
   const __amdgpu_buffer_rsrc_t er_r =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(er), 0, rbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dz_r =
@@ -469,13 +475,17 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (SMALL) {  // er and dz are 32 B per row of dout's: 32-bit offsets
-        const uint32_t o = static_cast<uint32_t>(pc[i]) * (H * 4u) + hc * 4u;
+        const uint32_t o = static_cast<uint32_t>(pc[i]) * (ERS * 4u) + hc * 4u;
         per[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(er_r, o, 0, 0));
-        pz[i] = dz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dz_r, o, 0, 0))
-                   : 0.0f;
+        if (PACK)
+          pz[i] = __builtin_bit_cast(float,
+                                     __builtin_amdgcn_raw_buffer_load_b32(er_r, o + H * 4u, 0, 0));
+        else
+          pz[i] = dz ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(dz_r, o, 0, 0))
+                     : 0.0f;
       } else {
-        per[i] = er[int64_t(pc[i]) * H + hc];
-        pz[i] = dz ? dz[int64_t(pc[i]) * H + hc] : 0.0f;
+        per[i] = er[int64_t(pc[i]) * ERS + hc];
+        pz[i] = PACK ? er[int64_t(pc[i]) * ERS + H + hc] : (dz ? dz[int64_t(pc[i]) * H + hc] : 0.0f);
       }
       pf[i] = fslot[k + pj[i]];
     }
@@ -538,7 +548,7 @@ __global__ __launch_bounds__(256) void gat_backward_t_kernel(
       const float a = pa[i];
       float tt = ld[hc * LU + j];
       if (DROP) tt = pk[i] ? tt * scale : 0.0f;
-      if (dz) tt = tt + pz[i];
+      if (PACK || dz) tt = tt + pz[i];
       float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
                           : tt * (a <= 0.0f ? alpha : 1.0f);
       g = (a > lo && a < hi) ? g : 0.0f;
@@ -790,14 +800,15 @@ int dglhip_gat_backward_t_ok(int64_t num_heads, int64_t head_dim) {
   return num_heads == 8 && head_dim == 16 ? 1 : 0;
 }
 
-int dglhip_gat_backward_t_device(
-    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+static int gat_backward_t_impl(
+    bool packed, int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
     int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
     int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
     const float* er, const float* dz, const float* dout, float alpha, float clamp_lo,
     float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
     float* d_ft, float* d_el, float* grad, void* stream_) {
   API_BEGIN();
+  DGLHIP_CHECK(!packed || er != nullptr, "the packed form takes er and dz as one table");
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(dglhip_gat_backward_t_ok(num_heads, head_dim) == 1,
                "the transposed GAT backward runs 8 heads x 16 features, got " << num_heads
@@ -819,12 +830,19 @@ int dglhip_gat_backward_t_device(
   const int64_t tbytes = num_rows * num_heads * head_dim * int64_t(sizeof(float));
   const bool small = tbytes < (int64_t(1) << 31);
   const int gpol = grad ? (g_gat_bwd_variant & 3) : 2;  // no grad buffer: nothing stored
+  const bool w5 = (g_gat_bwd_variant & 4) != 0;
   timed_launch(stream, [&] {
+#define DGLHIP_GBT_W(DD, SM, RPV, W, PK)                                                      \
+  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM, RPV, W, PK>), grid_1d(blocks), dim3(256),  \
+                     0, stream, num_items, item_row, item_beg, item_end, by_row, accumulate,    \
+                     cols, fslot, ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp,   \
+                     seed, seed_offset, thr, scale, d_ft, d_el, grad, tbytes, gpol)
 #define DGLHIP_GBT_R(DD, SM, RPV)                                                             \
-  hipLaunchKernelGGL((gat_backward_t_kernel<DD, SM, RPV>), grid_1d(blocks), dim3(256), 0,      \
-                     stream, num_items, item_row, item_beg, item_end, by_row, accumulate, cols, \
-                     fslot, ft, el, er, dz, dout, alpha, clamp_lo, clamp_hi, apply_exp, seed,   \
-                     seed_offset, thr, scale, d_ft, d_el, grad, tbytes, gpol)
+  do {                                                                                        \
+    if (packed) DGLHIP_GBT_W(DD, SM, RPV, 4, true);                                           \
+    else if (w5) DGLHIP_GBT_W(DD, SM, RPV, 5, false);                                         \
+    else DGLHIP_GBT_W(DD, SM, RPV, 4, false);                                                 \
+  } while (0)
 #define DGLHIP_GBT(DD, SM)                                                                    \
   do {                                                                                        \
     if (g_row_pol == 2) DGLHIP_GBT_R(DD, SM, 2);                                              \
@@ -838,8 +856,35 @@ int dglhip_gat_backward_t_device(
     }
 #undef DGLHIP_GBT
 #undef DGLHIP_GBT_R
+#undef DGLHIP_GBT_W
   });
   API_END();
+}
+
+int dglhip_gat_backward_t_device(
+    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+    int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
+    int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
+    const float* er, const float* dz, const float* dout, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
+    float* d_ft, float* d_el, float* grad, void* stream) {
+  return gat_backward_t_impl(false, num_items, item_row, item_beg, item_end, by_row, accumulate,
+                             num_rows, num_src, num_heads, head_dim, cols, fslot, ft, el, er, dz,
+                             dout, alpha, clamp_lo, clamp_hi, apply_exp, drop_p, seed, seed_offset,
+                             d_ft, d_el, grad, stream);
+}
+
+int dglhip_gat_backward_t_packed_device(
+    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+    int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
+    int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
+    const float* erdz, const float* dout, float alpha, float clamp_lo, float clamp_hi,
+    int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset, float* d_ft,
+    float* d_el, float* grad, void* stream) {
+  return gat_backward_t_impl(true, num_items, item_row, item_beg, item_end, by_row, accumulate,
+                             num_rows, num_src, num_heads, head_dim, cols, fslot, ft, el, erdz,
+                             nullptr, dout, alpha, clamp_lo, clamp_hi, apply_exp, drop_p, seed,
+                             seed_offset, d_ft, d_el, grad, stream);
 }
 
 int dglhip_rowsum_heads8_device(int64_t num_rows, const int64_t* indptr,
@@ -868,7 +913,7 @@ int dglhip_set_gat_variant(int variant) {
 
 int dglhip_set_gat_bwd_variant(int variant) {
   API_BEGIN();
-  DGLHIP_CHECK(variant >= 0 && variant <= 2, "unknown GAT backward variant " << variant);
+  DGLHIP_CHECK(variant >= 0 && variant <= 6 && (variant & 3) != 3, "unknown GAT backward variant " << variant);
   g_gat_bwd_variant = variant;
   API_END();
 }

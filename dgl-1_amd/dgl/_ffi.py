@@ -72,6 +72,10 @@ def _load():
                                          [_c_i64] * 4 + [_vp] * 7 +
                                          [_c_float, _c_float, _c_float, _c_int, _c_float,
                                           _c_u64, _vp, _vp, _vp, _vp, _vp]),
+        "dglhip_gat_backward_t_packed_device": (_c_int, [_c_i64, _vp, _vp, _vp, _c_int, _c_int] +
+                                                [_c_i64] * 4 + [_vp] * 6 +
+                                                [_c_float, _c_float, _c_float, _c_int, _c_float,
+                                                 _c_u64, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_rowsum_heads8_device": (_c_int, [_c_i64, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_gat_attention_grad_keep_ranges_device": (
             _c_int, [_c_i64, _c_i64, _c_i64] + [_vp] * 8 +
@@ -161,6 +165,21 @@ def _load():
         "dglhip_xent_bwd_ex_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _vp,
                                                _c_i64, _vp, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_timing_read": (_c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_c_i64)]),
+        "dglhip_spmm_get_policy": (_c_int, [_vp]),
+        "dglhip_spmm_set_policy": (_c_int, [_vp]),
+        "dglhip_spmm_split_threshold": (_c_int, [_c_i64, _c_i64, _c_i64, ctypes.POINTER(_c_i64)]),
+        "dglhip_spmm_padded_width": (_c_int, [_c_i64, ctypes.POINTER(_c_i64)]),
+        "dglhip_spmm_plan_create": (_c_int, [_c_int, _c_int, _c_i64, _c_i64, _c_i64, _vp, _vp,
+                                             _vp, _vp, _vp, ctypes.POINTER(_vp)]),
+        "dglhip_spmm_plan_free": (_c_int, [_vp]),
+        "dglhip_spmm_plan_workspace": (_c_int, [_vp, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                                                _c_i64, _c_int, _vp, _vp, ctypes.POINTER(_c_i64)]),
+        "dglhip_spmm_plan_run": (_c_int, [_vp, _c_int, _c_int, _c_i64, _vp, _c_i64, _c_i64, _vp,
+                                          _c_i64, _c_int, _vp, _vp, _vp, _vp, _c_i64, _vp]),
+        "dglhip_spmm_plan_schedule": (_c_int, [_vp, _c_int, _c_int, _c_i64, _c_i64, _c_i64,
+                                               _c_i64, _c_int, _vp, _vp, ctypes.POINTER(_c_int),
+                                               ctypes.POINTER(_c_i64)]),
+        "dglhip_spmm_plan_stats": (_c_int, [_vp, ctypes.POINTER(_c_i64)]),
         "DGLFuncGetGlobal": (_c_int, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
         "DGLFuncListGlobalNames": (_c_int, [ctypes.POINTER(_c_int),
                                             ctypes.POINTER(ctypes.POINTER(ctypes.c_char_p))]),

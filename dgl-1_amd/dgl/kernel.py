@@ -18,9 +18,14 @@ graphs), so the HIP kernels reproduce the reference's results bit for bit.
 
 Every compute call goes to libdgl_hip.so (HIP kernels for tensors on a ROCm
 device, the library's host kernels for CPU tensors). There is no other path.
+Each CSR's schedules (the source-blocked plan, the heavy-row split, the
+short-row tiers) live in its native launch plan (csrc/spmm_plan.*,
+dglhip_spmm_plan_*): this module passes tensors to it and wraps what it
+hands back, so the C-ABI and these operators run one schedule choice.
 """
 from __future__ import absolute_import
 
+import contextlib
 import ctypes
 import os
 import weakref
@@ -51,8 +56,14 @@ _MSG_NAMES = {"copy_src": MSG_COPY_U, "copy_u": MSG_COPY_U, "src_mul_edge": MSG_
 _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 
 
-# Heavy-row policy for the HIP sum/mean kernel (see dglhip_gspmm_chunked_device),
-# sized from the device: R = the headline kernel's resident waves
+
+# ---------------------------------------------------------------------------
+# Schedule policy: the native launch plan's (dglhip_spmm_get_policy /
+# dglhip_spmm_set_policy, include/dgl_hip.h). One policy serves the engine's
+# own operators and every C-ABI / PackedFunc caller of the plan.
+#
+# Heavy-row policy ("row_split") of the sum / mean kernels, sized from the
+# device: R = the headline kernel's resident waves
 # (dglhip_gspmm_resident_waves: compute units x waves per CU at its occupancy;
 # MI355X 256 x 28 = 7,168).
 #   "auto" : (default) a row is one wave's sequential chain, a launch spreads
@@ -62,11 +73,10 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 #            longer than 16,384 slots (~1.5 ms of chained gathers), below which
 #            the loss is bounded and every row stays one exact chain — are the
 #            rows longer than max(4096, (7168 / 12000) x nnz / R) slots (nnz /
-#            12,000 on MI355X) cut into chunks, sized (CSR.split_plan) to spread
-#            their slots over 4R/7 waves (4,096 on MI355X). A floor of 65,536 left
-#            the 60k-slot hub rows of RMAT-26's pipelined segments at 1/8
-#            unsplit: 13.2 -> 24.3 ms per step (bench.py --emulate-world 8
-#            --workload rmat).
+#            12,000 on MI355X) cut into chunks, sized to spread their slots
+#            over 4R/7 waves (4,096 on MI355X). A floor of 65,536 left the
+#            60k-slot hub rows of RMAT-26's pipelined segments at 1/8 unsplit:
+#            13.2 -> 24.3 ms per step (bench.py --emulate-world 8 --workload rmat).
 #            RMAT-26 (max in-degree ~855k, 2.9x the share) is split: GraphSAGE-
 #            mean epoch 0.693 -> 0.640 s (profiles/r02/graphsage_rmat26_row_split.log);
 #            Reddit (max 21,657 <= 114.8M / 3584 = 32,045) is not, and stays
@@ -75,12 +85,61 @@ _RED_NAMES = {"sum": RED_SUM, "max": RED_MAX, "mean": RED_MEAN}
 #   "off"  : every row is one sequential chain — bit-exact with the reference
 #            on every graph (the documented bit-exact switch)
 #   <int>  : explicit chunk length, applied whenever some row is longer
-_ROW_SPLIT = os.environ.get("DGLHIP_ROW_SPLIT", "auto")
+# (DGLHIP_ROW_SPLIT sets it from the environment.)
+# ---------------------------------------------------------------------------
 _REF_WAVES = 7168       # MI355X (and the host path, which never splits)
-_CRITICAL_MIN = 16384   # rows up to this length are never split by "auto"
-_CUT_NUM, _CUT_DEN = 7168, 12000  # cut rows longer than (7168/12000) of a wave's share
-_CHUNK_MIN = 1024
 _WAVES = {}
+
+
+class _Policy(ctypes.Structure):
+    _fields_ = [("row_split", ctypes.c_int64), ("blocked", ctypes.c_int32),
+                ("short_rows", ctypes.c_int32), ("pad_rows", ctypes.c_int32),
+                ("reserved", ctypes.c_int32), ("block_bytes", ctypes.c_int64),
+                ("block_table_min", ctypes.c_int64), ("block_table_max", ctypes.c_int64),
+                ("block_min_slots", ctypes.c_int64), ("block_max_stretch", ctypes.c_double),
+                ("block_max_suffix", ctypes.c_double), ("block_min_row_bytes", ctypes.c_int64),
+                ("tier_min_rows", ctypes.c_int64), ("pad_min_bytes", ctypes.c_int64)]
+
+
+_POLICY_KEYS = tuple(n for n, _ in _Policy._fields_ if n != "reserved")
+# bumped at every policy change: part of the keys of the Python-side caches
+# of native plan structures (a new policy may give a CSR another schedule)
+_POLICY_GEN = [0]
+
+
+def schedule_policy():
+    """The g-SpMM schedule policy as a dict (row_split -1 auto / 0 off / a
+    chunk length, blocked, short_rows, pad_rows, block_bytes, block_table_min,
+    block_table_max, block_min_slots, block_max_stretch, block_max_suffix,
+    block_min_row_bytes, tier_min_rows, pad_min_bytes)."""
+    p = _Policy()
+    check_call(LIB.dglhip_spmm_get_policy(ctypes.addressof(p)))
+    return {k: getattr(p, k) for k in _POLICY_KEYS}
+
+
+def set_schedule_policy(**changes):
+    """Change fields of the schedule policy; returns the old policy (a dict
+    that set_schedule_policy(**old) restores)."""
+    p = _Policy()
+    check_call(LIB.dglhip_spmm_get_policy(ctypes.addressof(p)))
+    old = {k: getattr(p, k) for k in _POLICY_KEYS}
+    for k, v in changes.items():
+        if k not in _POLICY_KEYS:
+            raise DGLError("unknown schedule policy field %r" % (k,))
+        setattr(p, k, v)
+    check_call(LIB.dglhip_spmm_set_policy(ctypes.addressof(p)))
+    _POLICY_GEN[0] += 1
+    return old
+
+
+@contextlib.contextmanager
+def scheduled(**changes):
+    """Context manager: the schedule policy with ``changes`` for its body."""
+    old = set_schedule_policy(**changes)
+    try:
+        yield
+    finally:
+        set_schedule_policy(**old)
 
 
 def _resident_waves(device=None):
@@ -97,26 +156,37 @@ def _resident_waves(device=None):
     return _WAVES[idx]
 
 
+def _row_split_name(v):
+    return "auto" if v < 0 else ("off" if v == 0 else str(v))
+
+
+def get_row_split():
+    """The heavy-row policy: "auto", "off" or a chunk length (as a string)."""
+    return _row_split_name(schedule_policy()["row_split"])
+
+
 def set_row_split(policy):
     """Set the heavy-row policy ("auto", "off" or a chunk length); returns the old one."""
-    global _ROW_SPLIT
-    old = _ROW_SPLIT
-    _ROW_SPLIT = str(policy)
-    return old
+    pol = str(policy)
+    if pol == "auto":
+        v = -1
+    elif pol in ("off", "0", "", "none", "None"):
+        v = 0
+    else:
+        v = int(pol)
+    return _row_split_name(set_schedule_policy(row_split=v)["row_split"])
 
 
 def _split_threshold(csr, waves=None):
     """Rows longer than this many slots are chunked (0: none), for a launch
-    over ``csr`` on a part with ``waves`` resident waves (None: csr's device)."""
-    pol = _ROW_SPLIT
-    if pol in ("off", "0", "", "none", "None"):
-        return 0
-    if pol == "auto":
-        R = waves if waves is not None else _resident_waves(getattr(csr, "device", None))
-        t = max(4096, csr.nnz * _CUT_NUM // (_CUT_DEN * R))
-        return t if csr.max_degree > max(_CRITICAL_MIN, csr.nnz // (R // 2)) else 0
-    t = int(pol)
-    return t if csr.max_degree > t else 0
+    over ``csr`` on a part with ``waves`` resident waves (None: csr's device):
+    the native plan's gate (dglhip_spmm_split_threshold)."""
+    R = waves if waves is not None else _resident_waves(getattr(csr, "device", None))
+    t = ctypes.c_int64()
+    check_call(LIB.dglhip_spmm_split_threshold(int(csr.nnz), int(csr.max_degree), int(R),
+                                               ctypes.byref(t)))
+    return int(t.value)
+
 
 
 def _stream_of(device):
@@ -145,6 +215,7 @@ class CSR(object):
         self._num_nonempty = None
         self._slot_eid = False  # not computed yet
         self._eid_loc = None
+        self._native = None  # the native launch plan (built on first use)
 
     @property
     def eid(self):
@@ -226,85 +297,54 @@ class CSR(object):
             self._num_nonempty = int((ip[1:] > ip[:-1]).sum()) if self.num_rows else 0
         return self._num_nonempty
 
-    def split_plan(self, threshold, skip_empty=False, chunk=None):
-        """Launch plan cutting rows longer than ``threshold`` slots into chunks
-        of ``chunk`` slots (cached per arguments): dict of device tensors for
-        dglhip_gspmm_chunked_device. ``skip_empty`` leaves rows without slots
-        out of the light list (accumulating launches need not touch them).
-        ``chunk`` None: enough chunks to spread the heavy rows' slots over
-        4R/7 waves (R = the device's resident waves; at least _CHUNK_MIN slots
-        each, at most ``threshold``). The chunk launch runs alone before the light rows, so
-        it must fill the chip: with chunks of ``threshold`` slots RMAT-26's 27
-        hub rows made 88 chunks, 88 waves chaining 89k gathers each for 6.6 ms
-        of a 82 ms call."""
-        key = (threshold, bool(skip_empty), chunk)
-        if key in self._plans:
-            return self._plans[key]
-        ip = self.host_indptr.numpy()
-        deg = ip[1:] - ip[:-1]
-        order = (self.row_order.cpu().numpy().astype(np.int64) if self.row_order is not None
-                 else np.argsort(-deg, kind="stable"))
-        if skip_empty:
-            order = order[deg[order] > 0]
-        heavy_mask = deg[order] > threshold
-        light = order[~heavy_mask].astype(np.int32)
-        heavy = order[heavy_mask]
-        if chunk is None:
-            heavy_slots = int(deg[heavy].sum())
-            chunk_waves = _resident_waves(self.device) * 4 // 7  # 4,096 on MI355X
-            chunk = min(threshold, max(_CHUNK_MIN, -(-heavy_slots // chunk_waves)))
-        threshold = int(chunk)  # the cut length below
-        nchunks = (deg[heavy] + threshold - 1) // threshold
-        ptr = np.concatenate([[0], np.cumsum(nchunks)]).astype(np.int64)
-        rep = np.repeat(np.arange(len(heavy)), nchunks)
-        k = np.arange(int(ptr[-1])) - ptr[rep]
-        beg = ip[heavy][rep] + k * threshold
-        end = np.minimum(beg + threshold, ip[heavy + 1][rep])
-        dev = self.device
-        plan = {"light": torch.from_numpy(light).to(dev),
-                "heavy": torch.from_numpy(heavy.astype(np.int32)).to(dev),
-                "chunk_ptr": torch.from_numpy(ptr).to(dev),
-                "beg": torch.from_numpy(beg.astype(np.int64)).to(dev),
-                "end": torch.from_numpy(end.astype(np.int64)).to(dev),
-                "num_chunks": int(ptr[-1])}
-        self._plans[key] = plan
-        return plan
+    @property
+    def plan(self):
+        """The native launch plan of this CSR (dglhip_spmm_plan_*, built on
+        first use): every g-SpMM over the CSR runs on it."""
+        if self._native is None:
+            self._native = _NativePlan(self)
+        return self._native
 
-    def tiers(self, rows, key):
-        """Row-length tiers of a degree-descending row list ``rows`` (device
-        int32, cached under ``key``): (n_long, [(max_deg, items), ...]). Rows
-        [0, n_long) have more than 8 slots; each tier lists rows of at most
-        max_deg (8, 4, 0) slots as a compacted CSR of their own for
-        dglhip_gspmm_short_rows_device: ``items`` = (rows, slot_ptr, slot_cols)
-        device tensors (slot_ptr / slot_cols None for the empty tier)."""
-        ck = ("tiers", key)
-        if ck in self._plans:
-            return self._plans[ck]
-        ip = self.host_indptr.numpy()
-        rows_h = rows.cpu().numpy().astype(np.int64)
-        deg = (ip[1:] - ip[:-1])[rows_h]
-        neg = -deg  # ascending
-        cut = [int(np.searchsorted(neg, -t, side="left")) for t in (8, 4, 0)]
-        n = len(deg)
-        tiers = []
-        for maxd, lo, hi in ((8, cut[0], cut[1]), (4, cut[1], cut[2]), (0, cut[2], n)):
-            if hi <= lo:
-                continue
-            r = rows[lo:hi].contiguous()
-            if maxd == 0:
-                tiers.append((maxd, (r, None, None), hi - lo))
-                continue
-            d = torch.from_numpy(deg[lo:hi]).to(self.device)
-            sp = torch.zeros(hi - lo + 1, dtype=torch.int64, device=self.device)
-            torch.cumsum(d, 0, out=sp[1:])
-            total = int(deg[lo:hi].sum())
-            start = self.indptr.index_select(0, r.long())
-            pos = torch.repeat_interleave(start - sp[:-1], d, output_size=total) + \
-                torch.arange(total, device=self.device)
-            tiers.append((maxd, (r, sp, self.indices.index_select(0, pos)), hi - lo))
-        res = (cut[0], tiers)
-        self._plans[ck] = res
-        return res
+    def split_plan(self, threshold, skip_empty=False, chunk=None):
+        """The plan's heavy-row launch plan cutting rows longer than
+        ``threshold`` slots into chunks of ``chunk`` slots (None: enough
+        chunks to spread the heavy slots over 4R/7 waves, R the device's
+        resident waves; at least 1,024 slots each, at most ``threshold``):
+        dict of tensors light, heavy, chunk_ptr, beg, end and num_chunks, as
+        dglhip_gspmm_chunked_device takes them. ``skip_empty`` leaves rows
+        without slots out of the light list (accumulating launches need not
+        touch them). The chunk launch runs alone before the light rows, so it
+        must fill the chip: with chunks of ``threshold`` slots RMAT-26's 27 hub
+        rows made 88 chunks, 88 waves chaining 89k gathers each for 6.6 ms of
+        a 82 ms call."""
+        p = self.plan
+        f = _retry_oom(lambda: _capi("SpmmPlanSplit")(p.arg, int(threshold), 1 if skip_empty else 0,
+                                                      int(chunk or 0), p.stream_arg()))
+        meta = f(0).tolist()
+        return {"light": f(1), "heavy": f(2), "chunk_ptr": f(3), "beg": f(4), "end": f(5),
+                "num_chunks": int(meta[2])}
+
+    def tiers(self, skip_empty=False, threshold=0):
+        """The plan's short-row tiers of the degree-descending schedule (the
+        first num_nonempty rows with ``skip_empty``), or with ``threshold`` of
+        the heavy-row split's light rows: (n_long, [(max_deg, (rows, slot_ptr,
+        slot_cols), n), ...]). Rows [0, n_long) of the list have more than 8
+        slots; each tier lists rows of at most max_deg (8, 4, 0) slots as a
+        compacted CSR of their own for dglhip_gspmm_short_rows_device
+        (slot_ptr / slot_cols None for the empty tier)."""
+        p = self.plan
+        f = _retry_oom(lambda: _capi("SpmmPlanTiers")(p.arg, 1 if skip_empty else 0,
+                                                      int(threshold), p.stream_arg()))
+        meta = f(0).tolist()
+        n_long, _, T = meta[:3]
+        out = []
+        for t in range(int(T)):
+            maxd, n = int(meta[3 + 2 * t]), int(meta[4 + 2 * t])
+            rows = f(1 + 3 * t)
+            sp = f(2 + 3 * t) if maxd else None
+            cols = f(3 + 3 * t) if maxd else None
+            out.append((maxd, (rows, sp, cols), n))
+        return int(n_long), out
 
     @property
     def nnz(self):
@@ -500,36 +540,118 @@ def _edge_len(eshape, fshape):
                    % (eshape, fshape))
 
 
-# tables past one XCD's 4 MiB L2 are gathered from the Infinity Cache / HBM in
-# whole 128-B lines (Reddit-shaped graph, tools/feat_sweep.py: F = 24 takes
-# 2.26 ms at 1.5 lines per row vs 1.75 ms for F = 32 at one line; F = 41 and
-# 50 padded both read 3.52 ms, F = 64 3.57)
-_PAD_MIN_BYTES = 4 << 20
+# ---------------------------------------------------------------------------
+# The native launch plan of a CSR (dglhip_spmm_plan_*, csrc/spmm_plan.*)
+# ---------------------------------------------------------------------------
+def _retry_oom(fn):
+    """Run ``fn``; when the library's hipMalloc fails, hand torch's cached
+    blocks back to the device once and retry (plan structures live in memory
+    the library allocates beside torch's caching allocator)."""
+    try:
+        return fn()
+    except DGLError as err:
+        msg = str(err)
+        if "hipMalloc" not in msg and "out of memory" not in msg.lower():
+            raise
+        if torch.cuda.is_available():
+            torch.cuda.empty_cache()
+        return fn()
 
 
-def _lines_per_row(F, ld):
-    """Mean number of 128-B lines one gathered row of F floats touches when
-    rows sit at a stride of ``ld`` floats (row starts cycle through the
-    offsets (u * ld * 4) mod 128)."""
-    tot = 0
-    for u in range(32):
-        off = (u * ld * 4) % 128
-        tot += (off + 4 * F + 127) // 128
-    return tot / 32.0
+def _capi(name):
+    return _ffi.get_global_func("dglhip._CAPI_" + name)
 
 
-def padded_width(F):
-    """Row stride (floats) for the source rows of a g-SpMM gather: F itself,
-    or F rounded up to 16 / 32 floats when that cuts the 128-B lines a row
-    touches by at least 5 % (F = 41: 2.28 -> 2.0 lines at a 48-float stride;
-    F = 24: 1.5 -> 1.0 at 32). Rows of 16, 32, 64, 128 floats already fit."""
-    best, best_lines = F, _lines_per_row(F, F)
-    for ld in (-(-F // 16) * 16, -(-F // 32) * 32):
-        if ld > F and ld % 2 == 0:
-            lines = _lines_per_row(F, ld)
-            if lines < best_lines * 0.95 and lines < _lines_per_row(F, best) - 1e-9:
-                best, best_lines = ld, lines
-    return best
+class _NativePlan(object):
+    """Handle on a CSR's launch plan (dglhip_spmm_plan_create / _free). The
+    plan borrows the CSR's indptr / indices / row_order (the CSR holds them for
+    as long as it holds the plan) and keeps the schedules the g-SpMM runs over
+    them, built natively on first use: the same object the
+    C-ABI and dglhip._CAPI_GSpMM hand out, so one implementation serves the
+    Python operators and every C / PackedFunc caller."""
+
+    __slots__ = ("handle", "device", "_ws", "_cache", "__weakref__")
+
+    def __init__(self, csr):
+        dev = csr.device
+        self.handle = None
+        self.device = dev
+        self._ws = {}
+        self._cache = {}
+        h = ctypes.c_void_p()
+        if dev.type == "cuda":
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
+            kind, stream = (10, idx), _stream_of(dev)
+            hip = csr._host_indptr
+        else:
+            kind, stream, hip = (1, 0), None, None
+
+        def make():
+            check_call(LIB.dglhip_spmm_plan_create(
+                kind[0], kind[1], csr.num_rows, csr.num_cols, csr.nnz, ptr(csr.indptr),
+                ptr(csr.indices) if csr.nnz else None, ptr(hip), ptr(csr.row_order), stream,
+                ctypes.byref(h)))
+        _retry_oom(make)
+        self.handle = h.value
+
+    @property
+    def arg(self):
+        return ("handle", self.handle)
+
+    def stream(self):
+        return _stream_of(self.device) if self.device.type == "cuda" else None
+
+    def stream_arg(self):
+        return ("handle", self.stream().value) if self.device.type == "cuda" else None
+
+    def __del__(self):
+        h, self.handle = self.handle, None
+        if h:
+            try:
+                LIB.dglhip_spmm_plan_free(h)
+            except Exception:  # noqa: BLE001 - interpreter shutdown
+                pass
+
+    def workspace(self, msg, red, F, ldu, urows, elen, emode, erow):
+        key = (msg, red, F, ldu, urows, elen, emode, _POLICY_GEN[0])
+        nbytes = self._ws.get(key)
+        if nbytes is None:
+            b = ctypes.c_int64()
+            _retry_oom(lambda: check_call(LIB.dglhip_spmm_plan_workspace(
+                self.handle, msg, red, F, ldu, urows, elen, emode, ptr(erow), self.stream(),
+                ctypes.byref(b))))
+            nbytes = self._ws[key] = int(b.value)
+        return nbytes
+
+    def schedule(self, msg, red, F, ldu=0, urows=0, elen=0, emode=0, erow=None):
+        """(path, launches) a run with these arguments takes
+        (DGLHIP_PLAN_PATH_*: 0 host, 1 rows, 2 blocked, 3 blocked max)."""
+        path, launches = ctypes.c_int(), ctypes.c_int64()
+        _retry_oom(lambda: check_call(LIB.dglhip_spmm_plan_schedule(
+            self.handle, msg, red, F, ldu, urows, elen, emode, ptr(erow), self.stream(),
+            ctypes.byref(path), ctypes.byref(launches))))
+        return int(path.value), int(launches.value)
+
+    def stats(self):
+        """dict: rows, cols, nnz, max_degree, nonempty, waves, heavy_threshold."""
+        s = (ctypes.c_int64 * 7)()
+        check_call(LIB.dglhip_spmm_plan_stats(self.handle, s))
+        return dict(zip(("rows", "cols", "nnz", "max_degree", "nonempty", "waves",
+                         "heavy_threshold"), list(s)))
+
+
+PLAN_PATH_HOST, PLAN_PATH_ROWS, PLAN_PATH_BLOCKED, PLAN_PATH_MAX_BLOCKED = 0, 1, 2, 3
+_EDGE_BY_SLOT, _EDGE_BY_EID, _EDGE_BY_MAP = 0, 1, 2
+
+
+def _edge_layout(csr, msg, emap):
+    """(layout, rows tensor) of the edge values for the plan: by slot, by the
+    CSR's edge ids (the plan caches what it derives from them), or a map."""
+    if msg in (MSG_COPY_U, MSG_COPY_U_BF16) or emap is SLOT:
+        return _EDGE_BY_SLOT, None
+    if emap is None:
+        return _EDGE_BY_EID, csr.eid
+    return _EDGE_BY_MAP, emap.contiguous()
 
 
 def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None, emap=None):
@@ -552,177 +674,36 @@ def _run_gspmm(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out=None
 
 
 def _run_gspmm_call(csr, msg, red, ufeat2, efeat2, elen, feat_len, want_arg, out, emap, dev):
+    """One product on the CSR's native plan (dglhip_spmm_plan_run): the plan
+    picks the source-blocked schedule, the heavy-row split, the short-row
+    tiers, the padded-stride copy and the edge values' order exactly as it
+    does for a C-ABI caller."""
     if csr.device != dev:
         raise DGLError("adjacency on %s but features on %s" % (csr.device, dev))
-    if (dev.type == "cuda" and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and efeat2 is None and
-            red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)):
-        blocks = _block_plan(csr, ufeat2, feat_len)
-        if blocks is not None:
-            return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out), None
-    if (dev.type == "cuda" and msg == MSG_U_MUL_E and red in (RED_SUM, RED_MEAN, RED_SUM_ACCUM)
-            and ufeat2 is not None and ufeat2.dtype == torch.float32 and efeat2 is not None):
-        blocks = _block_plan(csr, ufeat2, feat_len)
-        if blocks is not None:
-            # the edge value of each segment slot: its row of efeat2 through
-            # the plan's slot map (cached). Scalar values are gathered into
-            # the segments' slot order first (one pass: Reddit-shaped, eid
-            # order, 5.98 ms against 8.25 with a dependent 4-B load per slot
-            # in the kernel); wider rows (GAT's per-head weights) are read in
-            # the kernel (27.4 ms per GAT step against 51 through torch's
-            # gather of 32-B rows)
-            rows = _block_edge_rows(csr, blocks, emap)
-            if elen == 1:
-                return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out,
-                                    efeat2.index_select(0, rows), elen), None
-            return _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out, efeat2, elen,
-                                rows), None
-    if (dev.type == "cuda" and red == RED_MAX and out is None and ufeat2 is not None and
-            (msg == MSG_COPY_U or (msg == MSG_U_MUL_E and (
-                emap is SLOT or (emap is None and csr.slot_eid is None)))) and
-            ufeat2.dtype == torch.float32 and ufeat2.dim() == 2 and ufeat2.is_contiguous() and
-            ufeat2.shape[1] == feat_len):
-        # max over the blocks' row ranges, continued block by block: the
-        # same values and (strict >, slot order) the same argmax. Edge
-        # values by edge id stay in one launch: a dependent 4-B load per
-        # slot makes the blocked launches slower (8.75 vs 8.50 ms, Reddit-
-        # shaped); copy_u max 7.42 -> 4.16 ms
-        cuts = _block_cuts(csr, feat_len * 4, _BLOCK_BYTES)
-        if cuts is not None:
-            return _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg,
-                                    emap)
     if out is None:
         out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
     arg = None
     if red == RED_MAX and want_arg:
         arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev)
-    if msg in (MSG_COPY_U, MSG_COPY_U_BF16) or emap is SLOT:
-        eid = None
-    else:
-        eid = csr.slot_eid if emap is None else emap
-    split = _split_threshold(csr) if (dev.type == "cuda" and red != RED_MAX) else 0
-    skip = red in _ACCUM and csr.row_order is not None  # empty rows: nothing to add
-    ld = 0
+    plan = csr.plan
+    emode, erow = _edge_layout(csr, msg, emap)
+    ldu = 0
     if ufeat2 is not None and ufeat2.shape[0] > 1 and _row_strided(ufeat2, feat_len):
-        ld = ufeat2.stride(0)  # already row-padded by the caller (gspmm)
-    elif dev.type == "cuda" and _pad_rows(msg, red, ufeat2, feat_len):
-        # source rows straddle cache lines: every schedule below gathers them
-        # from a padded copy (same values, same chains: identical results,
-        # fewer lines per row)
-        ld = padded_width(feat_len)
-        up = ufeat2.new_empty(ufeat2.shape[0], ld)
-        up[:, :feat_len] = ufeat2
-        ufeat2 = up
-    tiered = (dev.type == "cuda" and _TIERED and msg in (MSG_COPY_U, MSG_COPY_U_BF16) and
-              red in (RED_SUM, RED_MEAN) + _ACCUM)
-    if split:
-        # "auto" sizes the chunks to fill the chip; an explicit policy is the chunk length
-        p = csr.split_plan(split, skip_empty=skip, chunk=None if _ROW_SPLIT == "auto" else split)
-        partial = torch.empty(p["num_chunks"], feat_len, dtype=torch.float32, device=dev)
-        light = p["light"]
-        n_light, tail = light.numel(), []
-        if tiered:
-            n_long, tail = csr.tiers(light, ("split", split, skip))
-            if sum(t[2] for t in tail) >= _TIER_MIN_ROWS:
-                n_light = n_long
-            else:
-                tail = []
-        check_call(LIB.dglhip_gspmm_chunked_device(
-            msg, red, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid), ptr(ufeat2),
-            ptr(efeat2), elen, ptr(out), n_light, ptr(light), p["num_chunks"],
-            ptr(p["beg"]), ptr(p["end"]), p["heavy"].numel(), ptr(p["heavy"]),
-            ptr(p["chunk_ptr"]), ptr(partial), ld, _stream_of(dev)))
-        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld)
-    elif tiered and csr.row_order is not None and \
-            _tail_rows(csr, csr.num_nonempty if skip else csr.num_rows, skip):
-        nrows = csr.num_nonempty if skip else csr.num_rows
-        n_long, tail = csr.tiers(csr.row_order[:nrows], ("plain", skip))
-        _run_rows(csr, msg, red, n_long, feat_len, ld, eid, ufeat2, efeat2, elen, out, arg)
-        _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld)
-    elif dev.type == "cuda":
-        _run_rows(csr, msg, red, csr.num_nonempty if skip else csr.num_rows, feat_len, ld,
-                  eid, ufeat2, efeat2, elen, out, arg)
-    else:
-        check_call(LIB.dglhip_gspmm_host(
-            msg, red, csr.num_rows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
-            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), 0))
+        ldu = ufeat2.stride(0)
+    urows = 0 if ufeat2 is None else ufeat2.shape[0]
+    elen = 0 if efeat2 is None else elen
+    nbytes = plan.workspace(msg, red, feat_len, ldu, urows, elen, emode, erow)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=dev) if nbytes else None
+    check_call(LIB.dglhip_spmm_plan_run(
+        plan.handle, msg, red, feat_len, ptr(ufeat2), ldu, urows, ptr(efeat2), elen, emode,
+        ptr(erow), ptr(out), ptr(arg), ptr(ws), nbytes, plan.stream()))
     return out, arg
-
-
-# Short-row tiers (dglhip_gspmm_short_rows_device): rows of <= 8 slots, and
-# rows without slots, of a degree-descending schedule go to the batched
-# short-row kernel once there are at least _TIER_MIN_ROWS of them (RMAT-26:
-# 55M of its 67M rows; tools/rmat_tail_study.py). Same chains, same bits.
-_TIERED = os.environ.get("DGLHIP_SHORT_ROWS", "on") != "off"
-_TIER_MIN_ROWS = 1 << 16
 
 
 def set_short_rows(on):
     """Route short / empty rows to the batched short-row kernel (default on);
     returns the old setting."""
-    global _TIERED
-    old = _TIERED
-    _TIERED = bool(on)
-    return old
-
-
-def _tail_rows(csr, nrows, skip):
-    """Whether the schedule's short tail is long enough to tier."""
-    _, tail = csr.tiers(csr.row_order[:nrows], ("plain", skip))
-    return sum(t[2] for t in tail) >= _TIER_MIN_ROWS
-
-
-def _run_rows(csr, msg, red, nrows, feat_len, ld, eid, ufeat2, efeat2, elen, out, arg):
-    """The one-wave-per-row kernel over the first ``nrows`` rows of the
-    schedule (ufeat rows at stride ``ld`` when it is nonzero)."""
-    if ld:
-        check_call(LIB.dglhip_gspmm_strided_device(
-            msg, red, nrows, feat_len, ld, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
-            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(csr.row_order), _stream_of(out.device)))
-    else:
-        check_call(LIB.dglhip_gspmm_device(
-            msg, red, nrows, feat_len, ptr(csr.indptr), ptr(csr.indices), ptr(eid),
-            ptr(ufeat2), ptr(efeat2), elen, ptr(out), ptr(arg), ptr(csr.row_order),
-            _stream_of(out.device)))
-
-
-def _run_short_rows(csr, msg, red, ufeat2, feat_len, out, tail, ld=0):
-    dev = out.device
-    for maxd, (rows, sp, cols), n in tail:
-        if maxd == 0 and red in _ACCUM:
-            continue  # nothing to add
-        check_call(LIB.dglhip_gspmm_short_rows_device(
-            msg, red, n, feat_len, maxd, csr.num_rows, ptr(rows), ptr(sp), ptr(cols),
-            ptr(ufeat2), ptr(out), ld, _stream_of(dev)))
-
-
-# Source-blocked schedule (copy_u with sum / mean, DESIGN.md §4.1): the
-# columns are cut into B contiguous blocks of about _BLOCK_BYTES of feature
-# rows each, every block a CSR of its own over all rows, run as B launches
-# that continue each row's chain (SUM_ACCUM). All 8 XCDs then gather from the
-# same slice of H at a time, which their 4 MiB L2s serve, instead of from the
-# whole table through the Infinity Cache (Reddit-shaped graph, F = 128: 7.41
-# -> 4.21 ms at B = 16, tools/blocked_study.py). Used only where it keeps
-# every chain: along each row's slots (edge-id order) the sources' blocks
-# never decrease over a prefix of the row — then block by block IS the
-# prefix's order — and the slots after it (at most 1/16 of all) continue the
-# chain in one last launch, in order. The results are bit-identical. Graphs
-# whose edges are numbered source-major qualify whole (the (src, dst)-sorted
-# loaders, the synthetic generators, the transposed CSR of any such graph),
-# and so do such graphs with edges appended later (GCN's self-loops: one
-# suffix slot per row). Other graphs, tables that fit one L2 or exceed the
-# Infinity Cache, and rows too short to split keep the one-launch schedule.
-_BLOCKED = os.environ.get("DGLHIP_BLOCKED", "auto")
-_BLOCK_BYTES = int(os.environ.get("DGLHIP_BLOCK_BYTES", 6 << 20))  # 6 MiB per block
-_BLOCK_TABLE_MIN = 16 << 20     # below: the table already fits the L2s' share
-_BLOCK_TABLE_MAX = 256 << 20    # above: out's per-block pass outweighs the L2 hits
-# slots per row and block, on average (the rows' per-block pass must pay)
-_BLOCK_MIN_SLOTS = int(os.environ.get("DGLHIP_BLOCK_MIN_SLOTS", 12))
-# rows of at most one 128-B line keep one launch: the Reddit-shaped graph at
-# F = 32 runs 1.74 ms in one launch against 1.89 in 5 blocks (F = 41 padded
-# to 192 B: 3.39 -> 2.05; F = 64: 3.56 -> 2.24; tools/blocked_width_sweep.py)
-_BLOCK_MIN_ROW_BYTES = 128
-# how far the slot rule may stretch the slices past the target (_block_count)
-_BLOCK_MAX_STRETCH = float(os.environ.get("DGLHIP_BLOCK_MAX_STRETCH", 3))
+    return bool(set_schedule_policy(short_rows=1 if on else 0)["short_rows"])
 
 
 def set_blocked(policy):
@@ -730,155 +711,42 @@ def set_blocked(policy):
     the fused GAT layer: "auto" (default: where it keeps the chains
     bit-identical and the table size pays) or "off". Returns the old
     policy."""
-    global _BLOCKED
-    old = _BLOCKED
-    _BLOCKED = str(policy)
-    return old
+    old = set_schedule_policy(blocked=0 if str(policy) == "off" else 1)
+    return "auto" if old["blocked"] else "off"
 
 
-def _block_count(csr, table_bytes, block_bytes=None):
-    # a plan holds about 12 B per slot and its build about 40 B per slot
-    # transiently: graphs past 2^31 slots keep one launch
-    if csr.num_rows == 0 or csr.nnz == 0 or csr.nnz >= (1 << 31):
-        return 0
-    if not _BLOCK_TABLE_MIN <= table_bytes <= _BLOCK_TABLE_MAX:
-        return 0
-    want = -(-table_bytes // (block_bytes or _BLOCK_BYTES))
-    B = min(want, csr.nnz // (_BLOCK_MIN_SLOTS * max(csr.num_nonempty, 1)))
-    # rows too short to cut the table into L2-sized slices: slices stretched
-    # past 3x the target gain nothing (tools/segment_block_study.py, emulated
-    # ranks: 12.8 MB slices 1.48 -> 1.26 ms; 24-26 MB slices 1.03 -> 1.04,
-    # 1.78 -> 1.78)
-    if _BLOCK_MAX_STRETCH * B < want:
-        return 0
-    return int(B) if B >= 2 else 0
+def set_pad_rows(policy):
+    """Padded-stride gathers for line-straddling rows: "auto" (default) or
+    "off"; returns the old policy."""
+    old = set_schedule_policy(pad_rows=1 if str(policy) == "auto" else 0)
+    return "auto" if old["pad_rows"] else "off"
 
 
-def _column_span(csr):
-    """(lo, hi): the range of columns the slots reference (cached); a segment
-    of a pipelined partition references one chunk of its halo buffer."""
-    span = csr._plans.get("span")
-    if span is None:
-        if csr.nnz:
-            lo, hi = torch.aminmax(csr.indices)
-            span = (int(lo), int(hi) + 1)
-        else:
-            span = (0, 0)
-        csr._plans["span"] = span
-    return span
+_PADDED = {}
 
 
-def _block_plan(csr, ufeat2, feat_len, block_bytes=None):
-    """The segment CSRs of the blocked schedule for ``csr`` (cached), or None
-    when the schedule does not apply or would reorder some row's chain. The
-    blocks cut the referenced column range evenly (``block_bytes`` of source
-    rows each, default _BLOCK_BYTES)."""
-    if _BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0:
-        return None
-    ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
-    row_bytes = max(ld, feat_len) * ufeat2.element_size()
-    if row_bytes <= _BLOCK_MIN_ROW_BYTES:
-        return None
-    lo, hi = _column_span(csr)
-    B = _block_count(csr, (hi - lo) * row_bytes, block_bytes)
-    if not B:
-        return None
-    if _split_threshold(csr):  # a row long enough to need the heavy-row split
-        return None
-    key = ("blocked", B)
-    if key not in csr._plans:
-        csr._plans[key] = _block_items(csr, B, lo, hi)
-    return csr._plans[key]
+def padded_width(F):
+    """Row stride (floats) for the source rows of a g-SpMM gather: F itself,
+    or F rounded up to 16 / 32 floats when that cuts the 128-B lines a row
+    touches by at least 5 % (F = 41: 2.28 -> 2.0 lines at a 48-float stride;
+    F = 24: 1.5 -> 1.0 at 32); the plan's rule (dglhip_spmm_padded_width)."""
+    w = _PADDED.get(F)
+    if w is None:
+        o = ctypes.c_int64()
+        check_call(LIB.dglhip_spmm_padded_width(int(F), ctypes.byref(o)))
+        w = _PADDED[F] = int(o.value)
+    return w
 
 
-class _BlockItems:
-    """One source block (or the suffix) of the blocked schedule as items:
-    ``rows`` (int32) the rows with slots in the block, longest first (stable
-    by row id); item i's slots are [ptr[i], ptr[i+1]) of ``indices``, laid out
-    in item order, in each row's slot order; ``pos`` the CSR slot each came
-    from (int32 below 2^31 slots)."""
-    __slots__ = ("rows", "ptr", "indices", "pos", "nnz", "suffix")
-
-    def __init__(self, csr, row_counts, pos_csr_order, suffix=False):
-        dev = csr.device
-        c = row_counts
-        cnt_sorted, order = torch.sort(c, descending=True, stable=True)
-        n = int((cnt_sorted > 0).sum())
-        order, cnt = order[:n], cnt_sorted[:n]
-        ptr_ = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(cnt, 0, out=ptr_[1:])
-        # where each row's slots sit in pos_csr_order (rows ascending)
-        start = torch.zeros(csr.num_rows, dtype=torch.int64, device=dev)
-        torch.cumsum(c[:-1], 0, out=start[1:])
-        nnz = int(ptr_[-1])
-        item = torch.repeat_interleave(torch.arange(n, device=dev), cnt, output_size=nnz)
-        within = torch.arange(nnz, device=dev) - ptr_[item]
-        pos = pos_csr_order[start[order][item] + within]
-        del item, within, start
-        self.indices = csr.indices[pos]
-        # int32 where it fits: the plan's slot map (edge-valued messages)
-        self.pos = pos.to(torch.int32) if csr.nnz < (1 << 31) else pos
-        del pos
-        self.rows = order.to(torch.int32)
-        self.ptr = ptr_
-        self.nnz = nnz
-        self.suffix = suffix
-
-
-def _block_items(csr, B, lo, hi):
-    """The blocked schedule of ``csr`` as _BlockItems (B blocks, then the
-    suffix if any), or None (_block_split)."""
-    split = _block_split(csr, B, lo, hi)
-    if split is None:
-        return None
-    blk, counts, pre, sfx = split
-    plan = []
-    for b in range(B):
-        sel = blk == b if pre is None else (blk == b) & pre
-        plan.append(_BlockItems(csr, counts[:, b], torch.nonzero(sel).squeeze(1)))
-        del sel
-    if pre is not None:
-        plan.append(_BlockItems(csr, sfx, torch.nonzero(~pre).squeeze(1), suffix=True))
-    return plan
-
-
-# at most this share of the slots may follow their row's monotone prefix
-# (GCN's self-loops, appended after the edges: one slot per row)
-_BLOCK_MAX_SUFFIX = 1.0 / 16
-
-
-def _block_split(csr, B, lo, hi):
-    """The blocked schedule of ``csr`` over B even blocks of columns [lo, hi):
-    (block of each slot, per-row counts (num_rows, B) of the slots in each
-    row's monotone prefix, prefix mask or None when every row is monotone,
-    per-row suffix counts or None). A row's prefix runs up to its first slot
-    whose block is lower than the previous slot's; blocks then keep the
-    prefix's chain, and the suffix continues it in one last launch. None when
-    the suffixes exceed _BLOCK_MAX_SUFFIX of the slots."""
-    dev = csr.device
-    R = csr.num_rows
-    bs = -(-(hi - lo) // B)
-    blk = torch.div(csr.indices - lo, bs, rounding_mode="floor")  # block of each slot
-    deg = csr.degrees()
-    dec = torch.zeros(csr.nnz, dtype=torch.bool, device=dev)
-    dec[1:] = blk[1:] < blk[:-1]
-    dec[csr.indptr[:-1][deg > 0]] = False  # a row's first slot starts its chain
-    rid = torch.repeat_interleave(torch.arange(R, device=dev), deg, output_size=csr.nnz)
-    pre = sfx = None
-    key = rid * B + blk
-    if bool(dec.any()):
-        cs = torch.cumsum(dec, 0)
-        # decreases before each row's first slot (not one itself): in-row count = cs - base
-        base = cs[csr.indptr[:-1].clamp(max=csr.nnz - 1)]
-        pre = (cs - base[rid]) == 0
-        del cs, base
-        if csr.nnz - int(pre.sum()) > csr.nnz * _BLOCK_MAX_SUFFIX:
-            return None
-        sfx = torch.bincount(rid[~pre], minlength=R)
-        key = key[pre]
-    del dec, rid
-    counts = torch.bincount(key, minlength=R * B).view(R, B)
-    return blk, counts, pre, sfx
+def _pad_rows(msg, red, ufeat2, feat_len):
+    """Whether the plan gathers these rows from a padded copy (the same rule:
+    callers that produce such rows write them padded instead)."""
+    if msg not in (MSG_COPY_U, MSG_U_MUL_E) or red not in (RED_SUM, RED_MEAN) + _ACCUM or \
+            ufeat2 is None or ufeat2.dtype != torch.float32:
+        return False
+    pol = schedule_policy()
+    return (bool(pol["pad_rows"]) and ufeat2.numel() * 4 >= pol["pad_min_bytes"] and
+            padded_width(feat_len) != feat_len)
 
 
 # the fused GAT kernels' blocks: their per-row work (the attention through LDS)
@@ -898,51 +766,98 @@ _GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 7 
 _GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 11 << 20))
 
 
+class _PlanLaunch(object):
+    """One launch of the plan's source-blocked schedule (views of the plan's
+    arrays): ``rows`` (int32) the rows with slots in the block, longest first
+    (stable by row id); item i's slots are [ptr[i], ptr[i+1]) of the plan's
+    global slot arrays (``ptr`` holds global offsets); ``indices`` / ``pos``
+    this launch's slots (column ids, and the CSR slot each came from)."""
+    __slots__ = ("rows", "ptr", "indices", "pos", "nnz", "off", "suffix")
+
+
+class _BlockedSchedule(list):
+    """The plan's source-blocked schedule: its launches (B blocks, then the
+    suffix if any) plus the global arrays: ``indices`` / ``pos`` (plan
+    order), ``absent`` (rows the first launch does not list)."""
+
+
+def _blocked_native(csr, row_bytes, block_bytes, blocks=0):
+    """The native plan's blocked schedule for gathered rows of ``row_bytes``
+    in ``block_bytes`` slices (or exactly ``blocks`` blocks), as torch views
+    of its arrays (cached per policy); None when none applies."""
+    plan = csr.plan
+    key = ("blocked", int(row_bytes), int(block_bytes), int(blocks), _POLICY_GEN[0])
+    if key in plan._cache:
+        return plan._cache[key]
+    f = _retry_oom(lambda: _capi("SpmmPlanBlocked")(plan.arg, int(row_bytes), int(block_bytes),
+                                                    int(blocks), plan.stream_arg()))
+    res = None
+    if f is not None:
+        meta = f(0).tolist()
+        B, sfx, _, L = meta[:4]
+        res = _BlockedSchedule()
+        res.indices, res.pos, res.absent = f(1), f(2), f(3)
+        res.B, res.has_suffix = int(B), bool(sfx)
+        for i in range(int(L)):
+            n_items, nnz, off, suffix = meta[4 + 4 * i:8 + 4 * i]
+            it = _PlanLaunch()
+            it.rows, it.ptr = f(4 + 2 * i), f(5 + 2 * i)
+            it.indices = res.indices[off:off + nnz]
+            it.pos = res.pos[off:off + nnz]
+            it.nnz, it.off, it.suffix = int(nnz), int(off), bool(suffix)
+            res.append(it)
+    plan._cache[key] = res
+    return res
+
+
+def _block_plan(csr, ufeat2, feat_len, block_bytes=None):
+    """The blocked schedule the plan runs for these source rows (None when
+    the product keeps one launch): the blocks cut the referenced column range
+    evenly (``block_bytes`` of source rows each, default the policy's)."""
+    ld = ufeat2.stride(0) if (ufeat2.dim() == 2 and ufeat2.shape[0] > 1) else feat_len
+    row_bytes = max(ld, feat_len) * ufeat2.element_size()
+    if csr.nnz == 0:
+        return None
+    return _blocked_native(csr, row_bytes, block_bytes or schedule_policy()["block_bytes"])
+
+
+def _block_items(csr, blocks):
+    """The plan's blocked schedule at exactly ``blocks`` source blocks (None:
+    some rows' suffixes exceed the policy's share)."""
+    return _blocked_native(csr, 0, 0, blocks)
+
+
+def _column_span(csr):
+    """(lo, hi): the range of columns the slots reference."""
+    if csr.nnz == 0:
+        return (0, 0)
+    ind = csr.indices
+    lo, hi = torch.aminmax(ind) if ind.is_cuda else (ind.min(), ind.max())
+    return int(lo), int(hi) + 1
+
+
+def _cuts_native(csr, row_bytes, block_bytes, blocks=0):
+    plan = csr.plan
+    key = ("cuts", int(row_bytes), int(block_bytes), int(blocks), _POLICY_GEN[0])
+    if key in plan._cache:
+        return plan._cache[key]
+    arr = _retry_oom(lambda: _capi("SpmmPlanCuts")(plan.arg, int(row_bytes), int(block_bytes),
+                                                   int(blocks), plan.stream_arg()))
+    res = None if arr is None else [arr[i] for i in range(arr.shape[0])]
+    plan._cache[key] = res
+    return res
+
+
 def _block_cuts(csr, row_bytes, block_bytes=None):
-    """The blocked schedule as row ranges (cached): B + 1 int64 arrays (B + 2
-    when some rows have a suffix, _block_split), row r's slots of range i being
-    [cuts[i][r], cuts[i + 1][r]) of the CSR itself (cuts[0] = indptr[:-1], the
-    last = indptr[1:]), for kernels that keep the CSR's slot indices (the
-    fused GAT layer). ``row_bytes``: bytes gathered per source. None when the
-    schedule does not apply."""
-    if (_BLOCKED == "off" or csr._plans.get("segment") or csr.nnz == 0 or
-            row_bytes <= _BLOCK_MIN_ROW_BYTES):
+    """The blocked schedule as row ranges (the plan's, cached): B + 1 int64
+    arrays (B + 2 when some rows have a suffix), row r's slots of range i
+    being [cuts[i][r], cuts[i + 1][r]) of the CSR itself (cuts[0] =
+    indptr[:-1], the last = indptr[1:]), for kernels that keep the CSR's slot
+    indices (the fused GAT layer, the g-SDDMM). ``row_bytes``: bytes gathered
+    per source. None when the schedule does not apply."""
+    if csr.nnz == 0:
         return None
-    lo, hi = _column_span(csr)
-    B = _block_count(csr, (hi - lo) * row_bytes, block_bytes or _GAT_BLOCK_BYTES)
-    if not B:
-        return None
-    key = ("cuts", B)
-    if key not in csr._plans:
-        split = _block_split(csr, B, lo, hi)
-        cuts = None
-        if split is not None:
-            _, counts, pre, _ = split
-            start = csr.indptr[:-1]
-            cum = torch.cumsum(counts, 1)
-            cuts = [start.contiguous()] + [(start + cum[:, b]).contiguous() for b in range(B)]
-            if pre is not None:  # the suffixes: one more range, run last
-                cuts.append(csr.indptr[1:].contiguous())
-            del cum, counts, split
-        csr._plans[key] = cuts
-    return csr._plans[key]
-
-
-def _run_max_blocked(csr, cuts, msg, ufeat2, efeat2, elen, feat_len, want_arg, emap):
-    """The max reducer as one dglhip_gspmm_max_ranges_device launch per
-    source block (row sub-ranges ``cuts``), every row continued from the
-    earlier blocks' max; argmax slot ids as the one-launch kernel's."""
-    dev = ufeat2.device
-    out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
-    arg = torch.empty(csr.num_rows, feat_len, dtype=torch.int64, device=dev) if want_arg else None
-    eid = None if msg == MSG_COPY_U or emap is SLOT else (
-        csr.slot_eid if emap is None else emap)
-    for b in range(len(cuts) - 1):
-        check_call(LIB.dglhip_gspmm_max_ranges_device(
-            msg, csr.num_rows, feat_len, ptr(csr.indptr), ptr(cuts[b]), ptr(cuts[b + 1]),
-            1 if b else 0, ptr(csr.indices), ptr(eid), ptr(ufeat2), ptr(efeat2), elen, ptr(out),
-            ptr(arg), ptr(csr.row_order), _stream_of(dev)))
-    return out, arg
+    return _cuts_native(csr, row_bytes, block_bytes or _GAT_BLOCK_BYTES)
 
 
 def _plan_tag(plan):
@@ -954,54 +869,18 @@ def _plan_tag(plan):
     return (len(plan) - int(sfx), sfx)
 
 
-def _run_block_items(csr, plan, msg, red, ufeat2, feat_len, out, efeat, elen, erows):
-    """The blocked schedule's items (_BlockItems), one dglhip_gspmm_items_device
-    launch per block, every later launch adding to the rows it lists. Unless
-    ``red`` is SUM_ACCUM the first block's launch writes its rows from zero
-    (the chains' own start: identical bits) and only the rows it does not
-    list are zero-filled (none on the Reddit-shaped graph: no 119 MB fill and
-    no read of it per call)."""
-    dev = ufeat2.device
-    ld = ufeat2.stride(0) if _row_strided(ufeat2, feat_len) else 0
-    first_writes = red != RED_SUM_ACCUM
-    if out is None:
-        out = torch.empty(csr.num_rows, feat_len, dtype=torch.float32, device=dev)
-    if first_writes:
-        key = ("blocked_absent",) + _plan_tag(plan)
-        absent = csr._plans.get(key)
-        if absent is None:
-            listed = torch.zeros(csr.num_rows, dtype=torch.bool, device=dev)
-            listed[plan[0].rows.long()] = True
-            absent = csr._plans[key] = torch.nonzero(~listed).squeeze(1)
-        if absent.numel():
-            out.index_fill_(0, absent, 0.0)
-    off = 0
-    for i, it in enumerate(plan):
-        if efeat is None:
-            e, eid = None, None
-        elif erows is None:  # values already in the plan's slot order
-            e, eid = efeat[off:off + it.nnz], None
-        else:
-            e, eid = efeat, erows[off:off + it.nnz]
-        check_call(LIB.dglhip_gspmm_items_device(
-            msg, it.rows.numel(), feat_len, ptr(it.rows), ptr(it.ptr),
-            0 if (i == 0 and first_writes) else 1, ptr(it.indices),
-            ptr(eid), ptr(ufeat2), ld, ptr(e), elen, ptr(out), _stream_of(dev)))
-        off += it.nnz
-    if red == RED_MEAN:
-        out.div_(csr.mean_divisor())
-    return out
-
-
 def blocked_schedule(adj, ufeat):
-    """The number of source blocks the copy_u sum / mean g-SpMM of ``ufeat``
-    over ``adj`` runs in (0: one launch), e.g. for a roofline's regime."""
+    """The number of source-blocked launches the copy_u sum / mean g-SpMM of
+    ``ufeat`` over ``adj`` runs in (0: one launch), as the plan schedules it."""
     adj = adj.to(ufeat.device)
     if ufeat.device.type != "cuda":
         return 0
     u2 = ufeat.reshape(ufeat.shape[0], -1)
-    plan = _block_plan(adj.fwd, u2, u2.shape[1])
-    return 0 if plan is None else len(plan)
+    F = u2.shape[1]
+    ldu = u2.stride(0) if (u2.shape[0] > 1 and _row_strided(u2, F)) else 0
+    msg = MSG_COPY_U_BF16 if u2.dtype == torch.bfloat16 else MSG_COPY_U
+    path, launches = adj.fwd.plan.schedule(msg, RED_SUM, F, ldu, u2.shape[0])
+    return launches if path == PLAN_PATH_BLOCKED else 0
 
 
 def _block_slots(csr, plan):
@@ -1009,7 +888,7 @@ def _block_slots(csr, plan):
     ``csr`` it came from (cached; for edge-valued messages)."""
     key = ("blocked_slots",) + _plan_tag(plan)
     if key not in csr._plans:
-        csr._plans[key] = torch.cat([it.pos.long() for it in plan])
+        csr._plans[key] = plan.pos.long()
     return csr._plans[key]
 
 
@@ -1043,47 +922,13 @@ def segment_blocks(csrs, feat_len, dtypes):
     partition's own and halo segments), 0 for a CSR that keeps one launch."""
     total = 0
     for csr, dt in zip(csrs, dtypes):
-        if csr.device.type != "cuda":
+        if csr.device.type != "cuda" or csr.nnz == 0:
             continue
-        proxy = torch.empty(2, feat_len, dtype=dt, device=csr.device)
-        plan = _block_plan(csr, proxy, feat_len)
-        total += 0 if plan is None else len(plan)
+        msg = MSG_COPY_U_BF16 if dt == torch.bfloat16 else MSG_COPY_U
+        path, launches = csr.plan.schedule(msg, RED_SUM_ACCUM, feat_len, 0, csr.num_cols)
+        total += launches if path == PLAN_PATH_BLOCKED else 0
     return total
 
-
-def _run_blocked(csr, blocks, msg, red, ufeat2, feat_len, out=None, efeat=None, elen=0,
-                 erows=None):
-    """copy_u (fp32 or bf16 rows) / u_mul_e + sum (mean, sum_accum) over the
-    blocked schedule's items, each row's chain continued block by block;
-    mean divides by the degree last (the kernel's own division: IEEE, by
-    max(deg, 1)). Edge values: ``efeat`` rows ``erows`` per plan slot, or
-    without ``erows`` already in the plan's slot order."""
-    if not _row_strided(ufeat2, feat_len) and _pad_rows(msg, RED_SUM, ufeat2, feat_len):
-        # line-straddling rows: one padded copy for every block's launch
-        ld = padded_width(feat_len)
-        up = ufeat2.new_empty(ufeat2.shape[0], ld)
-        up[:, :feat_len] = ufeat2
-        ufeat2 = up[:, :feat_len]
-    return _run_block_items(csr, blocks, msg, red, ufeat2, feat_len, out, efeat, elen, erows)
-
-
-_PAD_ROWS = os.environ.get("DGLHIP_PAD_ROWS", "auto")
-
-
-def set_pad_rows(policy):
-    """Padded-stride gathers for line-straddling rows: "auto" (default) or
-    "off"; returns the old policy."""
-    global _PAD_ROWS
-    old = _PAD_ROWS
-    _PAD_ROWS = str(policy)
-    return old
-
-
-def _pad_rows(msg, red, ufeat2, feat_len):
-    return (_PAD_ROWS == "auto" and msg in (MSG_COPY_U, MSG_U_MUL_E) and
-            red in (RED_SUM, RED_MEAN) + _ACCUM and ufeat2 is not None and
-            ufeat2.dtype == torch.float32 and
-            ufeat2.numel() * 4 >= _PAD_MIN_BYTES and padded_width(feat_len) != feat_len)
 
 
 def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1, slot=False):
@@ -1096,7 +941,8 @@ def _run_sddmm_dot(csr, lhs2, rhs2, num_edges, heads=1, slot=False):
     if dev.type == "cuda":
         # rows longest-first; the gathered rows one source block at a time
         # where the CSR has a blocked schedule (per-edge values: same bits)
-        cuts = _block_cuts(csr, F * 4, _BLOCK_BYTES) or [csr.indptr, csr.indptr[1:]]
+        cuts = (_block_cuts(csr, F * 4, schedule_policy()["block_bytes"]) or
+                [csr.indptr, csr.indptr[1:]])
         for b in range(len(cuts) - 1):
             check_call(LIB.dglhip_gsddmm_ranges_device(
                 0, csr.num_rows, F, heads, ptr(cuts[b]), ptr(cuts[b + 1]), ptr(csr.row_order),
@@ -1627,8 +1473,16 @@ class _RelationGroups(object):
         self.slot = rel.eid  # forward slot of each relation-major position
         self.dst = fwd.row_ids().index_select(0, self.slot).to(torch.int32)
         self.items = _typed_items(self.ptr, fwd.nnz) if fwd.device.type == "cuda" else None
-        self.etype = etype  # the relations it was built for (by identity and version)
+        self.etype = etype  # the relations it was built for (held: see matches)
         self.version = etype._version
+
+    def matches(self, etype):
+        # typed_block_spmm hands a new 1-D view of the relations at every call
+        # (r04 ADVICE: compared by object, the cache never hit). The held
+        # tensor keeps its memory from being reused, so the same address and
+        # length is the same memory, and views share one version counter
+        return (self.etype.device == etype.device and self.etype.numel() == etype.numel() and
+                self.etype.data_ptr() == etype.data_ptr() and self.version == etype._version)
 
 
 class _TypedBlock(torch.autograd.Function):
@@ -1654,7 +1508,7 @@ class _TypedBlock(torch.autograd.Function):
             du = _run_typed_block(adj.bwd, dout, wt, rel, nrm, nb, so, si)
         if ctx.needs_input_grad[4]:
             g = getattr(adj, "_rel_groups", None)
-            if g is None or g.etype is not etype or g.version != etype._version:
+            if g is None or not g.matches(etype):
                 g = adj._rel_groups = _RelationGroups(adj.fwd, etype, R)
             fwd_nrm = None if enorm is None else enorm.index_select(0, adj.fwd.eid)
             nrm = None if fwd_nrm is None else fwd_nrm.index_select(0, g.slot)
@@ -1771,6 +1625,20 @@ _GAT_SEED = {}
 # the GAT backward: "auto" (the one-pass transposed kernel where it applies,
 # 8 heads x 16) or "three" (r03's three passes, the attention stored)
 _GAT_BWD = os.environ.get("DGLHIP_GAT_BWD", "auto")
+
+
+# the one-pass backward reads er and dz packed into one [rows, 2H] table
+# (dglhip_gat_backward_t_packed_device); False: two tables (study knob)
+_GAT_BWD_PACK = os.environ.get("DGLHIP_GAT_BWD_PACK", "on") != "off"
+
+
+def set_gat_bwd_pack(on):
+    """Study knob: er and dz packed into one table for the one-pass GAT
+    backward (default on); returns the old setting. Same bits."""
+    global _GAT_BWD_PACK
+    old = _GAT_BWD_PACK
+    _GAT_BWD_PACK = bool(on)
+    return old
 
 
 def set_gat_backward(policy):
@@ -2012,31 +1880,34 @@ def _gat_backward_t(ctx, d_ft, d_z):
     # er needs no gradient: the kernel then stores nothing)
     g = torch.empty(fwd.nnz, H, dtype=torch.float32, device=dev) if need_er else None
     common = (fwd.num_rows, ft2.shape[0], H, D)
-    tail = (ptr(ft2), ptr(el), ptr(er), ptr(dz), ptr(dout), float(ctx.alpha), float(ctx.lo),
-            float(ctx.hi), 1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,
-            ptr(ctx.seed_off), ptr(d_ft2), ptr(d_el), ptr(g), _stream_of(dev))
+    rest = (float(ctx.alpha), float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0,
+            float(ctx.p), ctx.seed, ptr(ctx.seed_off), ptr(d_ft2), ptr(d_el), ptr(g),
+            _stream_of(dev))
+    if dz is not None and _GAT_BWD_PACK:
+        # er and dz side by side: a pair's two destination operands in one
+        # 64-B run, one line per slot instead of two (same bits)
+        erdz = torch.cat([er, dz], 1)
+        tail = (ptr(ft2), ptr(el), ptr(erdz), ptr(dout)) + rest
+        entry = LIB.dglhip_gat_backward_t_packed_device
+    else:
+        tail = (ptr(ft2), ptr(el), ptr(er), ptr(dz), ptr(dout)) + rest
+        entry = LIB.dglhip_gat_backward_t_device
     plan = _block_plan(bwd, dout, F, _GAT_BWD_BLOCK_BYTES) if bwd.nnz else None
     if plan is None:
-        check_call(LIB.dglhip_gat_backward_t_device(
+        check_call(entry(
             bwd.num_rows, ptr(bwd.row_order), ptr(bwd.indptr), ptr(bwd.indptr[1:]), 1, 0,
             *(common + (ptr(bwd.indices), ptr(emap)) + tail)))
     else:
+        # the plan's launches over its global slot arrays: item offsets (ptr)
+        # are global, so every launch takes the same column-id and map bases
         erows = _block_edge_rows(bwd, plan, emap)
-        key = ("blocked_absent",) + _plan_tag(plan)
-        absent = bwd._plans.get(key)
-        if absent is None:
-            listed = torch.zeros(bwd.num_rows, dtype=torch.bool, device=dev)
-            listed[plan[0].rows.long()] = True
-            absent = bwd._plans[key] = torch.nonzero(~listed).squeeze(1)
-        if absent.numel():
-            d_ft2.index_fill_(0, absent, 0.0)
-            d_el.index_fill_(0, absent, 0.0)
-        off = 0
+        if plan.absent.numel():
+            d_ft2.index_fill_(0, plan.absent.long(), 0.0)
+            d_el.index_fill_(0, plan.absent.long(), 0.0)
         for i, it in enumerate(plan):
-            check_call(LIB.dglhip_gat_backward_t_device(
+            check_call(entry(
                 it.rows.numel(), ptr(it.rows), ptr(it.ptr), ptr(it.ptr[1:]), 0, 1 if i else 0,
-                *(common + (ptr(it.indices), ptr(erows[off:off + it.nnz])) + tail)))
-            off += it.nnz
+                *(common + (ptr(plan.indices), ptr(erows)) + tail)))
     d_er = None
     if need_er:  # the copy_e sum of g over the CSR, one wave per row (same chain)
         d_er = torch.empty(fwd.num_rows, H, dtype=torch.float32, device=dev)
@@ -2066,26 +1937,12 @@ def _gat_el_grad(adj, g, H):
     bwd = adj.bwd
     emap = _fwd_slot_of_bwd(adj)
     cuts = None
-    if g.is_cuda and _BLOCKED != "off" and bwd.nnz and bwd.nnz < (1 << 31):
+    pol = schedule_policy()
+    if g.is_cuda and pol["blocked"] and bwd.nnz and bwd.nnz < (1 << 31):
         B = -(-(g.numel() * g.element_size()) // _EL_GRAD_BLOCK_BYTES)
-        B = min(B, bwd.nnz // (_BLOCK_MIN_SLOTS * max(bwd.num_nonempty, 1)))
+        B = min(B, bwd.nnz // (pol["block_min_slots"] * max(bwd.num_nonempty, 1)))
         if B >= 2:
-            key = ("el_grad_cuts", B)
-            if key not in bwd._plans:
-                lo, hi = _column_span(bwd)
-                split = _block_split(bwd, B, lo, hi)
-                cuts = None
-                if split is not None:
-                    _, counts, pre, _ = split
-                    start = bwd.indptr[:-1]
-                    cum = torch.cumsum(counts, 1)
-                    cuts = [start.contiguous()] + [(start + cum[:, b]).contiguous()
-                                                   for b in range(B)]
-                    if pre is not None:  # the suffixes: one more range, run last
-                        cuts.append(bwd.indptr[1:].contiguous())
-                    del cum, counts, split
-                bwd._plans[key] = cuts
-            cuts = bwd._plans[key]
+            cuts = _cuts_native(bwd, 0, 0, B)
     if cuts is None:
         return _run_gspmm(bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=emap)[0]
     out = torch.empty(bwd.num_rows, H, dtype=torch.float32, device=g.device)

@@ -173,7 +173,7 @@ def run(args):
     state = {k: v.detach().cpu() for k, v in
              (model.module if distributed else model).state_dict().items()}
     return {"graph": args.graph if args.graph == "rmat" else args.dataset, "world": world,
-            "epoch_s": mean, "edges": num_edges, "row_split": kernel._ROW_SPLIT,
+            "epoch_s": mean, "edges": num_edges, "row_split": kernel.get_row_split(),
             "edges_per_s": num_edges * (args.n_layers + 1) / mean, "loss": losses[-1],
             "state": state}
 

@@ -233,6 +233,118 @@ int dglhip_gspmm_short_rows_device(int msg_op, int reduce_op, int64_t num_items,
                                    int64_t ufeat_ld, void* stream);
 
 /* ------------------------------------------------------------------------ */
+/* Launch plan of a g-SpMM over one CSR (csrc/spmm_plan.{h,cc,hip}).         */
+/*                                                                           */
+/* Replaces what the reference caches per context and runs per call:         */
+/*   GraphIndex.adjacency_matrix (cached per ctx)  python/dgl/graph_index.py:537-585 */
+/*   F.spmm on it (SPMVExecutor.run)  backend/pytorch/tensor.py:145-146,    */
+/*                                    runtime/ir/executor.py:452-473,535-566 */
+/* A plan is built once per CSR and device and holds every schedule the      */
+/* g-SpMM runs over it: the source-blocked schedule (items  */
+/* per contiguous source block, each row's chain continued block by block,   */
+/* taken only where that is the row's own slot order: the same bits), the    */
+/* heavy-row split, the short-row tiers, the degree-descending row order.    */
+/* dglhip_spmm_plan_run picks among them per call exactly as the engine's    */
+/* Python operators do (they call it too), so a C / ctypes / PackedFunc       */
+/* caller gets the benchmarked schedule.                                     */
+/* ------------------------------------------------------------------------ */
+typedef struct DGLHipSpmmPlanObj* DGLHipSpmmPlan;
+
+/* Where the edge value of CSR slot k is (u_mul_e / copy_e):
+ *  BY_SLOT: efeat row k (values laid out in the CSR's slot order);
+ *  BY_EID : efeat row erow[k], erow = the CSR's edge ids (NULL: identity);
+ *           the plan caches what it derives from them (the same CSR's ids);
+ *  BY_MAP : efeat row erow[k] for an arbitrary int64 map. */
+#define DGLHIP_EDGE_BY_SLOT 0
+#define DGLHIP_EDGE_BY_EID 1
+#define DGLHIP_EDGE_BY_MAP 2
+
+/* Schedule policy (process-wide). Defaults: row_split -1 (auto: chunk a row
+ * only when it is the launch's critical path), blocked 1, short_rows 1,
+ * pad_rows 1, block_bytes 6 MiB, block_table_min 16 MiB, block_table_max
+ * 256 MiB, block_min_slots 12, block_max_stretch 3, block_max_suffix 1/16,
+ * block_min_row_bytes 128, tier_min_rows 65536, pad_min_bytes 4 MiB; the
+ * environment variables DGLHIP_ROW_SPLIT / _BLOCKED / _BLOCK_BYTES /
+ * _BLOCK_MIN_SLOTS / _BLOCK_MAX_STRETCH / _SHORT_ROWS / _PAD_ROWS set the
+ * initial values. Results never depend on it beyond the documented
+ * tolerance of the heavy-row split (re-association of a chunked row). */
+typedef struct {
+  int64_t row_split;      /* -1 auto, 0 off (every row one chain), > 0 chunk length */
+  int32_t blocked;        /* source-blocked schedule where exact */
+  int32_t short_rows;     /* short-row tiers */
+  int32_t pad_rows;       /* padded-stride gathers of line-straddling rows */
+  int32_t reserved;
+  int64_t block_bytes;    /* source slice per launch */
+  int64_t block_table_min, block_table_max;  /* gathered table range that blocks */
+  int64_t block_min_slots;                   /* slots per row and block */
+  double block_max_stretch;                  /* slices at most this x block_bytes */
+  double block_max_suffix;                   /* share of slots after the prefixes */
+  int64_t block_min_row_bytes;               /* rows of at most this keep one launch */
+  int64_t tier_min_rows;                     /* short rows needed to tier */
+  int64_t pad_min_bytes;                     /* tables smaller than this: no padding */
+} DGLHipSpmmPolicy;
+int dglhip_spmm_get_policy(DGLHipSpmmPolicy* out);
+int dglhip_spmm_set_policy(const DGLHipSpmmPolicy* policy);
+/* The heavy-row gate under the current policy: rows longer than *out slots
+ * are chunked (0: none) in a launch of nnz slots whose longest row has
+ * max_degree, on a part with `waves` resident waves (<= 0: MI355X's). */
+int dglhip_spmm_split_threshold(int64_t nnz, int64_t max_degree, int64_t waves, int64_t* out);
+/* Row stride (floats) the plan gathers F-float rows at (F: unpadded). */
+int dglhip_spmm_padded_width(int64_t feat_len, int64_t* out);
+
+/* Build the plan of a CSR on device_type 10 (ROCm, device_id) or 1 (host).
+ * indptr int64[num_rows+1] and indices int32[nnz] are borrowed: they must
+ * stay allocated and unchanged while the plan lives. host_indptr (optional,
+ * borrowed only during the call) spares a device-to-host copy; row_order
+ * (optional, borrowed like indptr): the degree-descending launch schedule
+ * (built when NULL). The structures of each schedule are built on first
+ * use, on the stream of that call (which waits for them); building inside a
+ * HIP-graph capture fails, so a captured caller runs once outside first.
+ * A plan serves one stream at a time (its lazily built structures). */
+int dglhip_spmm_plan_create(int device_type, int device_id, int64_t num_rows, int64_t num_cols,
+                            int64_t nnz, const int64_t* indptr, const int32_t* indices,
+                            const int64_t* host_indptr, const int32_t* row_order, void* stream,
+                            DGLHipSpmmPlan* out);
+/* Frees the plan's own memory (arrays handed out through the registry keep
+ * theirs until released). Work already enqueued must have finished. */
+int dglhip_spmm_plan_free(DGLHipSpmmPlan plan);
+/* Bytes of workspace dglhip_spmm_plan_run needs for these arguments (the
+ * padded copy of line-straddling rows, edge values in plan order, the
+ * heavy-row partials); may build plan structures on `stream`. */
+int dglhip_spmm_plan_workspace(DGLHipSpmmPlan plan, int msg_op, int reduce_op, int64_t feat_len,
+                               int64_t ufeat_ld, int64_t num_src_rows, int64_t efeat_len,
+                               int edge_layout, const int64_t* erow, void* stream, int64_t* bytes);
+/* The g-SpMM of dglhip_gspmm_device over the plan's CSR, on the schedule the
+ * plan picks: out[r, :] = REDUCE over r's slots of MSG(ufeat[col], efeat[..]).
+ * ufeat: num_src_rows rows at stride ufeat_ld (0 or feat_len: dense; else an
+ * even padded width, copy_u / u_mul_e sum-like reducers), fp32, or bf16 bits
+ * for DGLHIP_MSG_COPY_U_BF16. Edge values per edge_layout. arg_out (MAX,
+ * optional). workspace: device memory of dglhip_spmm_plan_workspace bytes.
+ * Bit-identical to dglhip_gspmm_device with the same arguments, except rows
+ * the heavy-row policy chunks (fp32 re-association, deterministic). A host
+ * plan runs dglhip_gspmm_host. Enqueues on `stream`; never synchronises once
+ * the plan's structures for these arguments exist. */
+int dglhip_spmm_plan_run(DGLHipSpmmPlan plan, int msg_op, int reduce_op, int64_t feat_len,
+                         const void* ufeat, int64_t ufeat_ld, int64_t num_src_rows,
+                         const float* efeat, int64_t efeat_len, int edge_layout,
+                         const int64_t* erow, float* out, int64_t* arg_out, void* workspace,
+                         int64_t workspace_bytes, void* stream);
+/* The schedule a run with these arguments takes: *path 0 host, 1 one wave per
+ * row (heavy-row chunks and short-row tiers included), 2 source-blocked items,
+ * 3 source-blocked max ranges; *launches the blocked launches (1 otherwise). */
+#define DGLHIP_PLAN_PATH_HOST 0
+#define DGLHIP_PLAN_PATH_ROWS 1
+#define DGLHIP_PLAN_PATH_BLOCKED 2
+#define DGLHIP_PLAN_PATH_MAX_BLOCKED 3
+int dglhip_spmm_plan_schedule(DGLHipSpmmPlan plan, int msg_op, int reduce_op, int64_t feat_len,
+                              int64_t ufeat_ld, int64_t num_src_rows, int64_t efeat_len,
+                              int edge_layout, const int64_t* erow, void* stream, int* path,
+                              int64_t* launches);
+/* stats[7] = rows, columns, nnz, max degree, rows with slots, resident waves
+ * of the part, heavy-row threshold (0: no row chunked). */
+int dglhip_spmm_plan_stats(DGLHipSpmmPlan plan, int64_t* stats);
+
+/* ------------------------------------------------------------------------ */
 /* Dense per-node Linear on the f32 MFMA (the Linear that follows a g-SpMM;  */
 /* csrc/node_linear.hip). No reference counterpart: the reference runs these */
 /* products as torch nn.Linear (examples/pytorch/gcn/gcn_spmv.py:45-62).     */
@@ -537,6 +649,18 @@ int dglhip_gat_backward_t_device(
     float clamp_hi, int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset,
     float* d_ft, float* d_el, float* grad, void* stream);
 
+/* dglhip_gat_backward_t_device with er and dz as one [num_rows, 2H] table
+ * erdz (row v: er[v, 0..H), then dz[v, 0..H)): a pair's two destination
+ * operands in one 64-B run, one cache line per slot instead of two. The same
+ * arithmetic and bits. */
+int dglhip_gat_backward_t_packed_device(
+    int64_t num_items, const int32_t* item_row, const int64_t* item_beg, const int64_t* item_end,
+    int by_row, int accumulate, int64_t num_rows, int64_t num_src, int64_t num_heads,
+    int64_t head_dim, const int32_t* cols, const int64_t* fslot, const float* ft, const float* el,
+    const float* erdz, const float* dout, float alpha, float clamp_lo, float clamp_hi,
+    int apply_exp, float drop_p, uint64_t seed, const int64_t* seed_offset, float* d_ft,
+    float* d_el, float* grad, void* stream);
+
 /* out[r, h] = sum over the slots k of row r of vals[k, h], 8 heads, as the
  * copy_e sum's chain ((0 + v0) + v1) + ... in slot order (the same bits as
  * dglhip_gspmm_device(COPY_E, SUM) with slot-ordered values), one wave per
@@ -791,7 +915,32 @@ int DGLExtTypeFree(void* handle, int type_code);
  * csrc/graph_index.cc and csrc/scheduler.cc):
  *   "dglhip._CAPI_GSpMM"        (msg, reduce, indptr, indices, eid, ufeat,
  *                                efeat|null, out, arg_out|null,
- *                                row_order|null, stream)
+ *                                row_order|null, stream[, plan|null
+ *                                [, edge_layout]]) — through the plan's
+ *                                schedule (a plan made for the call when none
+ *                                is given; edge_layout default BY_EID)
+ *   "dglhip._CAPI_SpmmPlanCreate" (indptr, indices, num_cols, row_order|null,
+ *                                stream) -> plan HANDLE
+ *   "dglhip._CAPI_SpmmPlanFree"  (plan)
+ *   "dglhip._CAPI_SpmmPlanSchedule" (plan, msg, reduce, feat_len, ufeat_ld,
+ *                                num_src_rows, efeat_len, edge_layout,
+ *                                stream) -> path * 2^32 + launches
+ *   "dglhip._CAPI_SpmmPlanBlocked" (plan, row_bytes, block_bytes, blocks,
+ *                                stream) -> NULL or an indexable function:
+ *                                0 meta int64 [B, suffix, n_absent, L, then
+ *                                per launch n_items, nnz, off, suffix],
+ *                                1 indices, 2 pos, 3 absent, 4 + 2i rows of
+ *                                launch i, 5 + 2i its ptr (global offsets)
+ *   "dglhip._CAPI_SpmmPlanCuts"  (plan, row_bytes, block_bytes, blocks,
+ *                                stream) -> NULL or int64 [n, rows] ranges
+ *   "dglhip._CAPI_SpmmPlanSplit" (plan, threshold, skip_empty, chunk, stream)
+ *                                -> indexable: 0 meta [n_light, n_heavy,
+ *                                n_chunks], 1 light, 2 heavy, 3 chunk_ptr,
+ *                                4 beg, 5 end
+ *   "dglhip._CAPI_SpmmPlanTiers" (plan, skip_empty, threshold|0, stream) ->
+ *                                indexable: 0 meta [n_long, n_tail, T, then
+ *                                per tier maxd, n], 1 + 3t rows, 2 + 3t
+ *                                slot_ptr, 3 + 3t slot_cols of tier t
  *   "dglhip._CAPI_GSDDMM"       (op, num_heads, indptr, indices, eid, lhs, rhs,
  *                                out, stream)
  *   "dglhip._CAPI_COOToCSR"     (num_rows, row, col, order, indptr, indices,

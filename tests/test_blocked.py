@@ -28,9 +28,9 @@ def _graph(n, m, seed, sorted_src):
 
 
 @pytest.fixture
-def small_blocks(monkeypatch):
-    monkeypatch.setattr(kernel, "_BLOCK_TABLE_MIN", 0)
-    monkeypatch.setattr(kernel, "_BLOCK_BYTES", 1 << 16)
+def small_blocks():
+    with kernel.scheduled(block_table_min=0, block_bytes=1 << 16):
+        yield
 
 
 def _chains_kept(csr, plan):
@@ -486,9 +486,8 @@ def test_plan_caches_keyed_on_blocks_not_length():
     n, src, dst = _tagged_graph()
     csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
                            kernel.ORDER_EID, "cpu")
-    lo, hi = kernel._column_span(csr)
-    p2 = kernel._block_items(csr, 2, lo, hi)
-    p3 = kernel._block_items(csr, 3, lo, hi)
+    p2 = kernel._block_items(csr, 2)
+    p3 = kernel._block_items(csr, 3)
     assert len(p2) == len(p3) == 3 and p2[-1].suffix and not p3[-1].suffix
     assert _chains_kept(csr, p2) and _chains_kept(csr, p3)
     s2 = kernel._block_slots(csr, p2)
@@ -515,15 +514,14 @@ def test_one_csr_two_block_counts_device():
     n, src, dst = _tagged_graph()
     gen = torch.Generator().manual_seed(22)
     w = torch.rand(len(src), 1, generator=gen)
-    old = (kernel._BLOCK_TABLE_MIN, kernel._BLOCK_BYTES, kernel._BLOCK_MIN_SLOTS)
+    old = kernel.set_schedule_policy(block_table_min=0, block_min_slots=1)
     try:
-        kernel._BLOCK_TABLE_MIN, kernel._BLOCK_MIN_SLOTS = 0, 1
         for widths in ((64, 96), (96, 64)):
             adj = kernel.from_coo(n, n, torch.from_numpy(dst), torch.from_numpy(src),
                                   kernel.ORDER_EID, dev)
             for F in widths:
                 # F = 64: 512 KB table -> 2 blocks; F = 96: 768 KB -> 3 blocks
-                kernel._BLOCK_BYTES = 256_000
+                kernel.set_schedule_policy(block_bytes=256_000)
                 H = torch.randn(n, F, generator=gen)
                 plan = kernel._block_plan(adj.fwd, H.to(dev), F)
                 assert plan is not None and len(plan) == 3
@@ -534,7 +532,7 @@ def test_one_csr_two_block_counts_device():
                 out = kernel.gspmm(adj, "copy_u", "sum", H.to(dev)).cpu()
                 assert np.array_equal(out.numpy(), O.spmm_coo(n, dst, src, H.numpy()))
     finally:
-        kernel._BLOCK_TABLE_MIN, kernel._BLOCK_BYTES, kernel._BLOCK_MIN_SLOTS = old
+        kernel.set_schedule_policy(**old)
 
 
 @pytest.mark.gpu

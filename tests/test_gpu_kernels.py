@@ -333,7 +333,7 @@ def test_padded_stride_gather(cuda, F, case):
     (and the oracle for sum)."""
     msg, red = case.split("-")
     rng = np.random.default_rng(F)
-    n = (kernel._PAD_MIN_BYTES // (4 * F)) + 1000
+    n = (kernel.schedule_policy()["pad_min_bytes"] // (4 * F)) + 1000
     row, col = rand_graph(rng, n, n, 400_000, skew=True)
     H = rng.uniform(-1, 1, (n, F)).astype(np.float32)
     W = rng.uniform(-1, 1, (400_000, 1)).astype(np.float32)
@@ -404,8 +404,8 @@ def test_short_row_tiers(cuda, red, F):
     H = rng.uniform(-1, 1, (n, F)).astype(np.float32)
     adj = kernel.from_coo(n, n, row, col, kernel.ORDER_EID, cuda)
     Hd = torch.from_numpy(H).to(cuda)
-    n_long, tail = adj.fwd.tiers(adj.fwd.row_order, ("plain", False))
-    assert sum(t[2] for t in tail) >= kernel._TIER_MIN_ROWS
+    n_long, tail = adj.fwd.tiers()
+    assert sum(t[2] for t in tail) >= kernel.schedule_policy()["tier_min_rows"]
     assert {t[0] for t in tail} == {0, 4, 8}
     outs = {}
     for split in ("off", 2000):

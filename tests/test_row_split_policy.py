@@ -20,7 +20,7 @@ def policy():
 
 
 def test_default_is_auto():
-    assert kernel._ROW_SPLIT in ("auto",) or "DGLHIP_ROW_SPLIT" in __import__("os").environ
+    assert kernel.get_row_split() == "auto" or "DGLHIP_ROW_SPLIT" in __import__("os").environ
 
 
 @pytest.mark.parametrize("nnz,max_degree,expect", [
