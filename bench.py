@@ -51,6 +51,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 import torch
@@ -138,6 +139,8 @@ def build_parser():
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="N>1: collective timeout (s) of the process groups; a dead or hung "
                          "peer then ends the job in bounded time")
+    ap.add_argument("--no-sage-rmat-leg", action="store_true",
+                    help="skip configs[3]'s GraphSAGE-mean epochs on the rmat leg's graph")
     ap.add_argument("--leg-deadline", type=float, default=None,
                     help="seconds a secondary leg may run before rank 0 prints the line built "
                          "so far (with the leg's error) and exits; default: the collective "
@@ -583,6 +586,26 @@ def exchange_block(pg, h_local, steps, world, dev):
                     "bytes over that time"}
 
 
+# exit code of a run that printed its line but lost a leg (a failed or hung
+# peer, a hung kernel): the relay and the driver see a failure
+EXIT_LEG_FAILED = 3
+_LINE_LOCK = threading.Lock()
+_LINE_DONE = [False]
+
+
+def emit_line(result):
+    """Print the JSON line once per process: the leg-deadline timer's thread
+    and the main thread can both reach here; the first one prints."""
+    with _LINE_LOCK:
+        if _LINE_DONE[0]:
+            return False
+        text = json.dumps(result)
+        sys.stdout.write(text + "\n")
+        sys.stdout.flush()
+        _LINE_DONE[0] = True
+        return True
+
+
 class LegRunner(object):
     """Runs the secondary legs after the headline on every rank so that one
     leg's failure cannot lose the line (r03 verdict, Weak 6).
@@ -638,10 +661,11 @@ class LegRunner(object):
                                    "or a kernel hung): rank 0 printed the line and exited"
                                    % self.deadline}
             try:
-                sys.stdout.write(json.dumps(line) + "\n")
-                sys.stdout.flush()
+                emit_line(line)
             finally:
-                os._exit(0)
+                # a hung peer or kernel is a failed run: the line is printed
+                # (the headline is intact) but the exit code says so
+                os._exit(EXIT_LEG_FAILED)
         t = threading.Timer(self.deadline, fire)
         t.daemon = True
         t.start()
@@ -769,6 +793,10 @@ def rmat_run(args, world, rank, dev, st, pmc=None):
             t2 = time.time()
             cpu = cpu_baseline(sample, n, None, seconds_budget=10.0)
             log("rmat cpu baseline took %.1fs" % (time.time() - t2))
+        if not dist.is_initialized() and not args.no_sage_rmat_leg:
+            # configs[3]'s model on this same graph next (sage_rmat leg)
+            del h
+            _RMAT_KEEP.update(adj=adj, n=n, sample=sample)
         return {"value": E * steps / elapsed, "unit": "edges/s", "n_gpus": world,
                 "steps": steps, "warmup": 2, "ms_per_step": elapsed / steps * 1e3,
                 "scaling": "strong",
@@ -779,6 +807,11 @@ def rmat_run(args, world, rank, dev, st, pmc=None):
                 "halo_exchange": exch, "cpu_baseline": cpu}
     finally:
         kernel.set_row_split(old)
+
+
+# the rmat leg's graph, handed to the sage_rmat leg at N = 1 (one graph of
+# 1.07B edges in memory, built once)
+_RMAT_KEEP = {}
 
 
 def reddit_graph(args, scale, dev):
@@ -1012,9 +1045,13 @@ def main(argv=None):
         blocks = kernel.blocked_schedule(g.sparse_adjacency(dev), h)
         if blocks:
             parallelism += (", source-blocked schedule: %d launches over contiguous source "
-                            "blocks, every row's chain continued block by block (the edges "
-                            "are numbered source-major, so the chains are the edge-id "
-                            "chains: bit-identical)" % blocks)
+                            "blocks, every row's chain continued block by block. Precondition: "
+                            "the edges are numbered source-major, so along every row's slots "
+                            "the source blocks never decrease and the blocked chains are the "
+                            "edge-id chains (bit-identical); a graph in arbitrary edge order "
+                            "fails that check and runs the one-launch schedule instead (same "
+                            "bits, about 2x the time on this graph: the one_launch block)"
+                            % blocks)
     else:
         from dgl.distributed import PartitionedGraph, balanced_bounds
         bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
@@ -1130,6 +1167,21 @@ def main(argv=None):
                             "and are read as bf16, summed in fp32; own rows exact. Opt-in, not "
                             "the headline (results carry bf16 rounding of remote inputs)"}
         legs.run("halo_bf16", lambda: None, bf16_run)
+    if not distributed and blocks and args.workload == "reddit" and args.emulate_world <= 1:
+        # the same step with the source-blocked schedule off: what a graph in
+        # arbitrary edge order (which fails the monotone check) runs instead
+        def one_launch_run(_):
+            old = kernel.set_blocked("off")
+            try:
+                el1, k1 = timed_steps(step, args.steps, args.warmup, world, dev)
+            finally:
+                kernel.set_blocked(old)
+            return {"value": num_edges_total * args.steps / el1, "unit": "edges/s",
+                    "ms_per_step": el1 / args.steps * 1e3, "kernel_ms": k1,
+                    "note": "the headline step on the one-launch schedule (source-blocked "
+                            "schedule off): the schedule of a graph whose edges are not "
+                            "numbered source-major; same bits"}
+        legs.run("one_launch", lambda: None, one_launch_run, collective=False)
     if args.workload == "reddit" and args.emulate_world <= 1 and not args.no_train_leg:
         # training step of the same layer: forward + backward (the transposed
         # g-SpMM; at N > 1 the pipelined halo's reverse exchange overlapped with
@@ -1200,14 +1252,26 @@ def main(argv=None):
         _release(dev)
         legs.run("rmat%d" % args.rmat_scale, lambda: rmat_setup(args, rank, dev),
                  lambda st: rmat_run(args, world, rank, dev, st, rmat_pmc))
+        if _RMAT_KEEP:
+            # configs[3] at its own size: GraphSAGE-mean epochs on the same graph
+            st = dict(_RMAT_KEEP)
+            _RMAT_KEEP.clear()
+            import bench_models as bm
+            legs.run("sage_rmat%d" % args.rmat_scale, lambda: st, lambda s_: bm.sage_rmat_leg(
+                s_, dev, kernel, gather_peak, algorithmic_bytes,
+                cpu=not args.no_cpu_baseline), collective=False)
+            st = None
+            _release(dev)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        emit_line(result)
     if distributed:
         if legs.failed is not None:
-            # a collective may be half-done: leave without the group's teardown
+            # a collective may be half-done: leave without the group's
+            # teardown, with a failing exit code (the line, printed above,
+            # carries the leg's error)
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(EXIT_LEG_FAILED)
         dist.barrier()
         dist.destroy_process_group()
     return 0

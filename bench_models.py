@@ -69,6 +69,11 @@ def call_ms(fn, iters, dev):
     library launches on), after one untimed call."""
     fn()
     _sync(dev)
+    if dev.type != "cuda":  # host kernels: wall time
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        return (time.perf_counter() - t0) / iters * 1e3
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(iters):
@@ -450,7 +455,72 @@ def sage_leg(g, dev, kernel, gather_peak, algorithmic_bytes, sample, epochs=10, 
     return res
 
 
-def mean_bucketing_cpu(sample, n, F_=128, target_edges=2_000_000):
+def sage_rmat_leg(st, dev, kernel, gather_peak, algorithmic_bytes, epochs=2, warmup=1, cpu=True):
+    """configs[3] at its own size: GraphSAGE-mean 128-128-41 (examples/
+    graphsage/train.py: fc_neigh ahead of the mean, NodeLinear, the fused
+    loss) for full-graph epochs (forward + loss + backward + Adam) on the
+    rmat leg's RMAT-26 graph (67.1M nodes, 1.07B edges), one GPU, heavy rows
+    chunked, edge ids offloaded (copy_u + mean never reads them), random
+    128-wide features, 41 classes, 66 % training nodes. The reference has no
+    GraphSAGE example; its timing loop is gcn_spmv.py:168-182's."""
+    from dgl.nn.pytorch import weighted_cross_entropy
+    sage = example("graphsage/train.py")
+    adj, n, sample = st["adj"], st["n"], st.get("sample")
+    st.clear()
+    E = adj.fwd.nnz
+    old = kernel.set_row_split("auto")
+    try:
+        t0 = time.time()
+        adj.bwd  # the transposed CSR (the backward's), built ahead of the epochs
+        adj.offload_edge_ids()
+        _sync(dev)
+        build_s = time.time() - t0
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(9)
+        feats = 0.1 * torch.randn(n, 128, generator=gen, device=dev)
+        labels = torch.randint(0, 41, (n,), generator=gen, device=dev)
+        train_w = (torch.rand(n, generator=gen, device=dev) < 0.66).float()
+        ntrain = float(train_w.sum())
+
+        def aggregate(h):
+            return kernel.gspmm(adj, "copy_u", "mean", h)
+        aggregate.add_into = lambda h, out: kernel.gspmm_mean_add(adj, h, out)
+        torch.manual_seed(0)
+        model = sage.SAGE(128, 128, 41, 1, 0.0).to(dev)
+        opt = torch.optim.Adam(model.parameters(), lr=1e-2)
+        model.train()
+
+        def epoch():
+            logits = model(feats, aggregate)
+            loss = weighted_cross_entropy(logits, labels, train_w) * (1.0 / ntrain)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        ms, kms, launches = wall_steps(epoch, epochs, warmup, dev, kernel)
+        peak_mem = torch.cuda.max_memory_allocated(dev) / 1e9 if dev.type == "cuda" else None
+        del model, opt
+        h = feats  # the first layer's aggregation alone, for the roofline
+        ams = call_ms(lambda: kernel.gspmm(adj, "copy_u", "mean", h), 2, dev)
+    finally:
+        kernel.set_row_split(old)
+    peak, src_ = gather_peak(n * 128 * 4, 0)
+    res = {"value": 1e3 / ms, "unit": "epochs/s", "ms_per_epoch": ms, "kernel_ms": kms,
+           "launches_per_epoch": launches, "epochs": epochs, "warmup": warmup,
+           "transposed_csr_build_s": build_s, "peak_hbm_gb": peak_mem,
+           "config": "configs[3] (GraphSAGE-mean 128-128-41, examples/graphsage/train.py) for "
+                     "full-graph epochs on the rmat leg's graph (RMAT-%d: %d nodes, %d edges), "
+                     "one GPU, heavy rows chunked, 66 %% training nodes, Adam"
+                     % (int(round(np.log2(max(n, 1)))), n, E),
+           "roofline": roof(algorithmic_bytes(E, n, 128), ams, peak, src_,
+                            "g-SpMM copy_u + mean, F = 128 (the first layer's aggregation "
+                            "over the whole graph; heavy-row chunks and short-row tiers)"),
+           "cpu_baseline": None}
+    if cpu and sample is not None:
+        res["cpu_baseline"] = mean_bucketing_cpu(sample, n, sparse_table=True)
+    return res
+
+
+def mean_bucketing_cpu(sample, n, F_=128, target_edges=2_000_000, sparse_table=False):
     """The reference's mean aggregation on the host: no builtin mean exists
     (function/reducer.py: sum, max), so ``lambda nodes: mailbox.mean(1)``
     runs under degree bucketing (runtime/degree_bucketing.py:13-84: rows
@@ -463,7 +533,15 @@ def mean_bucketing_cpu(sample, n, F_=128, target_edges=2_000_000):
     sel = d < r1
     d, s = d[sel], s[sel]
     e = int(s.numel())
-    h = torch.rand(n, F_, generator=torch.Generator().manual_seed(8))
+    if sparse_table:
+        # a full-size (n, F) table whose pages are touched only for the
+        # sample's source rows (RMAT-26: 34 GB of address space, the sample's
+        # rows resident), as bench.cpu_baseline does
+        h = torch.empty(n, F_)
+        uniq = torch.unique(s)
+        h[uniq] = torch.rand(uniq.numel(), F_, generator=torch.Generator().manual_seed(8))
+    else:
+        h = torch.rand(n, F_, generator=torch.Generator().manual_seed(8))
     order = torch.sort(d, stable=True)[1]  # mailbox order: edge order within a row
     d, s = d[order], s[order]
 
@@ -489,6 +567,6 @@ def mean_bucketing_cpu(sample, n, F_=128, target_edges=2_000_000):
             "kind": "port",
             "sample": "degree-bucketing mean (the reference's UDF route for mean, "
                       "degree_bucketing.py:13-84) restated with torch, on the in-edges of the "
-                      "first %d rows of the headline graph (%d edges, F = %d), %d reps, torch "
+                      "first %d rows of the graph (%d edges, F = %d), %d reps, torch "
                       "%d threads; GPU comparison: roofline.kernel_ms is one such aggregation "
                       "over the whole graph" % (r1, e, F_, reps, _threads())}

@@ -608,12 +608,15 @@ extern int g_var_vec, g_var_group, g_var_unroll, g_var_pipe;
 // -1: automatic (non-temporal output past 512 MiB, default otherwise).
 extern int g_cache_policy;
 // Row gathers of copy_u + sum at VEC 2 x 64 lanes through buffer descriptors
-// (dglhip_set_gather_mode), a bit mask: bit 0 one-launch (and first-block)
-// launches, bit 1 the blocked schedule's launches (the default, 2); 0 global
-// loads everywhere.
+// (dglhip_set_gather_mode), a bit mask: bit 0 the one-launch rows and the
+// heavy-row chunk launches, bit 1 the blocked schedule's item launches, the
+// first block's included (the default, 2); 0 global loads everywhere.
 extern int g_gather_buf;
-// Running-row cache policy of accumulating copy_u + sum items (load_out /
-// store_out; dglhip_set_row_policy): 2 by default.
+// Running-row cache policy of the blocked schedule's copy_u + sum item
+// launches (load_out / store_out; dglhip_set_row_policy): 2 by default. It
+// applies where no output cache policy does (g_cache_policy automatic with
+// an output under twice the Infinity Cache, or 0): an explicit or automatic
+// non-temporal output (POL_NT_OUT and the study policies) takes precedence.
 extern int g_row_pol;
 
 template <int VEC, int GROUP, int MSG, int EM, bool MEAN, int UNROLL_OVERRIDE = 0,
@@ -635,7 +638,10 @@ static inline void launch_sum(const SumLaunch& a, hipStream_t stream) {
     // the running-row cache policy study (dglhip_set_row_policy): only the
     // shapes POL_OK covers are instantiated
     if constexpr (POL_OK) {
-      if (a.chunk_beg && g_row_pol > 0 && (a.accumulate || g_row_pol >= 2)) {
+      // the blocked schedule's items only (item rows given; heavy-row chunk
+      // and row-range launches keep their own policy: r04 ADVICE)
+      if (a.chunk_beg && a.row_order && pol == POL_DEFAULT && g_row_pol > 0 &&
+          (a.accumulate || g_row_pol >= 2)) {
 #define DGLHIP_RP_LAUNCH_B(ACC, RPV, B)                                                         \
   hipLaunchKernelGGL((gspmm_sum_kernel<VEC, GROUP, UNROLL, MSG, EM, MEAN, true, ACC, false,     \
                                        POL_DEFAULT, B, RPV>),                                   \

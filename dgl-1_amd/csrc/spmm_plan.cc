@@ -157,17 +157,11 @@ SpmmPlan::SpmmPlan(int device_type, int device_id, int64_t num_rows, int64_t num
     max_degree_ = std::max(max_degree_, d);
     num_nonempty_ += d > 0;
   }
-  host_order_.resize(R_);
   if (row_order) {
-    if (device_type == rt::kDLCPU) {
-      std::memcpy(host_order_.data(), row_order, R_ * sizeof(int32_t));
-    } else {
-      hip_ok(hipMemcpyAsync(host_order_.data(), row_order, R_ * sizeof(int32_t),
-                            hipMemcpyDeviceToHost, s), "plan row order copy");
-      hip_ok(hipStreamSynchronize(s), "plan row order copy");
-    }
-    row_order_ = row_order;
+    row_order_ = row_order;  // its host copy is made when a split plan or tiers need it
   } else {
+    host_order_.resize(R_);
+    have_host_order_ = true;
     if (R_) DGLHIP_CHECK(dglhip_rows_by_degree_host(R_, ip, host_order_.data()) == 0,
                          DGLGetLastError());
     if (device_type == rt::kDLCPU) {
@@ -179,10 +173,36 @@ SpmmPlan::SpmmPlan(int device_type, int device_id, int64_t num_rows, int64_t num
   }
   waves_ = kRefWaves;
   if (on_device()) {
-    int64_t w = 0;
-    DGLHIP_CHECK(dglhip_gspmm_resident_waves(device_id_, &w) == 0, DGLGetLastError());
-    waves_ = w;
+    // queried once per device (graphs built per training step make plans)
+    static std::mutex wmu;
+    static std::map<int, int64_t> wcache;
+    std::lock_guard<std::mutex> lk(wmu);
+    auto hit = wcache.find(device_id_);
+    if (hit == wcache.end()) {
+      int64_t w = 0;
+      DGLHIP_CHECK(dglhip_gspmm_resident_waves(device_id_, &w) == 0, DGLGetLastError());
+      hit = wcache.emplace(device_id_, w).first;
+    }
+    waves_ = hit->second;
   }
+}
+
+const std::vector<int32_t>& SpmmPlan::host_order(hipStream_t s) {
+  // called with mu_ held
+  if (!have_host_order_) {
+    host_order_.resize(R_);
+    if (R_) {
+      if (on_device()) {
+        hip_ok(hipMemcpyAsync(host_order_.data(), row_order_, R_ * sizeof(int32_t),
+                              hipMemcpyDeviceToHost, s), "plan row order copy");
+        hip_ok(hipStreamSynchronize(s), "plan row order copy");
+      } else {
+        std::memcpy(host_order_.data(), row_order_, R_ * sizeof(int32_t));
+      }
+    }
+    have_host_order_ = true;
+  }
+  return host_order_;
 }
 
 rt::NDArray SpmmPlan::empty(const std::vector<int64_t>& shape, int code, int bits) const {
@@ -507,9 +527,10 @@ SplitPlan& SpmmPlan::split_plan(int64_t threshold, bool skip_empty, int64_t chun
   auto hit = split_plans_.find(key);
   if (hit != split_plans_.end()) return hit->second;
   const int64_t* ip = host_indptr_->data();
+  const std::vector<int32_t>& order = host_order(s);
   std::vector<int32_t> light, heavy;
   for (int64_t i = 0; i < R_; ++i) {
-    const int32_t r = host_order_[i];
+    const int32_t r = order[i];
     const int64_t d = ip[r + 1] - ip[r];
     if (skip_empty && d == 0) continue;
     (d > threshold ? heavy : light).push_back(r);
@@ -593,7 +614,8 @@ Tiers& SpmmPlan::tiers_plain(bool skip, hipStream_t s) {
   auto hit = tiers_.find(key);
   if (hit != tiers_.end()) return hit->second;
   const int64_t n = skip ? num_nonempty_ : R_;
-  return tiers_.emplace(key, build_tiers(host_order_.data(), rt::NDArray(), n, s)).first->second;
+  const std::vector<int32_t>& order = host_order(s);
+  return tiers_.emplace(key, build_tiers(order.data(), rt::NDArray(), n, s)).first->second;
 }
 
 Tiers& SpmmPlan::tiers_light(const SplitPlan& sp, int64_t threshold, bool skip, hipStream_t s) {
@@ -605,8 +627,9 @@ Tiers& SpmmPlan::tiers_light(const SplitPlan& sp, int64_t threshold, bool skip, 
   const int64_t* ip = host_indptr_->data();
   std::vector<int32_t> light;
   light.reserve(sp.n_light);
+  const std::vector<int32_t>& order = host_order(s);
   for (int64_t i = 0; i < R_; ++i) {
-    const int32_t r = host_order_[i];
+    const int32_t r = order[i];
     const int64_t d = ip[r + 1] - ip[r];
     if ((skip && d == 0) || d > threshold) continue;
     light.push_back(r);

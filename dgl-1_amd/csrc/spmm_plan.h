@@ -181,7 +181,10 @@ class SpmmPlan {
   const int64_t* indptr_;
   const int32_t* indices_;
   std::shared_ptr<std::vector<int64_t>> host_indptr_;
+  // the schedule's host copy (split plans, tiers): made on first use
+  const std::vector<int32_t>& host_order(hipStream_t s);
   std::vector<int32_t> host_order_;
+  bool have_host_order_ = false;
   rt::NDArray order_own_;
   const int32_t* row_order_ = nullptr;
   int64_t max_degree_ = 0, num_nonempty_ = 0, waves_ = 0;

@@ -180,7 +180,9 @@ class GraphIndex(object):
         key = ("adj", str(ctx))
         if key not in self._cache:
             src, dst, _ = self._id_order()
-            self._cache[key] = kernel.from_coo(self._n, self._n, dst, src, self._slot_order(), ctx)
+            # the native index validated every edge when it was added
+            self._cache[key] = kernel.from_coo(self._n, self._n, dst, src, self._slot_order(), ctx,
+                                               validate=False)
         return self._cache[key]
 
     def incidence_in(self, ctx):

@@ -459,8 +459,9 @@ int dglhip_gspmm_host(int msg_op, int reduce_op, int64_t num_rows,
  * wave per row) go through buffer descriptors built from the wave-uniform row
  * address (one 32-bit lane offset for every gather in flight instead of a
  * 64-bit address each) rather than global loads, as a bit mask: bit 0 the
- * one-launch calls, bit 1 the source-blocked schedule's launches (the default,
- * 2: 42 instead of 70 VGPRs there). Same values. */
+ * one-launch rows and heavy-row chunk launches, bit 1 the source-blocked
+ * schedule's item launches, the first block's included (the default, 2: 42
+ * instead of 70 VGPRs there). Same values. */
 int dglhip_set_gather_mode(int buffer_descriptors);
 
 /* Resident waves of the headline g-SpMM kernel (F = 128 copy_u + sum) on
@@ -792,7 +793,9 @@ int dglhip_set_cache_policy(int policy);
  * rewrite (and the fused GAT layer's 8-head rows): 0 plain, 1 non-temporal
  * load and store, 2 non-temporal load + sc1 store (the default), 3 sc0 sc1
  * load + sc1 store, 4 plain load + sc1 store (2-4: the first launch's stores
- * with sc1 too). Same values. */
+ * with sc1 too). Item launches only, and only where no output cache policy
+ * (dglhip_set_cache_policy, or the automatic non-temporal output past twice
+ * the Infinity Cache) applies. Same values. */
 int dglhip_set_row_policy(int policy);
 /* Synchronises on the recorded events and returns the summed kernel time
  * (ms) and launch count since the last enable/reset. */

@@ -394,7 +394,7 @@ def test_blocked_max_bits_with_ties(msg):
     gen = torch.Generator().manual_seed(18)
     H = torch.randint(-3, 4, (n, 128), generator=gen).float().to(dev)
     w = torch.randint(1, 3, (m, 1), generator=gen).float().to(dev)
-    assert kernel._block_cuts(adj.fwd, 128 * 4, kernel._BLOCK_BYTES) is not None
+    assert kernel._block_cuts(adj.fwd, 128 * 4, kernel.schedule_policy()["block_bytes"]) is not None
 
     def run(policy):
         old = kernel.set_blocked(policy)

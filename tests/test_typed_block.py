@@ -48,9 +48,20 @@ def test_typed_block(device, shape):
         W2 = W.clone().requires_grad_(True)
         ref = reference(src, dst, etype, h2, W2, n, None if nm is None else nm.double())
         ref.backward(G.double())
-        torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
-        torch.testing.assert_close(h1.grad.double(), h2.grad, rtol=1e-5, atol=1e-4)
-        torch.testing.assert_close(W1.grad.double(), W2.grad, rtol=1e-5, atol=1e-4)
+        # the fp32 chains' error bound, per element: 1e-5 of the sum of the
+        # absolute terms (the same products over |h|, |W|, |norm|, |G|), the
+        # bound tests/test_rmat26.py uses for chunked rows (r04 verdict, Weak 1)
+        ha = h.abs().requires_grad_(True)
+        Wa = W.abs().requires_grad_(True)
+        scale = reference(src, dst, etype, ha, Wa, n,
+                          None if nm is None else nm.double().abs())
+        scale.backward(G.double().abs())
+        for got, want, bound in ((out.double(), ref, scale.detach()),
+                                 (h1.grad.double(), h2.grad, ha.grad),
+                                 (W1.grad.double(), W2.grad, Wa.grad)):
+            err = (got - want).abs()
+            assert bool((err <= 1e-5 * bound + 1e-30).all()), \
+                float((err / (1e-5 * bound + 1e-30)).max())
 
 
 @pytest.mark.gpu
@@ -143,6 +154,17 @@ def test_typed_block_fb15k_shape(device):
         W2 = W.clone().requires_grad_(True)
         ref = reference(src_t, dst_t, etype, h2, W2, n, None if nm is None else nm.double())
         ref.backward(G.double())
-        torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
-        torch.testing.assert_close(h1.grad.double(), h2.grad, rtol=1e-5, atol=1e-4)
-        torch.testing.assert_close(W1.grad.double(), W2.grad, rtol=1e-5, atol=1e-4)
+        # the fp32 chains' error bound, per element: 1e-5 of the sum of the
+        # absolute terms (the same products over |h|, |W|, |norm|, |G|), the
+        # bound tests/test_rmat26.py uses for chunked rows (r04 verdict, Weak 1)
+        ha = h.abs().requires_grad_(True)
+        Wa = W.abs().requires_grad_(True)
+        scale = reference(src_t, dst_t, etype, ha, Wa, n,
+                          None if nm is None else nm.double().abs())
+        scale.backward(G.double().abs())
+        for got, want, bound in ((out.double(), ref, scale.detach()),
+                                 (h1.grad.double(), h2.grad, ha.grad),
+                                 (W1.grad.double(), W2.grad, Wa.grad)):
+            err = (got - want).abs()
+            assert bool((err <= 1e-5 * bound + 1e-30).all()), \
+                float((err / (1e-5 * bound + 1e-30)).max())

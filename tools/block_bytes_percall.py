@@ -39,7 +39,7 @@ def main():
     for _ in range(args.rounds):
         row = {}
         for mib in args.mib:
-            kernel._BLOCK_BYTES = int(mib * (1 << 20))
+            kernel.set_schedule_policy(block_bytes=int(mib * (1 << 20)))
             kernel.gspmm_into(csr, out, h)
             torch.cuda.synchronize()
             same = bool(torch.equal(out, ref))

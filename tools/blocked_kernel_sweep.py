@@ -51,7 +51,7 @@ def main():
             _ffi.check_call(_ffi.LIB.dglhip_set_spmm_variant(*v))
             kernel.set_gather_mode(gm)
             kernel.set_short_rows(short)
-            kernel._BLOCK_BYTES = bb
+            kernel.set_schedule_policy(block_bytes=bb)
             out = kernel.gspmm(adj, "copy_u", "sum", h)
             assert torch.equal(out, ref), c
             kernel.timing_enable(True)

@@ -26,7 +26,7 @@ def main():
     src, dst, n = data.reddit_like(device=dev)
     adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
     del src, dst
-    default_min = kernel._BLOCK_TABLE_MIN
+    default_min = kernel.schedule_policy()["block_table_min"]
     configs = [("one launch", "off", default_min), ("blocked", "auto", default_min),
                ("blocked, 4 MiB floor", "auto", 4 << 20)]
     res = []
@@ -40,7 +40,7 @@ def main():
         for _ in range(args.rounds):
             for name, pol, tmin in configs:
                 old = kernel.set_blocked(pol)
-                kernel._BLOCK_TABLE_MIN = tmin
+                kernel.set_schedule_policy(block_table_min=tmin)
                 out = kernel.gspmm(adj, "copy_u", "sum", h)
                 assert torch.equal(out, ref), (F, name)
                 kernel.timing_enable(True)
@@ -49,7 +49,7 @@ def main():
                 ms, cnt = kernel.timing_read()
                 kernel.timing_enable(False)
                 kernel.set_blocked(old)
-                kernel._BLOCK_TABLE_MIN = default_min
+                kernel.set_schedule_policy(block_table_min=default_min)
                 times[name].append(ms / args.iters)
                 launches[name] = cnt // args.iters
         e = {"feat": F, "table_MB": n * F * 4 / 1e6}

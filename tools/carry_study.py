@@ -1,6 +1,6 @@
 """How many slots a "carry" of small (row, block) items would move on the
 headline graph (r03 verdict, "Next" 5): the source-blocked plan of the
-Reddit-shaped graph (bench.py's N = 1 step, kernel._block_split at the
+Reddit-shaped graph (bench.py's N = 1 step, the plan's row ranges at the
 plan's block count), its items' slot counts, and what carrying a row's items
 of fewer than T slots into its next block's item would merge. Host only.
 
@@ -26,10 +26,14 @@ def main():
     src, dst, n = data.reddit_like(scale=1, seed=0, device="cpu")
     csr = kernel.build_csr(n, n, dst, src, kernel.ORDER_EID, "cpu")
     del src, dst
-    lo, hi = kernel._column_span(csr)
-    B = kernel._block_count(csr, (hi - lo) * 512)
-    _, counts, pre, sfx = kernel._block_split(csr, B, lo, hi)
-    c = counts.numpy()
+    # the plan's row ranges per block: counts = cuts[b + 1] - cuts[b]
+    cuts = kernel._block_cuts(csr, 512, kernel.schedule_policy()["block_bytes"])
+    B = len(cuts) - 1
+    sfx = None
+    if cuts[-1].equal(csr.indptr[1:]) and B > 1 and not cuts[-2].equal(csr.indptr[1:]):
+        sfx = cuts[-1] - cuts[-2]  # a suffix range (rows whose blocks decrease)
+        B -= 1
+    c = torch.stack([cuts[b + 1] - cuts[b] for b in range(B)], 1).numpy()
     nz = c[c > 0]
     res = {"rows": n, "edges": csr.nnz, "blocks": B, "items": int(nz.size),
            "slots_per_item_mean": float(nz.mean()), "slots_per_item_min": int(nz.min()),

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--mib", type=int, nargs="+", default=[4, 6, 8, 11, 14, 18])
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     src, dst, n = data.reddit_like(scale=1, seed=0, device=dev)
@@ -56,7 +57,7 @@ def main():
     res, same, launches = {}, {}, {}
     try:
         for _ in range(args.rounds):
-            for mib in (4, 6, 8, 11, 14, 18):
+            for mib in args.mib:
                 kernel._GAT_BWD_BLOCK_BYTES = mib << 20
                 got = fb()
                 same[mib] = all(bool(torch.equal(a, b)) for a, b in zip(got, ref))

@@ -34,12 +34,12 @@ def main():
     del src, dst
     h = torch.rand(n, 128, device=dev) * 2 - 1
     ref = kernel.gspmm(adj, "copy_u", "sum", h)
-    old_bytes = kernel._BLOCK_BYTES
+    old_bytes = kernel.schedule_policy()["block_bytes"]
     res, same = {}, {}
     try:
         for _ in range(args.rounds):
             for mib in args.mib:
-                kernel._BLOCK_BYTES = int(mib * (1 << 20))
+                kernel.set_schedule_policy(block_bytes=int(mib * (1 << 20)))
                 for mode in args.modes:
                     kernel.check_call(kernel.LIB.dglhip_set_gather_mode(mode))
                     key = "%g MiB / mode %d" % (mib, mode)
@@ -55,7 +55,7 @@ def main():
                     e.synchronize()
                     res.setdefault(key, []).append(s.elapsed_time(e) / args.calls)
     finally:
-        kernel._BLOCK_BYTES = old_bytes
+        kernel.set_schedule_policy(block_bytes=old_bytes)
         kernel.check_call(kernel.LIB.dglhip_set_gather_mode(2))  # the default
     line = json.dumps({"ms_per_call": res, "min": {k: min(v) for k, v in res.items()},
                        "bit_identical": same})

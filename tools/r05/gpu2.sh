@@ -5,8 +5,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 mkdir -p gpurun_out/r05
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r05
-timeout -k 10 300 python -u tools/gat_pack_ab.py --out $O/gat_pack_ab.json > $O/gat_pack_ab.log 2>&1 || exit $?
-tail -1 $O/gat_pack_ab.log
+# (gat pack A/B done in the first run of this script)
+
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?; tail -5 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?

@@ -59,7 +59,7 @@ def main():
         print(res[-1], file=sys.stderr, flush=True)
     # the same tail through the batched short-row kernel, tier by tier
     tiers = []
-    n_long, tail = csr.tiers(light, ("study",))
+    n_long, tail = csr.tiers(threshold=t)  # the plan's tiers of the same list
     lo = n_long
     for maxd, (rows_t, sp, cols), cnt_rows in tail:
         hi = lo + cnt_rows

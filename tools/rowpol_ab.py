@@ -21,12 +21,12 @@ from dgl import data, kernel  # noqa: E402
 def block_sweep(adj, h, ref, args):
     """ms per call at 5 / 6 / 7 / 8 / 9 MiB source blocks under row policies 0, 2 and
     4 (interleaved), and whether each keeps the bits."""
-    old_bytes = kernel._BLOCK_BYTES
+    old_bytes = kernel.schedule_policy()["block_bytes"]
     res, same = {}, {}
     try:
         for _ in range(args.rounds):
             for mib in (5, 6, 7, 8, 9):
-                kernel._BLOCK_BYTES = mib << 20
+                kernel.set_schedule_policy(block_bytes=mib << 20)
                 for p in (0, 2, 4):
                     kernel.check_call(kernel.LIB.dglhip_set_row_policy(p))
                     o = kernel.gspmm(adj, "copy_u", "sum", h)
@@ -43,7 +43,7 @@ def block_sweep(adj, h, ref, args):
                     e.synchronize()
                     res.setdefault(key, []).append(s.elapsed_time(e) / args.calls)
     finally:
-        kernel._BLOCK_BYTES = old_bytes
+        kernel.set_schedule_policy(block_bytes=old_bytes)
         kernel.check_call(kernel.LIB.dglhip_set_row_policy(0))
     return {"ms_per_call": res, "min": {k: min(v) for k, v in res.items()},
             "bit_identical": same}
