@@ -496,12 +496,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // the pairs: attention, keep bit, dropped weight (the forward's
     // expressions)
     float pa[2];
-    bool pk[2];
+    bool pk[2], px[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int j = jc + 8 * i;
       float x = elc + per[i];
-      x = x > 0.0f ? x : alpha * x;
+      px[i] = x > 0.0f;  // the slope from the logit's sign (torch's backward)
+      x = px[i] ? x : alpha * x;
       if (apply_exp) x = __expf(x);
       const float a = fminf(fmaxf(x, lo), hi);
       float w = a;
@@ -549,8 +550,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       float tt = ld[hc * LU + j];
       if (DROP) tt = pk[i] ? tt * scale : 0.0f;
       if (PACK || dz) tt = tt + pz[i];
-      float g = apply_exp ? (tt * a) * (a <= 1.0f ? alpha : 1.0f)
-                          : tt * (a <= 0.0f ? alpha : 1.0f);
+      const float sl = px[i] ? 1.0f : alpha;
+      float g = apply_exp ? (tt * a) * sl : tt * sl;
       g = (a > lo && a < hi) ? g : 0.0f;
       pg[i] = g;
       ld[hc * LU + j] = g;

@@ -31,8 +31,13 @@ namespace dglhip {
 //   t = d_w; t = keep ? t * scale : 0 (dropout: keep from the forward's hash
 //   of (seed, k * H + h) with hash_keep, else w[k, h] != 0);
 //   t = t + dz[row, h] (the normaliser's gradient);
-//   g = (t * a) * (a <= 1 ? alpha : 1) (exp; else t * (a <= 0 ? alpha : 1): the
-//       slope alpha where the logit x <= 0, as torch's leaky_relu backward);
+//   g = (t * a) * s (exp; else t * s), s = alpha where the logit x <= 0, else 1
+//       (torch's leaky_relu backward). With the logits given (el, er: x =
+//       el[u, h] + er[row, h], the forward's sum) s comes from x itself;
+//       without them from a (a <= 1 with exp, a <= 0 without), which differs
+//       from x's sign only for 0 < x < 2^-24, where exp(x) rounds to 1 (r04
+//       ADVICE: the fused backward and the engine's three-pass path take the
+//       logits, so every path follows torch there too);
 //   g = lo < a < hi ? g : 0
 // the float operations, and their order, of kernel._GATAggregate's torch
 // backward, so both give the same bits.
@@ -53,31 +58,40 @@ struct GatEpi {
   uint64_t seed = 0;
   const int64_t* seed_off = nullptr;
   uint32_t thr = 0;
+  // the attention's logits (the slope from x's sign; NULL: from a)
+  const float* el = nullptr;  // [num_src, H]
+  const float* er = nullptr;  // [rows, H]
 };
+
+// The leaky_relu slope of a pair: from the logit's sign when it is known
+// (xpos >= 0), else from the attention value (see GatEpi).
+__device__ __forceinline__ float gat_slope(const GatEpi& e, float a, int xpos) {
+  if (xpos >= 0) return xpos ? 1.0f : e.alpha;
+  return e.apply_exp ? (a <= 1.0f ? e.alpha : 1.0f) : (a <= 0.0f ? e.alpha : 1.0f);
+}
 
 __device__ __forceinline__ uint64_t gat_epi_seed(const GatEpi& e) {
   return e.seed + (e.seed_off ? static_cast<uint64_t>(*e.seed_off) : 0);
 }
 
 __device__ __forceinline__ float gat_epi(const GatEpi& e, float t, int64_t k, int64_t H,
-                                         int64_t h, int64_t row) {
+                                         int64_t h, int64_t row, int64_t u) {
   const float a = e.a[k * H + h];
   if (e.hash_keep) t = gat_keep(gat_epi_seed(e), k * H + h, e.thr) ? t * e.scale : 0.0f;
   else if (e.w) t = e.w[k * H + h] != 0.0f ? t * e.scale : 0.0f;
   if (e.dz) t = t + e.dz[row * H + h];
-  const float g = e.apply_exp ? (t * a) * (a <= 1.0f ? e.alpha : 1.0f)
-                              : t * (a <= 0.0f ? e.alpha : 1.0f);
+  const int xpos = e.el ? ((e.el[u * H + h] + e.er[row * H + h]) > 0.0f ? 1 : 0) : -1;
+  const float g = e.apply_exp ? (t * a) * gat_slope(e, a, xpos) : t * gat_slope(e, a, xpos);
   return (a > e.lo && a < e.hi) ? g : 0.0f;
 }
 
 // gat_epi on operands loaded ahead (the slot's attention a and keep bit,
 // the row's normaliser gradient dz): the same arithmetic.
 __device__ __forceinline__ float gat_epi_pre(const GatEpi& e, float t, float a, bool keep,
-                                             float dz) {
+                                             float dz, int xpos) {
   if (e.w || e.hash_keep) t = keep ? t * e.scale : 0.0f;
   if (e.dz) t = t + dz;
-  const float g = e.apply_exp ? (t * a) * (a <= 1.0f ? e.alpha : 1.0f)
-                              : t * (a <= 0.0f ? e.alpha : 1.0f);
+  const float g = e.apply_exp ? (t * a) * gat_slope(e, a, xpos) : t * gat_slope(e, a, xpos);
   return (a > e.lo && a < e.hi) ? g : 0.0f;
 }
 
@@ -99,18 +113,19 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   const float* a = lhs + wave * F;
   const int64_t D = F / H;
   for (int64_t k = row_beg[wave]; k < row_end[wave]; ++k) {
-    const float* c = rhs + int64_t(indices[k]) * F;
+    const int64_t col = indices[k];
+    const float* c = rhs + col * F;
     if (H == 1) {
       float acc = 0.0f;
       for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-      if (lane == 0) out[eid ? eid[k] : k] = EPI ? gat_epi(epi, acc, k, 1, 0, wave) : acc;
+      if (lane == 0) out[eid ? eid[k] : k] = EPI ? gat_epi(epi, acc, k, 1, 0, wave, col) : acc;
     } else {
       for (int64_t h = lane; h < H; h += 64) {
         float acc = 0.0f;
         for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);
-        out[(eid ? eid[k] : k) * H + h] = EPI ? gat_epi(epi, acc, k, H, h, wave) : acc;
+        out[(eid ? eid[k] : k) * H + h] = EPI ? gat_epi(epi, acc, k, H, h, wave, col) : acc;
       }
     }
   }
@@ -220,10 +235,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   auto keep_of = [&](int64_t k, int hh, float w) -> bool {
     return (EPI && epi.hash_keep) ? gat_keep(hseed, k * H + hh, epi.thr) : w != 0.0f;
   };
-  float dzv[T];
+  float dzv[T], erv[T];
+  const bool xl = EPI && epi.el != nullptr;  // the slope from the logits (wave-uniform)
 #pragma unroll
-  for (int t = 0; t < T; ++t)
+  for (int t = 0; t < T; ++t) {
     dzv[t] = (EPI && PRE && epi.dz) ? epi.dz[row * H + lane_head(t)] : 0.0f;
+    erv[t] = xl ? epi.er[row * H + lane_head(t)] : 0.0f;
+  }
   // the fused row sums: lanes of slot group s each chain the values of every
   // slot of the row in slot order (s = 0 stores them)
   const bool rs = EPI && epi.rsum != nullptr;  // wave-uniform
@@ -235,12 +253,14 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
   for (int i = 0; i < NB; ++i) a[i] = ldv<4>(lhs + row * F + 32 * i + 4 * j);
   for (int64_t k0 = beg; k0 < end; k0 += 8 * UNROLL) {
     f32x4 c[UNROLL][NB];
-    float ea[UNROLL][T], ew[UNROLL][T];
+    float ea[UNROLL][T], ew[UNROLL][T], ex[UNROLL][T];
+    int64_t ucol[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       int64_t k = k0 + 8 * u + s;
       k = k < end ? k : end - 1;  // idle slot lanes re-read the row's last slot
-      const float* r = rhs + int64_t(indices[k]) * F + 4 * j;
+      ucol[u] = indices[k];
+      const float* r = rhs + ucol[u] * F + 4 * j;
 #pragma unroll
       for (int i = 0; i < NB; ++i) c[u][i] = ldv<4>(r + 32 * i);
       // the epilogue's per-slot operands in flight with the gathers, not
@@ -249,6 +269,7 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
       for (int t = 0; t < T; ++t) {
         ea[u][t] = (EPI && PRE) ? epi.a[k * H + lane_head(t)] : 0.0f;
         ew[u][t] = (EPI && PRE && epi.w) ? epi.w[k * H + lane_head(t)] : 0.0f;
+        ex[u][t] = (EPI && PRE && xl) ? epi.el[ucol[u] * H + lane_head(t)] : 0.0f;
       }
     }
 #pragma unroll
@@ -277,13 +298,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (H >= 8 ? H / 8 : 1); ++t) {
             const int hh = j * (H / 8) + t;
-            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t]) : gat_epi(epi, q[t], k, H, hh, row)) : q[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, q[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t], xl ? ((ex[u][t] + erv[t]) > 0.0f ? 1 : 0) : -1) : gat_epi(epi, q[t], k, H, hh, row, ucol[u])) : q[t];
             if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = H >= 8 ? 1 : 8 / H;  // lanes holding the same head
           const int hh = j / DUP;
-          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0]) : gat_epi(epi, q[0], k, H, hh, row)) : q[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, q[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0], xl ? ((ex[u][0] + erv[0]) > 0.0f ? 1 : 0) : -1) : gat_epi(epi, q[0], k, H, hh, row, ucol[u])) : q[0];
           if (k < end && j % DUP == 0) out[obase + hh] = sv[0];
         }
       } else {
@@ -294,13 +315,13 @@ __global__ __launch_bounds__(256) void gsddmm_dot_sliced_kernel(
 #pragma unroll
           for (int t = 0; t < (NB >= LPH ? NB / LPH : 1); ++t) {
             const int hh = (r * (NB / LPH) + t) * HPB + g;
-            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t]) : gat_epi(epi, p[t], k, H, hh, row)) : p[t];
+            sv[t] = EPI ? (PRE ? gat_epi_pre(epi, p[t], ea[u][t], keep_of(k, hh, ew[u][t]), dzv[t], xl ? ((ex[u][t] + erv[t]) > 0.0f ? 1 : 0) : -1) : gat_epi(epi, p[t], k, H, hh, row, ucol[u])) : p[t];
             if (k < end) out[obase + hh] = sv[t];
           }
         } else {
           constexpr int DUP = NB >= LPH ? 1 : LPH / NB;
           const int hh = (r / DUP) * HPB + g;
-          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0]) : gat_epi(epi, p[0], k, H, hh, row)) : p[0];
+          sv[0] = EPI ? (PRE ? gat_epi_pre(epi, p[0], ea[u][0], keep_of(k, hh, ew[u][0]), dzv[0], xl ? ((ex[u][0] + erv[0]) > 0.0f ? 1 : 0) : -1) : gat_epi(epi, p[0], k, H, hh, row, ucol[u])) : p[0];
           if (k < end && r % DUP == 0) out[obase + hh] = sv[0];
         }
       }
@@ -844,6 +865,39 @@ int dglhip_gat_attention_grad_keep_ranges_device(
   epi.seed = seed;
   epi.seed_off = seed_offset;
   epi.thr = drop ? gat_drop_threshold(drop_p) : 0u;
+  launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
+                         nullptr, dout, ft, grad, epi, stream);
+  API_END();
+}
+
+int dglhip_gat_attention_grad_logits_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft, const float* attn, const float* attn_drop,
+    const float* dz, const float* el, const float* er, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_scale, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream_) {
+  API_BEGIN();
+  DGLHIP_CHECK(grad_rowsum == nullptr || dglhip_gat_attention_grad_rowsum_ok(feat_len, num_heads),
+               "fused row sums: unsupported shape F = " << feat_len << ", H = " << num_heads);
+  DGLHIP_CHECK(drop_p >= 0.0f && drop_p < 1.0f, "dropout probability must be in [0, 1)");
+  DGLHIP_CHECK(!(drop_p > 0.0f && attn_drop), "dropout: the hash (drop_p) or attn_drop, not both");
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0, "negative size");
+  DGLHIP_CHECK(num_heads >= 1 && feat_len % num_heads == 0,
+               "num_heads " << num_heads << " must divide feat_len " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(row_beg && row_end && indices && dout && ft && attn && grad && el && er,
+               "null pointer argument");
+  const bool hash = drop_p > 0.0f;
+  GatEpi epi{attn, attn_drop, dz, alpha, clamp_lo, clamp_hi,
+             hash ? 1.0f / (1.0f - drop_p) : drop_scale, apply_exp, grad_rowsum};
+  epi.hash_keep = hash ? 1 : 0;
+  epi.seed = seed;
+  epi.seed_off = seed_offset;
+  epi.thr = hash ? gat_drop_threshold(drop_p) : 0u;
+  epi.el = el;
+  epi.er = er;
   launch_sddmm_dot<true>(num_rows, feat_len, num_heads, row_beg, row_end, row_order, indices,
                          nullptr, dout, ft, grad, epi, stream);
   API_END();

@@ -80,6 +80,10 @@ def _load():
         "dglhip_gat_attention_grad_keep_ranges_device": (
             _c_int, [_c_i64, _c_i64, _c_i64] + [_vp] * 8 +
             [_c_float, _c_float, _c_float, _c_int, _c_float, _c_u64, _vp, _vp, _vp, _vp]),
+        "dglhip_gat_attention_grad_logits_ranges_device": (
+            _c_int, [_c_i64, _c_i64, _c_i64] + [_vp] * 11 +
+            [_c_float, _c_float, _c_float, _c_int, _c_float, _c_float, _c_u64, _vp, _vp, _vp,
+             _vp]),
         "dglhip_typed_block_spmm_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
                                            [_vp] * 9),
         "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),

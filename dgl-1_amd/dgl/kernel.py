@@ -1587,25 +1587,23 @@ class _EdgeAttention(torch.autograd.Function):
         else:
             check_call(LIB.dglhip_gsddmm_attention_host(*(args + (0,))))
         ctx.adj, ctx.alpha, ctx.lo, ctx.hi, ctx.apply_exp = adj, alpha, lo, hi, apply_exp
-        ctx.slot = slot
-        ctx.save_for_backward(out)
+        ctx.slot, ctx.tr = slot, tr
+        ctx.save_for_backward(out, a_src, a_dst)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        (out,) = ctx.saved_tensors
-        # d/dx clamp(exp(lrelu(x))): out * lrelu'(x) where not clamped
-        inside = (out > ctx.lo) & (out < ctx.hi)
-        if ctx.apply_exp:
-            # lrelu(x) = log(out); torch's leaky_relu backward takes the slope
-            # alpha where x <= 0 (x == 0 included)  <=>  out <= 1
-            slope = torch.where(out <= 1, torch.full_like(out, ctx.alpha), torch.ones_like(out))
-            g = dout * out * slope
-        else:
-            slope = torch.where(out <= 0, torch.full_like(out, ctx.alpha), torch.ones_like(out))
-            g = dout * slope
-        g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
+        out, a_src, a_dst = ctx.saved_tensors
         adj = ctx.adj
+        # d/dx clamp(exp(lrelu(x))): out * lrelu'(x) where not clamped, the
+        # slope alpha where the logit x <= 0 (x == 0 included), as torch's
+        # leaky_relu backward: from x itself, recomputed in out's order
+        # (out <= 1 would differ for 0 < x < 2^-24, where exp(x) rounds to 1)
+        x = _edge_logits(adj, a_src, a_dst, ctx.slot, ctx.tr, out.shape[0])
+        inside = (out > ctx.lo) & (out < ctx.hi)
+        slope = torch.where(x <= 0, torch.full_like(out, ctx.alpha), torch.ones_like(out))
+        g = dout * out * slope if ctx.apply_exp else dout * slope
+        g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
         # sum the per-edge gradient at the source (transposed CSR) and destination
         H = g.shape[1]
         d_src, _ = _run_gspmm(adj.bwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
@@ -1613,6 +1611,22 @@ class _EdgeAttention(torch.autograd.Function):
         d_dst, _ = _run_gspmm(adj.fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False,
                               emap=SLOT if ctx.slot else None)
         return None, None, None, None, None, None, d_src, d_dst, None
+
+
+def _edge_logits(adj, a_src, a_dst, slot, tr, num_edges):
+    """x = a_src[u] + a_dst[v] per edge u -> v (the attention kernels' sum,
+    float32): by forward slot, or by edge id through the CSR the forward ran
+    over (tr: the transpose, whose rows are the sources)."""
+    if slot:
+        fwd = adj.fwd
+        return a_src.index_select(0, fwd.indices.long()) + \
+            a_dst.index_select(0, fwd.row_ids())
+    csr, _ = _eid_major(adj)
+    rows, cols = csr.row_ids(), csr.indices.long()
+    u, v = (rows, cols) if tr else (cols, rows)
+    x = torch.empty(num_edges, a_src.shape[1], dtype=torch.float32, device=a_src.device)
+    x[csr.eid.long()] = a_src.index_select(0, u) + a_dst.index_select(0, v)
+    return x
 
 
 def edge_attention(adj, a_src, a_dst, num_edges, alpha=0.2, clamp=(-10.0, 10.0),
@@ -1787,15 +1801,15 @@ class _GATAggregate(torch.autograd.Function):
         if ctx.use_t:
             ctx.D = D
             ctx.save_for_backward(ft2, el, er)
-        else:
-            ctx.save_for_backward(ft2, a, w)
+        else:  # (el, er: the logits' sign gives the leaky_relu slope)
+            ctx.save_for_backward(ft2, a, w, el, er)
         return out_ft, out_z
 
     @staticmethod
     def backward(ctx, d_ft, d_z):
         if ctx.use_t:
             return _gat_backward_t(ctx, d_ft, d_z)
-        ft2, a, w = ctx.saved_tensors
+        ft2, a, w, el, er = ctx.saved_tensors
         adj = ctx.adj
         fwd = adj.fwd
         H = a.shape[1]
@@ -1827,21 +1841,16 @@ class _GATAggregate(torch.autograd.Function):
                            d_ft.data_ptr() % 16 == 0 and ft2c.data_ptr() % 16 == 0)
                 er_sum = (torch.zeros(fwd.num_rows, H, dtype=torch.float32, device=ft2.device)
                           if fuse_er else None)
+                # keep bits from the forward's hash (drop_p), not w != 0; the
+                # slope from the logits el[u] + er[v]
+                p_hash = float(ctx.p) if w is not None else 0.0
                 for b in range(len(cuts) - 1):
-                    if w is not None:  # keep bits from the forward's hash, not w != 0
-                        check_call(LIB.dglhip_gat_attention_grad_keep_ranges_device(
-                            fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
-                            ptr(fwd.row_order), ptr(fwd.indices), ptr(d_ft), ptr(ft2c), ptr(a),
-                            ptr(dz), float(ctx.alpha), float(ctx.lo), float(ctx.hi),
-                            1 if ctx.apply_exp else 0, float(ctx.p), ctx.seed,
-                            ptr(ctx.seed_off), ptr(g), ptr(er_sum), _stream_of(ft2.device)))
-                        continue
-                    check_call(LIB.dglhip_gat_attention_grad_rowsum_ranges_device(
+                    check_call(LIB.dglhip_gat_attention_grad_logits_ranges_device(
                         fwd.num_rows, F, H, ptr(cuts[b]), ptr(cuts[b + 1]),
-                        ptr(fwd.row_order), ptr(fwd.indices),
-                        ptr(d_ft), ptr(ft2c), ptr(a), ptr(w), ptr(dz), float(ctx.alpha),
-                        float(ctx.lo), float(ctx.hi), 1 if ctx.apply_exp else 0, float(scale),
-                        ptr(g), ptr(er_sum), _stream_of(ft2.device)))
+                        ptr(fwd.row_order), ptr(fwd.indices), ptr(d_ft), ptr(ft2c), ptr(a),
+                        None, ptr(dz), ptr(el), ptr(er), float(ctx.alpha), float(ctx.lo),
+                        float(ctx.hi), 1 if ctx.apply_exp else 0, 1.0, p_hash, ctx.seed,
+                        ptr(ctx.seed_off), ptr(g), ptr(er_sum), _stream_of(ft2.device)))
                 if fuse_er:
                     d_er = er_sum
             else:
@@ -1852,13 +1861,10 @@ class _GATAggregate(torch.autograd.Function):
                 if d_z is not None:
                     d_a = d_a + d_z.contiguous().index_select(0, fwd.row_ids())
                 # the attention's backward (_EdgeAttention.backward, slot order)
+                x = _edge_logits(adj, el, er, True, False, fwd.nnz)
                 inside = (a > ctx.lo) & (a < ctx.hi)
-                if ctx.apply_exp:
-                    slope = torch.where(a <= 1, torch.full_like(a, ctx.alpha), torch.ones_like(a))
-                    g = d_a * a * slope
-                else:
-                    slope = torch.where(a <= 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
-                    g = d_a * slope
+                slope = torch.where(x <= 0, torch.full_like(a, ctx.alpha), torch.ones_like(a))
+                g = d_a * a * slope if ctx.apply_exp else d_a * slope
                 g = torch.where(inside, g, torch.zeros_like(g)).contiguous()
             if need_el:
                 d_el = _gat_el_grad(adj, g, H)

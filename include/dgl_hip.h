@@ -681,6 +681,22 @@ int dglhip_gat_attention_grad_keep_ranges_device(
     float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
     const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream);
 
+/* The attention gradient with the leaky_relu slope taken from the logit's
+ * sign, x = el[u, h] + er[v, h] (the forward's sum): alpha where x <= 0, as
+ * torch's leaky_relu backward. The entries above read it from the stored
+ * attention (a <= 1 with exp), which differs only for 0 < x < 2^-24, where
+ * exp(x) rounds to 1 (r04 ADVICE); the fused one-pass backward
+ * (dglhip_gat_backward_t_device) has x and uses its sign too. Dropout: the hash
+ * keep bits when drop_p > 0 (attn_drop must then be NULL), else attn_drop != 0
+ * with drop_scale when attn_drop is given. grad_rowsum, dz may be NULL. */
+int dglhip_gat_attention_grad_logits_ranges_device(
+    int64_t num_rows, int64_t feat_len, int64_t num_heads, const int64_t* row_beg,
+    const int64_t* row_end, const int32_t* row_order, const int32_t* indices,
+    const float* dout, const float* ft, const float* attn, const float* attn_drop,
+    const float* dz, const float* el, const float* er, float alpha, float clamp_lo,
+    float clamp_hi, int apply_exp, float drop_scale, float drop_p, uint64_t seed,
+    const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream);
+
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
  * attention positions stay the CSR's); with accumulate != 0 both chains

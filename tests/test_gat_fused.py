@@ -444,3 +444,96 @@ def test_transposed_backward_without_er_grad():
         assert (er.grad is not None) == er_grad
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+def _tiny_logit_graph(n=96, seed=5):
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, n, 6 * n)
+    dst = rng.integers(0, n, 6 * n)
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+    return g, src, dst
+
+
+def _torch64_reference(src, dst, n, ft, el, er, alpha, lo, hi, R, S):
+    """The layer in float64 torch ops (leaky_relu's own backward): the slope
+    alpha where x <= 0, 1 where x > 0, however small."""
+    ft, el, er = (t.detach().double().cpu().requires_grad_(True) for t in (ft, el, er))
+    s, d = torch.from_numpy(src), torch.from_numpy(dst)
+    a = torch.clamp(torch.exp(F.leaky_relu(el[s] + er[d], alpha)), lo, hi)
+    fs = torch.zeros(n, *ft.shape[1:], dtype=torch.float64).index_add(0, d, a.unsqueeze(-1) * ft[s])
+    z = torch.zeros(n, el.shape[1], dtype=torch.float64).index_add(0, d, a)
+    loss = (fs * R.double().cpu()).sum() + (z * S.double().cpu().squeeze(-1)).sum()
+    return torch.autograd.grad(loss, (ft, el, er))
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("H,D", [(8, 16), (2, 5)])
+@pytest.mark.parametrize("bwd", ["auto", "three"])
+def test_slope_from_the_logit_sign(device, H, D, bwd):
+    """logits of exactly 0 and just above 0 (0 < x < 2^-24, where
+    exp(x) rounds to 1). torch's leaky_relu backward takes slope 1 for any
+    x > 0 and alpha for x <= 0; every GAT backward (the fused one-pass kernel,
+    the three-pass kernels, the host path) now takes it from x = el[u] + er[v]
+    itself, so the gradients match float64 torch within 1e-5 of the terms'
+    magnitude — with a slope read from a <= 1 the tiny positive logits' pairs
+    would be off by the factor 1 / alpha = 5."""
+    dev = _dev(device)
+    g, src, dst = _tiny_logit_graph()
+    n = g.number_of_nodes()
+    adj = g.sparse_adjacency(dev)
+    gen = torch.Generator().manual_seed(11)
+    ft = torch.randn(n, H, D, generator=gen)
+    # x = el[u] + 0: exactly 0, tiny positive (exp rounds to 1), tiny negative,
+    # ordinary values
+    choice = torch.tensor([0.0, 1e-8, 3e-8, -1e-8, 0.5, -0.5])
+    el = choice[torch.randint(0, 6, (n, H), generator=gen)]
+    er = torch.zeros(n, H)
+    R = torch.randn(n, H, D, generator=gen)
+    S = torch.randn(n, H, 1, generator=gen)
+    ft, el, er = (t.to(dev).requires_grad_(True) for t in (ft, el, er))
+    old = kernel.set_gat_backward(bwd)
+    try:
+        fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, clamp=(-10.0, 10.0))
+        got = torch.autograd.grad((fs * R.to(dev)).sum() + (z * S.to(dev)).sum(), (ft, el, er))
+    finally:
+        kernel.set_gat_backward(old)
+    ref = _torch64_reference(src, dst, n, ft, el, er, 0.2, -10.0, 10.0, R, S)
+    # magnitude of each gradient's terms: |a| <= e^0.5, |R|, |S|, |ft|
+    for x, r in zip(got, ref):
+        scale = r.abs() + 1.0
+        err = (x.double().cpu() - r).abs()
+        assert bool((err <= 1e-5 * 6 * scale * 8).all()), float(err.max())
+    # the tiny positive logits are where the old slope differed: el's gradient
+    # at those sources carries slope 1
+    pos = (el.detach().cpu() > 0) & (el.detach().cpu() < 1e-7)
+    assert bool(pos.any())
+    assert torch.allclose(got[1].cpu()[pos].double(), ref[1][pos], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("order", ["eid", "slot"])
+def test_edge_attention_slope_from_the_logit_sign(device, order):
+    """The same for kernel.edge_attention's backward (eid and slot order)."""
+    dev = _dev(device)
+    g, src, dst = _tiny_logit_graph()
+    n, E = g.number_of_nodes(), g.number_of_edges()
+    adj = g.sparse_adjacency(dev)
+    gen = torch.Generator().manual_seed(12)
+    choice = torch.tensor([0.0, 1e-8, -1e-8, 0.5])
+    el = choice[torch.randint(0, 4, (n, 4), generator=gen)].to(dev).requires_grad_(True)
+    er = torch.zeros(n, 4, device=dev, requires_grad=True)
+    a = kernel.edge_attention(adj, el, er, E, 0.2, clamp=(-10.0, 10.0), edge_order=order)
+    W = torch.randn(E, 4, generator=gen)
+    got = torch.autograd.grad((a * W.to(dev)).sum(), (el, er))
+    if order == "slot":  # forward slot order: the CSR's (dst-major) order of the edges
+        fwd = adj.fwd
+        s64 = fwd.indices.long().cpu()
+        d64 = fwd.row_ids().cpu()
+    else:
+        s64, d64 = torch.from_numpy(src), torch.from_numpy(dst)
+    el64 = el.detach().double().cpu().requires_grad_(True)
+    er64 = er.detach().double().cpu().requires_grad_(True)
+    a64 = torch.clamp(torch.exp(F.leaky_relu(el64[s64] + er64[d64], 0.2)), -10.0, 10.0)
+    ref = torch.autograd.grad((a64 * W.double()).sum(), (el64, er64))
+    for x, r in zip(got, ref):
+        assert bool(((x.double().cpu() - r).abs() <= 1e-5 * (r.abs() + 1.0) * 8).all())
