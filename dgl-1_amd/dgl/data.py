@@ -68,7 +68,7 @@ def reddit_like(scale=1, seed=0, device="cpu", self_loops=True):
     ``scale`` multiplies nodes and edges (weak-scaling family: scale = number
     of GPUs); scale=1 is the Reddit-shaped graph of BASELINE.json configs[1].
     """
-    return chung_lu(REDDIT_NODES * scale, REDDIT_EDGES * scale, REDDIT_MAX_OVER_MEAN,
+    return chung_lu(int(REDDIT_NODES * scale), int(REDDIT_EDGES * scale), REDDIT_MAX_OVER_MEAN,
                     seed, device, self_loops)
 
 

@@ -7,7 +7,7 @@ export HSA_ENABLE_IPC_MODE_LEGACY=0
 O=gpurun_out/r05
 # (gat pack A/B done in the first run of this script)
 
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?; tail -5 $O/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || exit $?
 tail -2 $O/smoke.log
