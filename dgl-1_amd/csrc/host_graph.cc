@@ -400,6 +400,92 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks, int64_t 
   API_END();
 }
 
+int dglhip_distmult_score_host(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                               int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                               const int64_t* obj, const float* h, const float* w_rel,
+                               float* score, int num_threads) {
+#pragma clang fp contract(off)
+  API_BEGIN();
+  DGLHIP_CHECK(num_samples >= 0 && feat_len >= 0 && num_nodes >= 0 && num_rels >= 0,
+               "bad sizes");
+  if (num_samples == 0) return 0;
+  DGLHIP_CHECK(subj && rel && obj && h && w_rel && score, "null pointer argument");
+  const int64_t F = feat_len;
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  parallel_for(num_samples, nt, [&](int64_t b0, int64_t b1, int) {
+    float lane[64];
+    for (int64_t i = b0; i < b1; ++i) {
+      const int64_t si = subj[i], ri = rel[i], oi = obj[i];
+      if (si < 0 || si >= num_nodes || oi < 0 || oi >= num_nodes || ri < 0 || ri >= num_rels) {
+        score[i] = std::nanf("");
+        continue;
+      }
+      const float *a = h + si * F, *b = w_rel + ri * F, *c = h + oi * F;
+      // the device kernel's association: 64 lane chains, then a xor butterfly
+      for (int l = 0; l < 64; ++l) {
+        float acc = 0.0f;
+        for (int64_t f = l; f < F; f += 64) {
+          const float ab = a[f] * b[f];
+          const float t = ab * c[f];
+          acc = acc + t;
+        }
+        lane[l] = acc;
+      }
+      for (int off = 32; off > 0; off >>= 1) {
+        float nxt[64];
+        for (int l = 0; l < 64; ++l) nxt[l] = lane[l] + lane[l ^ off];
+        for (int l = 0; l < 64; ++l) lane[l] = nxt[l];
+      }
+      score[i] = lane[0];
+    }
+  });
+  API_END();
+}
+
+int dglhip_distmult_grad_host(int task, int64_t num_rows, int64_t feat_len, int64_t num_samples,
+                              int64_t num_nodes, int64_t num_rels, const int64_t* ptr,
+                              const int32_t* order, const int64_t* subj, const int64_t* rel,
+                              const int64_t* obj, const float* dscore, const float* h,
+                              const float* w_rel, float* out, int num_threads) {
+#pragma clang fp contract(off)
+  API_BEGIN();
+  DGLHIP_CHECK(task == 0 || task == 1, "unknown DistMult gradient task " << task);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 0 && num_samples >= 0, "bad sizes");
+  if (num_rows == 0 || feat_len == 0) return 0;
+  DGLHIP_CHECK(ptr && out, "null pointer argument");
+  DGLHIP_CHECK(num_samples == 0 || (order && subj && rel && obj && dscore && h && w_rel),
+               "null pointer argument");
+  const int64_t F = feat_len, n = num_samples;
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  typed_chunked_rows(num_rows, F, ptr, out, nt, [&](int64_t k0, int64_t k1, float* o) {
+    for (int64_t k = k0; k < k1; ++k) {
+      const int64_t p = order[k];
+      const bool objp = task == 0 && p >= n;
+      const int64_t i = objp ? p - n : p;
+      const int64_t si = subj[i], ri = rel[i], oi = obj[i];
+      if (si < 0 || si >= num_nodes || oi < 0 || oi >= num_nodes || ri < 0 || ri >= num_rels) {
+        for (int64_t f = 0; f < F; ++f) o[f] = std::nanf("");
+        continue;
+      }
+      const float d = dscore[i];
+      const float* x = objp ? h + si * F : h + oi * F;
+      const float* y = task == 1 ? h + si * F : w_rel + ri * F;
+      for (int64_t f = 0; f < F; ++f) {
+        float t;
+        if (objp) {
+          const float xy = x[f] * y[f];
+          t = d * xy;
+        } else {
+          const float dx = d * x[f];
+          t = dx * y[f];
+        }
+        o[f] = o[f] + t;
+      }
+    }
+  });
+  API_END();
+}
+
 int dglhip_gsddmm_attention_host(int64_t num_rows, int64_t num_heads, const int64_t* indptr,
                                  const int32_t* indices, const int64_t* eid, const float* lhs,
                                  const float* rhs, float alpha, float clamp_lo,

@@ -221,6 +221,94 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
   (single ? dw + r * wr : partial + it * wr)[rem] = acc;
 }
 
+// DistMult decoder (R-GCN link prediction, the reference's calc_score:
+// examples/pytorch/rgcn/link_predict.py:50-55, s = h[s] * w_rel[r] * h[o],
+// score = s.sum(1)). One wave per sample: lane l takes features l, l + 64, ...
+// (acc + (a * b) * c in feature order), then a xor butterfly over the 64
+// lanes. The host entry emulates exactly that association. Indices out of
+// range give a NaN score (no host sync to check them; no read out of bounds).
+__global__ __launch_bounds__(256) void distmult_score_kernel(
+    int64_t n, int64_t F, int64_t num_nodes, int64_t num_rels, const int64_t* __restrict__ s,
+    const int64_t* __restrict__ r, const int64_t* __restrict__ o, const float* __restrict__ h,
+    const float* __restrict__ w, float* __restrict__ score) {
+#pragma clang fp contract(off)
+  const int64_t i = block_linear() * 4 +
+                    __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t si = s[i], ri = r[i], oi = o[i];
+  if (si < 0 || si >= num_nodes || oi < 0 || oi >= num_nodes || ri < 0 || ri >= num_rels) {
+    if (lane == 0) score[i] = __builtin_nanf("");
+    return;
+  }
+  const float* a = h + si * F;
+  const float* b = w + ri * F;
+  const float* c = h + oi * F;
+  float acc = 0.0f;
+  for (int64_t f = lane; f < F; f += 64) acc = acc + (a[f] * b[f]) * c[f];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+  if (lane == 0) score[i] = acc;
+}
+
+// The decoder's gradients as chains over positions grouped by target row
+// (kernel._DistMult: a stable sort of the index array, rows cut into
+// DGLHIP_TYPED_CHUNK-slot items, partials combined in order), each position's
+// term computed as torch's autograd of (h[s] * w[r]) * h[o] computes it:
+//   task 0 (dh, positions p in [0, 2n)): p < n, subject of sample p:
+//            (ds * h[o]) * w[r];  p >= n, object of sample p - n: ds * (h[s] * w[r])
+//   task 1 (dw, positions p in [0, n)): (ds * h[o]) * h[s]
+// chained acc + term in position order: the bits of kernel.gather_rows'
+// backward over those terms (the decoder before r05). One wave per (item,
+// 64-feature slice).
+__global__ __launch_bounds__(256) void distmult_grad_kernel(
+    int task, int64_t num_items, int64_t num_rows, int64_t npass, int64_t F, int64_t n,
+    int64_t num_nodes, int64_t num_rels, const int64_t* __restrict__ ptr,
+    const int64_t* __restrict__ item_ptr, const int32_t* __restrict__ item_row,
+    const int32_t* __restrict__ order, const int64_t* __restrict__ s,
+    const int64_t* __restrict__ r, const int64_t* __restrict__ o,
+    const float* __restrict__ ds, const float* __restrict__ h, const float* __restrict__ w,
+    float* __restrict__ out, float* __restrict__ partial) {
+#pragma clang fp contract(off)
+  constexpr int G = 8;
+  const int64_t wave = block_linear() * 4 +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t it = wave / npass, pass = wave - it * npass;
+  if (it >= num_items) return;
+  int64_t row, beg, end;
+  bool single;
+  if (!item_range(it, num_rows, ptr, item_ptr, item_row, &row, &beg, &end, &single)) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t f = pass * 64 + lane;
+  const bool active = f < F;
+  const int64_t fc = active ? f : 0;
+  float acc = 0.0f;
+  for (int64_t k = beg; k < end; k += G) {
+    const int64_t cnt = end - k;
+    float x[G], y[G], d[G];
+    bool first[G];
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      const int64_t p = order[q < cnt ? k + q : end - 1];
+      const bool obj = task == 0 && p >= n;
+      const int64_t i = obj ? p - n : p;
+      int64_t si = s[i], ri = r[i], oi = o[i];
+      const bool ok = si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes && ri >= 0 &&
+                      ri < num_rels;
+      if (!ok) si = oi = ri = 0;
+      d[q] = ok ? ds[i] : __builtin_nanf("");
+      first[q] = !obj;
+      // subject / relation terms: (ds * h[o]) * (w[r] or h[s]); object: ds * (h[s] * w[r])
+      x[q] = obj ? h[si * F + fc] : h[oi * F + fc];
+      y[q] = task == 1 ? h[si * F + fc] : w[ri * F + fc];
+    }
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      if (q < cnt) acc = acc + (first[q] ? (d[q] * x[q]) * y[q] : d[q] * (x[q] * y[q]));
+  }
+  if (active) (single ? out + row * F : partial + it * F)[f] = acc;
+}
+
 }  // namespace
 }  // namespace dglhip
 
@@ -306,6 +394,57 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
                          stream, num_heavy, wr, heavy_rel, item_ptr, partial, dweight);
     });
   }
+  API_END();
+}
+
+int dglhip_distmult_score_device(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                                 int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                                 const int64_t* obj, const float* h, const float* w_rel,
+                                 float* score, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_samples >= 0 && feat_len >= 0 && num_nodes >= 0 && num_rels >= 0,
+               "bad sizes");
+  if (num_samples == 0) return 0;
+  DGLHIP_CHECK(subj && rel && obj && h && w_rel && score, "null pointer argument");
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(distmult_score_kernel, grid_1d((num_samples + 3) / 4), dim3(256), 0,
+                       stream, num_samples, feat_len, num_nodes, num_rels, subj, rel, obj, h,
+                       w_rel, score);
+  });
+  API_END();
+}
+
+int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, int64_t feat_len,
+                                int64_t num_samples, int64_t num_nodes, int64_t num_rels,
+                                const int64_t* ptr, const int64_t* item_ptr,
+                                const int32_t* item_row, const int32_t* order,
+                                const int64_t* subj, const int64_t* rel, const int64_t* obj,
+                                const float* dscore, const float* h, const float* w_rel,
+                                float* out, float* partial, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(task == 0 || task == 1, "unknown DistMult gradient task " << task);
+  DGLHIP_CHECK(num_rows >= 0 && num_items >= 0 && feat_len >= 0 && num_samples >= 0,
+               "bad sizes");
+  if (num_rows == 0 || feat_len == 0) return 0;
+  DGLHIP_CHECK(ptr && item_ptr && item_row && out && partial, "null pointer argument");
+  DGLHIP_CHECK(num_samples == 0 || (order && subj && rel && obj && dscore && h && w_rel),
+               "null pointer argument");
+  const int64_t npass = (feat_len + 63) / 64;
+  const int64_t waves = num_items * npass;
+  DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(distmult_grad_kernel, grid_1d((waves + 3) / 4), dim3(256), 0, stream,
+                       task, num_items, num_rows, npass, feat_len, num_samples, num_nodes,
+                       num_rels, ptr, item_ptr, item_row, order, subj, rel, obj, dscore, h,
+                       w_rel, out, partial);
+  });
+  const int64_t total = num_rows * feat_len;
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                       stream, num_rows, feat_len, nullptr, item_ptr, partial, out);
+  });
   API_END();
 }
 

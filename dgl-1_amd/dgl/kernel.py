@@ -1426,6 +1426,85 @@ def gather_rows(x, idx):
 TYPED_CHUNK = 64  # DGLHIP_TYPED_CHUNK: slots per chain of the typed-block kernels
 
 
+def _position_groups(idx, num_rows):
+    """Positions of ``idx`` grouped by row in increasing position (a stable
+    sort; counts by an integer scatter-add; no host sync): (ptr int64[R+1],
+    order int32[m])."""
+    order = torch.sort(idx, stable=True)[1].to(torch.int32)
+    counts = torch.zeros(num_rows, dtype=torch.int64, device=idx.device).scatter_add_(
+        0, idx, torch.ones_like(idx))
+    ptr_ = torch.zeros(num_rows + 1, dtype=torch.int64, device=idx.device)
+    torch.cumsum(counts, 0, out=ptr_[1:])
+    return ptr_, order
+
+
+class _DistMult(torch.autograd.Function):
+    """score[i] = sum_f (h[s_i] * w[r_i] * h[o_i])_f in one kernel (no
+    [n, F] gathers or products), and its gradients as ordered chains per node
+    and relation (dglhip_distmult_*): each position's term as torch's autograd
+    of the three-way product computes it, chained as gather_rows' backward
+    chains them, so dh and dw carry the bits of the torch formulation
+    ``gather_rows(h, s) * gather_rows(w, r) * gather_rows(h, o)`` with its
+    duplicates summed by gather_rows; the score's sum runs in the kernel's
+    order (lane chains + butterfly) instead of torch's."""
+
+    @staticmethod
+    def forward(ctx, h, w, s, r, o):
+        n, F = s.numel(), h.shape[1]
+        score = torch.empty(n, dtype=torch.float32, device=h.device)
+        args = (n, F, h.shape[0], w.shape[0], ptr(s), ptr(r), ptr(o), ptr(h), ptr(w), ptr(score))
+        if h.is_cuda:
+            check_call(LIB.dglhip_distmult_score_device(*(args + (_stream_of(h.device),))))
+        else:
+            check_call(LIB.dglhip_distmult_score_host(*(args + (0,))))
+        ctx.save_for_backward(h, w, s, r, o)
+        return score
+
+    @staticmethod
+    def backward(ctx, dscore):
+        h, w, s, r, o = ctx.saved_tensors
+        ds = _f32c(dscore.reshape(-1))
+        n, F = s.numel(), h.shape[1]
+        grads = [None, None]
+        for task, (need, rows, idx) in enumerate(
+                ((ctx.needs_input_grad[0], h.shape[0], lambda: torch.cat([s, o])),
+                 (ctx.needs_input_grad[1], w.shape[0], lambda: r))):
+            if not need:
+                continue
+            ix = idx()
+            ptr_, order = _position_groups(ix, rows)
+            out = torch.empty(rows, F, dtype=torch.float32, device=h.device)
+            common = (n, h.shape[0], w.shape[0])
+            tail = (ptr(order), ptr(s), ptr(r), ptr(o), ptr(ds), ptr(h), ptr(w), ptr(out))
+            if h.is_cuda:
+                item_ptr, item_row = _typed_items(ptr_, ix.numel())
+                part = torch.empty(item_row.numel(), F, dtype=torch.float32, device=h.device)
+                check_call(LIB.dglhip_distmult_grad_device(
+                    task, rows, item_row.numel(), F, *common, ptr(ptr_), ptr(item_ptr),
+                    ptr(item_row), *tail, ptr(part), _stream_of(h.device)))
+            else:
+                check_call(LIB.dglhip_distmult_grad_host(task, rows, F, *common, ptr(ptr_),
+                                                         *tail, 0))
+            grads[task] = out
+        return grads[0], grads[1], None, None, None
+
+
+def distmult_score(h, w_rel, subj, rel, obj):
+    """DistMult scores of (subj, rel, obj) triples over node embeddings ``h``
+    and relation vectors ``w_rel`` (the reference's calc_score,
+    examples/pytorch/rgcn/link_predict.py:50-55) in one kernel; differentiable
+    in h and w_rel with deterministic gradients (see _DistMult). Indices out of
+    range give NaN scores."""
+    dev = h.device
+    idx = [t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
+           for t in (subj, rel, obj)]
+    if not (idx[0].numel() == idx[1].numel() == idx[2].numel()):
+        raise DGLError("distmult_score: subj, rel, obj lengths differ")
+    if w_rel.shape[1:] != h.shape[1:] or h.dim() != 2:
+        raise DGLError("distmult_score: h and w_rel must be 2-D of one width")
+    return _DistMult.apply(_f32c(h), _f32c(w_rel), *idx)
+
+
 def _typed_items(ptr, nnz):
     """The typed-block kernels' work items over a CSR-like ``ptr`` with
     ``nnz`` slots, built on the device with no host sync (cached by the

@@ -124,15 +124,15 @@ class LinkPredict(nn.Module):
         return h
 
     def loss(self, h, samples, labels):
-        # DistMult (the reference's calc_score); the fused model gathers the
-        # rows with a deterministic chunked backward (kernel.gather_rows)
+        # DistMult (the reference's calc_score); the fused model scores the
+        # triples in one kernel with deterministic chained gradients
+        # (kernel.distmult_score: no [samples, 500] gathers or products)
         if self.udf:
             s = h[samples[:, 0]] * self.w_relation[samples[:, 1]] * h[samples[:, 2]]
+            score = s.sum(1)
         else:
-            n = samples.shape[0]
-            ho = kernel.gather_rows(h, torch.cat([samples[:, 0], samples[:, 2]]))
-            s = ho[:n] * kernel.gather_rows(self.w_relation, samples[:, 1]) * ho[n:]
-        score = s.sum(1)
+            score = kernel.distmult_score(h, self.w_relation, samples[:, 0], samples[:, 1],
+                                          samples[:, 2])
         reg = h.pow(2).mean() + self.w_relation.pow(2).mean()
         return F.binary_cross_entropy_with_logits(score, labels) + self.reg * reg
 

@@ -786,6 +786,43 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
                                   const float* ufeat, const float* dout, float* dweight,
                                   int num_threads);
 
+/* DistMult decoder of R-GCN link prediction (the reference's calc_score,
+ * examples/pytorch/rgcn/link_predict.py:50-55: s = h[subj] * w_rel[rel] *
+ * h[obj], score = s.sum(1)), with no [num_samples, F] tensor in between.
+ * score[i] = sum_f (h[subj[i], f] * w_rel[rel[i], f]) * h[obj[i], f]: 64 lane
+ * chains over f = l, l + 64, ... then a xor butterfly (the host entry runs the
+ * same association). Indices outside [0, num_nodes) / [0, num_rels) give NaN. */
+int dglhip_distmult_score_device(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                                 int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                                 const int64_t* obj, const float* h, const float* w_rel,
+                                 float* score, void* stream);
+int dglhip_distmult_score_host(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                               int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                               const int64_t* obj, const float* h, const float* w_rel,
+                               float* score, int num_threads);
+/* Its gradients from dscore[num_samples], deterministic: out[row] = the chain
+ * acc + term over the row's positions in ptr / order (a stable grouping of an
+ * index array by row, cut into DGLHIP_TYPED_CHUNK-position items combined in
+ * order, item_ptr / item_row as the typed-block entries; partial =
+ * num_items x feat_len floats of workspace). Terms, as torch's autograd of
+ * (h[subj] * w_rel[rel]) * h[obj]:
+ *   task 0, rows = nodes, positions p in [0, 2 num_samples) over cat(subj, obj):
+ *     p < n: (dscore[p] * h[obj[p]]) * w_rel[rel[p]];
+ *     p >= n: dscore[i] * (h[subj[i]] * w_rel[rel[i]]), i = p - n;
+ *   task 1, rows = relations, positions i over rel: (dscore[i] * h[obj[i]]) * h[subj[i]]. */
+int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, int64_t feat_len,
+                                int64_t num_samples, int64_t num_nodes, int64_t num_rels,
+                                const int64_t* ptr, const int64_t* item_ptr,
+                                const int32_t* item_row, const int32_t* order,
+                                const int64_t* subj, const int64_t* rel, const int64_t* obj,
+                                const float* dscore, const float* h, const float* w_rel,
+                                float* out, float* partial, void* stream);
+int dglhip_distmult_grad_host(int task, int64_t num_rows, int64_t feat_len, int64_t num_samples,
+                              int64_t num_nodes, int64_t num_rels, const int64_t* ptr,
+                              const int32_t* order, const int64_t* subj, const int64_t* rel,
+                              const int64_t* obj, const float* dscore, const float* h,
+                              const float* w_rel, float* out, int num_threads);
+
 /* ------------------------------------------------------------------------ */
 /* Kernel timing (measurement support for bench.py): when enabled, every     */
 /* g-SpMM launch is bracketed by a pair of hipEvents on its own stream.     */

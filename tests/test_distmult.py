@@ -1,0 +1,105 @@
+"""The fused DistMult decoder (kernel.distmult_score, csrc/typed_block.hip):
+R-GCN link prediction's score (the reference's calc_score,
+examples/pytorch/rgcn/link_predict.py:50-55, s = h[s] * w[r] * h[o],
+score = s.sum(1)) in one kernel, and its gradients as ordered chains.
+
+* gradients: the bits of the torch formulation the fused model used before
+  (gather_rows(h, cat(s, o)) split, times gather_rows(w, r), its duplicates
+  summed by gather_rows' chains) — every term and chain is the same;
+* scores: within 1e-6 of that formulation's (the sum runs in the kernel's
+  lane-chain + butterfly order, not torch's) and of float64;
+* host = device bit for bit; out-of-range indices give NaN, not a fault.
+"""
+import numpy as np
+import pytest
+import torch
+
+import dgl
+from dgl import kernel
+
+DEVICES = ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)]
+
+
+def _dev(device):
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    return torch.device(device)
+
+
+def _case(N=700, R=40, F=500, n=3000, seed=0, hub=True):
+    gen = torch.Generator().manual_seed(seed)
+    h = torch.randn(N, F, generator=gen)
+    w = torch.randn(R, F, generator=gen)
+    s = torch.randint(0, N, (n,), generator=gen)
+    o = torch.randint(0, N, (n,), generator=gen)
+    r = torch.randint(0, R, (n,), generator=gen)
+    if hub:  # a hub entity and relation of > DGLHIP_TYPED_CHUNK positions
+        s[::7] = 3
+        r[::5] = 1
+    return h, w, s, r, o
+
+
+def _torch_form(h, w, s, r, o):
+    n = s.numel()
+    ho = kernel.gather_rows(h, torch.cat([s, o]))
+    return (ho[:n] * kernel.gather_rows(w, r) * ho[n:]).sum(1)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("F", [500, 64, 37])
+def test_distmult_grads_bits_of_the_torch_form(device, F):
+    dev = _dev(device)
+    h, w, s, r, o = (t.to(dev) for t in _case(F=F))
+    h1, w1 = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    h2, w2 = h.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    sc = kernel.distmult_score(h1, w1, s, r, o)
+    ref = _torch_form(h2, w2, s, r, o)
+    exact = (h.double()[s] * w.double()[r] * h.double()[o]).sum(1)
+    mag = (h.double()[s] * w.double()[r] * h.double()[o]).abs().sum(1)
+    assert ((sc.double() - exact).abs() <= 1e-6 * mag + 1e-30).all()
+    assert ((ref.double() - exact).abs() <= 1e-6 * mag + 1e-30).all()
+    dsc = torch.randn(s.numel(), generator=torch.Generator().manual_seed(3)).to(dev)
+    g1 = torch.autograd.grad(sc, (h1, w1), dsc)
+    g2 = torch.autograd.grad(ref, (h2, w2), dsc)
+    assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
+
+
+@pytest.mark.parametrize("device", DEVICES)
+def test_distmult_only_one_grad_and_empty(device):
+    dev = _dev(device)
+    h, w, s, r, o = (t.to(dev) for t in _case(n=500, hub=False))
+    h1 = h.clone().requires_grad_(True)
+    (dh,) = torch.autograd.grad(kernel.distmult_score(h1, w, s, r, o).sum(), (h1,))
+    h2 = h.clone().requires_grad_(True)
+    (dh2,) = torch.autograd.grad(_torch_form(h2, w, s, r, o).sum(), (h2,))
+    assert torch.equal(dh, dh2)
+    e = torch.empty(0, dtype=torch.int64, device=dev)
+    h3 = h.clone().requires_grad_(True)
+    sc = kernel.distmult_score(h3, w, e, e, e)
+    assert sc.shape == (0,)
+    (dh3,) = torch.autograd.grad(sc.sum(), (h3,), allow_unused=True)
+    assert dh3 is None or not dh3.any()
+
+
+def test_distmult_out_of_range_is_nan():
+    h, w, s, r, o = _case(n=10, hub=False)
+    s[4] = h.shape[0]
+    r[6] = -1
+    sc = kernel.distmult_score(h, w, s, r, o)
+    assert torch.isnan(sc[4]) and torch.isnan(sc[6])
+    assert torch.isfinite(sc[[0, 1, 2, 3, 5, 7, 8, 9]]).all()
+
+
+@pytest.mark.gpu
+def test_distmult_host_equals_device():
+    dev = _dev("cuda")
+    h, w, s, r, o = _case()
+    dsc = torch.randn(s.numel(), generator=torch.Generator().manual_seed(4))
+    res = []
+    for d in (torch.device("cpu"), dev):
+        hh, ww = h.to(d).requires_grad_(True), w.to(d).requires_grad_(True)
+        sc = kernel.distmult_score(hh, ww, s.to(d), r.to(d), o.to(d))
+        g = torch.autograd.grad(sc, (hh, ww), dsc.to(d))
+        res.append([sc.detach().cpu(), g[0].cpu(), g[1].cpu()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
