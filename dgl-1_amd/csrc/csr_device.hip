@@ -65,8 +65,10 @@ __global__ void fill_indptr(int64_t nnz, int64_t num_rows,
                             int64_t* __restrict__ indptr) {
   for (int64_t k = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; k < nnz;
        k += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t cur = row[eid[k]];
-    const int64_t prev = k == 0 ? -1 : row[eid[k - 1]];
+    // rows clamped to [-1, num_rows]: an unvalidated out-of-range row gives a
+    // wrong CSR, never a store outside indptr
+    const int64_t cur = min(max(row[eid[k]], int64_t(-1)), num_rows);
+    const int64_t prev = k == 0 ? -1 : min(max(row[eid[k - 1]], int64_t(-1)), num_rows);
     for (int64_t r = prev + 1; r <= cur; ++r) indptr[r] = k;
     if (k == nnz - 1)
       for (int64_t r = cur + 1; r <= num_rows; ++r) indptr[r] = nnz;

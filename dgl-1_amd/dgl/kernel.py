@@ -374,9 +374,24 @@ class CSR(object):
     def row_ids(self):
         """Row id of every slot (COO expansion), cached."""
         if self._row_ids is None:
+            # output_size: no host sync for the total
             self._row_ids = torch.repeat_interleave(
-                torch.arange(self.num_rows, device=self.device), self.degrees())
+                torch.arange(self.num_rows, device=self.device), self.degrees(),
+                output_size=self.nnz)
         return self._row_ids
+
+
+_PINNED_UPLOAD_MAX = 64 << 20
+
+
+def _upload(t, device):
+    """``t`` on ``device``; a small host tensor goes through pinned memory
+    without blocking the host (a pageable copy waits for the stream's queued
+    work: every sampled graph of an R-GCN step paid that wait)."""
+    if (t.device.type == "cpu" and device.type == "cuda" and
+            t.numel() * t.element_size() <= _PINNED_UPLOAD_MAX):
+        return t.contiguous().pin_memory().to(device, non_blocking=True)
+    return t.to(device)
 
 
 def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedule=True,
@@ -399,8 +414,8 @@ def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedu
         raise DGLError("row/col length mismatch: %d vs %d" % (nnz, col.numel()))
     device = torch.device(device) if device is not None else row.device
     if device.type == "cuda":
-        row = row.to(device).contiguous()
-        col = col.to(device).contiguous()
+        row = _upload(row, device).contiguous()
+        col = _upload(col, device).contiguous()
         if nnz and validate:
             b = torch.stack([row.min(), col.min(), row.max(), col.max()]).cpu().tolist()
             if min(b[0], b[1]) < 0 or b[2] >= num_rows or b[3] >= num_cols:
