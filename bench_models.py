@@ -240,7 +240,7 @@ def gat_pubmed_leg(dev, kernel, gather_peak, epochs=20, warmup=3, cpu=True):
         m = gat.GAT(g, 1, data.features.shape[1], 8, data.num_labels, [8, 8], F.elu, 0.6, 0.6,
                     0.2, False, udf).to(device)
         return m, torch.optim.Adam(m.parameters(), lr=0.005, weight_decay=5e-4,
-                                   capturable=capturable)
+                                   capturable=capturable, fused=device.type == "cuda")
     model, opt = build(dev)
     model.train()
     feats, labels = data.features, data.labels

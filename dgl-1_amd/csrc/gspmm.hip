@@ -112,16 +112,37 @@ __global__ __launch_bounds__(256) void gsddmm_dot_kernel(
   const int lane = threadIdx.x & 63;
   const float* a = lhs + wave * F;
   const int64_t D = F / H;
-  for (int64_t k = row_beg[wave]; k < row_end[wave]; ++k) {
-    const int64_t col = indices[k];
-    const float* c = rhs + col * F;
-    if (H == 1) {
+  const int64_t kb = row_beg[wave], ke = row_end[wave];
+  if (H == 1) {
+    for (int64_t k = kb; k < ke; ++k) {
+      const int64_t col = indices[k];
+      const float* c = rhs + col * F;
       float acc = 0.0f;
       for (int64_t f = lane; f < F; f += 64) acc = __builtin_fmaf(a[f], c[f], acc);
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
       if (lane == 0) out[eid ? eid[k] : k] = EPI ? gat_epi(epi, acc, k, 1, 0, wave, col) : acc;
-    } else {
+    }
+  } else if (H <= 64) {
+    // 64 / H slots at a time, lane (sub, h) taking head h of slot k0 + sub:
+    // the same per-head chain, 64 / H times the slots in flight (r05: the
+    // GAT output layer's 8 heads x 3 ran one slot per step on 8 lanes)
+    const int64_t S = 64 / H;
+    const int64_t sub = lane / H, h = lane - sub * H;
+    for (int64_t k0 = kb; k0 < ke; k0 += S) {
+      const int64_t k = k0 + sub;
+      if (sub < S && k < ke) {
+        const int64_t col = indices[k];
+        const float* c = rhs + col * F;
+        float acc = 0.0f;
+        for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);
+        out[(eid ? eid[k] : k) * H + h] = EPI ? gat_epi(epi, acc, k, H, h, wave, col) : acc;
+      }
+    }
+  } else {
+    for (int64_t k = kb; k < ke; ++k) {
+      const int64_t col = indices[k];
+      const float* c = rhs + col * F;
       for (int64_t h = lane; h < H; h += 64) {
         float acc = 0.0f;
         for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(a[h * D + d], c[h * D + d], acc);

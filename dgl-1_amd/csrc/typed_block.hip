@@ -29,6 +29,8 @@
 // Deterministic, no atomics; the host entry points run the same chains.
 #include <hip/hip_runtime.h>
 
+#include <rocprim/device/device_scan.hpp>
+
 #include <type_traits>
 
 #include "../../include/dgl_hip.h"
@@ -252,15 +254,21 @@ __global__ __launch_bounds__(256) void distmult_score_kernel(
 }
 
 // The decoder's gradients as chains over positions grouped by target row
-// (kernel._DistMult: a stable sort of the index array, rows cut into
+// (kernel._DistMult: a stable grouping of the index array, rows cut into
 // DGLHIP_TYPED_CHUNK-slot items, partials combined in order), each position's
 // term computed as torch's autograd of (h[s] * w[r]) * h[o] computes it:
 //   task 0 (dh, positions p in [0, 2n)): p < n, subject of sample p:
 //            (ds * h[o]) * w[r];  p >= n, object of sample p - n: ds * (h[s] * w[r])
 //   task 1 (dw, positions p in [0, n)): (ds * h[o]) * h[s]
 // chained acc + term in position order: the bits of kernel.gather_rows'
-// backward over those terms (the decoder before r05). One wave per (item,
-// 64-feature slice).
+// backward over those terms (the decoder before r05).
+// One wave per (item, slice of 64 * T features). An item holds at most 64
+// positions (DGLHIP_TYPED_CHUNK), so lane q first resolves position q — its
+// sample, both operand rows, ds — in two dependent round trips for the whole
+// item; the batches then only gather rows, at row bases read from lane q
+// (wave-uniform), G positions in flight.
+static_assert(kChunk == 64, "one position per lane");
+template <int T>
 __global__ __launch_bounds__(256) void distmult_grad_kernel(
     int task, int64_t num_items, int64_t num_rows, int64_t npass, int64_t F, int64_t n,
     int64_t num_nodes, int64_t num_rels, const int64_t* __restrict__ ptr,
@@ -270,7 +278,7 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
     const float* __restrict__ ds, const float* __restrict__ h, const float* __restrict__ w,
     float* __restrict__ out, float* __restrict__ partial) {
 #pragma clang fp contract(off)
-  constexpr int G = 8;
+  constexpr int G = 4;
   const int64_t wave = block_linear() * 4 +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t it = wave / npass, pass = wave - it * npass;
@@ -279,34 +287,95 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
   bool single;
   if (!item_range(it, num_rows, ptr, item_ptr, item_row, &row, &beg, &end, &single)) return;
   const int lane = threadIdx.x & 63;
-  const int64_t f = pass * 64 + lane;
-  const bool active = f < F;
-  const int64_t fc = active ? f : 0;
-  float acc = 0.0f;
-  for (int64_t k = beg; k < end; k += G) {
-    const int64_t cnt = end - k;
-    float x[G], y[G], d[G];
-    bool first[G];
+  const int cnt = static_cast<int>(end - beg);  // <= 64, wave-uniform
+  // lane q: position beg + q resolved (operand rows as element offsets)
+  int64_t xoff = 0, yoff = 0;
+  float dq = 0.0f;
+  int objq = 0;
+  if (lane < cnt) {
+    const int64_t p = order[beg + lane];
+    const bool obj = task == 0 && p >= n;
+    const int64_t i = obj ? p - n : p;
+    const int64_t si = s[i], ri = r[i], oi = o[i];
+    const bool ok = si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes && ri >= 0 &&
+                    ri < num_rels;
+    dq = ok ? ds[i] : __builtin_nanf("");
+    objq = obj ? 1 : 0;
+    xoff = ok ? (obj ? si : oi) * F : 0;
+    yoff = ok ? (task == 1 ? si * F : ri * F) : 0;
+  }
+  const float* ybase = task == 1 ? h : w;
+  const int64_t f0 = pass * 64 * T + lane;
+  float acc[T];
 #pragma unroll
-    for (int q = 0; q < G; ++q) {
-      const int64_t p = order[q < cnt ? k + q : end - 1];
-      const bool obj = task == 0 && p >= n;
-      const int64_t i = obj ? p - n : p;
-      int64_t si = s[i], ri = r[i], oi = o[i];
-      const bool ok = si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes && ri >= 0 &&
-                      ri < num_rels;
-      if (!ok) si = oi = ri = 0;
-      d[q] = ok ? ds[i] : __builtin_nanf("");
-      first[q] = !obj;
-      // subject / relation terms: (ds * h[o]) * (w[r] or h[s]); object: ds * (h[s] * w[r])
-      x[q] = obj ? h[si * F + fc] : h[oi * F + fc];
-      y[q] = task == 1 ? h[si * F + fc] : w[ri * F + fc];
+  for (int t = 0; t < T; ++t) acc[t] = 0.0f;
+  for (int q0 = 0; q0 < cnt; q0 += G) {
+    float x[G][T], y[G][T], d[G];
+    bool ob[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int q = q0 + g < cnt ? q0 + g : cnt - 1;  // idle slots re-read a valid one
+      const int64_t xo = __shfl(xoff, q, 64), yo = __shfl(yoff, q, 64);
+      d[g] = __shfl(dq, q, 64);
+      ob[g] = __shfl(objq, q, 64) != 0;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int64_t f = f0 + 64 * t;
+        const int64_t fc = f < F ? f : 0;
+        x[g][t] = h[xo + fc];
+        y[g][t] = ybase[yo + fc];
+      }
     }
 #pragma unroll
-    for (int q = 0; q < G; ++q)
-      if (q < cnt) acc = acc + (first[q] ? (d[q] * x[q]) * y[q] : d[q] * (x[q] * y[q]));
+    for (int g = 0; g < G; ++g) {
+      if (q0 + g < cnt) {
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+          acc[t] = acc[t] + (ob[g] ? d[g] * (x[g][t] * y[g][t]) : (d[g] * x[g][t]) * y[g][t]);
+      }
+    }
   }
-  if (active) (single ? out + row * F : partial + it * F)[f] = acc;
+  float* dst = single ? out + row * F : partial + it * F;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int64_t f = f0 + 64 * t;
+    if (f < F) dst[f] = acc[t];
+  }
+}
+
+// The chunked item list (kernel._typed_items): items per row, scanned by
+// rocPRIM, then every item index's row by a binary search of item_ptr.
+__global__ __launch_bounds__(256) void typed_nitems_kernel(int64_t num_rows,
+                                                           const int64_t* __restrict__ ptr,
+                                                           int64_t* __restrict__ nit) {
+  const int64_t r = block_linear() * blockDim.x + threadIdx.x;
+  if (r >= num_rows) return;
+  const int64_t deg = ptr[r + 1] - ptr[r];
+  const int64_t c = (deg + kChunk - 1) / kChunk;
+  nit[r] = c > 1 ? c : 1;
+}
+
+__global__ __launch_bounds__(256) void typed_item_rows_kernel(
+    int64_t num_rows, int64_t bound, const int64_t* __restrict__ item_ptr,
+    int32_t* __restrict__ item_row) {
+  const int64_t j = block_linear() * blockDim.x + threadIdx.x;
+  if (j >= bound) return;
+  // the row r with item_ptr[r] <= j < item_ptr[r + 1]; num_rows past the last
+  int64_t lo = 0, hi = num_rows;  // answer in [lo, hi]
+  while (lo < hi) {
+    const int64_t mid = (lo + hi + 1) >> 1;
+    if (item_ptr[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  item_row[j] = static_cast<int32_t>(lo);
+}
+
+size_t typed_items_scan_bytes(int64_t num_rows) {
+  size_t bytes = 0;
+  HIP_CALL(rocprim::inclusive_scan(nullptr, bytes, static_cast<const int64_t*>(nullptr),
+                                   static_cast<int64_t*>(nullptr), size_t(num_rows),
+                                   rocprim::plus<int64_t>()));
+  return bytes;
 }
 
 }  // namespace
@@ -397,6 +466,50 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
   API_END();
 }
 
+int64_t dglhip_typed_items_workspace_bytes(int64_t num_rows) {
+  try {
+    if (num_rows <= 0) return 0;
+    return ((num_rows * 8 + 255) & ~int64_t(255)) + int64_t(typed_items_scan_bytes(num_rows));
+  } catch (const std::exception& e) {
+    set_last_error(e.what());
+    return -1;
+  }
+}
+
+int dglhip_typed_items_device(int64_t num_rows, const int64_t* ptr, int64_t bound,
+                              int64_t* item_ptr, int32_t* item_row, void* workspace,
+                              int64_t workspace_bytes, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && bound >= num_rows, "bad sizes");
+  DGLHIP_CHECK(item_ptr, "null pointer argument");
+  HIP_CALL(hipMemsetAsync(item_ptr, 0, sizeof(int64_t), stream));
+  if (num_rows == 0) {
+    if (bound > 0) {
+      hipLaunchKernelGGL(typed_item_rows_kernel, grid_1d((bound + 255) / 256), dim3(256), 0,
+                         stream, num_rows, bound, item_ptr, item_row);
+    }
+    return 0;
+  }
+  DGLHIP_CHECK(ptr && item_row && workspace, "null pointer argument");
+  const int64_t need = dglhip_typed_items_workspace_bytes(num_rows);
+  DGLHIP_CHECK(workspace_bytes >= need, "workspace of " << workspace_bytes << " B, "
+                                                        << need << " needed");
+  char* ws = static_cast<char*>(workspace);
+  int64_t* nit = reinterpret_cast<int64_t*>(ws);
+  const int64_t nb = (num_rows * 8 + 255) & ~int64_t(255);
+  size_t tmp = size_t(workspace_bytes - nb);
+  hipLaunchKernelGGL(typed_nitems_kernel, grid_1d((num_rows + 255) / 256), dim3(256), 0, stream,
+                     num_rows, ptr, nit);
+  HIP_CALL(hipGetLastError());
+  HIP_CALL(rocprim::inclusive_scan(ws + nb, tmp, static_cast<const int64_t*>(nit), item_ptr + 1,
+                                   size_t(num_rows), rocprim::plus<int64_t>(), stream));
+  hipLaunchKernelGGL(typed_item_rows_kernel, grid_1d((bound + 255) / 256), dim3(256), 0, stream,
+                     num_rows, bound, item_ptr, item_row);
+  HIP_CALL(hipGetLastError());
+  API_END();
+}
+
 int dglhip_distmult_score_device(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
                                  int64_t num_rels, const int64_t* subj, const int64_t* rel,
                                  const int64_t* obj, const float* h, const float* w_rel,
@@ -431,15 +544,26 @@ int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, i
   DGLHIP_CHECK(ptr && item_ptr && item_row && out && partial, "null pointer argument");
   DGLHIP_CHECK(num_samples == 0 || (order && subj && rel && obj && dscore && h && w_rel),
                "null pointer argument");
-  const int64_t npass = (feat_len + 63) / 64;
+  // features per lane: up to 8 (F = 500: one wave covers the row)
+  const int64_t lanes64 = (feat_len + 63) / 64;
+  const int T = lanes64 >= 8 ? 8 : (lanes64 >= 4 ? 4 : (lanes64 >= 2 ? 2 : 1));
+  const int64_t npass = (feat_len + 64 * T - 1) / (64 * T);
   const int64_t waves = num_items * npass;
   DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
+#define DGLHIP_DM(TT)                                                                       \
+  hipLaunchKernelGGL(distmult_grad_kernel<TT>, grid_1d((waves + 3) / 4), dim3(256), 0, stream, \
+                     task, num_items, num_rows, npass, feat_len, num_samples, num_nodes,      \
+                     num_rels, ptr, item_ptr, item_row, order, subj, rel, obj, dscore, h,     \
+                     w_rel, out, partial)
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL(distmult_grad_kernel, grid_1d((waves + 3) / 4), dim3(256), 0, stream,
-                       task, num_items, num_rows, npass, feat_len, num_samples, num_nodes,
-                       num_rels, ptr, item_ptr, item_row, order, subj, rel, obj, dscore, h,
-                       w_rel, out, partial);
+    switch (T) {
+      case 8: DGLHIP_DM(8); break;
+      case 4: DGLHIP_DM(4); break;
+      case 2: DGLHIP_DM(2); break;
+      default: DGLHIP_DM(1); break;
+    }
   });
+#undef DGLHIP_DM
   const int64_t total = num_rows * feat_len;
   timed_launch(stream, [&] {
     hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,

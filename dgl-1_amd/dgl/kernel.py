@@ -200,14 +200,18 @@ class CSR(object):
     schedule handed to the HIP kernel.
     """
 
-    def __init__(self, indptr, indices, eid, num_cols, row_order=None, host_indptr=None):
+    def __init__(self, indptr, indices, eid, num_cols, row_order=None, host_indptr=None,
+                 lazy_order=False):
         self.indptr = indptr
         self.indices = indices
         self._eid = eid
         self._eid_host = None
         self.num_rows = indptr.numel() - 1
         self.num_cols = int(num_cols)
-        self.row_order = row_order
+        self._row_order = row_order
+        # a device CSR's schedule is sorted on first use: products that never
+        # launch by rows (the typed-block items, the blocked items) skip it
+        self._lazy_order = bool(lazy_order) and row_order is None
         self._row_ids = None
         self._host_indptr = host_indptr
         self._plans = {}
@@ -216,6 +220,23 @@ class CSR(object):
         self._slot_eid = False  # not computed yet
         self._eid_loc = None
         self._native = None  # the native launch plan (built on first use)
+
+    @property
+    def row_order(self):
+        """int32[R]: rows by degree, descending, ties by row id (a stable sort:
+        the host builder's counting sort gives the same order); None when the
+        CSR was built without a schedule."""
+        if self._row_order is None and self._lazy_order:
+            self._lazy_order = False
+            if self.num_rows > 0:
+                deg = self.indptr[1:] - self.indptr[:-1]
+                self._row_order = torch.sort(deg, descending=True,
+                                             stable=True)[1].to(torch.int32)
+        return self._row_order
+
+    @row_order.setter
+    def row_order(self, value):
+        self._row_order, self._lazy_order = value, False
 
     @property
     def eid(self):
@@ -357,6 +378,9 @@ class CSR(object):
     def to(self, device):
         if self.device == torch.device(device):
             return self
+        if self._row_order is None and self._lazy_order and torch.device(device).type == "cuda":
+            return CSR(self.indptr.to(device), self.indices.to(device), self.eid.to(device),
+                       self.num_cols, None, self._host_indptr, lazy_order=True)
         ro = None if self.row_order is None else self.row_order.to(device)
         return CSR(self.indptr.to(device), self.indices.to(device), self.eid.to(device),
                    self.num_cols, ro, self._host_indptr)
@@ -433,13 +457,8 @@ def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedu
             ptr(eid), ptr(ws), int(ws_bytes), _stream_of(device)))
         del ws
         host_indptr = None  # fetched when something needs it (CSR.host_indptr)
-        row_order = None
-        if schedule and num_rows > 0:
-            # degree-descending, ties by row id (a stable sort: the host
-            # builder's counting sort gives the same order)
-            deg = indptr[1:] - indptr[:-1]
-            row_order = torch.sort(deg, descending=True, stable=True)[1].to(torch.int32)
-        return CSR(indptr, indices, eid, num_cols, row_order, host_indptr)
+        # the degree-descending schedule: sorted on the device at first use
+        return CSR(indptr, indices, eid, num_cols, None, host_indptr, lazy_order=schedule)
     else:
         row = row.cpu().contiguous()
         col = col.cpu().contiguous()
@@ -1411,11 +1430,7 @@ class _GatherRows(torch.autograd.Function):
         dev = dy2.device
         # positions grouped by row, in increasing position (a stable sort; the
         # counts by an integer scatter-add): no host sync
-        order = torch.sort(idx, stable=True)[1].to(torch.int32)
-        counts = torch.zeros(n, dtype=torch.int64, device=dev).scatter_add_(
-            0, idx, torch.ones_like(idx))
-        ptr_ = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-        torch.cumsum(counts, 0, out=ptr_[1:])
+        ptr_, order = _position_groups(idx, n)
         # the sum per row as the typed-block kernel over F blocks of 1 x 1
         # ones (fma(1, x, acc) == acc + x): chains of TYPED_CHUNK positions,
         # the chunks of a long row added in order
@@ -1442,9 +1457,17 @@ TYPED_CHUNK = 64  # DGLHIP_TYPED_CHUNK: slots per chain of the typed-block kerne
 
 
 def _position_groups(idx, num_rows):
-    """Positions of ``idx`` grouped by row in increasing position (a stable
-    sort; counts by an integer scatter-add; no host sync): (ptr int64[R+1],
-    order int32[m])."""
+    """Positions of ``idx`` grouped by row in increasing position, no host
+    sync: (ptr int64[R+1], order int32[m]). On a device, the library's CSR
+    builder over (idx, position) — an LSD radix sort, stable, and each row's
+    first slot found by the fill — instead of torch's merge sort, scatter-add
+    and scan (a quarter of the launches); the same arrays."""
+    m = idx.numel()
+    if idx.is_cuda and m:
+        pos = torch.arange(m, dtype=torch.int64, device=idx.device)
+        c = build_csr(num_rows, m, idx, pos, ORDER_EID, idx.device, schedule=False,
+                      validate=False)
+        return c.indptr, c.indices
     order = torch.sort(idx, stable=True)[1].to(torch.int32)
     counts = torch.zeros(num_rows, dtype=torch.int64, device=idx.device).scatter_add_(
         0, idx, torch.ones_like(idx))
@@ -1520,20 +1543,32 @@ def distmult_score(h, w_rel, subj, rel, obj):
     return _DistMult.apply(_f32c(h), _f32c(w_rel), *idx)
 
 
-def _typed_items(ptr, nnz):
-    """The typed-block kernels' work items over a CSR-like ``ptr`` with
+def _typed_items(rowptr, nnz):
+    """The typed-block kernels' work items over a CSR-like ``rowptr`` with
     ``nnz`` slots, built on the device with no host sync (cached by the
     caller): (item_ptr int64[R+1] — each row's first item, a row of deg slots
     having max(1, ceil(deg / TYPED_CHUNK)) items —, item_row int32[I_max],
     I_max = R + ceil(nnz / TYPED_CHUNK) >= the item count, the entries past
     the last item = R (padding the kernels skip))."""
-    R = ptr.numel() - 1
-    deg = ptr[1:] - ptr[:-1]
+    R = rowptr.numel() - 1
+    if rowptr.is_cuda:  # three launches in the library (nit, rocPRIM scan, search)
+        bound = R + -(-nnz // TYPED_CHUNK)
+        item_ptr = torch.empty(R + 1, dtype=torch.int64, device=rowptr.device)
+        item_row = torch.empty(max(bound, 1), dtype=torch.int32, device=rowptr.device)[:bound]
+        nb = LIB.dglhip_typed_items_workspace_bytes(R)
+        if nb < 0:
+            check_call(-1)
+        ws = torch.empty(max(int(nb), 1), dtype=torch.uint8, device=rowptr.device)
+        check_call(LIB.dglhip_typed_items_device(R, ptr(rowptr), bound,
+                                                 ptr(item_ptr), ptr(item_row), ptr(ws), int(nb),
+                                                 _stream_of(rowptr.device)))
+        return item_ptr, item_row
+    deg = rowptr[1:] - rowptr[:-1]
     nit = torch.clamp((deg + (TYPED_CHUNK - 1)) // TYPED_CHUNK, min=1)
-    item_ptr = torch.zeros(R + 1, dtype=torch.int64, device=ptr.device)
+    item_ptr = torch.zeros(R + 1, dtype=torch.int64, device=rowptr.device)
     torch.cumsum(nit, 0, out=item_ptr[1:])
     bound = R + -(-nnz // TYPED_CHUNK)
-    item_row = torch.searchsorted(item_ptr[1:], torch.arange(bound, device=ptr.device),
+    item_row = torch.searchsorted(item_ptr[1:], torch.arange(bound, device=rowptr.device),
                                   right=True).to(torch.int32)
     return item_ptr, item_row
 

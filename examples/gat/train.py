@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
                                 "dgl-1_amd"))
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph, kernel  # noqa: E402
+from dgl.nn.pytorch.linear import NodeLinear  # noqa: E402
 from dgl.data import load_data  # noqa: E402
 
 
@@ -44,7 +45,10 @@ class GraphAttention(nn.Module):
         self.unfused = unfused
         self.alpha = alpha
         self.num_heads = num_heads
-        self.fc = nn.Linear(in_dim, num_heads * out_dim, bias=False)
+        # the engine's per-node Linear (nn.Linear's parameters, initialisation
+        # and forward; its weight gradient split over the node dimension: torch's
+        # GEMM ran Pubmed's 19,717-deep reductions on one to 33 workgroups)
+        self.fc = NodeLinear(in_dim, num_heads * out_dim, bias=False)
         self.feat_drop = nn.Dropout(feat_drop) if feat_drop else None
         self.attn_drop = nn.Dropout(attn_drop) if attn_drop else None
         self.attn_l = nn.Parameter(torch.Tensor(size=(num_heads, out_dim, 1)))
@@ -55,16 +59,21 @@ class GraphAttention(nn.Module):
         self.residual = residual
         self.res_fc = None
         if residual and in_dim != num_heads * out_dim:
-            self.res_fc = nn.Linear(in_dim, num_heads * out_dim, bias=False)
+            self.res_fc = NodeLinear(in_dim, num_heads * out_dim, bias=False)
             nn.init.xavier_normal_(self.res_fc.weight.data, gain=1.414)
 
     def forward(self, h):
         if self.feat_drop is not None:
             h = self.feat_drop(h)
         ft = self.fc(h).reshape((h.shape[0], self.num_heads, -1))     # N x H x D
-        head_ft = ft.transpose(0, 1)                                   # H x N x D
-        a1 = torch.bmm(head_ft, self.attn_l).transpose(0, 1)           # N x H x 1
-        a2 = torch.bmm(head_ft, self.attn_r).transpose(0, 1)           # N x H x 1
+        # the reference's bmm(head_ft, attn_l) (gat/train.py:66-67) as a
+        # broadcast product and a sum over D: the same values; its backward
+        # reduces attn's gradient over the nodes in torch's column reduction
+        # instead of a GEMM with an H x D x 1 output and a 19,717-deep K
+        # (0.1 ms per call on one workgroup per head, four per epoch)
+        H, D = self.num_heads, ft.shape[2]
+        a1 = (ft * self.attn_l.view(1, H, D)).sum(-1, keepdim=True)    # N x H x 1
+        a2 = (ft * self.attn_r.view(1, H, D)).sum(-1, keepdim=True)    # N x H x 1
         if self.feat_drop is not None:
             ft = self.feat_drop(ft)
         if self.udf:  # the reference's edge UDF (gat/train.py:90-96)
@@ -134,8 +143,10 @@ def run(args):
                 heads, F.elu, args.in_drop, args.attn_drop, args.alpha, args.residual, args.udf,
                 args.unfused)
     model = model.to(device)
+    # one fused kernel per step on the device (torch's multi-tensor Adam: 20
+    # launches per epoch)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=args.weight_decay,
-                           capturable=args.hip_graph)
+                           capturable=args.hip_graph, fused=device.type == "cuda")
     if args.hip_graph:
         return run_captured(args, model, opt, data, g)
     dur = []

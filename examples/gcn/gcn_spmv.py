@@ -98,7 +98,7 @@ def run(args):
     model = GCN(g, data.features.shape[1], args.n_hidden, data.num_labels, args.n_layers,
                 F.relu, args.dropout).to(device)
     opt = torch.optim.Adam(model.parameters(), lr=args.lr, weight_decay=args.weight_decay,
-                           capturable=args.hip_graph)
+                           capturable=args.hip_graph, fused=device.type == "cuda")
     loss_fcn = nn.CrossEntropyLoss()
     dur = []
     if args.hip_graph:

@@ -786,6 +786,16 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
                                   const float* ufeat, const float* dout, float* dweight,
                                   int num_threads);
 
+/* The typed-block entries' item list from a CSR-like ptr[num_rows+1]: item_ptr
+ * [num_rows+1] (row r has max(1, ceil(deg / DGLHIP_TYPED_CHUNK)) items) and
+ * item_row[bound] (each item's row; entries past the last item = num_rows),
+ * bound >= the item count (num_rows + ceil(nnz / DGLHIP_TYPED_CHUNK) always
+ * is). No host sync; workspace of dglhip_typed_items_workspace_bytes bytes. */
+int64_t dglhip_typed_items_workspace_bytes(int64_t num_rows);
+int dglhip_typed_items_device(int64_t num_rows, const int64_t* ptr, int64_t bound,
+                              int64_t* item_ptr, int32_t* item_row, void* workspace,
+                              int64_t workspace_bytes, void* stream);
+
 /* DistMult decoder of R-GCN link prediction (the reference's calc_score,
  * examples/pytorch/rgcn/link_predict.py:50-55: s = h[subj] * w_rel[rel] *
  * h[obj], score = s.sum(1)), with no [num_samples, F] tensor in between.

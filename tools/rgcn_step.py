@@ -60,7 +60,7 @@ def build_model(args, dev):
     torch.manual_seed(args.seed)
     model = lp.LinkPredict(args.num_entities, args.n_hidden, args.num_rels, args.n_bases,
                            args.dropout, args.regularization, args.udf).to(dev)
-    return model, torch.optim.Adam(model.parameters(), lr=args.lr)
+    return model, torch.optim.Adam(model.parameters(), lr=args.lr, fused=dev.type == "cuda")
 
 
 def one_step(model, opt, s, args, sync=None):
