@@ -46,6 +46,7 @@ Run: python bench.py [--gpus N --steps K --warmup W]
 from __future__ import absolute_import
 
 import argparse
+import gc
 import json
 import os
 import socket
@@ -463,18 +464,28 @@ def timed_steps(step, steps, warmup, world, dev):
     for _ in range(warmup):
         step()
     _sync(dev)
-    if dist.is_initialized():
-        dist.barrier()
-    kernel.timing_enable(True, per_call=dev.type == "cuda")
-    _sync(dev)
-    t_start = time.perf_counter()
-    for _ in range(steps):
-        step()
-    _sync(dev)
-    own = time.perf_counter() - t_start
-    if dist.is_initialized():
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    # the setup's garbage collected now, and no collection inside the timed
+    # region (as timeit does): a collection there once freed the setup's
+    # 0.9-GB host edge arrays in the middle of a step (r05, a 170-ms stall)
+    gc.collect()
+    gc_was = gc.isenabled()
+    gc.disable()
+    try:
+        if dist.is_initialized():
+            dist.barrier()
+        kernel.timing_enable(True, per_call=dev.type == "cuda")
+        _sync(dev)
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            step()
+        _sync(dev)
+        own = time.perf_counter() - t_start
+        if dist.is_initialized():
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+    finally:
+        if gc_was:
+            gc.enable()
     kms, launches = kernel.timing_read()
     kernel.timing_enable(False)
     if launches == 0:

@@ -17,6 +17,8 @@ reducer as a UDF: the reference has no builtin mean) degree_bucketing.py.
 """
 from __future__ import absolute_import
 
+import contextlib
+import gc
 import importlib.util
 import os
 import time
@@ -47,18 +49,33 @@ def _sync(dev):
         torch.cuda.synchronize(dev)
 
 
+@contextlib.contextmanager
+def _no_gc():
+    """Setup garbage collected first, no collection inside the timed region
+    (bench.timed_steps does the same)."""
+    gc.collect()
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
+
+
 def wall_steps(step, steps, warmup, dev, kernel):
     """(wall ms per step, library kernel ms per step) over ``steps`` steps
     after ``warmup``; kernel ms from the library's per-launch events."""
     for _ in range(warmup):
         step()
     _sync(dev)
-    kernel.timing_enable(True)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    _sync(dev)
-    el = time.perf_counter() - t0
+    with _no_gc():
+        kernel.timing_enable(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        _sync(dev)
+        el = time.perf_counter() - t0
     kms, launches = kernel.timing_read()
     kernel.timing_enable(False)
     return el / steps * 1e3, kms / steps, launches // max(steps, 1)
@@ -75,11 +92,12 @@ def call_ms(fn, iters, dev):
             fn()
         return (time.perf_counter() - t0) / iters * 1e3
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    s.record()
-    for _ in range(iters):
-        fn()
-    e.record()
-    e.synchronize()
+    with _no_gc():
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        e.synchronize()
     return s.elapsed_time(e) / iters
 
 

@@ -275,11 +275,24 @@ class _DGLHipValue(ctypes.Union):
 _DTYPE_CODE = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32)}
 
 
+_ARRAY_TYPES = {}
+
+
+def _array_type(ctype, n):
+    """``ctype * n``, made once per (type, length): a fresh array type per call
+    is a cyclic object that only the garbage collector frees."""
+    key = (ctype, n)
+    t = _ARRAY_TYPES.get(key)
+    if t is None:
+        t = _ARRAY_TYPES[key] = ctype * n
+    return t
+
+
 def tensor_arg(t):
     """Wrap a torch tensor as a non-owning DGLHipTensor (src/c_api_common.cc:16-23)."""
     code, bits = _DTYPE_CODE[t.dtype]
-    shape = (_c_i64 * t.dim())(*t.shape)
-    strides = (_c_i64 * t.dim())(*t.stride())
+    shape = _array_type(_c_i64, t.dim())(*t.shape)
+    strides = _array_type(_c_i64, t.dim())(*t.stride())
     dev = 10 if t.is_cuda else 1
     st = _DGLHipTensor(t.data_ptr(), dev, t.device.index or 0, t.dim(), code, bits, 1,
                        shape, strides, 0)
@@ -319,6 +332,11 @@ def _dltensor_capsule_deleter(capsule):
         LIB.DGLDLManagedTensorCallDeleter(ctypes.pythonapi.PyCapsule_GetPointer(cap, b"dltensor"))
 
 
+# the deleter's address, taken once (a cast per call would link the function
+# object's keep-alive dict to a new object every time)
+_DELETER_ADDR = ctypes.cast(_dltensor_capsule_deleter, _vp).value
+
+
 def _ndarray_to_torch(handle):
     """Library-owned NDArray container -> torch tensor without a copy
     (zerocopy_from_dgl_ndarray: DGLArrayToDLPack, then the container's own
@@ -329,8 +347,7 @@ def _ndarray_to_torch(handle):
         check_call(LIB.DGLArrayToDLPack(handle, ctypes.byref(mt)))
     finally:
         check_call(LIB.DGLArrayFree(handle))
-    cap = ctypes.pythonapi.PyCapsule_New(mt, b"dltensor",
-                                         ctypes.cast(_dltensor_capsule_deleter, _vp))
+    cap = ctypes.pythonapi.PyCapsule_New(mt, b"dltensor", _DELETER_ADDR)
     return torch.utils.dlpack.from_dlpack(cap)
 
 
@@ -357,9 +374,14 @@ class PackedFunction(object):
                 pass
 
     def __call__(self, *args):
+        # raw addresses (ctypes.addressof), not ctypes.cast / pointer objects:
+        # a cast links the two objects' keep-alive dicts into a reference
+        # cycle, so every tensor argument stayed alive until a garbage
+        # collection (r05: the bench graph's 0.9-GB edge arrays were freed by a
+        # collection inside the timed region, a 170-ms host stall)
         n = len(args)
-        vals = (_DGLHipValue * max(n, 1))()
-        codes = (_c_int * max(n, 1))()
+        vals = _array_type(_DGLHipValue, max(n, 1))()
+        codes = _array_type(_c_int, max(n, 1))()
         keep = []
         for i, a in enumerate(args):
             if a is None:
@@ -367,7 +389,7 @@ class PackedFunction(object):
             elif isinstance(a, torch.Tensor):
                 st = tensor_arg(a)
                 keep.append(st)
-                vals[i].v_handle = ctypes.cast(ctypes.pointer(st), _vp)
+                vals[i].v_handle = ctypes.addressof(st)
                 codes[i] = _TC_ARRAY
             elif isinstance(a, tuple) and a[0] == "handle":
                 vals[i].v_handle = a[1]
@@ -385,8 +407,8 @@ class PackedFunction(object):
                 codes[i] = _TC_INT
         ret = _DGLHipValue()
         rc = _c_int()
-        check_call(LIB.DGLFuncCall(self.handle, ctypes.cast(vals, _vp), codes, n,
-                                   ctypes.cast(ctypes.pointer(ret), _vp), ctypes.byref(rc)))
+        check_call(LIB.DGLFuncCall(self.handle, ctypes.addressof(vals), codes, n,
+                                   ctypes.addressof(ret), ctypes.byref(rc)))
         del keep
         code = rc.value
         if code == _TC_INT:
