@@ -140,6 +140,9 @@ def build_parser():
     ap.add_argument("--dist-timeout", type=float, default=300.0,
                     help="N>1: collective timeout (s) of the process groups; a dead or hung "
                          "peer then ends the job in bounded time")
+    ap.add_argument("--no-one-launch-leg", action="store_true",
+                    help="skip the one_launch block (the headline step with the source-blocked "
+                         "schedule off)")
     ap.add_argument("--no-sage-rmat-leg", action="store_true",
                     help="skip configs[3]'s GraphSAGE-mean epochs on the rmat leg's graph")
     ap.add_argument("--leg-deadline", type=float, default=None,
@@ -916,8 +919,10 @@ def main(argv=None):
     if world == 1 and not args.no_traffic and args.workload == "reddit" and not args.dist_rehearsal:
         t0 = time.time()  # before this process initialises the GPU
         # every g-SpMM kernel of the 3 calls (warm-up + 2 steps), per call
+        # (no other leg: every g-SpMM kernel of the child run is summed)
         pmc = pmc_traffic(["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-traffic",
-                           "--no-rmat-leg", "--no-train-leg", "--no-model-legs"],
+                           "--no-rmat-leg", "--no-train-leg", "--no-model-legs",
+                           "--no-one-launch-leg", "--no-sage-rmat-leg"],
                           per_call_calls=3)
         if not args.no_rmat_leg and args.emulate_world <= 1:
             # the rmat leg's kernels: every g-SpMM kernel of a call, per call
@@ -1178,7 +1183,8 @@ def main(argv=None):
                             "and are read as bf16, summed in fp32; own rows exact. Opt-in, not "
                             "the headline (results carry bf16 rounding of remote inputs)"}
         legs.run("halo_bf16", lambda: None, bf16_run)
-    if not distributed and blocks and args.workload == "reddit" and args.emulate_world <= 1:
+    if (not distributed and blocks and args.workload == "reddit" and args.emulate_world <= 1
+            and not args.no_one_launch_leg):
         # the same step with the source-blocked schedule off: what a graph in
         # arbitrary edge order (which fails the monotone check) runs instead
         def one_launch_run(_):

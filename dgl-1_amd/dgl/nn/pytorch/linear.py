@@ -28,12 +28,18 @@ from ..._handoff import GradHandoff, is_output, output_ref, take
 __all__ = ["NodeLinear", "sage_dense"]
 
 _ROWS_PER_CHUNK = 1 << 16
+_SMALL_ROWS_PER_CHUNK = 1 << 11
 
 
 def _splitk_tn(a, b):
     """aᵀ·b for tall a (n, p), b (n, q): split-K over row chunks, summed in order."""
     n = a.shape[0]
     chunks = min(256, n // _ROWS_PER_CHUNK)
+    if chunks <= 1:
+        # below two 64K-row chunks: 2K-row chunks, so a small output still gets
+        # workgroups (Pubmed's 19,717 x 500 -> 64 x 500 weight gradient ran on
+        # one workgroup in torch's GEMM: 0.14 ms)
+        chunks = n // _SMALL_ROWS_PER_CHUNK
     if chunks <= 1:
         return a.t().matmul(b)
     k = n // chunks
