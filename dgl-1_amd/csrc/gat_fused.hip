@@ -47,7 +47,8 @@ namespace dglhip {
 // them gathered before it
 int g_gat_variant = 0;
 // study knob of the transposed backward (dglhip_set_gat_bwd_variant): bits 0-1
-// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid);
+// the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid,
+// 3 16-B write-through stores regrouped through LDS);
 // bit 2 the kernel built for 5 waves per SIMD (96 VGPRs) instead of 4 (97)
 int g_gat_bwd_variant = 0;
 
@@ -570,11 +571,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
       }
     }
     // g at its forward slot, for d_er's sum over the CSR
+    if (gpol == 3) {
+      // 16-B write-through stores that drop the line from the XCD's L2
+      // (sc1): lane 2j + half takes heads 4 half .. 4 half + 3 of slot j
+      // from the LDS rows (already holding g by head), so the scattered
+      // partial lines stop evicting the block's dout rows
+      const int j = lane >> 1, half = lane & 1;
+      const int64_t p0 = __shfl(pf[0], 8 * (j & 7), 64), p1 = __shfl(pf[1], 8 * (j & 7), 64);
+      if (j < U && (FULL || j < nb)) {
+        const int64_t pj = j < 8 ? p0 : p1;
+        f32x4 gv;
+        gv.x = ld[(4 * half + 0) * LU + j];
+        gv.y = ld[(4 * half + 1) * LU + j];
+        gv.z = ld[(4 * half + 2) * LU + j];
+        gv.w = ld[(4 * half + 3) * LU + j];
+        float* dst = g_out + pj * H + 4 * half;
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(dst), "v"(gv) : "memory");
+      }
+    } else {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if (FULL || jc + 8 * i < nb) {
-        if (gpol == 0) g_out[pf[i] * H + hc] = pg[i];
-        else if (gpol == 1) __builtin_nontemporal_store(pg[i], g_out + pf[i] * H + hc);
+      for (int i = 0; i < 2; ++i) {
+        if (FULL || jc + 8 * i < nb) {
+          if (gpol == 0) g_out[pf[i] * H + hc] = pg[i];
+          else if (gpol == 1) __builtin_nontemporal_store(pg[i], g_out + pf[i] * H + hc);
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -914,7 +934,7 @@ int dglhip_set_gat_variant(int variant) {
 
 int dglhip_set_gat_bwd_variant(int variant) {
   API_BEGIN();
-  DGLHIP_CHECK(variant >= 0 && variant <= 6 && (variant & 3) != 3, "unknown GAT backward variant " << variant);
+  DGLHIP_CHECK(variant >= 0 && variant <= 7, "unknown GAT backward variant " << variant);
   g_gat_bwd_variant = variant;
   API_END();
 }
