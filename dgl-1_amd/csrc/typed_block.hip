@@ -44,6 +44,11 @@ namespace {
 
 constexpr int64_t kChunk = DGLHIP_TYPED_CHUNK;
 
+// most output slices per wave of the typed-block g-SpMM: 1 by default (one
+// wave per 64 outputs); 8 — one wave per item at R-GCN's 500 — ran the
+// configs[4] forward at 0.20 ms against 0.12 (r05, fewer waves in flight)
+int g_typed_t = 1;
+
 // slots in flight per wave at block width SI (their row and weight values
 // in VGPRs: 2 * SI * kEdges of them)
 template <int SI>
@@ -73,12 +78,16 @@ __device__ __forceinline__ bool item_range(int64_t it, int64_t num_rows,
   return true;
 }
 
-// One wave per (item, 64-wide slice of the output features): the slices of
-// an item run in parallel waves (8 for R-GCN's 500 features). For every
-// output element:  m_e = fma chain over i of h[u, b*si+i] * W[r, b, i, j];
-// acc = fma(norm_e, m_e, acc) over the item's slots in slot order.
-// SI > 0: the block width as a compile-time constant; SI == 0: runtime width.
-template <int SI>
+// One wave per (item, slice of 64 * T output features): lane l of pass p
+// takes outputs p * 64 * T + 64 t + l, t < T (R-GCN's 500 features: T = 8, one
+// wave per item; r05 — eight waves per item had each resolved the same slots'
+// column, relation and norm, 95k waves of two dependent round trips for a
+// 30,000-edge sample). For every output element:
+//   m_e = fma chain over i of h[u, b*si+i] * W[r, b, i, j];
+//   acc = fma(norm_e, m_e, acc) over the item's slots in slot order
+// (the same per-element arithmetic at every T). SI > 0: the block width as a
+// compile-time constant; SI == 0: runtime width (T = 1 only).
+template <int SI, int T>
 __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
     int64_t num_items, int64_t num_rows, int64_t npass, int64_t nb, int64_t si_rt, int64_t so,
     const int64_t* __restrict__ indptr, const int64_t* __restrict__ item_ptr,
@@ -86,7 +95,10 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
     const int32_t* __restrict__ slot_rel, const float* __restrict__ slot_norm,
     const float* __restrict__ ufeat, const float* __restrict__ weight,
     float* __restrict__ out, float* __restrict__ partial) {
-  constexpr int G = EdgesInFlight<SI>::value;
+  // slots in flight: the T = 1 depths; at T > 1 every slot's T rows and
+  // weight columns are loaded per t, so fewer slots per batch
+  constexpr int G1 = EdgesInFlight<SI>::value;
+  constexpr int G = T == 1 ? G1 : (G1 >= 4 ? 4 : G1);
   const int64_t si = SI > 0 ? SI : si_rt;
   const int64_t wave = block_linear() * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -97,12 +109,20 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
   if (!item_range(it, num_rows, indptr, item_ptr, item_row, &row, &beg, &end, &single)) return;
   const int lane = threadIdx.x & 63;
   const int64_t Fi = nb * si, Fo = nb * so, wr = nb * si * so;
-  const int64_t jg = pass * 64 + lane;
-  const bool active = jg < Fo;
-  // idle lanes of the last slice read block 0 (valid addresses) and never store
-  const int64_t b = active ? jg / so : 0, j = active ? jg - b * so : 0;
-  const int64_t hoff = b * si, woff = b * si * so + j;
-  float acc = 0.0f;
+  int64_t hoff[T], woff[T];
+  bool active[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int64_t jg = pass * 64 * T + 64 * t + lane;
+    active[t] = jg < Fo;
+    // idle lanes of the last slice read block 0 (valid addresses) and never store
+    const int64_t b = active[t] ? jg / so : 0, j = active[t] ? jg - b * so : 0;
+    hoff[t] = b * si;
+    woff[t] = b * si * so + j;
+  }
+  float acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = 0.0f;
   // one batch of up to GB slots from k (slots q >= cnt predicated off: their
   // loads read a valid slot, their products are dropped)
   auto batch = [&](int64_t k, auto gb_tag) {
@@ -114,44 +134,48 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
 #pragma unroll
     for (int q = 0; q < GB; ++q) {
       const int64_t kk = q < cnt ? k + q : end - 1;  // a valid slot for idle q
-      hb[q] = ufeat + int64_t(indices[kk]) * Fi + hoff;
-      wb[q] = weight + int64_t(slot_rel[kk]) * wr + woff;
+      hb[q] = ufeat + int64_t(indices[kk]) * Fi;
+      wb[q] = weight + int64_t(slot_rel[kk]) * wr;
       nrm[q] = slot_norm ? slot_norm[kk] : 1.0f;
     }
-    if (SI > 0) {
-      float hv[GB][SI > 0 ? SI : 1], wv[GB][SI > 0 ? SI : 1];
 #pragma unroll
-      for (int q = 0; q < GB; ++q) {
+    for (int t = 0; t < T; ++t) {
+      if (SI > 0) {
+        float hv[GB][SI > 0 ? SI : 1], wv[GB][SI > 0 ? SI : 1];
 #pragma unroll
-        for (int i = 0; i < SI; ++i) {
-          hv[q][i] = hb[q][i];
-          wv[q][i] = wb[q][i * so];
+        for (int q = 0; q < GB; ++q) {
+#pragma unroll
+          for (int i = 0; i < SI; ++i) {
+            hv[q][i] = hb[q][hoff[t] + i];
+            wv[q][i] = wb[q][woff[t] + i * so];
+          }
         }
+#pragma unroll
+        for (int q = 0; q < GB; ++q) {
+          float m = 0.0f;
+#pragma unroll
+          for (int i = 0; i < SI; ++i) m = __builtin_fmaf(hv[q][i], wv[q][i], m);
+          if (q < cnt) acc[t] = __builtin_fmaf(nrm[q], m, acc[t]);
+        }
+      } else {
+        float m[GB];
+#pragma unroll
+        for (int q = 0; q < GB; ++q) m[q] = 0.0f;
+        for (int64_t i = 0; i < si; ++i) {
+#pragma unroll
+          for (int q = 0; q < GB; ++q)
+            m[q] = __builtin_fmaf(hb[q][hoff[t] + i], wb[q][woff[t] + i * so], m[q]);
+        }
+#pragma unroll
+        for (int q = 0; q < GB; ++q)
+          if (q < cnt) acc[t] = __builtin_fmaf(nrm[q], m[q], acc[t]);
       }
-#pragma unroll
-      for (int q = 0; q < GB; ++q) {
-        float m = 0.0f;
-#pragma unroll
-        for (int i = 0; i < SI; ++i) m = __builtin_fmaf(hv[q][i], wv[q][i], m);
-        if (q < cnt) acc = __builtin_fmaf(nrm[q], m, acc);
-      }
-    } else {
-      float m[GB];
-#pragma unroll
-      for (int q = 0; q < GB; ++q) m[q] = 0.0f;
-      for (int64_t i = 0; i < si; ++i) {
-#pragma unroll
-        for (int q = 0; q < GB; ++q) m[q] = __builtin_fmaf(hb[q][i], wb[q][i * so], m[q]);
-      }
-#pragma unroll
-      for (int q = 0; q < GB; ++q)
-        if (q < cnt) acc = __builtin_fmaf(nrm[q], m[q], acc);
     }
   };
   // short batches (most items of a sampled KG hold 1-4 slots) at a quarter
   // or half of the width: a G-wide batch issues its loads for every q, idle
   // or not
-  constexpr int G4 = G >= 8 ? G / 4 : G, G2 = G >= 8 ? G / 2 : G;
+  constexpr int G4 = G >= 8 ? G / 4 : (G >= 4 ? G / 2 : G), G2 = G >= 4 ? G / 2 : G;
   for (int64_t k = beg; k < end; k += G) {
     if (end - k <= G4) {
       batch(k, std::integral_constant<int, G4>());
@@ -163,7 +187,10 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
     }
     batch(k, std::integral_constant<int, G>());
   }
-  if (active) (single ? out + row * Fo : partial + it * Fo)[jg] = acc;
+  float* dst = single ? out + row * Fo : partial + it * Fo;
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+    if (active[t]) dst[pass * 64 * T + 64 * t + lane] = acc[t];
 }
 
 // out[row] = ((p0 + p1) + p2) ... over the row's items in order, for the
@@ -402,25 +429,41 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t 
   DGLHIP_CHECK(indptr && item_ptr && item_row && indices && slot_rel && ufeat && weight && out,
                "null pointer argument");
   DGLHIP_CHECK(num_heavy == 0 || partial, "chunked rows need their partials");
-  const int64_t npass = (Fo + 63) / 64;
+  // outputs per lane: a wave covers up to 64 * T of them, T capped by
+  // g_typed_t (the study knob dglhip_set_typed_block_width; default 1)
+  const int64_t n64 = (Fo + 63) / 64;
+  int T = n64 >= 8 ? 8 : (n64 >= 4 ? 4 : (n64 >= 2 ? 2 : 1));
+  if (T > g_typed_t) T = g_typed_t;
+  const bool known = in_block == 1 || in_block == 2 || in_block == 4 || in_block == 5 ||
+                     in_block == 8 || in_block == 16;
+  if (!known || in_block > 8) T = 1;
+  const int64_t npass = (Fo + 64 * T - 1) / (64 * T);
   const int64_t waves = num_items * npass;
   DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
   const dim3 grid = grid_1d((waves + 3) / 4), block(256);
-#define DGLHIP_TB(S)                                                                       \
-  hipLaunchKernelGGL(typed_block_spmm_kernel<S>, grid, block, 0, stream, num_items,       \
-                     num_rows, npass, num_blocks, in_block, out_block, indptr, item_ptr, item_row, indices, \
-                     slot_rel, slot_norm, ufeat, weight, out, partial)
+#define DGLHIP_TB(S, TT)                                                                      \
+  hipLaunchKernelGGL((typed_block_spmm_kernel<S, TT>), grid, block, 0, stream, num_items,      \
+                     num_rows, npass, num_blocks, in_block, out_block, indptr, item_ptr,       \
+                     item_row, indices, slot_rel, slot_norm, ufeat, weight, out, partial)
+#define DGLHIP_TBT(S)                       \
+  switch (T) {                              \
+    case 8: DGLHIP_TB(S, 8); break;         \
+    case 4: DGLHIP_TB(S, 4); break;         \
+    case 2: DGLHIP_TB(S, 2); break;         \
+    default: DGLHIP_TB(S, 1); break;        \
+  }
   timed_launch(stream, [&] {
     switch (in_block) {
-      case 1: DGLHIP_TB(1); break;
-      case 2: DGLHIP_TB(2); break;
-      case 4: DGLHIP_TB(4); break;
-      case 5: DGLHIP_TB(5); break;
-      case 8: DGLHIP_TB(8); break;
-      case 16: DGLHIP_TB(16); break;
-      default: DGLHIP_TB(0); break;
+      case 1: DGLHIP_TBT(1); break;
+      case 2: DGLHIP_TBT(2); break;
+      case 4: DGLHIP_TBT(4); break;
+      case 5: DGLHIP_TBT(5); break;
+      case 8: DGLHIP_TBT(8); break;
+      case 16: DGLHIP_TB(16, 1); break;
+      default: DGLHIP_TB(0, 1); break;
     }
   });
+#undef DGLHIP_TBT
 #undef DGLHIP_TB
   if (num_heavy > 0) {
     const int64_t total = num_heavy * Fo;
@@ -507,6 +550,14 @@ int dglhip_typed_items_device(int64_t num_rows, const int64_t* ptr, int64_t boun
   hipLaunchKernelGGL(typed_item_rows_kernel, grid_1d((bound + 255) / 256), dim3(256), 0, stream,
                      num_rows, bound, item_ptr, item_row);
   HIP_CALL(hipGetLastError());
+  API_END();
+}
+
+int dglhip_set_typed_block_width(int slices) {
+  API_BEGIN();
+  DGLHIP_CHECK(slices == 1 || slices == 2 || slices == 4 || slices == 8,
+               "typed-block width must be 1, 2, 4 or 8 slices, got " << slices);
+  g_typed_t = slices;
   API_END();
 }
 

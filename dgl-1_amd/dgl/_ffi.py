@@ -84,6 +84,7 @@ def _load():
             _c_int, [_c_i64, _c_i64, _c_i64] + [_vp] * 11 +
             [_c_float, _c_float, _c_float, _c_int, _c_float, _c_float, _c_u64, _vp, _vp, _vp,
              _vp]),
+        "dglhip_set_typed_block_width": (_c_int, [_c_int]),
         "dglhip_typed_items_workspace_bytes": (_c_i64, [_c_i64]),
         "dglhip_typed_items_device": (_c_int, [_c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _vp]),
         "dglhip_distmult_score_device": (_c_int, [_c_i64] * 4 + [_vp] * 7),

@@ -1456,6 +1456,13 @@ def gather_rows(x, idx):
 TYPED_CHUNK = 64  # DGLHIP_TYPED_CHUNK: slots per chain of the typed-block kernels
 
 
+def set_typed_block_width(slices):
+    """Study knob: at most ``slices`` (1, 2, 4, 8) slices of 64 outputs per
+    wave of the typed-block g-SpMM (default 1; 8 was slower at configs[4]).
+    Same bits."""
+    check_call(LIB.dglhip_set_typed_block_width(int(slices)))
+
+
 def _position_groups(idx, num_rows):
     """Positions of ``idx`` grouped by row in increasing position, no host
     sync: (ptr int64[R+1], order int32[m]). On a device, the library's CSR

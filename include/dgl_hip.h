@@ -765,6 +765,10 @@ int dglhip_typed_block_spmm_host(int64_t num_rows, int64_t num_blocks,
                                  const int32_t* slot_rel, const float* slot_norm,
                                  const float* ufeat, const float* weight, float* out,
                                  int num_threads);
+/* Study knob: at most `slices` (1, 2, 4, 8) slices of 64 outputs per wave of
+ * the typed-block g-SpMM (default 1: one wave per 64 outputs; 8: one wave per
+ * item at R-GCN's 500 outputs, slower there). Same bits. */
+int dglhip_set_typed_block_width(int slices);
 /* Weight gradient: dweight[r,b,i,j] = sum over the edges k of relation r
  * (relation-major CSR rel_ptr[R+1] with per-edge rel_src / rel_dst /
  * rel_norm, norm may be NULL) of norm[k] * ufeat[src, b*si+i] *

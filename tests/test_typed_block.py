@@ -92,19 +92,26 @@ def test_typed_block_device_matches_host_bits(shape):
     assert int(torch.bincount(etype).min()) > kernel.TYPED_CHUNK
     for nm in (norm, None):
         outs, grads, wgrads = [], [], []
-        for dev in ("cpu", "cuda"):
-            adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
-            h1 = h.detach().to(dev).clone().requires_grad_(True)
-            W1 = W.detach().to(dev).clone().requires_grad_(True)
-            out = kernel.typed_block_spmm(adj, h1, W1, etype.to(dev),
-                                          None if nm is None else nm.to(dev))
-            out.backward(G.to(dev))
+        # the host, then the device at 8 output slices per wave and at 1
+        # (the default)
+        for dev, width in (("cpu", 8), ("cuda", 8), ("cuda", 1)):
+            kernel.set_typed_block_width(width)
+            try:
+                adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+                h1 = h.detach().to(dev).clone().requires_grad_(True)
+                W1 = W.detach().to(dev).clone().requires_grad_(True)
+                out = kernel.typed_block_spmm(adj, h1, W1, etype.to(dev),
+                                              None if nm is None else nm.to(dev))
+                out.backward(G.to(dev))
+            finally:
+                kernel.set_typed_block_width(1)
             outs.append(out.detach().cpu())
             grads.append(h1.grad.cpu())
             wgrads.append(W1.grad.cpu())
-        assert torch.equal(outs[0], outs[1])
-        assert torch.equal(grads[0], grads[1])
-        assert torch.equal(wgrads[0], wgrads[1])
+        for k in (1, 2):
+            assert torch.equal(outs[0], outs[k])
+            assert torch.equal(grads[0], grads[k])
+            assert torch.equal(wgrads[0], wgrads[k])
 
 
 def _example():

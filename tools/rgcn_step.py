@@ -155,9 +155,12 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--kernels", action="store_true")
+    ap.add_argument("--typed-width", type=int, default=1,
+                    help="output slices of 64 per typed-block wave (study knob)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    kernel.set_typed_block_width(args.typed_width)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     raw = make_samples(args, args.warmup + args.steps)
     samples = [to_dev(s, dev) for s in raw]
