@@ -1064,9 +1064,11 @@ def main(argv=None):
                             "blocks, every row's chain continued block by block. Precondition: "
                             "the edges are numbered source-major, so along every row's slots "
                             "the source blocks never decrease and the blocked chains are the "
-                            "edge-id chains (bit-identical); a graph in arbitrary edge order "
-                            "fails that check and runs the one-launch schedule instead (same "
-                            "bits, about 2x the time on this graph: the one_launch block)"
+                            "edge-id chains (bit-identical); a mutable graph in arbitrary edge "
+                            "order fails that check and runs the one-launch schedule instead "
+                            "(same bits, about 2x the time on this graph: the one_launch "
+                            "block), while a readonly graph's slots are (dst, src)-sorted as "
+                            "the reference's ImmutableGraph, so it is blocked in any edge order"
                             % blocks)
     else:
         from dgl.distributed import PartitionedGraph, balanced_bounds

@@ -588,3 +588,57 @@ def test_gather_modes_same_bits():
         kernel.set_blocked("auto")
         kernel.set_gather_mode(2)
         kernel.check_call(kernel.LIB.dglhip_set_row_policy(2))
+
+
+@pytest.mark.gpu
+def test_readonly_random_order_graph_is_blocked_and_exact():
+    """The edge-order precondition concerns mutable graphs only. A readonly
+    graph's adjacency keeps its slots sorted by (dst, src), as the
+    reference's ImmutableGraph CSR (immutable_graph.cc:206-237), so its
+    chains run in source order and the source-blocked schedule applies to an
+    edge list in random order: blocked launches, and the oracle's bits for
+    that slot order (the in-edges of each row sorted by source, stable)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 12_000_000
+    gen = torch.Generator().manual_seed(21)
+    src = torch.randint(0, n, (m,), generator=gen)
+    dst = torch.randint(0, n, (m,), generator=gen)
+    h = torch.rand(n, 128, generator=gen) * 2 - 1
+    out = {}
+    for ro in (False, True):
+        g = dgl.DGLGraph((src, dst), readonly=ro) if ro else dgl.DGLGraph((src, dst))
+        g.ndata["h"] = h.to(dev)
+        launches = kernel.blocked_schedule(g.sparse_adjacency(dev), g.ndata["h"])
+        assert (launches > 1) == ro, (ro, launches)
+        g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+        out[ro] = g.ndata["o"].cpu().numpy()
+    s_np, d_np = src.numpy(), dst.numpy()
+    hn = h.numpy()
+    # mutable: the edge-id chains; readonly: the (dst, src)-sorted chains
+    ip, ix, pos = O.coo_to_csr(n, d_np, s_np)
+    assert np.array_equal(out[False], O.spmm_csr(ip, ix, pos, hn, num_threads=16))
+    order = np.lexsort((s_np, d_np))
+    ip, ix, pos = O.coo_to_csr(n, d_np[order], s_np[order])
+    assert np.array_equal(out[True], O.spmm_csr(ip, ix, pos, hn, num_threads=16))
+
+
+def test_readonly_and_mutable_chain_orders_host():
+    """The two slot orders on the host: a mutable graph's chains run in edge-id
+    order (the reference's COO adjacency, graph.cc:509-524), a readonly
+    graph's in (dst, src) order (ImmutableGraph's CSR,
+    immutable_graph.cc:206-237); each equals the oracle over that order."""
+    n, m = 3000, 300_000
+    gen = torch.Generator().manual_seed(21)
+    src = torch.randint(0, n, (m,), generator=gen)
+    dst = torch.randint(0, n, (m,), generator=gen)
+    h = torch.rand(n, 16, generator=gen) * 2 - 1
+    s_np, d_np, hn = src.numpy(), dst.numpy(), h.numpy()
+    for ro in (False, True):
+        g = dgl.DGLGraph((src, dst), readonly=ro) if ro else dgl.DGLGraph((src, dst))
+        g.ndata["h"] = h
+        g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+        order = np.lexsort((s_np, d_np)) if ro else np.arange(m)
+        ip, ix, pos = O.coo_to_csr(n, d_np[order], s_np[order])
+        assert np.array_equal(g.ndata["o"].numpy(), O.spmm_csr(ip, ix, pos, hn))
