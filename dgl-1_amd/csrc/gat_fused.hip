@@ -51,6 +51,9 @@ int g_gat_variant = 0;
 // 3 16-B write-through stores regrouped through LDS);
 // bit 2 the kernel built for 5 waves per SIMD (96 VGPRs) instead of 4 (97)
 int g_gat_bwd_variant = 0;
+// study knob: 1 ignores attn_l in dglhip_gat_aggregate_logits_ranges_device
+// (el gathered as before; same bits)
+int g_gat_no_logit = 0;
 
 // One row of VEC floats per lane through a buffer descriptor built from the
 // wave-uniform row address: a 32-bit per-lane byte offset instead of a 64-bit
@@ -199,15 +202,35 @@ __global__ __launch_bounds__(256) void gat_aggregate_kernel(
 // head's 16-B reads stay aligned
 #define GAT_LDS_STRIDE 20
 
-template <int H, int VEC, bool DROP, bool SMALL, bool FULL, bool EARLY>
+// The quad and half-row butterflies of gat_logit_tree (DPP: the same
+// pairings as __shfl_xor 1, 2 and a mirror of the 8 lanes).
+__device__ __forceinline__ float gat_dpp_xor1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float gat_dpp_xor2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float gat_dpp_half_mirror(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
+}
+
+// LOGIT (8 heads x 16, two-float lanes): the source's logit el[u, h] is not
+// gathered but recomputed from the gathered feature row and the head's
+// attention vector attn_l (alv: this lane's two entries), in
+// dglhip_gat_logits_device's association, so the value is el's bit for bit
+// and the slot needs 4 lines instead of 5.
+template <int H, int VEC, bool DROP, bool SMALL, bool FULL, bool EARLY, bool LOGIT = false>
 __device__ __forceinline__ void gat_batch(
     int64_t k, int nb, int64_t F, uint32_t voff, int64_t h, int hc, int jc, float rc,
     const int32_t* __restrict__ indices, const float* __restrict__ el,
     const float* __restrict__ ft, const GatTable& tab, float alpha, float lo, float hi, int apply_exp,
     uint64_t seed, uint32_t thr, float scale, float* la, float* lw, float* __restrict__ a_out,
-    float* __restrict__ w_out, typename Vec<VEC>::T& acc, float& zacc) {
+    float* __restrict__ w_out, typename Vec<VEC>::T& acc, float& zacc,
+    typename Vec<VEC>::T alv = typename Vec<VEC>::T()) {
+#pragma clang fp contract(off)
   typedef typename Vec<VEC>::T V;
   constexpr int U = 16;
+  static_assert(!LOGIT || (H == 8 && VEC == 2 && EARLY), "LOGIT: 8 heads x 16, early gathers");
   constexpr int LA = GAT_LDS_STRIDE;
   constexpr int SPP = 64 / H;               // slots covered per pass of the wave
   constexpr int PPL = (U + SPP - 1) / SPP;  // attention values per lane per batch
@@ -229,11 +252,34 @@ __device__ __forceinline__ void gat_batch(
       for (int t = 1; t < SPP; ++t)
         if (SPP * i + t < U) c = jc == t ? cj[SPP * i + t] : c;
       if (!((SPP * PPL == U || j < U) && (FULL || j < nb))) c = cj[0];
-      lg[i] = el[int64_t(c) * H + hc];
+      if (!LOGIT) lg[i] = el[int64_t(c) * H + hc];
     }
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (FULL || j < nb) u[j] = gat_gather<VEC, SMALL>(ft, tab, cj[j], F, voff);
+  }
+  if constexpr (LOGIT) {
+    // lane 8 h + t holds features 2t, 2t + 1 of head h: its pair product,
+    // then the head's 8 lanes summed ((p0 + p1) + (p2 + p3)) + ((p4 + p5) +
+    // (p6 + p7)) in every lane of the head; lane t keeps slot t's (and
+    // t + 8's) and the pair lane (hc, jc) reads slot jc of head hc from lane
+    // 8 hc + jc
+    const int t = static_cast<int>(threadIdx.x & 7);
+    float s0 = 0.0f, s1 = 0.0f;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (FULL || j < nb) {
+        float p = __builtin_fmaf(u[j].y, alv.y, u[j].x * alv.x);
+        p = p + gat_dpp_xor1(p);
+        p = p + gat_dpp_xor2(p);
+        p = p + gat_dpp_half_mirror(p);
+        if (j < 8) s0 = t == j ? p : s0;
+        else s1 = t == j - 8 ? p : s1;
+      }
+    }
+    const int src = 8 * hc + jc;
+    lg[0] = __shfl(s0, src, 64);
+    lg[1] = __shfl(s1, src, 64);
   }
 #pragma unroll
   for (int i = 0; i < PPL; ++i) {
@@ -290,7 +336,38 @@ __device__ __forceinline__ void gat_batch(
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false, int RP = 0>
+// el[n, h] = the logit of node n's head h, sum_d ft[n, h, d] * attn[h, d]: at
+// 16 features per head the tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) + (p6 +
+// p7)), p_l = fma(x[2l+1], a[2l+1], x[2l] * a[2l]) (the association LOGIT
+// recomputes in gat_batch), else one fma chain over d. One thread per (n, h).
+__device__ __forceinline__ float gat_logit(const float* __restrict__ x,
+                                           const float* __restrict__ a, int64_t D) {
+#pragma clang fp contract(off)
+  if (D == 16) {
+    float p[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) p[l] = __builtin_fmaf(x[2 * l + 1], a[2 * l + 1], x[2 * l] * a[2 * l]);
+    return ((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]));
+  }
+  float acc = 0.0f;
+  for (int64_t d = 0; d < D; ++d) acc = __builtin_fmaf(x[d], a[d], acc);
+  return acc;
+}
+
+__global__ __launch_bounds__(256) void gat_logits_kernel(
+    int64_t total, int64_t H, int64_t D, const float* __restrict__ ft,
+    const float* __restrict__ attn_l, const float* __restrict__ attn_r, float* __restrict__ el,
+    float* __restrict__ er) {
+  const int64_t i = block_linear() * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t h = i % H;
+  const float* x = ft + i * D;  // row n, head h: (n * H + h) * D
+  el[i] = gat_logit(x, attn_l + h * D, D);
+  if (er) er[i] = gat_logit(x, attn_r + h * D, D);
+}
+
+template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false, int RP = 0,
+          bool LOGIT = false>
 __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     int64_t num_rows, int64_t D, const int64_t* __restrict__ row_beg,
     const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
@@ -298,7 +375,7 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
     float alpha, float lo, float hi, int apply_exp, uint64_t seed0,
     const int64_t* __restrict__ seed_off, uint32_t thr, float scale, float* __restrict__ out_ft,
     float* __restrict__ out_z, float* __restrict__ a_out, float* __restrict__ w_out,
-    int64_t table_bytes) {
+    int64_t table_bytes, const float* __restrict__ attn_l = nullptr) {
   typedef typename Vec<VEC>::T V;
   constexpr int U = 16;
   constexpr int LA = GAT_LDS_STRIDE;
@@ -333,16 +410,17 @@ __global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
       acc = load_out<VEC, RP>(out_ft + row * F, f0);
       if (f0 - h * D == 0) zacc = out_z[row * H + h];
     }
+    V alv = Vec<VEC>::zero();
+    if (LOGIT) alv = ldv<VEC>(attn_l + fa);  // attn_l [H, D]: this lane's two entries
     int64_t k = beg;
     for (; k + U <= end; k += U)
-      gat_batch<H, VEC, DROP, SMALL, true, EARLY>(k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab,
-                                           alpha, lo, hi,
-                                    apply_exp, seed, thr, scale, s_a[wi], s_w[wi], a_out, w_out,
-                                    acc, zacc);
+      gat_batch<H, VEC, DROP, SMALL, true, EARLY, LOGIT>(
+          k, U, F, voff, h, hc, jc, rc, indices, el, ft, tab, alpha, lo, hi, apply_exp, seed, thr,
+          scale, s_a[wi], s_w[wi], a_out, w_out, acc, zacc, alv);
     if (k < end)
-      gat_batch<H, VEC, DROP, SMALL, false, EARLY>(k, static_cast<int>(end - k), F, voff, h, hc, jc,
-                                            rc, indices, el, ft, tab, alpha, lo, hi, apply_exp, seed, thr, scale, s_a[wi],
-                                     s_w[wi], a_out, w_out, acc, zacc);
+      gat_batch<H, VEC, DROP, SMALL, false, EARLY, LOGIT>(
+          k, static_cast<int>(end - k), F, voff, h, hc, jc, rc, indices, el, ft, tab, alpha, lo,
+          hi, apply_exp, seed, thr, scale, s_a[wi], s_w[wi], a_out, w_out, acc, zacc, alv);
     if (active) {
       store_out<VEC, RP>(out_ft + row * F, f0, acc);
       if (f0 - h * D == 0) out_z[row * H + h] = zacc;
@@ -695,6 +773,19 @@ int dglhip_gat_aggregate_ranges_device(
     float clamp_lo, float clamp_hi, int apply_exp, float drop_p, uint64_t seed,
     const int64_t* seed_offset, float* out_ft, float* out_z, float* attn_out,
     float* attn_drop_out, void* stream_) {
+  return dglhip_gat_aggregate_logits_ranges_device(
+      num_rows, num_src, num_heads, head_dim, row_beg, row_end, accumulate, indices, row_order,
+      el, er, ft, nullptr, alpha, clamp_lo, clamp_hi, apply_exp, drop_p, seed, seed_offset,
+      out_ft, out_z, attn_out, attn_drop_out, stream_);
+}
+
+int dglhip_gat_aggregate_logits_ranges_device(
+    int64_t num_rows, int64_t num_src, int64_t num_heads, int64_t head_dim,
+    const int64_t* row_beg, const int64_t* row_end, int accumulate, const int32_t* indices,
+    const int32_t* row_order, const float* el, const float* er, const float* ft,
+    const float* attn_l, float alpha, float clamp_lo, float clamp_hi, int apply_exp,
+    float drop_p, uint64_t seed, const int64_t* seed_offset, float* out_ft, float* out_z,
+    float* attn_out, float* attn_drop_out, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && num_src >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
@@ -739,13 +830,25 @@ int dglhip_gat_aggregate_ranges_device(
     const bool early = g_gat_variant == 3 || (g_gat_variant == 0 && v2);
     if (num_heads == 8 && v2 && early && (g_row_pol == 2 || g_row_pol == 4)) {
       // the running rows' cache policy (dglhip_set_row_policy) on the 8-head
-      // two-float shape (the Reddit-shaped 8 x 16 layer)
+      // two-float shape (the Reddit-shaped 8 x 16 layer); with attn_l the
+      // sources' logits recomputed from their gathered rows (LOGIT)
+      const bool logit = attn_l != nullptr && head_dim == 16 && !g_gat_no_logit;
       timed_launch(stream, [&] {
 #define DGLHIP_GATRP(DD, SM, RPV)                                                              \
-  hipLaunchKernelGGL((gat_aggregate_lds_kernel<8, 2, DD, SM, true, RPV>), grid_1d(blocks),       \
-                     dim3(256), 0, stream, num_rows, head_dim, row_beg, row_end, accumulate,    \
-                     indices, row_order, el, er, ft, alpha, clamp_lo, clamp_hi, apply_exp, seed, \
-                     seed_offset, thr, scale, out_ft, out_z, attn_out, attn_drop_out, tbytes)
+  do {                                                                                         \
+    if (logit)                                                                                 \
+      hipLaunchKernelGGL((gat_aggregate_lds_kernel<8, 2, DD, SM, true, RPV, true>),             \
+                         grid_1d(blocks), dim3(256), 0, stream, num_rows, head_dim, row_beg,    \
+                         row_end, accumulate, indices, row_order, el, er, ft, alpha, clamp_lo,  \
+                         clamp_hi, apply_exp, seed, seed_offset, thr, scale, out_ft, out_z,     \
+                         attn_out, attn_drop_out, tbytes, attn_l);                              \
+    else                                                                                       \
+      hipLaunchKernelGGL((gat_aggregate_lds_kernel<8, 2, DD, SM, true, RPV>), grid_1d(blocks),  \
+                         dim3(256), 0, stream, num_rows, head_dim, row_beg, row_end,           \
+                         accumulate, indices, row_order, el, er, ft, alpha, clamp_lo,          \
+                         clamp_hi, apply_exp, seed, seed_offset, thr, scale, out_ft, out_z,    \
+                         attn_out, attn_drop_out, tbytes, nullptr);                            \
+  } while (0)
         if (g_row_pol == 2) {
           if (drop) { if (small) DGLHIP_GATRP(true, true, 2); else DGLHIP_GATRP(true, false, 2); }
           else { if (small) DGLHIP_GATRP(false, true, 2); else DGLHIP_GATRP(false, false, 2); }
@@ -929,6 +1032,29 @@ int dglhip_set_gat_variant(int variant) {
   API_BEGIN();
   DGLHIP_CHECK(variant >= 0 && variant <= 3, "unknown GAT kernel variant " << variant);
   g_gat_variant = variant;
+  API_END();
+}
+
+int dglhip_set_gat_logit_recompute(int on) {
+  API_BEGIN();
+  g_gat_no_logit = on ? 0 : 1;
+  API_END();
+}
+
+int dglhip_gat_logits_device(int64_t num_nodes, int64_t num_heads, int64_t head_dim,
+                             const float* ft, const float* attn_l, const float* attn_r, float* el,
+                             float* er, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_nodes >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
+  const int64_t total = num_nodes * num_heads;
+  if (total == 0) return 0;
+  DGLHIP_CHECK(ft && attn_l && el && (attn_r == nullptr) == (er == nullptr),
+               "null pointer argument");
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(gat_logits_kernel, grid_1d((total + 255) / 256), dim3(256), 0, stream,
+                       total, num_heads, head_dim, ft, attn_l, attn_r, el, er);
+  });
   API_END();
 }
 

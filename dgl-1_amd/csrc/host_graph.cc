@@ -400,6 +400,43 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks, int64_t 
   API_END();
 }
 
+int dglhip_gat_logits_host(int64_t num_nodes, int64_t num_heads, int64_t head_dim,
+                           const float* ft, const float* attn_l, const float* attn_r, float* el,
+                           float* er, int num_threads) {
+#pragma clang fp contract(off)
+  API_BEGIN();
+  DGLHIP_CHECK(num_nodes >= 0 && num_heads >= 1 && head_dim >= 1, "bad sizes");
+  const int64_t total = num_nodes * num_heads, H = num_heads, D = head_dim;
+  if (total == 0) return 0;
+  DGLHIP_CHECK(ft && attn_l && el && (attn_r == nullptr) == (er == nullptr),
+               "null pointer argument");
+  // dglhip_gat_logits_device's association (gat_fused.hip, gat_logit)
+  auto logit = [D](const float* x, const float* a) {
+    if (D == 16) {
+      float p[8];
+      for (int l = 0; l < 8; ++l) {
+        const float m = x[2 * l] * a[2 * l];
+        p[l] = std::fma(x[2 * l + 1], a[2 * l + 1], m);
+      }
+      const float s01 = p[0] + p[1], s23 = p[2] + p[3], s45 = p[4] + p[5], s67 = p[6] + p[7];
+      const float s0123 = s01 + s23, s4567 = s45 + s67;
+      return s0123 + s4567;
+    }
+    float acc = 0.0f;
+    for (int64_t d = 0; d < D; ++d) acc = std::fma(x[d], a[d], acc);
+    return acc;
+  };
+  const int nt = num_threads > 0 ? num_threads : default_num_threads();
+  parallel_for(total, nt, [&](int64_t b0, int64_t b1, int) {
+    for (int64_t i = b0; i < b1; ++i) {
+      const int64_t h = i % H;
+      el[i] = logit(ft + i * D, attn_l + h * D);
+      if (er) er[i] = logit(ft + i * D, attn_r + h * D);
+    }
+  });
+  API_END();
+}
+
 int dglhip_distmult_score_host(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
                                int64_t num_rels, const int64_t* subj, const int64_t* rel,
                                const int64_t* obj, const float* h, const float* w_rel,

@@ -108,6 +108,13 @@ def _load():
                                                  _vp, ctypes.c_float, ctypes.c_float,
                                                  ctypes.c_float, _c_int, ctypes.c_float,
                                                  ctypes.c_uint64, _vp, _vp, _vp, _vp, _vp, _vp]),
+        "dglhip_gat_aggregate_logits_ranges_device": (
+            _c_int, [_c_i64] * 4 + [_vp, _vp, _c_int] + [_vp] * 6 +
+            [ctypes.c_float, ctypes.c_float, ctypes.c_float, _c_int, ctypes.c_float,
+             ctypes.c_uint64] + [_vp] * 6),
+        "dglhip_gat_logits_device": (_c_int, [_c_i64] * 3 + [_vp] * 6),
+        "dglhip_gat_logits_host": (_c_int, [_c_i64] * 3 + [_vp] * 5 + [_c_int]),
+        "dglhip_set_gat_logit_recompute": (_c_int, [_c_int]),
         "dglhip_gat_aggregate_ranges_device": (_c_int, [_c_i64, _c_i64, _c_i64, _c_i64, _vp,
                                                         _vp, _c_int, _vp, _vp, _vp, _vp, _vp,
                                                         ctypes.c_float, ctypes.c_float,

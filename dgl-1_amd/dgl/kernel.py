@@ -1884,7 +1884,8 @@ class _GATAggregate(torch.autograd.Function):
     dot, the copy_e gather, the attention's backward): same bits."""
 
     @staticmethod
-    def forward(ctx, adj, alpha, lo, hi, apply_exp, p, seed, seed_off, el, er, ft2, D, grad_mode):
+    def forward(ctx, adj, alpha, lo, hi, apply_exp, p, seed, seed_off, el, er, ft2, D, grad_mode,
+                attn_l=None):
         fwd = adj.fwd
         H = el.shape[1]
         F = ft2.shape[1]
@@ -1910,13 +1911,15 @@ class _GATAggregate(torch.autograd.Function):
                                None if a is not None else _GAT_BLOCK_BYTES_NOGRAD)
             if cuts is None:
                 cuts = [fwd.indptr, fwd.indptr[1:]]
+            # attn_l (el known to be gat_logits(ft, attn_l)): the 8 x 16
+            # blocked kernel recomputes each source's logit from its row
             for b in range(len(cuts) - 1):
-                check_call(LIB.dglhip_gat_aggregate_ranges_device(
+                check_call(LIB.dglhip_gat_aggregate_logits_ranges_device(
                     fwd.num_rows, ft2.shape[0], H, D, ptr(cuts[b]), ptr(cuts[b + 1]),
                     1 if b else 0, ptr(fwd.indices), ptr(fwd.row_order), ptr(el), ptr(er),
-                    ptr(ft2), float(alpha), float(lo), float(hi), 1 if apply_exp else 0,
-                    float(p), int(seed), ptr(seed_off), ptr(out_ft), ptr(out_z), ptr(a), ptr(w),
-                    _stream_of(dev)))
+                    ptr(ft2), ptr(attn_l), float(alpha), float(lo), float(hi),
+                    1 if apply_exp else 0, float(p), int(seed), ptr(seed_off), ptr(out_ft),
+                    ptr(out_z), ptr(a), ptr(w), _stream_of(dev)))
         else:  # host: the same per-edge values and chains from the host kernels
             a = _attention_slots(fwd, el, er, alpha, lo, hi, apply_exp)
             w = None
@@ -1944,7 +1947,7 @@ class _GATAggregate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_ft, d_z):
         if ctx.use_t:
-            return _gat_backward_t(ctx, d_ft, d_z)
+            return _gat_backward_t(ctx, d_ft, d_z) + (None,)
         ft2, a, w, el, er = ctx.saved_tensors
         adj = ctx.adj
         fwd = adj.fwd
@@ -2006,7 +2009,7 @@ class _GATAggregate(torch.autograd.Function):
                 d_el = _gat_el_grad(adj, g, H)
             if need_er and d_er is None:
                 d_er, _ = _run_gspmm(fwd, MSG_COPY_E, RED_SUM, None, g, H, H, False, emap=SLOT)
-        return (None,) * 8 + (d_el, d_er, d_ft2, None, None)
+        return (None,) * 8 + (d_el, d_er, d_ft2, None, None, None)
 
 
 def _gat_backward_t(ctx, d_ft, d_z):
@@ -2145,5 +2148,71 @@ def gat_aggregate(adj, ft, el, er, alpha=0.2, clamp=(-10.0, 10.0), attn_drop=0.0
             seed = int(torch.randint(0, 1 << 62, (1,)).item())
     ft_sum, z = _GATAggregate.apply(adj, float(alpha), float(clamp[0]), float(clamp[1]),
                                     bool(apply_exp), p, int(seed or 0), seed_off, el2, er2,
-                                    ft2, D, torch.is_grad_enabled())
+                                    ft2, D, torch.is_grad_enabled(), _logits_source(el, ft))
     return ft_sum.view(-1, H, D), z.view(-1, H, 1)
+
+
+class _GATLogits(torch.autograd.Function):
+    """(el, er) = ((ft * attn_l).sum(-1), (ft * attn_r).sum(-1)) per node and
+    head in the library's fixed association (dglhip_gat_logits_*); backward
+    in torch: d_ft = d_el * attn_l + d_er * attn_r, d_attn = sum_n d_e * ft."""
+
+    @staticmethod
+    def forward(ctx, ft, attn_l, attn_r):
+        N, H, D = ft.shape
+        el = torch.empty(N, H, dtype=torch.float32, device=ft.device)
+        er = torch.empty_like(el)
+        args = (N, H, D, ptr(ft), ptr(attn_l), ptr(attn_r), ptr(el), ptr(er))
+        if ft.is_cuda:
+            check_call(LIB.dglhip_gat_logits_device(*(args + (_stream_of(ft.device),))))
+        else:
+            check_call(LIB.dglhip_gat_logits_host(*(args + (0,))))
+        ctx.save_for_backward(ft, attn_l, attn_r)
+        return el, er
+
+    @staticmethod
+    def backward(ctx, d_el, d_er):
+        ft, attn_l, attn_r = ctx.saved_tensors
+        H, D = attn_l.shape
+        d_el = torch.zeros(ft.shape[:2], device=ft.device) if d_el is None else d_el
+        d_er = torch.zeros(ft.shape[:2], device=ft.device) if d_er is None else d_er
+        d_ft = d_attn_l = d_attn_r = None
+        if ctx.needs_input_grad[0]:
+            d_ft = d_el.unsqueeze(-1) * attn_l + d_er.unsqueeze(-1) * attn_r
+        if ctx.needs_input_grad[1]:
+            d_attn_l = (d_el.unsqueeze(-1) * ft).sum(0)
+        if ctx.needs_input_grad[2]:
+            d_attn_r = (d_er.unsqueeze(-1) * ft).sum(0)
+        return d_ft, d_attn_l, d_attn_r
+
+
+def gat_logits(ft, attn_l, attn_r):
+    """The GAT layer's attention logits (examples/pytorch/gat/train.py:66-67,
+    ``bmm(head_ft, attn_l)``): el, er (N, H, 1) with el[n, h] = sum_d
+    ft[n, h, d] * attn_l[h, d], in the library's association
+    (dglhip_gat_logits_*). Differentiable in ft, attn_l and attn_r. When
+    gat_aggregate is then given this el with the same ft, its 8-head x 16
+    source-blocked forward recomputes each source's logit from the feature
+    row it gathers anyway (same bits, a fifth fewer line requests)."""
+    N, H, D = ft.shape
+    ftc = _f32c(ft)
+    al = _f32c(attn_l.reshape(H, D))
+    ar = _f32c(attn_r.reshape(H, D))
+    el, er = _GATLogits.apply(ftc, al, ar)
+    el, er = el.view(N, H, 1), er.view(N, H, 1)
+    # what the aggregation may recompute el from: this ft (data, shape,
+    # version) and attn_l's values at this call
+    el._dglhip_logits = (ftc.data_ptr(), tuple(ftc.shape), ftc._version, al.detach().clone())
+    return el, er
+
+
+def _logits_source(el, ft):
+    """attn_l when ``el`` came from gat_logits(ft, attn_l, ...) on this very ft
+    (same data, shape and version) at 8 heads x 16 on a device, else None."""
+    tag = getattr(el, "_dglhip_logits", None)
+    if tag is None or not ft.is_cuda or tuple(ft.shape[1:]) != (8, 16):
+        return None
+    ptr_, shape, version, al = tag
+    if ft.data_ptr() != ptr_ or tuple(ft.shape) != shape or ft._version != version:
+        return None
+    return al if al.device == ft.device else None

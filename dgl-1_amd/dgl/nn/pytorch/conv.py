@@ -87,8 +87,10 @@ class GATConv(nn.Module):
     def forward(self, g, feat):
         h = self.feat_drop(feat) if self.feat_drop is not None else feat
         ft = self.fc(h).view(-1, self.num_heads, self.out_feats)
-        el = (ft * self.attn_l).sum(-1)  # N x H
-        er = (ft * self.attn_r).sum(-1)
+        # (ft * attn).sum(-1) in the library's association (kernel.gat_logits):
+        # with the same ft, gat_aggregate's blocked forward then recomputes
+        # each source's logit from its gathered row instead of reading el
+        el, er = kernel.gat_logits(ft, self.attn_l, self.attn_r)  # N x H x 1
         adj = g.sparse_adjacency(feat.device)
         # attention, its dropout, the weighted sum and the normaliser in one
         # kernel (kernel.gat_aggregate); the attention is kept, in CSR slot

@@ -66,14 +66,14 @@ class GraphAttention(nn.Module):
         if self.feat_drop is not None:
             h = self.feat_drop(h)
         ft = self.fc(h).reshape((h.shape[0], self.num_heads, -1))     # N x H x D
-        # the reference's bmm(head_ft, attn_l) (gat/train.py:66-67) as a
-        # broadcast product and a sum over D: the same values; its backward
+        # the reference's bmm(head_ft, attn_l) (gat/train.py:66-67) in the
+        # library (kernel.gat_logits: a fixed association; its backward
         # reduces attn's gradient over the nodes in torch's column reduction
-        # instead of a GEMM with an H x D x 1 output and a 19,717-deep K
-        # (0.1 ms per call on one workgroup per head, four per epoch)
-        H, D = self.num_heads, ft.shape[2]
-        a1 = (ft * self.attn_l.view(1, H, D)).sum(-1, keepdim=True)    # N x H x 1
-        a2 = (ft * self.attn_r.view(1, H, D)).sum(-1, keepdim=True)    # N x H x 1
+        # instead of a GEMM with an H x D x 1 output and a 19,717-deep K, 0.1 ms
+        # per call on one workgroup per head). Given the same ft (no feature
+        # dropout in between), the fused aggregation recomputes el from the
+        # rows it gathers
+        a1, a2 = kernel.gat_logits(ft, self.attn_l, self.attn_r)      # N x H x 1
         if self.feat_drop is not None:
             ft = self.feat_drop(ft)
         if self.udf:  # the reference's edge UDF (gat/train.py:90-96)

@@ -697,6 +697,34 @@ int dglhip_gat_attention_grad_logits_ranges_device(
     float clamp_hi, int apply_exp, float drop_scale, float drop_p, uint64_t seed,
     const int64_t* seed_offset, float* grad, float* grad_rowsum, void* stream);
 
+/* GAT logits el[n, h] = sum_d ft[n, h, d] * attn_l[h, d] (and er with attn_r;
+ * attn_r / er may both be NULL), ft [N, H, D], attn [H, D], el / er [N, H]:
+ * the reference's bmm(head_ft, attn_l) (gat/train.py:66-67) in a fixed
+ * association: at D = 16 the tree ((p0 + p1) + (p2 + p3)) + ((p4 + p5) +
+ * (p6 + p7)) with p_l = fma(x[2l+1], a[2l+1], x[2l] * a[2l]), else one fma
+ * chain over d. Host and device give the same bits. */
+int dglhip_gat_logits_device(int64_t num_nodes, int64_t num_heads, int64_t head_dim,
+                             const float* ft, const float* attn_l, const float* attn_r, float* el,
+                             float* er, void* stream);
+int dglhip_gat_logits_host(int64_t num_nodes, int64_t num_heads, int64_t head_dim,
+                           const float* ft, const float* attn_l, const float* attn_r, float* el,
+                           float* er, int num_threads);
+/* dglhip_gat_aggregate_ranges_device with attn_l [H, D] given: where the
+ * 8-head x 16 source-blocked kernel runs, each slot's el[u] is recomputed
+ * from the gathered ft[u] row in dglhip_gat_logits_device's association
+ * instead of gathered (4 lines per slot instead of 5). The caller guarantees
+ * el == dglhip_gat_logits(ft, attn_l) (the same bits then); attn_l NULL, or
+ * other shapes and schedules: the plain entry. */
+int dglhip_gat_aggregate_logits_ranges_device(
+    int64_t num_rows, int64_t num_src, int64_t num_heads, int64_t head_dim,
+    const int64_t* row_beg, const int64_t* row_end, int accumulate, const int32_t* indices,
+    const int32_t* row_order, const float* el, const float* er, const float* ft,
+    const float* attn_l, float alpha, float clamp_lo, float clamp_hi, int apply_exp,
+    float drop_p, uint64_t seed, const int64_t* seed_offset, float* out_ft, float* out_z,
+    float* attn_out, float* attn_drop_out, void* stream);
+/* Study knob: 0 makes the entry above ignore attn_l (el gathered; same bits). */
+int dglhip_set_gat_logit_recompute(int on);
+
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of indices (slot indices, the dropout hash and the
  * attention positions stay the CSR's); with accumulate != 0 both chains

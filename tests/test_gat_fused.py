@@ -537,3 +537,76 @@ def test_edge_attention_slope_from_the_logit_sign(device, order):
     ref = torch.autograd.grad((a64 * W.double()).sum(), (el64, er64))
     for x, r in zip(got, ref):
         assert bool(((x.double().cpu() - r).abs() <= 1e-5 * (r.abs() + 1.0) * 8).all())
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("H,D", [(8, 16), (8, 8), (2, 5)])
+def test_gat_logits_association_and_grads(device, H, D):
+    """kernel.gat_logits: el = (ft * attn_l).sum(-1) in the library's
+    association (a pairwise tree at D = 16, one fma chain otherwise), host ==
+    device, within 1e-6 of float64; gradients as torch's for the same
+    formula."""
+    dev = _dev(device)
+    gen = torch.Generator().manual_seed(31)
+    n = 700
+    ft = torch.randn(n, H, D, generator=gen)
+    al = torch.randn(H, D, 1, generator=gen)
+    ar = torch.randn(H, D, 1, generator=gen)
+    ft1, al1, ar1 = (t.to(dev).requires_grad_(True) for t in (ft, al, ar))
+    el, er = kernel.gat_logits(ft1, al1, ar1)
+    assert el.shape == (n, H, 1) and er.shape == (n, H, 1)
+    ref_l = (ft.double() * al.double().view(1, H, D)).sum(-1, keepdim=True)
+    ref_r = (ft.double() * ar.double().view(1, H, D)).sum(-1, keepdim=True)
+    mag = (ft.double().abs() * al.double().abs().view(1, H, D)).sum(-1, keepdim=True)
+    assert ((el.double().cpu() - ref_l).abs() <= 1e-6 * mag + 1e-30).all()
+    assert ((er.double().cpu() - ref_r).abs() <= 1e-6 * mag.max() + 1e-30).all()
+    if dev.type == "cuda":
+        el_h, er_h = kernel.gat_logits(ft, al, ar)
+        assert torch.equal(el.detach().cpu(), el_h) and torch.equal(er.detach().cpu(), er_h)
+    gl = torch.randn(n, H, 1, generator=gen).to(dev)
+    gr = torch.randn(n, H, 1, generator=gen).to(dev)
+    got = torch.autograd.grad((el * gl).sum() + (er * gr).sum(), (ft1, al1, ar1))
+    ft2, al2, ar2 = (t.detach().clone().to(dev).requires_grad_(True) for t in (ft, al, ar))
+    e2 = (ft2 * al2.view(1, H, D)).sum(-1, keepdim=True)
+    r2 = (ft2 * ar2.view(1, H, D)).sum(-1, keepdim=True)
+    want = torch.autograd.grad((e2 * gl).sum() + (r2 * gr).sum(), (ft2, al2, ar2))
+    for x, y in zip(got, want):
+        assert torch.allclose(x, y, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.5])
+def test_gat_forward_recomputes_logits_same_bits(p):
+    """With el from kernel.gat_logits on the same ft, the 8 x 16 source-blocked
+    forward recomputes every source's logit from its gathered row
+    (dglhip_gat_aggregate_logits_ranges_device) instead of reading el: the
+    outputs and every gradient equal the el-reading kernel's bit for bit."""
+    dev = _dev("cuda")
+    n, m = 60_000, 6_000_000
+    gen = torch.Generator().manual_seed(33)
+    src = torch.randint(0, n, (m,), generator=gen)
+    dst = torch.randint(0, n, (m,), generator=gen)
+    order = torch.from_numpy(np.lexsort((dst.numpy(), src.numpy())))  # source-major
+    g = dgl.DGLGraph((src[order], dst[order]))
+    adj = g.sparse_adjacency(dev)
+    ft0 = torch.randn(n, 8, 16, generator=gen) * 0.5
+    al0 = torch.randn(8, 16, 1, generator=gen) * 0.3
+    ar0 = torch.randn(8, 16, 1, generator=gen) * 0.3
+    R = torch.randn(n, 8, 16, generator=gen).to(dev)
+    S = torch.randn(n, 8, 1, generator=gen).to(dev)
+    cuts = kernel._block_cuts(adj.fwd, (128 + 8) * 4, None)
+    assert cuts is not None and len(cuts) > 2  # the source-blocked forward
+    res = []
+    for recompute in (True, False):
+        kernel.LIB.dglhip_set_gat_logit_recompute(1 if recompute else 0)
+        try:
+            ft, al, ar = (t.to(dev).requires_grad_(True) for t in (ft0, al0, ar0))
+            el, er = kernel.gat_logits(ft, al, ar)
+            assert kernel._logits_source(el, ft) is not None
+            fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, attn_drop=p, seed=77)
+            grads = torch.autograd.grad((fs * R).sum() + (z * S).sum(), (ft, al, ar))
+        finally:
+            kernel.LIB.dglhip_set_gat_logit_recompute(1)
+        res.append([fs.detach(), z.detach()] + [x.detach() for x in grads])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
