@@ -136,31 +136,32 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
     gen = torch.Generator(device=dev)
     gen.manual_seed(5)
     ft = (torch.rand(n, H, D, generator=gen, device=dev) * 2 - 1).requires_grad_(True)
-    # the layer's attention vectors: el, er = gat_logits(ft, attn_l, attn_r)
-    # inside the step, as the layer computes them (gat/train.py:66-67)
-    al = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
-    ar = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
+    el = (torch.rand(n, H, generator=gen, device=dev) - 0.5).requires_grad_(True)
+    er = (torch.rand(n, H, generator=gen, device=dev) - 0.5).requires_grad_(True)
     gout = torch.rand(n, H, D, generator=gen, device=dev)
     gz = torch.rand(n, H, 1, generator=gen, device=dev)
 
     def step():
-        el, er = kernel.gat_logits(ft, al, ar)
         fs, z = kernel.gat_aggregate(adj, ft, el, er)
         torch.autograd.backward([fs, z], [gout, gz])
-        ft.grad = al.grad = ar.grad = None
+        ft.grad = el.grad = er.grad = None
     ms, kms, launches = wall_steps(step, steps, warmup, dev, kernel)
-    el, er = kernel.gat_logits(ft, al, ar)
-    recompute = kernel._logits_source(el, ft) is not None
 
     def fwd():
         kernel.gat_aggregate(adj, ft, el, er)  # training forward
     fms = call_ms(fwd, steps, dev)
-    # the same forward with the sources' logits gathered (the study knob)
-    kernel.LIB.dglhip_set_gat_logit_recompute(0)
+    # study: the forward with el from gat_logits(ft, attn_l, attn_r) and the
+    # sources' logits recomputed from their gathered rows (off by default:
+    # slower)
+    al = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
+    ar = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
+    el_t, er_t = kernel.gat_logits(ft, al, ar)
+    kernel.LIB.dglhip_set_gat_logit_recompute(1)
     try:
-        fms_gathered = call_ms(fwd, steps, dev)
+        fms_recomputed = call_ms(lambda: kernel.gat_aggregate(adj, ft, el_t, er_t), steps, dev)
     finally:
-        kernel.LIB.dglhip_set_gat_logit_recompute(1)
+        kernel.LIB.dglhip_set_gat_logit_recompute(0)
+    del el_t, er_t
     # the one-pass transposed backward recomputes the attention: nothing stored
     stored = kernel.LIB.dglhip_gat_backward_t_ok(H, D) != 1
     # the forward's row ranges as gat_aggregate cuts them (nothing stored:
@@ -173,17 +174,14 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
     bpeak, bsrc = gather_peak(n * H * D * 4, 0 if bplan is None else len(bplan))
     res = {"value": E / (ms * 1e-3), "unit": "edges/s (fwd+bwd)", "ms_per_step": ms,
            "kernel_ms": kms, "launches_per_step": launches, "steps": steps, "warmup": warmup,
-           "config": "GAT layer, %d heads x %d, on the headline graph (%d nodes, %d edges): "
-                     "el, er = kernel.gat_logits(ft, attn_l, attn_r), then "
-                     "kernel.gat_aggregate forward + backward, dropout 0" % (H, D, n, E),
-           "forward_ms_logits_gathered": fms_gathered,
-           "roofline": roof(gat_fwd_bytes(E, n, H, D, stored, logits_read=not recompute), fms,
-                            peak, src,
-                            "fused GAT forward (dglhip_gat_aggregate_logits_ranges_device%s%s)"
+           "config": "GAT layer aggregation, %d heads x %d, on the headline graph (%d nodes, "
+                     "%d edges): kernel.gat_aggregate forward + backward, dropout 0"
+                     % (H, D, n, E),
+           "forward_ms_logits_recomputed": fms_recomputed,
+           "roofline": roof(gat_fwd_bytes(E, n, H, D, stored), fms, peak, src,
+                            "fused GAT forward (dglhip_gat_aggregate_device%s)"
                             % (", attention stored for the backward" if stored else
-                               "; the backward recomputes the attention",
-                               "; each source's logits recomputed from its gathered row"
-                               if recompute else "")),
+                               "; the backward recomputes the attention")),
            "cpu_baseline": None}
     if not stored:
         # the backward's kernels (the transposed pass and d_er's row sums): the

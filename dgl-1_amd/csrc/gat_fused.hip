@@ -51,9 +51,13 @@ int g_gat_variant = 0;
 // 3 16-B write-through stores regrouped through LDS);
 // bit 2 the kernel built for 5 waves per SIMD (96 VGPRs) instead of 4 (97)
 int g_gat_bwd_variant = 0;
-// study knob: 1 ignores attn_l in dglhip_gat_aggregate_logits_ranges_device
-// (el gathered as before; same bits)
-int g_gat_no_logit = 0;
+// study knob (dglhip_set_gat_logit_recompute): 1 lets
+// dglhip_gat_aggregate_logits_ranges_device recompute the sources' logits
+// from their gathered rows. Off by default: on the Reddit-shaped 8 x 16 layer
+// the forward ran 5.93 ms against 5.12 with the logits gathered (r05) — the
+// attention then waits for the rows instead of being computed while they
+// are in flight, which costs more than the fifth line per slot saves.
+int g_gat_logit_on = 0;
 
 // One row of VEC floats per lane through a buffer descriptor built from the
 // wave-uniform row address: a 32-bit per-lane byte offset instead of a 64-bit
@@ -832,7 +836,7 @@ int dglhip_gat_aggregate_logits_ranges_device(
       // the running rows' cache policy (dglhip_set_row_policy) on the 8-head
       // two-float shape (the Reddit-shaped 8 x 16 layer); with attn_l the
       // sources' logits recomputed from their gathered rows (LOGIT)
-      const bool logit = attn_l != nullptr && head_dim == 16 && !g_gat_no_logit;
+      const bool logit = attn_l != nullptr && head_dim == 16 && g_gat_logit_on;
       timed_launch(stream, [&] {
 #define DGLHIP_GATRP(DD, SM, RPV)                                                              \
   do {                                                                                         \
@@ -1037,7 +1041,7 @@ int dglhip_set_gat_variant(int variant) {
 
 int dglhip_set_gat_logit_recompute(int on) {
   API_BEGIN();
-  g_gat_no_logit = on ? 0 : 1;
+  g_gat_logit_on = on ? 1 : 0;
   API_END();
 }
 

@@ -709,12 +709,14 @@ int dglhip_gat_logits_device(int64_t num_nodes, int64_t num_heads, int64_t head_
 int dglhip_gat_logits_host(int64_t num_nodes, int64_t num_heads, int64_t head_dim,
                            const float* ft, const float* attn_l, const float* attn_r, float* el,
                            float* er, int num_threads);
-/* dglhip_gat_aggregate_ranges_device with attn_l [H, D] given: where the
- * 8-head x 16 source-blocked kernel runs, each slot's el[u] is recomputed
- * from the gathered ft[u] row in dglhip_gat_logits_device's association
- * instead of gathered (4 lines per slot instead of 5). The caller guarantees
- * el == dglhip_gat_logits(ft, attn_l) (the same bits then); attn_l NULL, or
- * other shapes and schedules: the plain entry. */
+/* dglhip_gat_aggregate_ranges_device with attn_l [H, D] given: with the
+ * recompute switched on (dglhip_set_gat_logit_recompute(1); off by default,
+ * slower on the Reddit-shaped layer: DESIGN.md §4.2.1) and where the 8-head x
+ * 16 source-blocked kernel runs, each slot's el[u] is recomputed from the
+ * gathered ft[u] row in dglhip_gat_logits_device's association instead of
+ * gathered (4 lines per slot instead of 5). The caller guarantees el ==
+ * dglhip_gat_logits(ft, attn_l) (the same bits then); otherwise the plain
+ * entry. */
 int dglhip_gat_aggregate_logits_ranges_device(
     int64_t num_rows, int64_t num_src, int64_t num_heads, int64_t head_dim,
     const int64_t* row_beg, const int64_t* row_end, int accumulate, const int32_t* indices,
@@ -722,7 +724,7 @@ int dglhip_gat_aggregate_logits_ranges_device(
     const float* attn_l, float alpha, float clamp_lo, float clamp_hi, int apply_exp,
     float drop_p, uint64_t seed, const int64_t* seed_offset, float* out_ft, float* out_z,
     float* attn_out, float* attn_drop_out, void* stream);
-/* Study knob: 0 makes the entry above ignore attn_l (el gathered; same bits). */
+/* Study knob: 1 switches the recompute above on (default 0; same bits). */
 int dglhip_set_gat_logit_recompute(int on);
 
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are

@@ -577,7 +577,8 @@ def test_gat_logits_association_and_grads(device, H, D):
 @pytest.mark.gpu
 @pytest.mark.parametrize("p", [0.0, 0.5])
 def test_gat_forward_recomputes_logits_same_bits(p):
-    """With el from kernel.gat_logits on the same ft, the 8 x 16 source-blocked
+    """With el from kernel.gat_logits on the same ft and the recompute switched
+    on (a study knob, off by default: slower), the 8 x 16 source-blocked
     forward recomputes every source's logit from its gathered row
     (dglhip_gat_aggregate_logits_ranges_device) instead of reading el: the
     outputs and every gradient equal the el-reading kernel's bit for bit."""
@@ -606,7 +607,7 @@ def test_gat_forward_recomputes_logits_same_bits(p):
             fs, z = kernel.gat_aggregate(adj, ft, el, er, 0.2, attn_drop=p, seed=77)
             grads = torch.autograd.grad((fs * R).sum() + (z * S).sum(), (ft, al, ar))
         finally:
-            kernel.LIB.dglhip_set_gat_logit_recompute(1)
+            kernel.LIB.dglhip_set_gat_logit_recompute(0)
         res.append([fs.detach(), z.detach()] + [x.detach() for x in grads])
     for a, b in zip(*res):
         assert torch.equal(a, b)
