@@ -156,11 +156,11 @@ def gat_layer_leg(g, dev, kernel, gather_peak, sample, steps=10, warmup=3, H=8, 
     al = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
     ar = ((torch.rand(H, D, 1, generator=gen, device=dev) - 0.5) * 0.25).requires_grad_(True)
     el_t, er_t = kernel.gat_logits(ft, al, ar)
-    kernel.LIB.dglhip_set_gat_logit_recompute(1)
+    kernel.check_call(kernel.LIB.dglhip_set_gat_logit_recompute(1))
     try:
         fms_recomputed = call_ms(lambda: kernel.gat_aggregate(adj, ft, el_t, er_t), steps, dev)
     finally:
-        kernel.LIB.dglhip_set_gat_logit_recompute(0)
+        kernel.check_call(kernel.LIB.dglhip_set_gat_logit_recompute(0))
     del el_t, er_t
     # the one-pass transposed backward recomputes the attention: nothing stored
     stored = kernel.LIB.dglhip_gat_backward_t_ok(H, D) != 1

@@ -2201,8 +2201,10 @@ def gat_logits(ft, attn_l, attn_r):
     el, er = _GATLogits.apply(ftc, al, ar)
     el, er = el.view(N, H, 1), er.view(N, H, 1)
     # what the aggregation may recompute el from: this ft (data, shape,
-    # version) and attn_l's values at this call
-    el._dglhip_logits = (ftc.data_ptr(), tuple(ftc.shape), ftc._version, al.detach().clone())
+    # version) and attn_l's values at this call; el's own version too (an
+    # in-place change of el voids the tag)
+    el._dglhip_logits = (ftc.data_ptr(), tuple(ftc.shape), ftc._version, el._version,
+                         al.detach().clone())
     return el, er
 
 
@@ -2212,7 +2214,8 @@ def _logits_source(el, ft):
     tag = getattr(el, "_dglhip_logits", None)
     if tag is None or not ft.is_cuda or tuple(ft.shape[1:]) != (8, 16):
         return None
-    ptr_, shape, version, al = tag
-    if ft.data_ptr() != ptr_ or tuple(ft.shape) != shape or ft._version != version:
+    ptr_, shape, version, el_version, al = tag
+    if (ft.data_ptr() != ptr_ or tuple(ft.shape) != shape or ft._version != version or
+            el._version != el_version):
         return None
     return al if al.device == ft.device else None

@@ -611,3 +611,22 @@ def test_gat_forward_recomputes_logits_same_bits(p):
         res.append([fs.detach(), z.detach()] + [x.detach() for x in grads])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_gat_logits_tag_follows_versions():
+    """gat_aggregate may only recompute el from ft when el is gat_logits'
+    unchanged output for that very ft: another ft, an in-place change of ft
+    or of el voids the tag (kernel._logits_source)."""
+    ft = torch.randn(50, 8, 16)
+    al, ar = torch.randn(8, 16, 1), torch.randn(8, 16, 1)
+    el, _ = kernel.gat_logits(ft, al, ar)
+    # (host tensors: the recompute is a device path, so the tag reads None here;
+    # check the tag's fields directly)
+    tag = el._dglhip_logits
+    assert tag[0] == ft.data_ptr() and tag[1] == tuple(ft.shape)
+    assert tag[2] == ft._version and tag[3] == el._version
+    ft.add_(0.0)
+    assert ft._version != tag[2]
+    el2, _ = kernel.gat_logits(ft, al, ar)
+    el2.mul_(1.0)
+    assert el2._version != el2._dglhip_logits[3]
