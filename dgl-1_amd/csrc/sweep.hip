@@ -1,0 +1,401 @@
+// Source-swept g-SpMM (copy_u + sum / mean, fp32 rows of 64 * VEC floats):
+// one launch per "generation" of destination rows whose running sums live in
+// LDS, each wave walking its rows' slots source block by source block.
+//
+// The source-blocked schedule (spmm_plan.cc) gets the L2 hit
+// rate of small source slices by running one launch per slice; each launch
+// re-reads and re-writes every row's running sum (19 passes over the 119 MB
+// output on the Reddit-shaped graph) and ends on its longest items. Here a
+// wave owns up to RPW rows for the whole launch and keeps their sums in LDS
+// (160 KB per CU: 320 rows of 512 B), so a block boundary costs an LDS read and
+// write instead of an HBM-side pass, and all waves of a launch sweep the same
+// blocks in the same order (they start together and carry the same work per
+// block, rows being dealt to waves in a snake over the degree-descending order).
+//
+// Chain order: every row's slots are taken strictly in slot order. In block b
+// a wave advances a row's cursor over the slots whose source lies below block
+// b's end, stopping at the first that does not; the last block takes the
+// rest. So the sum is the one-launch kernel's chain for ANY edge order (a row
+// whose sources go back down just does part of its work in a later block) —
+// the blocked schedule's precondition (source-monotone chains) only decides
+// how well the L2s serve the gathers, not the bits.
+//
+// Reference: the product this evaluates is the COO spmm of
+// python/dgl/backend/pytorch/tensor.py:145-146 on the adjacency of
+// src/graph/graph.cc:509-524; the chain is the oracle's
+// (oracle/spmm_oracle.c).
+#include <hip/hip_runtime.h>
+
+#include <climits>
+
+#include "gspmm_impl.h"
+
+namespace dglhip {
+namespace {
+
+constexpr int kSweepWaves = 4;  // waves per workgroup
+
+__device__ __forceinline__ int32_t lane_of(int32_t v, int j) {
+  return __builtin_amdgcn_readlane(v, j);
+}
+
+// Kernel arguments: rows [0, num_rows) of the CSR (indptr, indices) are dealt
+// to waves_total waves over all launches of one call; this launch runs waves
+// [wave_base, wave_base + gridDim.x * 4). Source block b covers columns
+// [lo + b * bs, lo + (b + 1) * bs); block nblocks - 1 takes everything left.
+template <int VEC, int RPW, int UNROLL, bool MEAN>
+__global__ __launch_bounds__(256) void gspmm_sweep_kernel(
+    int64_t num_rows, int64_t waves_total, int64_t wave_base,
+    const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+    const float* __restrict__ ufeat, float* __restrict__ out,
+    const int32_t* __restrict__ row_order, int64_t lo, int64_t bs, int nblocks) {
+  typedef typename Vec<VEC>::T V;
+  constexpr int F = 64 * VEC;
+  __shared__ float sums[kSweepWaves * RPW * F];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t wv = wave_base + int64_t(blockIdx.x) * kSweepWaves + w;
+  const int64_t f0 = int64_t(lane) * VEC;
+  // lane j < RPW describes the wave's j-th row: round j of a snake deal of
+  // the degree-descending rows over all waves (rows are a prefix of the lanes)
+  int32_t row = -1, len = 0, cur = 0, beg_lo = 0, beg_hi = 0;
+  if (lane < RPW && wv < waves_total) {
+    const int64_t pos = (lane & 1) ? (waves_total - 1 - wv) : wv;
+    const int64_t i = int64_t(lane) * waves_total + pos;
+    if (i < num_rows) {
+      row = row_order ? row_order[i] : static_cast<int32_t>(i);
+      const int64_t b = indptr[row];
+      len = static_cast<int32_t>(indptr[row + 1] - b);
+      beg_lo = static_cast<int32_t>(b);
+      beg_hi = static_cast<int32_t>(b >> 32);
+    }
+  }
+  const int nrows = __builtin_popcountll(__ballot(row >= 0));
+  float* my = sums + w * RPW * F;
+  for (int j = 0; j < nrows; ++j) stv<VEC>(my + j * F + f0, Vec<VEC>::zero());
+
+  // a row's slot chunk: the column ids of its next min(64, left) slots
+  auto chunk = [&](int j, int32_t c, int32_t n_all) -> int32_t {
+    const int64_t beg = (int64_t(lane_of(beg_hi, j)) << 32) |
+                        static_cast<uint32_t>(lane_of(beg_lo, j));
+    return lane < n_all - c ? indices[beg + c + lane] : INT_MAX;
+  };
+  // the next visit's first chunk is loaded before this visit's gathers, so
+  // its latency hides behind them (not with one row: its cursor moves)
+  int32_t pre = INT_MAX;
+  bool have_pre = false;
+  for (int b = 0; b < nblocks; ++b) {
+    const int64_t bend = (b == nblocks - 1) ? INT64_MAX : lo + int64_t(b + 1) * bs;
+    for (int j = 0; j < nrows; ++j) {
+      const int32_t c0 = lane_of(cur, j);
+      const int32_t n_all = lane_of(len, j);
+      const bool had = have_pre;
+      have_pre = false;
+      if (c0 >= n_all) continue;
+      int32_t col = had ? pre : chunk(j, c0, n_all);
+      if (nrows > 1 && !(j + 1 == nrows && b + 1 == nblocks)) {
+        const int jn = j + 1 < nrows ? j + 1 : 0;
+        const int32_t cn = lane_of(cur, jn), ln = lane_of(len, jn);
+        if (cn < ln) {
+          pre = chunk(jn, cn, ln);
+          have_pre = true;
+        }
+      }
+      V acc = ldv<VEC>(my + j * F + f0);
+      int32_t c = c0;
+      while (true) {
+        const int32_t avail = min(64, n_all - c);
+        const uint64_t ok = __ballot(lane < avail && int64_t(col) < bend);
+        const int n = ~ok == 0 ? 64 : __builtin_ctzll(~ok);
+        int t = 0;
+        for (; t + UNROLL <= n; t += UNROLL) {
+          V s[UNROLL];
+#pragma unroll
+          for (int u = 0; u < UNROLL; ++u)
+            s[u] = gather_row_buf<VEC>(ufeat + int64_t(lane_of(col, t + u)) * F, F, f0);
+#pragma unroll
+          for (int u = 0; u < UNROLL; ++u) acc += s[u];
+        }
+        if (t < n) {
+          // the last n - t < UNROLL slots as one predicated batch
+          const int rem = n - t;
+          V s[UNROLL];
+#pragma unroll
+          for (int u = 0; u < UNROLL - 1; ++u)
+            if (u < rem)
+              s[u] = gather_row_buf<VEC>(ufeat + int64_t(lane_of(col, t + u)) * F, F, f0);
+#pragma unroll
+          for (int u = 0; u < UNROLL - 1; ++u)
+            if (u < rem) acc += s[u];
+        }
+        c += n;
+        if (n < avail || c >= n_all) break;
+        col = chunk(j, c, n_all);
+      }
+      stv<VEC>(my + j * F + f0, acc);
+      if (lane == j) cur = c;
+    }
+  }
+  for (int j = 0; j < nrows; ++j) {
+    const int32_t r = lane_of(row, j);
+    V acc = ldv<VEC>(my + j * F + f0);
+    if (MEAN) {
+      const int32_t d = lane_of(len, j);
+      if (d > 1) acc = acc / Vec<VEC>::splat(static_cast<float>(d));
+    }
+    stv<VEC>(out + int64_t(r) * F + f0, acc);
+  }
+}
+
+// Streamed variant: the slots are laid out per (launch, block, wave, row) by
+// the host (tools/r05/sweep_study.py builds the layout), so a wave's work in
+// block b is one contiguous run of column ids lay[seg_beg[wave, b] ...]
+// holding its rows' block-b slots back to back (counts[row, b] each). The
+// gathers stream through it in batches of UNROLL across row boundaries; the
+// running sum switches rows (LDS store + load) where a row's run ends. Exact
+// for source-monotone chains (each row's block-b slots contiguous in slot
+// order), which the layout builder checks.
+template <int VEC, int RPW, int UNROLL, bool MEAN>
+__global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
+    int64_t num_rows, int64_t waves_total, int64_t wave_base,
+    const int32_t* __restrict__ row_order, const int32_t* __restrict__ counts, int nblocks,
+    const int64_t* __restrict__ seg_beg, const int32_t* __restrict__ lay,
+    const int64_t* __restrict__ indptr, const float* __restrict__ ufeat,
+    float* __restrict__ out, int* __restrict__ arrive, int lag, int max_spin) {
+  typedef typename Vec<VEC>::T V;
+  constexpr int F = 64 * VEC;
+  __shared__ float sums[kSweepWaves * RPW * F];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t wv = wave_base + int64_t(blockIdx.x) * kSweepWaves + w;
+  const int64_t f0 = int64_t(lane) * VEC;
+  const int need = static_cast<int>(gridDim.x) * kSweepWaves;
+  // soft barrier: a wave starts block b once every wave of the launch has
+  // finished block b - lag (device-scope counters, one per block), or after
+  // max_spin polls — the results never depend on it, only the L2 locality
+  auto arrive_at = [&](int b) {
+    if (lag > 0 && lane == 0)
+      __hip_atomic_fetch_add(arrive + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto wait_for = [&](int b) {
+    if (lag <= 0 || b < lag) return;
+    for (int spin = 0; spin < max_spin; ++spin) {
+      int seen = 0;
+      if (lane == 0)
+        seen = __hip_atomic_fetch_add(arrive + (b - lag), 0, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_readfirstlane(seen) >= need) return;
+      __builtin_amdgcn_s_sleep(8);
+    }
+  };
+  int32_t row = -1, deg = 0;
+  if (lane < RPW && wv < waves_total) {
+    const int64_t pos = (lane & 1) ? (waves_total - 1 - wv) : wv;
+    const int64_t i = int64_t(lane) * waves_total + pos;
+    if (i < num_rows) {
+      row = row_order ? row_order[i] : static_cast<int32_t>(i);
+      if (MEAN) deg = static_cast<int32_t>(indptr[row + 1] - indptr[row]);
+    }
+  }
+  const int nrows = __builtin_popcountll(__ballot(row >= 0));
+  if (nrows == 0) {
+    for (int b = 0; b < nblocks; ++b) arrive_at(b);
+    return;
+  }
+  float* my = sums + w * RPW * F;
+  for (int j = 0; j < nrows; ++j) stv<VEC>(my + j * F + f0, Vec<VEC>::zero());
+  int32_t cnt_next = row >= 0 ? counts[int64_t(row) * nblocks] : 0;
+  int64_t base_next = seg_beg[wv * nblocks];
+  for (int b = 0; b < nblocks; ++b) {
+    const int32_t cnt = cnt_next;
+    // uniform by construction; said so, the column ids load through SGPRs
+    const int32_t* run = lay + ((int64_t(__builtin_amdgcn_readfirstlane(
+                                     static_cast<int32_t>(base_next >> 32))) << 32) |
+                                static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+                                    static_cast<int32_t>(base_next))));
+    if (b + 1 < nblocks) {
+      cnt_next = row >= 0 ? counts[int64_t(row) * nblocks + b + 1] : 0;
+      base_next = seg_beg[wv * nblocks + b + 1];
+    }
+    int32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    const int32_t total = lane_of(incl, 63);
+    wait_for(b);
+    if (total == 0) {
+      arrive_at(b);
+      continue;
+    }
+    const uint64_t live = __ballot(cnt > 0);
+    int j = __builtin_ctzll(live);
+    int32_t rend = lane_of(incl, j);
+    V acc = ldv<VEC>(my + j * F + f0);
+    for (int32_t t = 0; t < total; t += UNROLL) {
+      const int rem = min(UNROLL, total - t);
+      V s[UNROLL];
+      if (rem == UNROLL) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+          s[u] = gather_row_buf<VEC>(ufeat + int64_t(run[t + u]) * F, F, f0);
+      } else {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+          if (u < rem) s[u] = gather_row_buf<VEC>(ufeat + int64_t(run[t + u]) * F, F, f0);
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        if (u < rem) {
+          if (t + u == rend) {
+            stv<VEC>(my + j * F + f0, acc);
+            j = __builtin_ctzll(live & (~0ull << (j + 1)));
+            rend = lane_of(incl, j);
+            acc = ldv<VEC>(my + j * F + f0);
+          }
+          acc += s[u];
+        }
+      }
+    }
+    stv<VEC>(my + j * F + f0, acc);
+    arrive_at(b);
+  }
+  for (int j = 0; j < nrows; ++j) {
+    const int32_t r = lane_of(row, j);
+    V acc = ldv<VEC>(my + j * F + f0);
+    if (MEAN) {
+      const int32_t d = lane_of(deg, j);
+      if (d > 1) acc = acc / Vec<VEC>::splat(static_cast<float>(d));
+    }
+    stv<VEC>(out + int64_t(r) * F + f0, acc);
+  }
+}
+
+template <typename K>
+int64_t sweep_waves_per_launch(K kern) {
+  int dev = 0, cus = 0, per_cu = 0;
+  HIP_CALL(hipGetDevice(&dev));
+  HIP_CALL(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CALL(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kSweepWaves, 0));
+  DGLHIP_CHECK(cus > 0 && per_cu > 0, "sweep kernel does not fit a CU");
+  return int64_t(cus) * per_cu * kSweepWaves;
+}
+
+template <int RPW>
+auto stream_kernel(bool mean) {
+  return mean ? gspmm_sweep_stream_kernel<2, RPW, 16, true>
+              : gspmm_sweep_stream_kernel<2, RPW, 16, false>;
+}
+
+template <int VEC, int RPW, bool MEAN>
+void launch_sweep(int64_t num_rows, const int64_t* indptr, const int32_t* indices,
+                  const float* ufeat, float* out, const int32_t* row_order, int64_t lo,
+                  int64_t bs, int nblocks, hipStream_t stream) {
+  constexpr int UNROLL = 16;
+  auto kern = gspmm_sweep_kernel<VEC, RPW, UNROLL, MEAN>;
+  int dev = 0, cus = 0, per_cu = 0;
+  HIP_CALL(hipGetDevice(&dev));
+  HIP_CALL(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  HIP_CALL(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kSweepWaves, 0));
+  DGLHIP_CHECK(cus > 0 && per_cu > 0, "sweep kernel does not fit a CU");
+  // one launch = every workgroup resident at once, so its waves sweep the
+  // source blocks together
+  const int64_t wgs = int64_t(cus) * per_cu;
+  const int64_t rows_per_launch = wgs * kSweepWaves * RPW;
+  const int64_t launches = (num_rows + rows_per_launch - 1) / rows_per_launch;
+  const int64_t waves_total = launches * wgs * kSweepWaves;
+  for (int64_t l = 0; l < launches; ++l) {
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(wgs)), dim3(64 * kSweepWaves), 0, stream,
+                         num_rows, waves_total, l * wgs * kSweepWaves, indptr, indices, ufeat,
+                         out, row_order, lo, bs, nblocks);
+    });
+  }
+}
+
+}  // namespace
+}  // namespace dglhip
+
+using namespace dglhip;
+
+extern "C" {
+
+int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t* indptr,
+                              const int32_t* indices, const float* ufeat, float* out,
+                              const int32_t* row_order, int64_t col_lo, int64_t block_cols,
+                              int num_blocks, int mean, int rows_per_wave, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && num_rows < (int64_t(1) << 31), "row count " << num_rows);
+  DGLHIP_CHECK(num_blocks >= 1 && block_cols >= 1 && col_lo >= 0,
+               "blocks " << num_blocks << " of " << block_cols << " columns from " << col_lo);
+  DGLHIP_CHECK(feat_len == 64 || feat_len == 128 || feat_len == 256,
+               "sweep rows are 64, 128 or 256 floats, not " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && out && (ufeat || indices == nullptr), "null indptr/ufeat/out");
+  const int rpw = rows_per_wave > 0 ? rows_per_wave : 20;
+  const bool m = mean != 0;
+#define DGLHIP_SWEEP(VEC, R)                                                                 \
+  do {                                                                                       \
+    if (m) launch_sweep<VEC, R, true>(num_rows, indptr, indices, ufeat, out, row_order,      \
+                                      col_lo, block_cols, num_blocks, stream);               \
+    else launch_sweep<VEC, R, false>(num_rows, indptr, indices, ufeat, out, row_order,       \
+                                     col_lo, block_cols, num_blocks, stream);                \
+  } while (0)
+  if (feat_len == 128) {
+    DGLHIP_CHECK(rpw == 10 || rpw == 20, "rows per wave " << rpw << " at 128 floats: 10 or 20");
+    if (rpw == 10) DGLHIP_SWEEP(2, 10);
+    else DGLHIP_SWEEP(2, 20);
+  } else if (feat_len == 64) {
+    DGLHIP_CHECK(rpw == 20 || rpw == 40, "rows per wave " << rpw << " at 64 floats: 20 or 40");
+    if (rpw == 20) DGLHIP_SWEEP(1, 20);
+    else DGLHIP_SWEEP(1, 40);
+  } else {
+    DGLHIP_CHECK(rpw == 5 || rpw == 10, "rows per wave " << rpw << " at 256 floats: 5 or 10");
+    if (rpw == 5) DGLHIP_SWEEP(4, 5);
+    else DGLHIP_SWEEP(4, 10);
+  }
+#undef DGLHIP_SWEEP
+  API_END();
+}
+
+int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch) {
+  API_BEGIN();
+  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 20, "rows per wave " << rows_per_wave);
+  *waves_per_launch = rows_per_wave == 10 ? sweep_waves_per_launch(stream_kernel<10>(false))
+                                          : sweep_waves_per_launch(stream_kernel<20>(false));
+  API_END();
+}
+
+int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
+                                     const int32_t* row_order, const int32_t* counts,
+                                     int num_blocks, const int64_t* seg_beg, const int32_t* lay,
+                                     const int64_t* indptr, const float* ufeat, float* out,
+                                     int mean, int rows_per_wave, int* arrive, int lag,
+                                     int max_spin, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 20, "rows per wave " << rows_per_wave);
+  DGLHIP_CHECK(num_rows >= 0 && num_rows < (int64_t(1) << 31) && num_blocks >= 1, "sizes");
+  if (num_rows == 0) return 0;
+  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mean != 0) : stream_kernel<20>(mean != 0);
+  const int64_t wpl = sweep_waves_per_launch(kern);
+  DGLHIP_CHECK(waves_total % wpl == 0 && waves_total * rows_per_wave >= num_rows,
+               "layout for " << waves_total << " waves, launches hold " << wpl);
+  DGLHIP_CHECK(lag <= 0 || arrive, "the soft barrier needs its counters");
+  const int64_t launches = waves_total / wpl;
+  if (lag > 0)  // launches x num_blocks counters
+    HIP_CALL(hipMemsetAsync(arrive, 0, sizeof(int) * launches * num_blocks, stream));
+  for (int64_t l = 0; l < launches; ++l) {
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(wpl / kSweepWaves)),
+                         dim3(64 * kSweepWaves), 0, stream, num_rows, waves_total, l * wpl,
+                         row_order, counts, num_blocks, seg_beg, lay, indptr, ufeat, out,
+                         lag > 0 ? arrive + l * num_blocks : nullptr, lag, max_spin);
+    });
+  }
+  API_END();
+}
+
+}  // extern "C"

@@ -129,6 +129,12 @@ def _load():
                                                       ctypes.c_float, _vp, _vp]),
         "dglhip_gspmm_items_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
                                                _vp, _c_i64, _vp, _c_i64, _vp, _vp]),
+        "dglhip_gspmm_sweep_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_i64,
+                                               _c_i64, _c_int, _c_int, _c_int, _vp]),
+        "dglhip_gspmm_sweep_stream_geometry": (_c_int, [_c_int, _vp]),
+        "dglhip_gspmm_sweep_stream_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
+                                                      _vp, _vp, _vp, _c_int, _c_int, _vp, _c_int,
+                                                      _c_int, _vp]),
         "dglhip_gspmm_max_ranges_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _c_int,
                                                     _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                                     _vp]),

@@ -569,6 +569,23 @@ int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
                               int64_t ufeat_ld, const float* efeat, int64_t efeat_len,
                               float* out, void* stream);
 
+/* Source-swept copy_u + sum (mean != 0: mean) of fp32 rows of feat_len = 64,
+ * 128 or 256 floats over the CSR (indptr, indices), every row of out
+ * written. Each wave keeps rows_per_wave rows' running sums in LDS for a
+ * whole launch and walks their slots source block by source block (block b:
+ * columns below col_lo + (b + 1) * block_cols; the last block takes the
+ * rest), always in slot order — so the result is dglhip_gspmm_device's chain,
+ * bit for bit, for any edge order; the blocks only set the L2 locality.
+ * row_order (int32[num_rows], may be NULL): the degree-descending order rows
+ * are dealt to waves from. rows_per_wave: 10 or 20 at 128 floats (0: 20),
+ * 20 or 40 at 64, 5 or 10 at 256. DESIGN.md §4.1 "Source sweep". Replaces,
+ * like dglhip_gspmm_device, the reference's F.spmm
+ * (python/dgl/backend/pytorch/tensor.py:145-146). */
+int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t* indptr,
+                              const int32_t* indices, const float* ufeat, float* out,
+                              const int32_t* row_order, int64_t col_lo, int64_t block_cols,
+                              int num_blocks, int mean, int rows_per_wave, void* stream);
+
 /* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of the CSR (argmax slot ids stay the CSR's: k,
  * mapped as dglhip_gspmm_device's), rows in row_order. With accumulate != 0
