@@ -34,6 +34,33 @@ namespace dglhip {
 namespace {
 
 constexpr int kSweepWaves = 4;  // waves per workgroup
+constexpr int kMaxLagBlocks = 64;  // source blocks the soft barrier covers
+constexpr int kShards = 8, kStride = 32;
+
+// the soft barrier's two halves, out of line: they run once per block and
+// wave, and inlined they cost the gather loop ~40 VGPRs
+__device__ __noinline__ void sweep_arrive(int* wg_done, int* arrive, int b) {
+  const int lane = threadIdx.x & 63;
+  int last = 0;
+  if (lane == 0) last = atomicAdd(&wg_done[b], 1) == kSweepWaves - 1;
+  if (__builtin_amdgcn_readfirstlane(last) && lane == 0)
+    __hip_atomic_fetch_add(arrive + (int64_t(b) * kShards + blockIdx.x % kShards) * kStride, 1,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __noinline__ void sweep_wait(const int* arrive, int b, int need, int max_spin) {
+  const int lane = threadIdx.x & 63;
+  const int* c = arrive + int64_t(b) * kShards * kStride;
+  for (int spin = 0; spin < max_spin; ++spin) {
+    int seen = lane < kShards ? __hip_atomic_load(c + lane * kStride, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0;
+#pragma unroll
+    for (int d = 1; d < kShards; d <<= 1) seen += __shfl_xor(seen, d);
+    if (__builtin_amdgcn_readfirstlane(seen) >= need) return;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
 
 __device__ __forceinline__ int32_t lane_of(int32_t v, int j) {
   return __builtin_amdgcn_readlane(v, j);
@@ -169,24 +196,24 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t wv = wave_base + int64_t(blockIdx.x) * kSweepWaves + w;
   const int64_t f0 = int64_t(lane) * VEC;
-  const int need = static_cast<int>(gridDim.x) * kSweepWaves;
-  // soft barrier: a wave starts block b once every wave of the launch has
-  // finished block b - lag (device-scope counters, one per block), or after
-  // max_spin polls — the results never depend on it, only the L2 locality
+  // Soft barrier (lag > 0): a wave starts block b once every workgroup of
+  // the launch has finished block b - lag, or after max_spin polls (the
+  // results never depend on it, only the L2 locality). The last wave of a
+  // workgroup to finish a block (an LDS counter per block) adds 1 to one of 8
+  // device-scope counters of that block (sharded by workgroup, each on its
+  // own 128-B line); a waiting wave polls the 8 with device-scope loads.
+  __shared__ int wg_done[kMaxLagBlocks];
+  const int need = static_cast<int>(gridDim.x);
+  const bool sync = lag > 0 && nblocks <= kMaxLagBlocks;
+  if (sync) {
+    for (int i = threadIdx.x; i < kMaxLagBlocks; i += blockDim.x) wg_done[i] = 0;
+    __syncthreads();
+  }
   auto arrive_at = [&](int b) {
-    if (lag > 0 && lane == 0)
-      __hip_atomic_fetch_add(arrive + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sync) sweep_arrive(wg_done, arrive, b);
   };
   auto wait_for = [&](int b) {
-    if (lag <= 0 || b < lag) return;
-    for (int spin = 0; spin < max_spin; ++spin) {
-      int seen = 0;
-      if (lane == 0)
-        seen = __hip_atomic_fetch_add(arrive + (b - lag), 0, __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
-      if (__builtin_amdgcn_readfirstlane(seen) >= need) return;
-      __builtin_amdgcn_s_sleep(8);
-    }
+    if (sync && b >= lag) sweep_wait(arrive, b - lag, need, max_spin);
   };
   int32_t row = -1, deg = 0;
   if (lane < RPW && wv < waves_total) {
@@ -272,18 +299,25 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   }
 }
 
+int g_sweep_per_cu = 0;  // study knob: workgroups per CU of a launch (0: occupancy)
+int g_sweep_unroll = 16;  // study knob: row gathers in flight per wave (16 or 32)
+
 template <typename K>
 int64_t sweep_waves_per_launch(K kern) {
   int dev = 0, cus = 0, per_cu = 0;
   HIP_CALL(hipGetDevice(&dev));
   HIP_CALL(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_CALL(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kSweepWaves, 0));
+  if (g_sweep_per_cu > 0) per_cu = std::min(per_cu, g_sweep_per_cu);
   DGLHIP_CHECK(cus > 0 && per_cu > 0, "sweep kernel does not fit a CU");
   return int64_t(cus) * per_cu * kSweepWaves;
 }
 
 template <int RPW>
 auto stream_kernel(bool mean) {
+  if (g_sweep_unroll == 32)
+    return mean ? gspmm_sweep_stream_kernel<2, RPW, 32, true>
+                : gspmm_sweep_stream_kernel<2, RPW, 32, false>;
   return mean ? gspmm_sweep_stream_kernel<2, RPW, 16, true>
               : gspmm_sweep_stream_kernel<2, RPW, 16, false>;
 }
@@ -360,11 +394,25 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
   API_END();
 }
 
+int dglhip_set_sweep_per_cu(int per_cu) {
+  API_BEGIN();
+  DGLHIP_CHECK(per_cu >= 0, "workgroups per CU " << per_cu);
+  g_sweep_per_cu = per_cu;
+  API_END();
+}
+
+int dglhip_set_sweep_unroll(int unroll) {
+  API_BEGIN();
+  DGLHIP_CHECK(unroll == 16 || unroll == 32, "gathers in flight " << unroll);
+  g_sweep_unroll = unroll;
+  API_END();
+}
+
 int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch) {
   API_BEGIN();
-  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 20, "rows per wave " << rows_per_wave);
+  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
   *waves_per_launch = rows_per_wave == 10 ? sweep_waves_per_launch(stream_kernel<10>(false))
-                                          : sweep_waves_per_launch(stream_kernel<20>(false));
+                                          : sweep_waves_per_launch(stream_kernel<19>(false));
   API_END();
 }
 
@@ -376,23 +424,25 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      int max_spin, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 20, "rows per wave " << rows_per_wave);
+  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
   DGLHIP_CHECK(num_rows >= 0 && num_rows < (int64_t(1) << 31) && num_blocks >= 1, "sizes");
   if (num_rows == 0) return 0;
-  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mean != 0) : stream_kernel<20>(mean != 0);
+  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mean != 0) : stream_kernel<19>(mean != 0);
   const int64_t wpl = sweep_waves_per_launch(kern);
   DGLHIP_CHECK(waves_total % wpl == 0 && waves_total * rows_per_wave >= num_rows,
                "layout for " << waves_total << " waves, launches hold " << wpl);
   DGLHIP_CHECK(lag <= 0 || arrive, "the soft barrier needs its counters");
   const int64_t launches = waves_total / wpl;
-  if (lag > 0)  // launches x num_blocks counters
-    HIP_CALL(hipMemsetAsync(arrive, 0, sizeof(int) * launches * num_blocks, stream));
+  // per launch and block 8 counters on 128-B lines of their own
+  const int64_t per_launch = int64_t(num_blocks) * 8 * 32;
+  if (lag > 0)
+    HIP_CALL(hipMemsetAsync(arrive, 0, sizeof(int) * launches * per_launch, stream));
   for (int64_t l = 0; l < launches; ++l) {
     timed_launch(stream, [&] {
       hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(wpl / kSweepWaves)),
                          dim3(64 * kSweepWaves), 0, stream, num_rows, waves_total, l * wpl,
                          row_order, counts, num_blocks, seg_beg, lay, indptr, ufeat, out,
-                         lag > 0 ? arrive + l * num_blocks : nullptr, lag, max_spin);
+                         lag > 0 ? arrive + l * per_launch : nullptr, lag, max_spin);
     });
   }
   API_END();

@@ -586,6 +586,29 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
                               const int32_t* row_order, int64_t col_lo, int64_t block_cols,
                               int num_blocks, int mean, int rows_per_wave, void* stream);
 
+/* The streamed form of the source sweep (a study, DESIGN.md §4.1 "Source
+ * sweep"): the slots laid out per (launch, block, wave, row) in lay, wave w's
+ * block-b run starting at seg_beg[w * num_blocks + b], counts[row *
+ * num_blocks + b] slots of each of its rows back to back (the layout of
+ * tools/r05/sweep_study.py stream_layout, exact for source-monotone rows);
+ * waves_total a multiple of dglhip_gspmm_sweep_stream_geometry's waves per
+ * launch. lag > 0: a soft barrier (a wave starts block b once every
+ * workgroup has finished block b - lag, or after max_spin polls) over
+ * device-scope counters in arrive (launches * num_blocks * 256 ints, zeroed
+ * by the call); results never depend on it. rows_per_wave 10 or 19;
+ * feat_len 128. */
+int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch);
+int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
+                                     const int32_t* row_order, const int32_t* counts,
+                                     int num_blocks, const int64_t* seg_beg, const int32_t* lay,
+                                     const int64_t* indptr, const float* ufeat, float* out,
+                                     int mean, int rows_per_wave, int* arrive, int lag,
+                                     int max_spin, void* stream);
+/* Study knobs of the sweep kernels: workgroups per CU of a launch (0: the
+ * occupancy limit) and row gathers in flight per wave (16 or 32). */
+int dglhip_set_sweep_per_cu(int per_cu);
+int dglhip_set_sweep_unroll(int unroll);
+
 /* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are
  * [row_beg[r], row_end[r]) of the CSR (argmax slot ids stay the CSR's: k,
  * mapped as dglhip_gspmm_device's), rows in row_order. With accumulate != 0

@@ -104,3 +104,50 @@ def test_sweep_tiny_graphs():
             out = torch.full((n, 128), float("nan"), device=dev)
             _sweep(csr, H.to(dev), out, nb, 20)
             assert np.array_equal(out.cpu().numpy(), ref), (n, m, nb)
+
+
+def _study_tool():
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "tools", "r05", "sweep_study.py")
+    spec = importlib.util.spec_from_file_location("sweep_study", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.mark.parametrize("lag", [0, 2])
+@pytest.mark.parametrize("rpw", [10, 19])
+def test_sweep_stream_bits(lag, rpw):
+    """The streamed layout (rows' block runs back to back per wave) and its
+    soft barrier: the oracle's bits, sum and mean, with and without the
+    barrier; a random-order graph has no such layout."""
+    dev = _dev()
+    n, m = 50_000, 1_500_000
+    src, dst = _graph(n, m, 7, "sorted")
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst).to(dev), torch.from_numpy(src).to(dev),
+                           kernel.ORDER_EID, dev)
+    H = torch.randn(n, 128, generator=torch.Generator().manual_seed(8))
+    ref = O.spmm_coo(n, dst, src, H.numpy())
+    deg = np.bincount(dst, minlength=n).astype(np.float32)[:, None]
+    ref_mean = np.where(deg > 1, ref / np.maximum(deg, 1), ref).astype(np.float32)
+    tool = _study_tool()
+    lo, hi = int(csr.indices.min()), int(csr.indices.max()) + 1
+    lt = tool.stream_layout(csr, 128, lo, hi, csr.row_order, 1, rpw)  # 1-MiB slices: 25 blocks
+    assert lt is not None and lt["B"] > 8
+    arrive = torch.zeros(lt["launches"] * lt["B"] * 256, dtype=torch.int32, device=dev)
+    h = H.to(dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    for mean, want in ((0, ref), (1, ref_mean)):
+        out = torch.full((n, 128), float("nan"), device=dev)
+        check_call(LIB.dglhip_gspmm_sweep_stream_device(
+            n, lt["W"], ptr(csr.row_order), ptr(lt["counts"]), lt["B"], ptr(lt["seg"]),
+            ptr(lt["lay"]), ptr(csr.indptr), ptr(h), ptr(out), mean, rpw, ptr(arrive), lag, 2000,
+            stream))
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want), mean
+    src, dst = _graph(n, m, 7, "random")
+    rnd = kernel.build_csr(n, n, torch.from_numpy(dst).to(dev), torch.from_numpy(src).to(dev),
+                           kernel.ORDER_EID, dev)
+    assert tool.stream_layout(rnd, 128, lo, hi, rnd.row_order, 1, rpw) is None

@@ -30,6 +30,45 @@ def timed(fn, iters):
     return sum(a.elapsed_time(b) for a, b in ev) / iters
 
 
+def stream_layout(csr, F, lo, hi, order, mib, rpw):
+    """Slots laid out per (launch, block, wave, row), as the stream kernel
+    (dglhip_gspmm_sweep_stream_device) reads them: the kernel deals row i of
+    ``order`` to wave (i // W odd ? W - 1 - i % W : i % W) as its row i // W,
+    and reads wave w's block-b run at seg[w, b]. None when a row's source
+    blocks go back down (the layout keeps each row's block-b slots together)."""
+    dev = csr.indptr.device
+    n = csr.num_rows
+    bs = max(1, int(mib * (1 << 20)) // (F * 4))
+    B = max(1, -(-(hi - lo) // bs))
+    deg = csr.indptr[1:] - csr.indptr[:-1]
+    rows = torch.repeat_interleave(torch.arange(n, device=dev), deg)
+    blk = (csr.indices.long() - lo) // bs
+    if bool(((rows[1:] == rows[:-1]) & (blk[1:] < blk[:-1])).any()):
+        return None
+    wpl = ctypes.c_int64()
+    check_call(LIB.dglhip_gspmm_sweep_stream_geometry(rpw, ctypes.byref(wpl)))
+    wpl = wpl.value
+    L = -(-n // (wpl * rpw))
+    W = L * wpl
+    i = torch.arange(n, device=dev)
+    j, pos = i // W, i % W
+    wave = torch.where(j % 2 == 1, W - 1 - pos, pos)
+    ro = order.long() if order is not None else i
+    wave_of = torch.empty(n, dtype=torch.int64, device=dev)
+    j_of = torch.empty(n, dtype=torch.int64, device=dev)
+    wave_of[ro] = wave
+    j_of[ro] = j
+    key = (((wave_of[rows] // wpl) * B + blk) * W + wave_of[rows]) * rpw + j_of[rows]
+    skey, perm = torch.sort(key, stable=True)
+    lay = csr.indices[perm].contiguous()
+    w_all = torch.arange(W, device=dev)
+    q = (((w_all[:, None] // wpl) * B + torch.arange(B, device=dev)[None, :]) * W
+         + w_all[:, None]) * rpw
+    seg = torch.searchsorted(skey, q.reshape(-1)).contiguous()
+    counts = torch.bincount(rows * B + blk, minlength=n * B).to(torch.int32)
+    return {"W": W, "B": B, "lay": lay, "seg": seg, "counts": counts, "launches": L}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mib", type=float, nargs="+", default=[2, 3, 4, 6])
@@ -40,6 +79,8 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--stream", action="store_true", help="also the streamed layout kernel")
     ap.add_argument("--lag", type=int, nargs="+", default=[0, 1, 2])
+    ap.add_argument("--per-cu", type=int, default=0, help="workgroups per CU (0: occupancy)")
+    ap.add_argument("--unroll", type=int, default=16)
     ap.add_argument("--no-cursor", action="store_true", help="skip the cursor kernel")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -72,40 +113,9 @@ def main():
         return nb
 
     def layout(mib, rpw):
-        """Slots laid out per (launch, block, wave, row), as the stream kernel
-        reads them; None when a row's blocks go back down."""
-        bs = max(1, int(mib * (1 << 20)) // (F * 4))
-        B = max(1, -(-(hi - lo) // bs))
-        deg = csr.indptr[1:] - csr.indptr[:-1]
-        rows = torch.repeat_interleave(torch.arange(n, device=dev), deg)
-        blk = (csr.indices.long() - lo) // bs
-        if bool(((rows[1:] == rows[:-1]) & (blk[1:] < blk[:-1])).any()):
-            return None
-        wpl = ctypes.c_int64()
-        check_call(LIB.dglhip_gspmm_sweep_stream_geometry(rpw, ctypes.byref(wpl)))
-        wpl = wpl.value
-        L = -(-n // (wpl * rpw))
-        W = L * wpl
-        i = torch.arange(n, device=dev)
-        j, pos = i // W, i % W
-        wave = torch.where(j % 2 == 1, W - 1 - pos, pos)
-        ro = order.long() if order is not None else i
-        wave_of = torch.empty(n, dtype=torch.int64, device=dev)
-        j_of = torch.empty(n, dtype=torch.int64, device=dev)
-        wave_of[ro] = wave
-        j_of[ro] = j
-        key = (((wave_of[rows] // wpl) * B + blk) * W + wave_of[rows]) * rpw + j_of[rows]
-        skey, perm = torch.sort(key, stable=True)
-        lay = csr.indices[perm].contiguous()
-        w_all = torch.arange(W, device=dev)
-        q = (((w_all[:, None] // wpl) * B + torch.arange(B, device=dev)[None, :]) * W
-             + w_all[:, None]) * rpw
-        seg = torch.searchsorted(skey, q.reshape(-1)).contiguous()
-        counts = torch.bincount(rows * B + blk, minlength=n * B).to(torch.int32)
-        del rows, blk, key, skey, perm
-        return {"W": W, "B": B, "lay": lay, "seg": seg, "counts": counts, "launches": L}
+        return stream_layout(csr, F, lo, hi, order, mib, rpw)
 
-    arrive = torch.zeros(1 << 16, dtype=torch.int32, device=dev)
+    arrive = torch.zeros(1 << 22, dtype=torch.int32, device=dev)
 
     def stream_run(lt, rpw, lag):
         check_call(LIB.dglhip_gspmm_sweep_stream_device(
@@ -114,6 +124,9 @@ def main():
 
     res = {"graph": "reddit_like", "order": args.order, "rounds": []}
     layouts = {}
+    if args.per_cu:
+        check_call(LIB.dglhip_set_sweep_per_cu(args.per_cu))
+    check_call(LIB.dglhip_set_sweep_unroll(args.unroll))
     if args.stream:
         for mib in args.mib:
             for rpw in args.rpw:
@@ -123,7 +136,7 @@ def main():
         torch.cuda.synchronize()
         row["engine_bits_equal"] = bool(torch.equal(out, ref))
         for mib in ([] if args.no_cursor else args.mib):
-            for rpw in args.rpw:
+            for rpw in sorted({20 if r == 19 else r for r in args.rpw}):  # cursor: 10 or 20
                 out.fill_(float("nan"))
                 nb = sweep(mib, rpw)
                 torch.cuda.synchronize()
