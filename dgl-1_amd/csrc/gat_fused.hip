@@ -46,6 +46,7 @@ namespace dglhip {
 // batch's feature rows gathered after its attention, 3 the same kernel with
 // them gathered before it
 int g_gat_variant = 0;
+int g_gat_fwd_waves = 0;  // study knob: minimum waves per SIMD of the 8 x 16 forward (0, 5, 6)
 // study knob of the transposed backward (dglhip_set_gat_bwd_variant): bits 0-1
 // the g store (0 default, 1 non-temporal, 2 none: d_er is then not valid,
 // 3 16-B write-through stores regrouped through LDS);
@@ -320,6 +321,9 @@ __device__ __forceinline__ void gat_batch(
   // the head's values four at a time (one 16-B LDS read), consumed in slot order
 #pragma unroll
   for (int q = 0; q < U / 4; ++q) {
+    // with dropout, keep the two 16-B LDS reads of each quad next to their
+    // use (hoisted, the eight reads held 32 VGPRs: 109 -> 4 waves per SIMD)
+    if (q > 0) __builtin_amdgcn_sched_barrier(0);
     const f32x4 t = *reinterpret_cast<const f32x4*>(la + h * LA + 4 * q);
     const float av[4] = {t.x, t.y, t.z, t.w};
     f32x4 t2 = t;
@@ -371,8 +375,9 @@ __global__ __launch_bounds__(256) void gat_logits_kernel(
 }
 
 template <int H, int VEC, bool DROP, bool SMALL, bool EARLY = false, int RP = 0,
-          bool LOGIT = false>
-__global__ __launch_bounds__(256) void gat_aggregate_lds_kernel(
+          bool LOGIT = false, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void gat_aggregate_lds_kernel(
     int64_t num_rows, int64_t D, const int64_t* __restrict__ row_beg,
     const int64_t* __restrict__ row_end, int accumulate, const int32_t* __restrict__ indices, const int32_t* __restrict__ row_order,
     const float* __restrict__ el, const float* __restrict__ er, const float* __restrict__ ft,
@@ -853,7 +858,21 @@ int dglhip_gat_aggregate_logits_ranges_device(
                          clamp_hi, apply_exp, seed, seed_offset, thr, scale, out_ft, out_z,    \
                          attn_out, attn_drop_out, tbytes, nullptr);                            \
   } while (0)
-        if (g_row_pol == 2) {
+#define DGLHIP_GATW(DD, SM, W)                                                                 \
+  hipLaunchKernelGGL((gat_aggregate_lds_kernel<8, 2, DD, SM, true, 2, false, W>),              \
+                     grid_1d(blocks), dim3(256), 0, stream, num_rows, head_dim, row_beg, row_end, \
+                     accumulate, indices, row_order, el, er, ft, alpha, clamp_lo, clamp_hi,      \
+                     apply_exp, seed, seed_offset, thr, scale, out_ft, out_z, attn_out,          \
+                     attn_drop_out, tbytes, nullptr)
+        if (g_row_pol == 2 && !logit && g_gat_fwd_waves == 6) {
+          // study knob: at least 6 waves per SIMD (the no-dropout kernel is 81
+          // VGPRs, one over the 80 that 6 waves allow)
+          if (drop) { if (small) DGLHIP_GATW(true, true, 6); else DGLHIP_GATW(true, false, 6); }
+          else { if (small) DGLHIP_GATW(false, true, 6); else DGLHIP_GATW(false, false, 6); }
+        } else if (g_row_pol == 2 && !logit && g_gat_fwd_waves == 5) {
+          if (drop) { if (small) DGLHIP_GATW(true, true, 5); else DGLHIP_GATW(true, false, 5); }
+          else { if (small) DGLHIP_GATW(false, true, 5); else DGLHIP_GATW(false, false, 5); }
+        } else if (g_row_pol == 2) {
           if (drop) { if (small) DGLHIP_GATRP(true, true, 2); else DGLHIP_GATRP(true, false, 2); }
           else { if (small) DGLHIP_GATRP(false, true, 2); else DGLHIP_GATRP(false, false, 2); }
         } else {
@@ -861,6 +880,7 @@ int dglhip_gat_aggregate_logits_ranges_device(
           else { if (small) DGLHIP_GATRP(false, true, 4); else DGLHIP_GATRP(false, false, 4); }
         }
 #undef DGLHIP_GATRP
+#undef DGLHIP_GATW
       });
       return 0;
     }
@@ -1036,6 +1056,13 @@ int dglhip_set_gat_variant(int variant) {
   API_BEGIN();
   DGLHIP_CHECK(variant >= 0 && variant <= 3, "unknown GAT kernel variant " << variant);
   g_gat_variant = variant;
+  API_END();
+}
+
+int dglhip_set_gat_fwd_waves(int waves) {
+  API_BEGIN();
+  DGLHIP_CHECK(waves == 0 || waves == 5 || waves == 6, "forward waves per SIMD " << waves);
+  g_gat_fwd_waves = waves;
   API_END();
 }
 

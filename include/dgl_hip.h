@@ -765,6 +765,9 @@ int dglhip_gat_aggregate_logits_ranges_device(
     float drop_p, uint64_t seed, const int64_t* seed_offset, float* out_ft, float* out_z,
     float* attn_out, float* attn_drop_out, void* stream);
 /* Study knob: 1 switches the recompute above on (default 0; same bits). */
+/* Study knob: the 8 x 16 fused forward (row policy 2, logits gathered)
+ * compiled for at least 5 or 6 waves per SIMD (0: as the compiler allocates). */
+int dglhip_set_gat_fwd_waves(int waves);
 int dglhip_set_gat_logit_recompute(int on);
 
 /* dglhip_gat_aggregate_device over row ranges: row r's slots are
