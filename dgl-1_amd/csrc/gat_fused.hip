@@ -608,6 +608,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     // per slot: d_ft's chain and the head's dot (as below)
 #pragma unroll
     for (int q = 0; q < U / 4; ++q) {
+      // each quad's LDS read next to its use (here and in d_el's sum below:
+      // hoisted, they held the one-pass kernel at 103 VGPRs, 4 waves per SIMD;
+      // kept in place 95, 5 waves)
+      if (q > 0) __builtin_amdgcn_sched_barrier(0);
       const f32x4 w4 = *reinterpret_cast<const f32x4*>(lw + h * LU + 4 * q);
       const float wv[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
@@ -650,6 +654,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE))) void
     if (head_lane) {
 #pragma unroll
       for (int q = 0; q < U / 4; ++q) {
+        if (q > 0) __builtin_amdgcn_sched_barrier(0);
         const f32x4 g4 = *reinterpret_cast<const f32x4*>(ld + h * LU + 4 * q);
         const float gv[4] = {g4.x, g4.y, g4.z, g4.w};
 #pragma unroll
