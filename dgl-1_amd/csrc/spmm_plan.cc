@@ -88,6 +88,23 @@ SpmmPolicy spmm_policy() {
   return pol_ref();
 }
 
+namespace {
+SweepPolicy& sweep_ref() {
+  static SweepPolicy p = [] {
+    SweepPolicy q;
+    const char* e = std::getenv("DGLHIP_SWEEP");
+    if (e && (std::strcmp(e, "0") == 0 || std::strcmp(e, "off") == 0)) q.on = 0;
+    return q;
+  }();
+  return p;
+}
+}  // namespace
+
+SweepPolicy sweep_policy() {
+  std::lock_guard<std::mutex> lk(g_pol_mu);
+  return sweep_ref();
+}
+
 void set_spmm_policy(const SpmmPolicy& p) {
   DGLHIP_CHECK(p.block_bytes > 0 && p.block_min_slots >= 1 && p.block_max_stretch > 0 &&
                    p.block_table_min >= 0 && p.block_table_max >= p.block_table_min &&
@@ -488,6 +505,73 @@ std::shared_ptr<Cuts> SpmmPlan::cuts_for(int B, hipStream_t s) {
   return c;
 }
 
+std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
+  const SweepPolicy sp = sweep_policy();
+  constexpr int RPW = 19;  // rows per wave of the 128-float sweep kernel
+  if (!sp.on || !on_device() || nnz_ == 0 || nnz_ >= (int64_t(1) << 31) || R_ == 0) return nullptr;
+  const auto lh = span(s);
+  const int64_t table = (lh.second - lh.first) * row_bytes;
+  if (table < sp.table_min) return nullptr;
+  const int64_t want = cdiv(table, sp.block_bytes);
+  if (want < 2 || want > 256) return nullptr;  // the barrier covers 256 blocks
+  const int B = static_cast<int>(want);
+  std::lock_guard<std::mutex> lk(mu_);
+  auto hit = sweeps_.find(B);
+  if (hit != sweeps_.end()) return hit->second;
+  auto split = block_split(B, s);
+  if (split->total_suffix != 0) {  // a row's blocks go back down: no run layout
+    sweeps_[B] = nullptr;
+    return nullptr;
+  }
+  int64_t wpl = 0;
+  DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry(RPW, &wpl) == 0 && wpl > 0, DGLGetLastError());
+  auto sw = std::make_shared<SweepPlan>();
+  sw->B = B;
+  sw->rows_per_wave = RPW;
+  sw->launches = cdiv(R_, wpl * RPW);
+  const int64_t W = sw->launches * wpl;
+  sw->waves_total = W;
+  // the kernel's deal: row i of the schedule order -> wave (i / W odd ?
+  // W - 1 - i % W : i % W), its row i / W; each wave's run in block b holds
+  // its rows' block-b slots in that order; runs ordered (launch, block, wave)
+  const std::vector<int32_t>& order = host_order(s);
+  const int32_t* cnt = split->counts.data();
+  std::vector<int64_t> item_start(static_cast<size_t>(R_) * B, 0);
+  std::vector<int64_t> seg(static_cast<size_t>(W) * B, 0);
+  int64_t off = 0;
+  for (int64_t l = 0; l < sw->launches; ++l) {
+    for (int b = 0; b < B; ++b) {
+      for (int64_t w = l * wpl; w < (l + 1) * wpl; ++w) {
+        seg[w * B + b] = off;
+        for (int j = 0; j < RPW; ++j) {
+          const int64_t pos = (j & 1) ? (W - 1 - w) : w;
+          const int64_t i = int64_t(j) * W + pos;
+          if (i >= R_) break;  // rows of a wave are a prefix of its rounds
+          const int64_t r = order.empty() ? i : order[i];
+          item_start[r * B + b] = off;
+          off += cnt[r * B + b];
+        }
+      }
+    }
+  }
+  DGLHIP_CHECK(off == nnz_, "sweep layout covers " << off << " of " << nnz_ << " slots");
+  sw->lay = empty({nnz_}, 0, 32);
+  sw->pos = empty({nnz_}, 0, 32);
+  {
+    rt::NDArray ist = upload(item_start.data(), R_ * B, 0, 64, s);
+    rt::NDArray pend = upload(split->pend.data(), R_, 0, 64, s);
+    plan_block_scatter_device(R_, indptr_, indices_, split->lo, split->bs, B,
+                              pend.data<int64_t>(), ist.data<int64_t>(), nullptr,
+                              sw->lay.data<int32_t>(), sw->pos.data<int32_t>(), s);
+    sw->seg = upload(seg.data(), W * B, 0, 64, s);
+    sw->counts = upload(cnt, R_ * B, 0, 32, s);
+    hip_ok(hipStreamSynchronize(s), "sweep layout");  // the staging arrays go out of scope
+  }
+  sw->arrive = empty({sw->launches * B * 256}, 0, 32);
+  sweeps_[B] = sw;
+  return sw;
+}
+
 const int64_t* SpmmPlan::plan_pos64(BlockedPlan& bp, hipStream_t s) {
   std::lock_guard<std::mutex> lk(mu_);
   if (!bp.pos64.defined()) {
@@ -671,12 +755,13 @@ struct RunArgs {
   int64_t* arg;
 };
 
-enum Path { PATH_HOST = 0, PATH_ROWS = 1, PATH_BLOCKED = 2, PATH_MAX_BLOCKED = 3 };
+enum Path { PATH_HOST = 0, PATH_ROWS = 1, PATH_BLOCKED = 2, PATH_MAX_BLOCKED = 3, PATH_SWEEP = 4 };
 
 struct Decision {
   Path path = PATH_ROWS;
   std::shared_ptr<BlockedPlan> bp;
   std::shared_ptr<Cuts> cuts;
+  std::shared_ptr<SweepPlan> sw;
   bool pad = false;     // gather from a padded copy (workspace)
   int64_t ld = 0;       // row stride the kernels read (0: dense)
   int64_t split = 0;
@@ -731,6 +816,16 @@ Decision decide(SpmmPlan& plan, const RunArgs& a, hipStream_t s) {
   const int64_t ld_in = strided ? a.ldu : a.F;
   const bool fp32u = a.msg != DGLHIP_MSG_COPY_U_BF16;
   if (a.F == 0 || plan.num_rows() == 0) return d;
+  if ((a.red == DGLHIP_REDUCE_SUM || a.red == DGLHIP_REDUCE_MEAN) && a.msg == DGLHIP_MSG_COPY_U &&
+      a.ufeat && !a.efeat && !strided && a.F == 128) {
+    // tables past the L2-sized blocked schedule's range: the source sweep
+    // (running sums in LDS, no per-block pass over out)
+    d.sw = plan.sweep(a.F * 4, s);
+    if (d.sw) {
+      d.path = PATH_SWEEP;
+      return d;
+    }
+  }
   if (sumlike && a.ufeat && ((cu && !a.efeat) || (a.msg == DGLHIP_MSG_U_MUL_E && a.efeat))) {
     d.bp = plan.blocked(ld_in * elem, p.block_bytes, s);
     if (d.bp) {
@@ -835,6 +930,19 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
     hip_ok(hipMemcpy2DAsync(up, d.ld * 4, a.ufeat, rb, rb, a.urows, hipMemcpyDeviceToDevice, s),
            "padded rows copy");
     uf = up;
+  }
+  if (d.path == PATH_SWEEP) {
+    const SweepPlan& sw = *d.sw;
+    const SweepPolicy sp = sweep_policy();
+    DGLHIP_CHECK(dglhip_gspmm_sweep_stream_device(
+                     plan.num_rows(), sw.waves_total, plan.row_order(),
+                     sw.counts.data<int32_t>(), sw.B, sw.seg.data<int64_t>(),
+                     sw.lay.data<int32_t>(), plan.indptr(), static_cast<const float*>(uf), a.out,
+                     a.red == DGLHIP_REDUCE_MEAN ? 1 : 0, sw.rows_per_wave,
+                     sw.arrive.data<int32_t>(), sp.lag, sp.max_spin,
+                     s) == 0,
+                 DGLGetLastError());
+    return;
   }
   if (d.path == PATH_BLOCKED) {
     BlockedPlan& bp = *d.bp;
@@ -995,7 +1103,8 @@ int spmm_plan_path(SpmmPlan& plan, int msg, int red, int64_t F, int64_t ldu, int
   const Decision d = decide(plan, a, s);
   if (launches) {
     *launches = d.path == PATH_BLOCKED ? static_cast<int64_t>(d.bp->launches.size())
-                : d.path == PATH_MAX_BLOCKED ? d.cuts->n - 1 : 1;
+                : d.path == PATH_MAX_BLOCKED ? d.cuts->n - 1
+                : d.path == PATH_SWEEP ? d.sw->launches : 1;
   }
   return d.path;
 }
@@ -1005,6 +1114,29 @@ int spmm_plan_path(SpmmPlan& plan, int msg, int red, int64_t F, int64_t ldu, int
 using namespace dglhip;
 
 extern "C" {
+
+int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
+                              int max_spin) {
+  API_BEGIN();
+  DGLHIP_CHECK(table_min >= 0 && block_bytes > 0 && lag >= 0 && max_spin >= 0,
+               "invalid sweep schedule");
+  std::lock_guard<std::mutex> lk(g_pol_mu);
+  sweep_ref() = SweepPolicy{on != 0 ? 1 : 0, table_min, block_bytes, lag, max_spin};
+  API_END();
+}
+
+int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes, int* lag,
+                              int* max_spin) {
+  API_BEGIN();
+  DGLHIP_CHECK(on && table_min && block_bytes && lag && max_spin, "null pointer argument");
+  const SweepPolicy p = sweep_policy();
+  *on = p.on;
+  *table_min = p.table_min;
+  *block_bytes = p.block_bytes;
+  *lag = p.lag;
+  *max_spin = p.max_spin;
+  API_END();
+}
 
 int dglhip_spmm_get_policy(DGLHipSpmmPolicy* out) {
   API_BEGIN();

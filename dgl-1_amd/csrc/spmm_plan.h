@@ -106,6 +106,34 @@ struct BlockSplit {
   int64_t total_suffix = 0;
 };
 
+// The source sweep (DESIGN.md §4.1 "Source sweep", csrc/sweep.hip): every
+// row's running sum in LDS for a whole launch, the slots laid out per
+// (launch, block, wave, row) so a wave's block is one run of column ids;
+// one launch per generation of rows, a soft barrier keeping the waves on
+// the same source blocks.
+struct SweepPlan {
+  int B = 0;
+  int rows_per_wave = 0;
+  int64_t waves_total = 0, launches = 0;
+  rt::NDArray lay;     // int32[nnz]: column ids in sweep order
+  rt::NDArray pos;     // int32[nnz]: the CSR slot of each (the scatter's by-product)
+  rt::NDArray seg;     // int64[waves_total * B]: each wave's run per block
+  rt::NDArray counts;  // int32[num_rows * B]: each row's slots per block
+  rt::NDArray arrive;  // int32[launches * B * 256]: the barrier's counters
+};
+
+// Sweep schedule knobs (process-wide; dglhip_set_sweep_schedule): on where
+// it applies (copy_u sum / mean of fp32 rows of 128 floats, a source-monotone
+// CSR, source tables of table_min bytes or more, at most 256 blocks)
+struct SweepPolicy {
+  int on = 1;
+  int64_t table_min = int64_t(256) << 20;  // past the blocked schedule's range
+  int64_t block_bytes = 6 << 20;
+  int lag = 4;
+  int max_spin = 2000;
+};
+SweepPolicy sweep_policy();
+
 struct SplitPlan {
   rt::NDArray light, heavy, chunk_ptr, beg, end;
   int64_t n_light = 0, n_heavy = 0, n_chunks = 0;
@@ -160,6 +188,9 @@ class SpmmPlan {
   const int64_t* plan_pos64(BlockedPlan& bp, hipStream_t s);
   const int64_t* plan_eidmap(BlockedPlan& bp, const int64_t* eid, hipStream_t s);
 
+  // the sweep plan for row_bytes (nullptr when it does not apply)
+  std::shared_ptr<SweepPlan> sweep(int64_t row_bytes, hipStream_t s);
+
   int64_t heavy_threshold() const;  // split_threshold on this CSR and part
   SplitPlan& split_plan(int64_t threshold, bool skip_empty, int64_t chunk, hipStream_t s);
   // tiers of the first n rows of the degree-descending schedule (key 0), or
@@ -195,6 +226,7 @@ class SpmmPlan {
   std::map<int, std::shared_ptr<BlockSplit>> splits_;
   std::map<int, std::shared_ptr<BlockedPlan>> blocked_;
   std::map<int, std::shared_ptr<Cuts>> cuts_;
+  std::map<int, std::shared_ptr<SweepPlan>> sweeps_;
   std::map<std::tuple<int64_t, bool, int64_t>, SplitPlan> split_plans_;
   std::map<int64_t, Tiers> tiers_;
 };

@@ -34,7 +34,7 @@ namespace dglhip {
 namespace {
 
 constexpr int kSweepWaves = 4;  // waves per workgroup
-constexpr int kMaxLagBlocks = 64;  // source blocks the soft barrier covers
+constexpr int kMaxLagBlocks = 256;  // source blocks the soft barrier covers
 constexpr int kShards = 8, kStride = 32;
 
 // the soft barrier's two halves, out of line: they run once per block and
@@ -48,7 +48,9 @@ __device__ __noinline__ void sweep_arrive(int* wg_done, int* arrive, int b) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __noinline__ void sweep_wait(const int* arrive, int b, int need, int max_spin) {
+// false when max_spin polls ran out (the wave then stops waiting: a launch
+// whose workgroups are not all resident costs one bounded wait per wave)
+__device__ __noinline__ bool sweep_wait(const int* arrive, int b, int need, int max_spin) {
   const int lane = threadIdx.x & 63;
   const int* c = arrive + int64_t(b) * kShards * kStride;
   for (int spin = 0; spin < max_spin; ++spin) {
@@ -57,9 +59,10 @@ __device__ __noinline__ void sweep_wait(const int* arrive, int b, int need, int 
                               : 0;
 #pragma unroll
     for (int d = 1; d < kShards; d <<= 1) seen += __shfl_xor(seen, d);
-    if (__builtin_amdgcn_readfirstlane(seen) >= need) return;
+    if (__builtin_amdgcn_readfirstlane(seen) >= need) return true;
     __builtin_amdgcn_s_sleep(8);
   }
+  return false;
 }
 
 __device__ __forceinline__ int32_t lane_of(int32_t v, int j) {
@@ -212,8 +215,9 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   auto arrive_at = [&](int b) {
     if (sync) sweep_arrive(wg_done, arrive, b);
   };
+  bool waiting = true;
   auto wait_for = [&](int b) {
-    if (sync && b >= lag) sweep_wait(arrive, b - lag, need, max_spin);
+    if (sync && waiting && b >= lag) waiting = sweep_wait(arrive, b - lag, need, max_spin);
   };
   int32_t row = -1, deg = 0;
   if (lane < RPW && wv < waves_total) {

@@ -142,6 +142,32 @@ def scheduled(**changes):
         set_schedule_policy(**old)
 
 
+def sweep_schedule():
+    """The source-sweep schedule's knobs (DESIGN.md §4.1 "Source sweep"):
+    {"on", "table_min", "block_bytes", "lag", "max_spin"}."""
+    on, lag, spin = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    tmin, bb = ctypes.c_int64(), ctypes.c_int64()
+    check_call(LIB.dglhip_get_sweep_schedule(ctypes.byref(on), ctypes.byref(tmin),
+                                             ctypes.byref(bb), ctypes.byref(lag),
+                                             ctypes.byref(spin)))
+    return {"on": bool(on.value), "table_min": tmin.value, "block_bytes": bb.value,
+            "lag": lag.value, "max_spin": spin.value}
+
+
+def set_sweep_schedule(**changes):
+    """Change the source-sweep knobs; returns the old ones (for restoring).
+    A plan keeps the sweep layouts it built; the choice is made per call."""
+    old = sweep_schedule()
+    new = dict(old, **changes)
+    unknown = set(changes) - set(old)
+    if unknown:
+        raise DGLError("unknown sweep knobs: %s" % sorted(unknown))
+    check_call(LIB.dglhip_set_sweep_schedule(int(bool(new["on"])), int(new["table_min"]),
+                                             int(new["block_bytes"]), int(new["lag"]),
+                                             int(new["max_spin"])))
+    return old
+
+
 def _resident_waves(device=None):
     """R: the headline g-SpMM kernel's resident waves on ``device`` (queried
     once per device from the library); _REF_WAVES for host / unknown devices."""
@@ -672,7 +698,7 @@ class _NativePlan(object):
 
     def schedule(self, msg, red, F, ldu=0, urows=0, elen=0, emode=0, erow=None):
         """(path, launches) a run with these arguments takes
-        (DGLHIP_PLAN_PATH_*: 0 host, 1 rows, 2 blocked, 3 blocked max)."""
+        (DGLHIP_PLAN_PATH_*: 0 host, 1 rows, 2 blocked, 3 blocked max, 4 sweep)."""
         path, launches = ctypes.c_int(), ctypes.c_int64()
         _retry_oom(lambda: check_call(LIB.dglhip_spmm_plan_schedule(
             self.handle, msg, red, F, ldu, urows, elen, emode, ptr(erow), self.stream(),
@@ -687,7 +713,8 @@ class _NativePlan(object):
                          "heavy_threshold"), list(s)))
 
 
-PLAN_PATH_HOST, PLAN_PATH_ROWS, PLAN_PATH_BLOCKED, PLAN_PATH_MAX_BLOCKED = 0, 1, 2, 3
+PLAN_PATH_HOST, PLAN_PATH_ROWS, PLAN_PATH_BLOCKED, PLAN_PATH_MAX_BLOCKED, PLAN_PATH_SWEEP = \
+    0, 1, 2, 3, 4
 _EDGE_BY_SLOT, _EDGE_BY_EID, _EDGE_BY_MAP = 0, 1, 2
 
 

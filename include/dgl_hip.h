@@ -331,11 +331,13 @@ int dglhip_spmm_plan_run(DGLHipSpmmPlan plan, int msg_op, int reduce_op, int64_t
                          int64_t workspace_bytes, void* stream);
 /* The schedule a run with these arguments takes: *path 0 host, 1 one wave per
  * row (heavy-row chunks and short-row tiers included), 2 source-blocked items,
- * 3 source-blocked max ranges; *launches the blocked launches (1 otherwise). */
+ * 3 source-blocked max ranges, 4 the source sweep; *launches the blocked
+ * launches, the sweep's launches (row generations), 1 otherwise. */
 #define DGLHIP_PLAN_PATH_HOST 0
 #define DGLHIP_PLAN_PATH_ROWS 1
 #define DGLHIP_PLAN_PATH_BLOCKED 2
 #define DGLHIP_PLAN_PATH_MAX_BLOCKED 3
+#define DGLHIP_PLAN_PATH_SWEEP 4
 int dglhip_spmm_plan_schedule(DGLHipSpmmPlan plan, int msg_op, int reduce_op, int64_t feat_len,
                               int64_t ufeat_ld, int64_t num_src_rows, int64_t efeat_len,
                               int edge_layout, const int64_t* erow, void* stream, int* path,
@@ -606,6 +608,16 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      int max_spin, void* stream);
 /* Study knobs of the sweep kernels: workgroups per CU of a launch (0: the
  * occupancy limit) and row gathers in flight per wave (16 or 32). */
+/* The plan's source-sweep schedule (DGLHIP_PLAN_PATH_SWEEP, DESIGN.md §4.1
+ * "Source sweep"): taken for copy_u sum / mean of fp32 rows of 128 floats
+ * over a source-monotone CSR whose referenced source table is table_min
+ * bytes or more, in ceil(table / block_bytes) <= 256 blocks; lag and
+ * max_spin are the soft barrier's (dglhip_gspmm_sweep_stream_device).
+ * Defaults: on (DGLHIP_SWEEP=off: off), 256 MiB, 6 MiB, 4, 2000. */
+int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
+                              int max_spin);
+int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes, int* lag,
+                              int* max_spin);
 int dglhip_set_sweep_per_cu(int per_cu);
 int dglhip_set_sweep_unroll(int unroll);
 

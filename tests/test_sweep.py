@@ -151,3 +151,52 @@ def test_sweep_stream_bits(lag, rpw):
     rnd = kernel.build_csr(n, n, torch.from_numpy(dst).to(dev), torch.from_numpy(src).to(dev),
                            kernel.ORDER_EID, dev)
     assert tool.stream_layout(rnd, 128, lo, hi, rnd.row_order, 1, rpw) is None
+
+
+def test_plan_takes_the_sweep_for_large_tables():
+    """A source table past the sweep's threshold (here lowered to 32 MiB):
+    the plan schedules the sweep (path 4) for copy_u sum and mean of 128
+    floats; update_all's forward and backward keep the oracle's bits, the
+    same as with the sweep off; a 64-float table and a random-order graph
+    stay on the other schedules."""
+    import dgl
+    import dgl.function as fn
+    dev = _dev()
+    n_src, n_dst, m = 120_000, 30_000, 2_000_000   # 61 MB source table
+    rng = np.random.default_rng(11)
+    src = rng.integers(0, n_src, m)
+    dst = rng.integers(0, n_dst, m)
+    o = np.lexsort((dst, src))
+    src, dst = src[o], dst[o]
+    H = torch.randn(n_src, 128, generator=torch.Generator().manual_seed(12))
+    G = torch.randn(n_src, 128, generator=torch.Generator().manual_seed(13))
+    ref = O.spmm_coo(n_src, dst, src, H.numpy())
+    old = kernel.set_sweep_schedule(table_min=32 << 20, block_bytes=2 << 20)
+    try:
+        adj = kernel.from_coo(n_src, n_src, torch.from_numpy(dst).to(dev),
+                              torch.from_numpy(src).to(dev), kernel.ORDER_EID, dev)
+        path, launches = adj.fwd.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM, 128, 0, n_src)
+        assert path == kernel.PLAN_PATH_SWEEP and launches >= 1
+        path64, _ = adj.fwd.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM, 64, 0, n_src)
+        assert path64 != kernel.PLAN_PATH_SWEEP
+        res = {}
+        for on in (True, False):
+            kernel.set_sweep_schedule(on=on)
+            g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+            h = H.to(dev).requires_grad_(True)
+            g.ndata["h"] = h
+            g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+            g.ndata["o"].backward(G.to(dev))
+            o_sum = g.ndata["o"].detach().cpu()
+            g.update_all(fn.copy_src("h", "m"), fn.mean("m", "o"))
+            res[on] = (o_sum, g.ndata["o"].detach().cpu(), h.grad.cpu())
+        assert np.array_equal(res[True][0].numpy(), ref)
+        for a, b in zip(res[True], res[False]):
+            assert torch.equal(a, b)
+        rnd = rng.permutation(m)
+        adj_r = kernel.from_coo(n_src, n_src, torch.from_numpy(dst[rnd]).to(dev),
+                                torch.from_numpy(src[rnd]).to(dev), kernel.ORDER_EID, dev)
+        path_r, _ = adj_r.fwd.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM, 128, 0, n_src)
+        assert path_r != kernel.PLAN_PATH_SWEEP
+    finally:
+        kernel.set_sweep_schedule(**old)

@@ -81,19 +81,30 @@ def main():
     ap.add_argument("--lag", type=int, nargs="+", default=[0, 1, 2])
     ap.add_argument("--per-cu", type=int, default=0, help="workgroups per CU (0: occupancy)")
     ap.add_argument("--unroll", type=int, default=16)
+    ap.add_argument("--scale", type=int, default=1, help="weak-scaled graph, rank 0's rows")
     ap.add_argument("--no-cursor", action="store_true", help="skip the cursor kernel")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    src, dst, n = data.reddit_like(device=dev)
+    src, dst, n = data.reddit_like(scale=args.scale, device=dev)
+    n_src = n
+    if args.scale > 1:
+        # rank 0 of a weak-scaled N-rank row split: its rows' in-edges, sources
+        # over all N x 232,965 nodes (the table N times the headline's)
+        n = n // args.scale
+        keep = dst < n
+        src, dst = src[keep], dst[keep]
+        o = torch.argsort(src * n + dst)  # source-major, as the generator numbers them
+        src, dst = src[o], dst[o]
+        del keep, o
     if args.order == "random":
         g = torch.Generator(device=dev).manual_seed(5)
         p = torch.randperm(src.numel(), device=dev, generator=g)
         src, dst = src[p], dst[p]
-    adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+    adj = kernel.from_coo(n, n_src, dst, src, kernel.ORDER_EID, dev)
     del src, dst
     csr = adj.fwd
     F = 128
-    h = torch.rand(n, F, device=dev) * 2 - 1
+    h = torch.rand(n_src, F, device=dev) * 2 - 1
     out = torch.empty(n, F, device=dev)
     old = kernel.set_blocked("off")
     kernel.gspmm_into(csr, out, h)
