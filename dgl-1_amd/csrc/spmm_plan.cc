@@ -514,6 +514,10 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
   if (table < sp.table_min) return nullptr;
   const int64_t want = cdiv(table, sp.block_bytes);
   if (want < 2 || want > 256) return nullptr;  // the barrier covers 256 blocks
+  // measured on rows of 108-493 slots: sparser rows switch
+  // rows every slot and many generations re-sweep every block, so those keep
+  // the other schedules
+  if (nnz_ < 128 * std::max<int64_t>(num_nonempty_, 1)) return nullptr;
   const int B = static_cast<int>(want);
   std::lock_guard<std::mutex> lk(mu_);
   auto hit = sweeps_.find(B);
@@ -529,6 +533,10 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
   sw->B = B;
   sw->rows_per_wave = RPW;
   sw->launches = cdiv(R_, wpl * RPW);
+  if (sw->launches > 16) {
+    sweeps_[B] = nullptr;
+    return nullptr;
+  }
   const int64_t W = sw->launches * wpl;
   sw->waves_total = W;
   // the kernel's deal: row i of the schedule order -> wave (i / W odd ?

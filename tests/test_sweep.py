@@ -162,7 +162,7 @@ def test_plan_takes_the_sweep_for_large_tables():
     import dgl
     import dgl.function as fn
     dev = _dev()
-    n_src, n_dst, m = 120_000, 30_000, 2_000_000   # 61 MB source table
+    n_src, n_dst, m = 120_000, 12_000, 2_000_000   # 61 MB source table, 167 slots per row
     rng = np.random.default_rng(11)
     src = rng.integers(0, n_src, m)
     dst = rng.integers(0, n_dst, m)
