@@ -836,8 +836,10 @@ _GAT_BLOCK_BYTES_NOGRAD = int(os.environ.get("DGLHIP_GAT_BLOCK_BYTES_NOGRAD", 7 
 # attention recomputed per pair, the dot's exchanges, the epilogue): larger
 # slices, as the forward's (Reddit-shaped 8 x 16, forward + backward: 4 / 6 /
 # 8 / 11 / 14 / 18 MiB 17.97 / 16.86 / 16.48 / 16.18 / 16.25 / 16.39 ms, the
-# same bits; tools/gat_bwd_sweep.py, profiles/r04/gat_bwd_sweep.json)
-_GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 11 << 20))
+# same bits; tools/gat_bwd_sweep.py, profiles/r04/gat_bwd_sweep.json); at 5
+# waves per SIMD (r05) 6 / 8 / 11 / 14 / 18 / 24 MiB 14.63 / 14.30 / 14.15 /
+# 14.06 / 14.29 / 14.65 ms (profiles/r05/gat_fwd/bwd_block_sweep_*.json)
+_GAT_BWD_BLOCK_BYTES = int(os.environ.get("DGLHIP_GAT_BWD_BLOCK_BYTES", 14 << 20))
 
 
 class _PlanLaunch(object):
