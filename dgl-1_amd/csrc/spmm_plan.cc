@@ -947,7 +947,7 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
                      sw.counts.data<int32_t>(), sw.B, sw.seg.data<int64_t>(),
                      sw.lay.data<int32_t>(), plan.indptr(), static_cast<const float*>(uf), a.out,
                      a.red == DGLHIP_REDUCE_MEAN ? 1 : 0, sw.rows_per_wave,
-                     sw.arrive.data<int32_t>(), sp.lag, sp.max_spin,
+                     sw.arrive.data<int32_t>(), sw.arrive.numel(), sp.lag, sp.max_spin,
                      s) == 0,
                  DGLGetLastError());
     return;

@@ -424,8 +424,8 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      const int32_t* row_order, const int32_t* counts,
                                      int num_blocks, const int64_t* seg_beg, const int32_t* lay,
                                      const int64_t* indptr, const float* ufeat, float* out,
-                                     int mean, int rows_per_wave, int* arrive, int lag,
-                                     int max_spin, void* stream_) {
+                                     int mean, int rows_per_wave, int* arrive,
+                                     int64_t arrive_len, int lag, int max_spin, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
@@ -439,6 +439,8 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
   const int64_t launches = waves_total / wpl;
   // per launch and block 8 counters on 128-B lines of their own
   const int64_t per_launch = int64_t(num_blocks) * 8 * 32;
+  DGLHIP_CHECK(lag <= 0 || arrive_len >= launches * per_launch,
+               "the barrier needs " << launches * per_launch << " counters, got " << arrive_len);
   if (lag > 0)
     HIP_CALL(hipMemsetAsync(arrive, 0, sizeof(int) * launches * per_launch, stream));
   for (int64_t l = 0; l < launches; ++l) {

@@ -596,16 +596,17 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
  * waves_total a multiple of dglhip_gspmm_sweep_stream_geometry's waves per
  * launch. lag > 0: a soft barrier (a wave starts block b once every
  * workgroup has finished block b - lag, or after max_spin polls) over
- * device-scope counters in arrive (launches * num_blocks * 256 ints, zeroed
- * by the call); results never depend on it. rows_per_wave 10 or 19;
+ * device-scope counters in arrive (arrive_len >= launches * num_blocks * 256
+ * ints, zeroed by the call; concurrent calls need their own); results never
+ * depend on it. rows_per_wave 10 or 19;
  * feat_len 128. */
 int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch);
 int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      const int32_t* row_order, const int32_t* counts,
                                      int num_blocks, const int64_t* seg_beg, const int32_t* lay,
                                      const int64_t* indptr, const float* ufeat, float* out,
-                                     int mean, int rows_per_wave, int* arrive, int lag,
-                                     int max_spin, void* stream);
+                                     int mean, int rows_per_wave, int* arrive,
+                                     int64_t arrive_len, int lag, int max_spin, void* stream);
 /* Study knobs of the sweep kernels: workgroups per CU of a launch (0: the
  * occupancy limit) and row gathers in flight per wave (16 or 32). */
 /* The plan's source-sweep schedule (DGLHIP_PLAN_PATH_SWEEP, DESIGN.md §4.1

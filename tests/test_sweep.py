@@ -143,7 +143,8 @@ def test_sweep_stream_bits(lag, rpw):
         out = torch.full((n, 128), float("nan"), device=dev)
         check_call(LIB.dglhip_gspmm_sweep_stream_device(
             n, lt["W"], ptr(csr.row_order), ptr(lt["counts"]), lt["B"], ptr(lt["seg"]),
-            ptr(lt["lay"]), ptr(csr.indptr), ptr(h), ptr(out), mean, rpw, ptr(arrive), lag, 2000,
+            ptr(lt["lay"]), ptr(csr.indptr), ptr(h), ptr(out), mean, rpw, ptr(arrive),
+            arrive.numel(), lag, 2000,
             stream))
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy(), want), mean

@@ -131,7 +131,8 @@ def main():
     def stream_run(lt, rpw, lag):
         check_call(LIB.dglhip_gspmm_sweep_stream_device(
             n, lt["W"], ptr(order), ptr(lt["counts"]), lt["B"], ptr(lt["seg"]), ptr(lt["lay"]),
-            ptr(csr.indptr), ptr(h), ptr(out), 0, rpw, ptr(arrive), lag, 2000, stream))
+            ptr(csr.indptr), ptr(h), ptr(out), 0, rpw, ptr(arrive), arrive.numel(), lag, 2000,
+            stream))
 
     res = {"graph": "reddit_like", "order": args.order, "rounds": []}
     layouts = {}
