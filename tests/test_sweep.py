@@ -194,6 +194,16 @@ def test_plan_takes_the_sweep_for_large_tables():
         assert np.array_equal(res[True][0].numpy(), ref)
         for a, b in zip(res[True], res[False]):
             assert torch.equal(a, b)
+        # the C-ABI route (DGLFuncCall, a plan made for the call) takes it too
+        kernel.set_sweep_schedule(on=True)
+        from dgl import _ffi
+        fwd = adj.fwd
+        out = torch.full((n_src, 128), float("nan"), device=dev)
+        stream = ("handle", torch.cuda.current_stream().cuda_stream)
+        _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, fwd.indptr, fwd.indices, None, H.to(dev),
+                         None, out, None, fwd.row_order, stream)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), ref)
         rnd = rng.permutation(m)
         adj_r = kernel.from_coo(n_src, n_src, torch.from_numpy(dst[rnd]).to(dev),
                                 torch.from_numpy(src[rnd]).to(dev), kernel.ORDER_EID, dev)
