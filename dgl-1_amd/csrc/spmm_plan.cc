@@ -505,36 +505,44 @@ std::shared_ptr<Cuts> SpmmPlan::cuts_for(int B, hipStream_t s) {
   return c;
 }
 
-std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
+std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStream_t s) {
   const SweepPolicy sp = sweep_policy();
   constexpr int RPW = 19;  // rows per wave of the 128-float sweep kernel
   if (!sp.on || !on_device() || nnz_ == 0 || nnz_ >= (int64_t(1) << 31) || R_ == 0) return nullptr;
   const auto lh = span(s);
   const int64_t table = (lh.second - lh.first) * row_bytes;
-  if (table < sp.table_min) return nullptr;
+  if (table < (accum ? sp.accum_table_min : sp.table_min)) return nullptr;
   const int64_t want = cdiv(table, sp.block_bytes);
   if (want < 2 || want > 256) return nullptr;  // the barrier covers 256 blocks
   // measured on rows of 108-493 slots: sparser rows switch
   // rows every slot and many generations re-sweep every block, so those keep
   // the other schedules
-  if (nnz_ < 128 * std::max<int64_t>(num_nonempty_, 1)) return nullptr;
+  if (nnz_ < (accum ? sp.accum_min_slots : 128) * std::max<int64_t>(num_nonempty_, 1))
+    return nullptr;
   const int B = static_cast<int>(want);
+  const int key = B * 2 + (accum ? 1 : 0);
   std::lock_guard<std::mutex> lk(mu_);
-  auto hit = sweeps_.find(B);
+  auto hit = sweeps_.find(key);
   if (hit != sweeps_.end()) return hit->second;
   auto split = block_split(B, s);
   if (split->total_suffix != 0) {  // a row's blocks go back down: no run layout
-    sweeps_[B] = nullptr;
+    sweeps_[key] = nullptr;
     return nullptr;
   }
-  int64_t wpl = 0;
-  DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry(RPW, &wpl) == 0 && wpl > 0, DGLGetLastError());
   auto sw = std::make_shared<SweepPlan>();
+  sw->per_cu = accum ? sp.accum_per_cu : 0;
+  int64_t wpl = 0;
+  DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry(RPW, sw->per_cu, &wpl) == 0 && wpl > 0,
+               DGLGetLastError());
   sw->B = B;
   sw->rows_per_wave = RPW;
-  sw->launches = cdiv(R_, wpl * RPW);
+  sw->accum = accum;
+  // an accumulating run leaves rows without slots as they are: it deals only
+  // the schedule's non-empty prefix (the degree-descending order)
+  sw->rows_dealt = accum ? num_nonempty_ : R_;
+  sw->launches = cdiv(sw->rows_dealt, wpl * RPW);
   if (sw->launches > 16) {
-    sweeps_[B] = nullptr;
+    sweeps_[key] = nullptr;
     return nullptr;
   }
   const int64_t W = sw->launches * wpl;
@@ -554,7 +562,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
         for (int j = 0; j < RPW; ++j) {
           const int64_t pos = (j & 1) ? (W - 1 - w) : w;
           const int64_t i = int64_t(j) * W + pos;
-          if (i >= R_) break;  // rows of a wave are a prefix of its rounds
+          if (i >= sw->rows_dealt) break;  // rows of a wave are a prefix of its rounds
           const int64_t r = order.empty() ? i : order[i];
           item_start[r * B + b] = off;
           off += cnt[r * B + b];
@@ -576,7 +584,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, hipStream_t s) {
     hip_ok(hipStreamSynchronize(s), "sweep layout");  // the staging arrays go out of scope
   }
   sw->arrive = empty({sw->launches * B * 256}, 0, 32);
-  sweeps_[B] = sw;
+  sweeps_[key] = sw;
   return sw;
 }
 
@@ -824,11 +832,12 @@ Decision decide(SpmmPlan& plan, const RunArgs& a, hipStream_t s) {
   const int64_t ld_in = strided ? a.ldu : a.F;
   const bool fp32u = a.msg != DGLHIP_MSG_COPY_U_BF16;
   if (a.F == 0 || plan.num_rows() == 0) return d;
-  if ((a.red == DGLHIP_REDUCE_SUM || a.red == DGLHIP_REDUCE_MEAN) && a.msg == DGLHIP_MSG_COPY_U &&
+  if ((a.red == DGLHIP_REDUCE_SUM || a.red == DGLHIP_REDUCE_MEAN ||
+       a.red == DGLHIP_REDUCE_SUM_ACCUM) && a.msg == DGLHIP_MSG_COPY_U &&
       a.ufeat && !a.efeat && !strided && a.F == 128) {
     // tables past the L2-sized blocked schedule's range: the source sweep
     // (running sums in LDS, no per-block pass over out)
-    d.sw = plan.sweep(a.F * 4, s);
+    d.sw = plan.sweep(a.F * 4, a.red == DGLHIP_REDUCE_SUM_ACCUM, s);
     if (d.sw) {
       d.path = PATH_SWEEP;
       return d;
@@ -943,11 +952,11 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
     const SweepPlan& sw = *d.sw;
     const SweepPolicy sp = sweep_policy();
     DGLHIP_CHECK(dglhip_gspmm_sweep_stream_device(
-                     plan.num_rows(), sw.waves_total, plan.row_order(),
+                     sw.rows_dealt, sw.waves_total, plan.row_order(),
                      sw.counts.data<int32_t>(), sw.B, sw.seg.data<int64_t>(),
                      sw.lay.data<int32_t>(), plan.indptr(), static_cast<const float*>(uf), a.out,
-                     a.red == DGLHIP_REDUCE_MEAN ? 1 : 0, sw.rows_per_wave,
-                     sw.arrive.data<int32_t>(), sw.arrive.numel(), sp.lag, sp.max_spin,
+                     sw.accum ? 2 : (a.red == DGLHIP_REDUCE_MEAN ? 1 : 0), sw.rows_per_wave,
+                     sw.per_cu, sw.arrive.data<int32_t>(), sw.arrive.numel(), sp.lag, sp.max_spin,
                      s) == 0,
                  DGLGetLastError());
     return;
@@ -1124,25 +1133,41 @@ using namespace dglhip;
 extern "C" {
 
 int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
-                              int max_spin) {
+                              int max_spin, int64_t accum_table_min, int64_t accum_min_slots,
+                              int accum_per_cu) {
   API_BEGIN();
-  DGLHIP_CHECK(table_min >= 0 && block_bytes > 0 && lag >= 0 && max_spin >= 0,
+  DGLHIP_CHECK(table_min >= 0 && block_bytes > 0 && lag >= 0 && max_spin >= 0 &&
+                   accum_table_min >= 0 && accum_min_slots >= 0 && accum_per_cu >= 0,
                "invalid sweep schedule");
   std::lock_guard<std::mutex> lk(g_pol_mu);
-  sweep_ref() = SweepPolicy{on != 0 ? 1 : 0, table_min, block_bytes, lag, max_spin};
+  SweepPolicy& p = sweep_ref();
+  p.on = on != 0 ? 1 : 0;
+  p.table_min = table_min;
+  p.block_bytes = block_bytes;
+  p.lag = lag;
+  p.max_spin = max_spin;
+  p.accum_table_min = accum_table_min;
+  p.accum_min_slots = accum_min_slots;
+  p.accum_per_cu = accum_per_cu;
   API_END();
 }
 
 int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes, int* lag,
-                              int* max_spin) {
+                              int* max_spin, int64_t* accum_table_min, int64_t* accum_min_slots,
+                              int* accum_per_cu) {
   API_BEGIN();
-  DGLHIP_CHECK(on && table_min && block_bytes && lag && max_spin, "null pointer argument");
+  DGLHIP_CHECK(on && table_min && block_bytes && lag && max_spin && accum_table_min &&
+                   accum_min_slots && accum_per_cu,
+               "null pointer argument");
   const SweepPolicy p = sweep_policy();
   *on = p.on;
   *table_min = p.table_min;
   *block_bytes = p.block_bytes;
   *lag = p.lag;
   *max_spin = p.max_spin;
+  *accum_table_min = p.accum_table_min;
+  *accum_min_slots = p.accum_min_slots;
+  *accum_per_cu = p.accum_per_cu;
   API_END();
 }
 

@@ -114,6 +114,9 @@ struct BlockSplit {
 struct SweepPlan {
   int B = 0;
   int rows_per_wave = 0;
+  int per_cu = 0;         // workgroups per CU of a launch (0: occupancy)
+  bool accum = false;     // continues the rows' chains (SUM_ACCUM)
+  int64_t rows_dealt = 0; // rows of the schedule order the launches cover
   int64_t waves_total = 0, launches = 0;
   rt::NDArray lay;     // int32[nnz]: column ids in sweep order
   rt::NDArray pos;     // int32[nnz]: the CSR slot of each (the scatter's by-product)
@@ -131,6 +134,12 @@ struct SweepPolicy {
   int64_t block_bytes = 6 << 20;
   int lag = 4;
   int max_spin = 2000;
+  // accumulating runs (the pipelined multi-GPU segments, SUM_ACCUM): their
+  // own table and row-length floors, and a cap of 3 workgroups per CU that
+  // leaves room for the exchange's kernels on the comm stream
+  int64_t accum_table_min = int64_t(160) << 20;
+  int64_t accum_min_slots = 64;
+  int accum_per_cu = 3;
 };
 SweepPolicy sweep_policy();
 
@@ -189,7 +198,7 @@ class SpmmPlan {
   const int64_t* plan_eidmap(BlockedPlan& bp, const int64_t* eid, hipStream_t s);
 
   // the sweep plan for row_bytes (nullptr when it does not apply)
-  std::shared_ptr<SweepPlan> sweep(int64_t row_bytes, hipStream_t s);
+  std::shared_ptr<SweepPlan> sweep(int64_t row_bytes, bool accum, hipStream_t s);
 
   int64_t heavy_threshold() const;  // split_threshold on this CSR and part
   SplitPlan& split_plan(int64_t threshold, bool skip_empty, int64_t chunk, hipStream_t s);

@@ -185,7 +185,9 @@ __global__ __launch_bounds__(256) void gspmm_sweep_kernel(
 // running sum switches rows (LDS store + load) where a row's run ends. Exact
 // for source-monotone chains (each row's block-b slots contiguous in slot
 // order), which the layout builder checks.
-template <int VEC, int RPW, int UNROLL, bool MEAN>
+// MODE 0 sum, 1 mean, 2 sum continuing every row's chain from its value in
+// out (the pipelined multi-GPU segments' SUM_ACCUM)
+template <int VEC, int RPW, int UNROLL, int MODE>
 __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     int64_t num_rows, int64_t waves_total, int64_t wave_base,
     const int32_t* __restrict__ row_order, const int32_t* __restrict__ counts, int nblocks,
@@ -225,7 +227,7 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     const int64_t i = int64_t(lane) * waves_total + pos;
     if (i < num_rows) {
       row = row_order ? row_order[i] : static_cast<int32_t>(i);
-      if (MEAN) deg = static_cast<int32_t>(indptr[row + 1] - indptr[row]);
+      if (MODE == 1) deg = static_cast<int32_t>(indptr[row + 1] - indptr[row]);
     }
   }
   const int nrows = __builtin_popcountll(__ballot(row >= 0));
@@ -234,7 +236,9 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     return;
   }
   float* my = sums + w * RPW * F;
-  for (int j = 0; j < nrows; ++j) stv<VEC>(my + j * F + f0, Vec<VEC>::zero());
+  for (int j = 0; j < nrows; ++j)
+    stv<VEC>(my + j * F + f0, MODE == 2 ? ldv<VEC>(out + int64_t(lane_of(row, j)) * F + f0)
+                                        : Vec<VEC>::zero());
   int32_t cnt_next = row >= 0 ? counts[int64_t(row) * nblocks] : 0;
   int64_t base_next = seg_beg[wv * nblocks];
   for (int b = 0; b < nblocks; ++b) {
@@ -295,7 +299,7 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   for (int j = 0; j < nrows; ++j) {
     const int32_t r = lane_of(row, j);
     V acc = ldv<VEC>(my + j * F + f0);
-    if (MEAN) {
+    if (MODE == 1) {
       const int32_t d = lane_of(deg, j);
       if (d > 1) acc = acc / Vec<VEC>::splat(static_cast<float>(d));
     }
@@ -307,23 +311,27 @@ int g_sweep_per_cu = 0;  // study knob: workgroups per CU of a launch (0: occupa
 int g_sweep_unroll = 16;  // study knob: row gathers in flight per wave (16 or 32)
 
 template <typename K>
-int64_t sweep_waves_per_launch(K kern) {
+int64_t sweep_waves_per_launch(K kern, int cap = 0) {
   int dev = 0, cus = 0, per_cu = 0;
   HIP_CALL(hipGetDevice(&dev));
   HIP_CALL(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   HIP_CALL(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64 * kSweepWaves, 0));
-  if (g_sweep_per_cu > 0) per_cu = std::min(per_cu, g_sweep_per_cu);
+  if (cap <= 0) cap = g_sweep_per_cu;
+  if (cap > 0) per_cu = std::min(per_cu, cap);
   DGLHIP_CHECK(cus > 0 && per_cu > 0, "sweep kernel does not fit a CU");
   return int64_t(cus) * per_cu * kSweepWaves;
 }
 
+template <int RPW, int U>
+auto stream_kernel_u(int mode) {
+  return mode == 2 ? gspmm_sweep_stream_kernel<2, RPW, U, 2>
+         : mode == 1 ? gspmm_sweep_stream_kernel<2, RPW, U, 1>
+                     : gspmm_sweep_stream_kernel<2, RPW, U, 0>;
+}
+
 template <int RPW>
-auto stream_kernel(bool mean) {
-  if (g_sweep_unroll == 32)
-    return mean ? gspmm_sweep_stream_kernel<2, RPW, 32, true>
-                : gspmm_sweep_stream_kernel<2, RPW, 32, false>;
-  return mean ? gspmm_sweep_stream_kernel<2, RPW, 16, true>
-              : gspmm_sweep_stream_kernel<2, RPW, 16, false>;
+auto stream_kernel(int mode) {
+  return g_sweep_unroll == 32 ? stream_kernel_u<RPW, 32>(mode) : stream_kernel_u<RPW, 16>(mode);
 }
 
 template <int VEC, int RPW, bool MEAN>
@@ -412,11 +420,13 @@ int dglhip_set_sweep_unroll(int unroll) {
   API_END();
 }
 
-int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch) {
+int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int per_cu,
+                                       int64_t* waves_per_launch) {
   API_BEGIN();
   DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
-  *waves_per_launch = rows_per_wave == 10 ? sweep_waves_per_launch(stream_kernel<10>(false))
-                                          : sweep_waves_per_launch(stream_kernel<19>(false));
+  DGLHIP_CHECK(per_cu >= 0, "workgroups per CU " << per_cu);
+  *waves_per_launch = rows_per_wave == 10 ? sweep_waves_per_launch(stream_kernel<10>(0), per_cu)
+                                          : sweep_waves_per_launch(stream_kernel<19>(0), per_cu);
   API_END();
 }
 
@@ -424,15 +434,16 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      const int32_t* row_order, const int32_t* counts,
                                      int num_blocks, const int64_t* seg_beg, const int32_t* lay,
                                      const int64_t* indptr, const float* ufeat, float* out,
-                                     int mean, int rows_per_wave, int* arrive,
+                                     int mode, int rows_per_wave, int per_cu, int* arrive,
                                      int64_t arrive_len, int lag, int max_spin, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
   DGLHIP_CHECK(num_rows >= 0 && num_rows < (int64_t(1) << 31) && num_blocks >= 1, "sizes");
+  DGLHIP_CHECK(mode >= 0 && mode <= 2 && per_cu >= 0, "mode " << mode << ", per_cu " << per_cu);
   if (num_rows == 0) return 0;
-  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mean != 0) : stream_kernel<19>(mean != 0);
-  const int64_t wpl = sweep_waves_per_launch(kern);
+  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mode) : stream_kernel<19>(mode);
+  const int64_t wpl = sweep_waves_per_launch(kern, per_cu);
   DGLHIP_CHECK(waves_total % wpl == 0 && waves_total * rows_per_wave >= num_rows,
                "layout for " << waves_total << " waves, launches hold " << wpl);
   DGLHIP_CHECK(lag <= 0 || arrive, "the soft barrier needs its counters");

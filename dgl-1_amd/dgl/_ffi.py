@@ -131,15 +131,16 @@ def _load():
                                                _vp, _c_i64, _vp, _c_i64, _vp, _vp]),
         "dglhip_gspmm_sweep_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp, _c_i64,
                                                _c_i64, _c_int, _c_int, _c_int, _vp]),
-        "dglhip_gspmm_sweep_stream_geometry": (_c_int, [_c_int, _vp]),
+        "dglhip_gspmm_sweep_stream_geometry": (_c_int, [_c_int, _c_int, _vp]),
         "dglhip_set_sweep_per_cu": (_c_int, [_c_int]),
-        "dglhip_set_sweep_schedule": (_c_int, [_c_int, _c_i64, _c_i64, _c_int, _c_int]),
-        "dglhip_get_sweep_schedule": (_c_int, [_vp, _vp, _vp, _vp, _vp]),
+        "dglhip_set_sweep_schedule": (_c_int, [_c_int, _c_i64, _c_i64, _c_int, _c_int, _c_i64,
+                                               _c_i64, _c_int]),
+        "dglhip_get_sweep_schedule": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
         "dglhip_set_gat_fwd_waves": (_c_int, [_c_int]),
         "dglhip_set_sweep_unroll": (_c_int, [_c_int]),
         "dglhip_gspmm_sweep_stream_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _c_int, _vp, _vp,
-                                                      _vp, _vp, _vp, _c_int, _c_int, _vp, _c_i64,
-                                                      _c_int, _c_int, _vp]),
+                                                      _vp, _vp, _vp, _c_int, _c_int, _c_int, _vp,
+                                                      _c_i64, _c_int, _c_int, _vp]),
         "dglhip_gspmm_max_ranges_device": (_c_int, [_c_int, _c_i64, _c_i64, _vp, _vp, _vp, _c_int,
                                                     _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp,
                                                     _vp]),

@@ -144,14 +144,17 @@ def scheduled(**changes):
 
 def sweep_schedule():
     """The source-sweep schedule's knobs (DESIGN.md §4.1 "Source sweep"):
-    {"on", "table_min", "block_bytes", "lag", "max_spin"}."""
-    on, lag, spin = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    tmin, bb = ctypes.c_int64(), ctypes.c_int64()
+    {"on", "table_min", "block_bytes", "lag", "max_spin", "accum_table_min",
+    "accum_min_slots", "accum_per_cu"}."""
+    on, lag, spin, apc = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    tmin, bb, atm, ams = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
     check_call(LIB.dglhip_get_sweep_schedule(ctypes.byref(on), ctypes.byref(tmin),
                                              ctypes.byref(bb), ctypes.byref(lag),
-                                             ctypes.byref(spin)))
+                                             ctypes.byref(spin), ctypes.byref(atm),
+                                             ctypes.byref(ams), ctypes.byref(apc)))
     return {"on": bool(on.value), "table_min": tmin.value, "block_bytes": bb.value,
-            "lag": lag.value, "max_spin": spin.value}
+            "lag": lag.value, "max_spin": spin.value, "accum_table_min": atm.value,
+            "accum_min_slots": ams.value, "accum_per_cu": apc.value}
 
 
 def set_sweep_schedule(**changes):
@@ -164,7 +167,9 @@ def set_sweep_schedule(**changes):
         raise DGLError("unknown sweep knobs: %s" % sorted(unknown))
     check_call(LIB.dglhip_set_sweep_schedule(int(bool(new["on"])), int(new["table_min"]),
                                              int(new["block_bytes"]), int(new["lag"]),
-                                             int(new["max_spin"])))
+                                             int(new["max_spin"]), int(new["accum_table_min"]),
+                                             int(new["accum_min_slots"]),
+                                             int(new["accum_per_cu"])))
     return old
 
 

@@ -598,14 +598,18 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
  * workgroup has finished block b - lag, or after max_spin polls) over
  * device-scope counters in arrive (arrive_len >= launches * num_blocks * 256
  * ints, zeroed by the call; concurrent calls need their own); results never
- * depend on it. rows_per_wave 10 or 19;
+ * depend on it. mode 0 sum, 1 mean, 2 sum continuing each dealt row's chain
+ * from its value in out (SUM_ACCUM); num_rows rows of row_order are dealt.
+ * per_cu > 0 caps the workgroups per CU of a launch (room for kernels on
+ * other streams, e.g. RCCL's); the layout's waves_total must be a multiple
+ * of the geometry's waves per launch for the same rows_per_wave and per_cu. rows_per_wave 10 or 19;
  * feat_len 128. */
-int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int64_t* waves_per_launch);
+int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int per_cu, int64_t* waves_per_launch);
 int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      const int32_t* row_order, const int32_t* counts,
                                      int num_blocks, const int64_t* seg_beg, const int32_t* lay,
                                      const int64_t* indptr, const float* ufeat, float* out,
-                                     int mean, int rows_per_wave, int* arrive,
+                                     int mode, int rows_per_wave, int per_cu, int* arrive,
                                      int64_t arrive_len, int lag, int max_spin, void* stream);
 /* Study knobs of the sweep kernels: workgroups per CU of a launch (0: the
  * occupancy limit) and row gathers in flight per wave (16 or 32). */
@@ -614,11 +618,16 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
  * over a source-monotone CSR whose referenced source table is table_min
  * bytes or more, in ceil(table / block_bytes) <= 256 blocks; lag and
  * max_spin are the soft barrier's (dglhip_gspmm_sweep_stream_device).
- * Defaults: on (DGLHIP_SWEEP=off: off), 256 MiB, 6 MiB, 4, 2000. */
+ * Accumulating runs (SUM_ACCUM: the pipelined multi-GPU segments) take it
+ * from accum_table_min bytes with accum_min_slots slots per non-empty row,
+ * at accum_per_cu workgroups per CU. Defaults: on (DGLHIP_SWEEP=off: off),
+ * 256 MiB, 6 MiB, 4, 2000; 160 MiB, 64, 3. */
 int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
-                              int max_spin);
+                              int max_spin, int64_t accum_table_min, int64_t accum_min_slots,
+                              int accum_per_cu);
 int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes, int* lag,
-                              int* max_spin);
+                              int* max_spin, int64_t* accum_table_min,
+                              int64_t* accum_min_slots, int* accum_per_cu);
 int dglhip_set_sweep_per_cu(int per_cu);
 int dglhip_set_sweep_unroll(int unroll);
 

@@ -143,7 +143,7 @@ def test_sweep_stream_bits(lag, rpw):
         out = torch.full((n, 128), float("nan"), device=dev)
         check_call(LIB.dglhip_gspmm_sweep_stream_device(
             n, lt["W"], ptr(csr.row_order), ptr(lt["counts"]), lt["B"], ptr(lt["seg"]),
-            ptr(lt["lay"]), ptr(csr.indptr), ptr(h), ptr(out), mean, rpw, ptr(arrive),
+            ptr(lt["lay"]), ptr(csr.indptr), ptr(h), ptr(out), mean, rpw, 0, ptr(arrive),
             arrive.numel(), lag, 2000,
             stream))
         torch.cuda.synchronize()
@@ -209,5 +209,37 @@ def test_plan_takes_the_sweep_for_large_tables():
                                 torch.from_numpy(src[rnd]).to(dev), kernel.ORDER_EID, dev)
         path_r, _ = adj_r.fwd.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM, 128, 0, n_src)
         assert path_r != kernel.PLAN_PATH_SWEEP
+    finally:
+        kernel.set_sweep_schedule(**old)
+
+
+def test_accumulating_sweep_continues_the_chains():
+    """SUM_ACCUM (the pipelined multi-GPU segments) through the plan's sweep:
+    each non-empty row's chain continues from its value in out, rows without
+    slots keep theirs; the same bits as the other schedules."""
+    dev = _dev()
+    n_src, n_dst, m = 120_000, 12_000, 2_000_000
+    rng = np.random.default_rng(21)
+    src = rng.integers(0, n_src, m)
+    dst = rng.integers(0, n_dst // 2, m)     # half the rows have no slots
+    o = np.lexsort((dst, src))
+    src, dst = src[o], dst[o]
+    csr = kernel.build_csr(n_dst, n_src, torch.from_numpy(dst).to(dev),
+                           torch.from_numpy(src).to(dev), kernel.ORDER_EID, dev)
+    h = torch.randn(n_src, 128, generator=torch.Generator().manual_seed(22)).to(dev)
+    base = torch.randn(n_dst, 128, generator=torch.Generator().manual_seed(23)).to(dev)
+    old = kernel.set_sweep_schedule(accum_table_min=32 << 20, block_bytes=2 << 20)
+    try:
+        path, _ = csr.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, 128, 0, n_src)
+        assert path == kernel.PLAN_PATH_SWEEP
+        res = []
+        for on in (True, False):
+            kernel.set_sweep_schedule(on=on)
+            out = base.clone()
+            kernel.gspmm_into(csr, out, h, accumulate=True)
+            torch.cuda.synchronize()
+            res.append(out.cpu())
+        assert torch.equal(res[0], res[1])
+        assert torch.equal(res[0][n_dst // 2:], base[n_dst // 2:].cpu())
     finally:
         kernel.set_sweep_schedule(**old)

@@ -46,7 +46,7 @@ def stream_layout(csr, F, lo, hi, order, mib, rpw):
     if bool(((rows[1:] == rows[:-1]) & (blk[1:] < blk[:-1])).any()):
         return None
     wpl = ctypes.c_int64()
-    check_call(LIB.dglhip_gspmm_sweep_stream_geometry(rpw, ctypes.byref(wpl)))
+    check_call(LIB.dglhip_gspmm_sweep_stream_geometry(rpw, 0, ctypes.byref(wpl)))
     wpl = wpl.value
     L = -(-n // (wpl * rpw))
     W = L * wpl
@@ -131,7 +131,7 @@ def main():
     def stream_run(lt, rpw, lag):
         check_call(LIB.dglhip_gspmm_sweep_stream_device(
             n, lt["W"], ptr(order), ptr(lt["counts"]), lt["B"], ptr(lt["seg"]), ptr(lt["lay"]),
-            ptr(csr.indptr), ptr(h), ptr(out), 0, rpw, ptr(arrive), arrive.numel(), lag, 2000,
+            ptr(csr.indptr), ptr(h), ptr(out), 0, rpw, 0, ptr(arrive), arrive.numel(), lag, 2000,
             stream))
 
     res = {"graph": "reddit_like", "order": args.order, "rounds": []}
