@@ -583,7 +583,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStr
     sw->counts = upload(cnt, R_ * B, 0, 32, s);
     hip_ok(hipStreamSynchronize(s), "sweep layout");  // the staging arrays go out of scope
   }
-  sw->arrive = empty({sw->launches * B * 256}, 0, 32);
+  sw->arrive = empty({sw->launches * (int64_t(B) * 8 + 1) * 32}, 0, 32);
   sweeps_[key] = sw;
   return sw;
 }

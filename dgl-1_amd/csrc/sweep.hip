@@ -48,18 +48,26 @@ __device__ __noinline__ void sweep_arrive(int* wg_done, int* arrive, int b) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// false when max_spin polls ran out (the wave then stops waiting: a launch
-// whose workgroups are not all resident costs one bounded wait per wave)
-__device__ __noinline__ bool sweep_wait(const int* arrive, int b, int need, int max_spin) {
+// Waits until every workgroup of the launch that has STARTED (the counter
+// `started`, one add per workgroup as it begins) has finished block b; a
+// workgroup not yet resident (the CU held by another stream's kernel) is
+// not waited for — it runs later, on its own. false when max_spin polls ran
+// out (a safety net: the wave then stops waiting).
+__device__ __noinline__ bool sweep_wait(const int* arrive, const int* started, int b,
+                                        int max_spin) {
   const int lane = threadIdx.x & 63;
   const int* c = arrive + int64_t(b) * kShards * kStride;
   for (int spin = 0; spin < max_spin; ++spin) {
     int seen = lane < kShards ? __hip_atomic_load(c + lane * kStride, __ATOMIC_RELAXED,
                                                   __HIP_MEMORY_SCOPE_AGENT)
                               : 0;
+    const int need =
+        lane == kShards ? __hip_atomic_load(started, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                        : 0;
 #pragma unroll
     for (int d = 1; d < kShards; d <<= 1) seen += __shfl_xor(seen, d);
-    if (__builtin_amdgcn_readfirstlane(seen) >= need) return true;
+    if (__builtin_amdgcn_readfirstlane(seen) >= __builtin_amdgcn_readlane(need, kShards))
+      return true;
     __builtin_amdgcn_s_sleep(8);
   }
   return false;
@@ -208,10 +216,13 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   // device-scope counters of that block (sharded by workgroup, each on its
   // own 128-B line); a waiting wave polls the 8 with device-scope loads.
   __shared__ int wg_done[kMaxLagBlocks];
-  const int need = static_cast<int>(gridDim.x);
   const bool sync = lag > 0 && nblocks <= kMaxLagBlocks;
+  // the launch's workgroups that have begun: after the nblocks blocks' counters
+  int* started = sync ? arrive + int64_t(nblocks) * kShards * kStride : nullptr;
   if (sync) {
     for (int i = threadIdx.x; i < kMaxLagBlocks; i += blockDim.x) wg_done[i] = 0;
+    if (threadIdx.x == 0)
+      __hip_atomic_fetch_add(started, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
   }
   auto arrive_at = [&](int b) {
@@ -219,7 +230,7 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   };
   bool waiting = true;
   auto wait_for = [&](int b) {
-    if (sync && waiting && b >= lag) waiting = sweep_wait(arrive, b - lag, need, max_spin);
+    if (sync && waiting && b >= lag) waiting = sweep_wait(arrive, started, b - lag, max_spin);
   };
   int32_t row = -1, deg = 0;
   if (lane < RPW && wv < waves_total) {
@@ -448,8 +459,9 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                "layout for " << waves_total << " waves, launches hold " << wpl);
   DGLHIP_CHECK(lag <= 0 || arrive, "the soft barrier needs its counters");
   const int64_t launches = waves_total / wpl;
-  // per launch and block 8 counters on 128-B lines of their own
-  const int64_t per_launch = int64_t(num_blocks) * 8 * 32;
+  // per launch and block 8 counters on 128-B lines of their own, then the
+  // launch's count of workgroups begun
+  const int64_t per_launch = (int64_t(num_blocks) * 8 + 1) * 32;
   DGLHIP_CHECK(lag <= 0 || arrive_len >= launches * per_launch,
                "the barrier needs " << launches * per_launch << " counters, got " << arrive_len);
   if (lag > 0)

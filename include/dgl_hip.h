@@ -595,10 +595,11 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
  * tools/r05/sweep_study.py stream_layout, exact for source-monotone rows);
  * waves_total a multiple of dglhip_gspmm_sweep_stream_geometry's waves per
  * launch. lag > 0: a soft barrier (a wave starts block b once every
- * workgroup has finished block b - lag, or after max_spin polls) over
- * device-scope counters in arrive (arrive_len >= launches * num_blocks * 256
- * ints, zeroed by the call; concurrent calls need their own); results never
- * depend on it. mode 0 sum, 1 mean, 2 sum continuing each dealt row's chain
+ * workgroup that has begun has finished block b - lag, or after max_spin
+ * polls) over
+ * device-scope counters in arrive (arrive_len >= launches * (num_blocks * 8 +
+ * 1) * 32 ints, zeroed by the call; concurrent calls need their own; a
+ * workgroup not yet resident is not waited for); results never depend on it. mode 0 sum, 1 mean, 2 sum continuing each dealt row's chain
  * from its value in out (SUM_ACCUM); num_rows rows of row_order are dealt.
  * per_cu > 0 caps the workgroups per CU of a launch (room for kernels on
  * other streams, e.g. RCCL's); the layout's waves_total must be a multiple

@@ -437,6 +437,75 @@ def _overlap_worker(rank, world, port, graph, q):
         dist.destroy_process_group()
 
 
+def _sweep_segments_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "dgl-1_amd")]
+    from dgl import data, kernel
+    from dgl.distributed import PartitionedGraph, balanced_bounds
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, F = 20000, 128
+        src, dst, n = data.chung_lu(n, 60 * n, 30.0, seed=13)
+        bounds = balanced_bounds(torch.bincount(dst, minlength=n), world)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        sel = (dst >= lo) & (dst < hi)
+        gen = torch.Generator().manual_seed(17)
+        H = torch.rand(n, F, generator=gen) * 2 - 1
+        G = torch.randn(n, F, generator=gen)
+        res = {}
+        for on in (True, False):
+            # the accumulating sweep's floors lowered to this small graph
+            old = kernel.set_sweep_schedule(on=on, accum_table_min=0, accum_min_slots=1,
+                                            block_bytes=256 << 10)
+            try:
+                pg = PartitionedGraph(n, src[sel], dst[sel], bounds, dev, pipeline_chunks=2,
+                                      overlap=True)
+                if on:  # the halo chunks' segments take the sweep
+                    seg = pg.seg_csrs[-1]
+                    path, _ = seg.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, F, 0,
+                                                seg.num_cols)
+                    assert path == kernel.PLAN_PATH_SWEEP, path
+                outs = []
+                for it in range(3):
+                    h = (H[lo:hi] * float(it + 1)).to(dev).requires_grad_(True)
+                    o = pg.update_all(h)
+                    o.backward((G[lo:hi] * float(it + 1)).to(dev))
+                    torch.cuda.synchronize()
+                    outs.append((o.detach().cpu(), h.grad.cpu()))
+                res[on] = outs
+            finally:
+                kernel.set_sweep_schedule(**old)
+        for (a, ga), (b, gb) in zip(res[True], res[False]):
+            assert torch.equal(a, b) and torch.equal(ga, gb)
+        q.put((rank, "ok"))
+    except Exception as e:  # report to the parent, then fail the worker
+        q.put((rank, repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_pipelined_segments_on_the_accumulating_sweep():
+    """Two gloo ranks on the one GPU, F = 128, the pipelined exchange on its
+    side stream: with the accumulating sweep's floors lowered the halo
+    chunks' SUM_ACCUM segments run the source sweep; forward rows and
+    backward gradients over three steps equal the other schedules' bit for
+    bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.spawn(_sweep_segments_worker, args=(2, _free_port(), q), nprocs=2, join=True)
+    got = sorted(q.get(timeout=5) for _ in range(2))
+    assert got == [(0, "ok"), (1, "ok")], got
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("graph", ["chung_lu", "banded"])
 def test_pipelined_comm_stream_two_gloo_ranks_one_gpu(graph):

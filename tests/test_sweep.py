@@ -136,7 +136,7 @@ def test_sweep_stream_bits(lag, rpw):
     lo, hi = int(csr.indices.min()), int(csr.indices.max()) + 1
     lt = tool.stream_layout(csr, 128, lo, hi, csr.row_order, 1, rpw)  # 1-MiB slices: 25 blocks
     assert lt is not None and lt["B"] > 8
-    arrive = torch.zeros(lt["launches"] * lt["B"] * 256, dtype=torch.int32, device=dev)
+    arrive = torch.zeros(lt["launches"] * (lt["B"] * 8 + 1) * 32, dtype=torch.int32, device=dev)
     h = H.to(dev)
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     for mean, want in ((0, ref), (1, ref_mean)):
