@@ -538,8 +538,16 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStr
   sw->rows_per_wave = RPW;
   sw->accum = accum;
   // an accumulating run leaves rows without slots as they are: it deals only
-  // the schedule's non-empty prefix (the degree-descending order)
-  sw->rows_dealt = accum ? num_nonempty_ : R_;
+  // the schedule's non-empty prefix when the order is degree-descending (a
+  // caller's order that is not: every row, the empty ones rewritten as they are)
+  const std::vector<int32_t>& ord = host_order(s);
+  const int64_t* ip = host_indptr_->data();
+  bool prefix = accum;
+  for (int64_t i = 0; prefix && i < num_nonempty_; ++i) {
+    const int64_t r = ord.empty() ? i : ord[i];
+    prefix = ip[r + 1] > ip[r];
+  }
+  sw->rows_dealt = prefix ? num_nonempty_ : R_;
   sw->launches = cdiv(sw->rows_dealt, wpl * RPW);
   if (sw->launches > 16) {
     sweeps_[key] = nullptr;
@@ -550,7 +558,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStr
   // the kernel's deal: row i of the schedule order -> wave (i / W odd ?
   // W - 1 - i % W : i % W), its row i / W; each wave's run in block b holds
   // its rows' block-b slots in that order; runs ordered (launch, block, wave)
-  const std::vector<int32_t>& order = host_order(s);
+  const std::vector<int32_t>& order = ord;
   const int32_t* cnt = split->counts.data();
   std::vector<int64_t> item_start(static_cast<size_t>(R_) * B, 0);
   std::vector<int64_t> seg(static_cast<size_t>(W) * B, 0);

@@ -241,5 +241,17 @@ def test_accumulating_sweep_continues_the_chains():
             res.append(out.cpu())
         assert torch.equal(res[0], res[1])
         assert torch.equal(res[0][n_dst // 2:], base[n_dst // 2:].cpu())
+        # a schedule order that is not degree-descending (empty rows first):
+        # the sweep deals every row, same bits
+        kernel.set_sweep_schedule(on=True)
+        rev = kernel.build_csr(n_dst, n_src, torch.from_numpy(dst).to(dev),
+                               torch.from_numpy(src).to(dev), kernel.ORDER_EID, dev)
+        rev.row_order = torch.arange(n_dst - 1, -1, -1, dtype=torch.int32, device=dev)
+        path, _ = rev.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, 128, 0, n_src)
+        assert path == kernel.PLAN_PATH_SWEEP
+        out = base.clone()
+        kernel.gspmm_into(rev, out, h, accumulate=True)
+        torch.cuda.synchronize()
+        assert torch.equal(out.cpu(), res[1])
     finally:
         kernel.set_sweep_schedule(**old)
