@@ -94,6 +94,8 @@ SweepPolicy& sweep_ref() {
     SweepPolicy q;
     const char* e = std::getenv("DGLHIP_SWEEP");
     if (e && (std::strcmp(e, "0") == 0 || std::strcmp(e, "off") == 0)) q.on = 0;
+    const char* pc = std::getenv("DGLHIP_SWEEP_ACCUM_PER_CU");
+    if (pc) q.accum_per_cu = std::max(0, std::atoi(pc));
     return q;
   }();
   return p;

@@ -135,11 +135,13 @@ struct SweepPolicy {
   int lag = 4;
   int max_spin = 2000;
   // accumulating runs (the pipelined multi-GPU segments, SUM_ACCUM): their
-  // own table and row-length floors, and a cap of 3 workgroups per CU that
-  // leaves room for the exchange's kernels on the comm stream
+  // own table and row-length floors, and workgroups per CU (0: occupancy, 4;
+  // emulated N = 8 rank: 4 / 3 / 2 per CU 7.16 / 7.75 / 9.19 ms; a workgroup
+  // held back by the exchange's kernels is not waited for, so the full grid
+  // costs at most its late workgroups' solo time; DGLHIP_SWEEP_ACCUM_PER_CU)
   int64_t accum_table_min = int64_t(160) << 20;
   int64_t accum_min_slots = 64;
-  int accum_per_cu = 3;
+  int accum_per_cu = 0;
 };
 SweepPolicy sweep_policy();
 

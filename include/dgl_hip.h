@@ -621,8 +621,9 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
  * max_spin are the soft barrier's (dglhip_gspmm_sweep_stream_device).
  * Accumulating runs (SUM_ACCUM: the pipelined multi-GPU segments) take it
  * from accum_table_min bytes with accum_min_slots slots per non-empty row,
- * at accum_per_cu workgroups per CU. Defaults: on (DGLHIP_SWEEP=off: off),
- * 256 MiB, 6 MiB, 4, 2000; 160 MiB, 64, 3. */
+ * at accum_per_cu workgroups per CU (0: the occupancy limit). Defaults: on
+ * (DGLHIP_SWEEP=off: off), 256 MiB, 6 MiB, 4, 2000; 160 MiB, 64, 0
+ * (DGLHIP_SWEEP_ACCUM_PER_CU). */
 int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
                               int max_spin, int64_t accum_table_min, int64_t accum_min_slots,
                               int accum_per_cu);
