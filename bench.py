@@ -524,6 +524,20 @@ def pipelined_blocks(pg):
                                  [torch.float32] + [halo] * (len(pg.seg_csrs) - 1))
 
 
+def sweep_segments(pg):
+    """Segments of a pipelined partition the plan runs on the accumulating
+    source sweep (DESIGN.md §4.1 "Source sweep"; the N = 8 halo chunks)."""
+    if pg.chunks <= 0 or pg.device.type != "cuda":
+        return 0
+    n = 0
+    for csr in pg.seg_csrs:
+        if csr.nnz:
+            path, _ = csr.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, FEAT, 0,
+                                        csr.num_cols)
+            n += path == kernel.PLAN_PATH_SWEEP
+    return n
+
+
 def gather_peak(table_bytes, blocks=0):
     """(peak GB/s, source) of a row gather from a ``table_bytes`` table: with
     the source-blocked schedule (``blocks`` > 0) the guide's L2 indexed-row
@@ -1089,6 +1103,11 @@ def main(argv=None):
             pg.update_all(h_local)
         parallelism = describe_partition(pg, world, args)
         blocks = pipelined_blocks(pg)
+        nsw = sweep_segments(pg) if pg.halo_dtype is None else 0
+        if nsw:
+            parallelism += ("; %d of the %d segments on the accumulating source sweep (running "
+                            "sums in LDS, DESIGN.md 4.1), the rest as listed"
+                            % (nsw, len(pg.seg_csrs)))
     del src, dst
     _sync(dev)
     if dev.type == "cuda":
