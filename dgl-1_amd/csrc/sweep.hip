@@ -37,8 +37,7 @@ constexpr int kSweepWaves = 4;  // waves per workgroup
 constexpr int kMaxLagBlocks = 256;  // source blocks the soft barrier covers
 constexpr int kShards = 8, kStride = 32;
 
-// the soft barrier's two halves, out of line: they run once per block and
-// wave, and inlined they cost the gather loop ~40 VGPRs
+// the soft barrier's two halves (once per block and wave)
 __device__ __noinline__ void sweep_arrive(int* wg_done, int* arrive, int b) {
   const int lane = threadIdx.x & 63;
   int last = 0;
@@ -253,6 +252,9 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   int32_t cnt_next = row >= 0 ? counts[int64_t(row) * nblocks] : 0;
   int64_t base_next = seg_beg[wv * nblocks];
   for (int b = 0; b < nblocks; ++b) {
+    // the previous block's arrival, at one site for both of its exits (two
+    // sites cost the gather loop 30 VGPRs: 88 -> 58)
+    if (b > 0) arrive_at(b - 1);
     const int32_t cnt = cnt_next;
     // uniform by construction; said so, the column ids load through SGPRs
     const int32_t* run = lay + ((int64_t(__builtin_amdgcn_readfirstlane(
@@ -271,10 +273,7 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     }
     const int32_t total = lane_of(incl, 63);
     wait_for(b);
-    if (total == 0) {
-      arrive_at(b);
-      continue;
-    }
+    if (total == 0) continue;
     const uint64_t live = __ballot(cnt > 0);
     int j = __builtin_ctzll(live);
     int32_t rend = lane_of(incl, j);
@@ -305,8 +304,8 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
       }
     }
     stv<VEC>(my + j * F + f0, acc);
-    arrive_at(b);
   }
+  arrive_at(nblocks - 1);
   for (int j = 0; j < nrows; ++j) {
     const int32_t r = lane_of(row, j);
     V acc = ldv<VEC>(my + j * F + f0);
