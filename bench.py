@@ -972,6 +972,7 @@ def main(argv=None):
     t0 = time.time()
     real_reddit = None
     blocks = 0
+    nsw = 0  # pipelined segments on the accumulating source sweep
     if args.workload == "rmat":
         src, dst, n = data.rmat(args.rmat_scale, 16, seed=0, device=dev)
         kernel.set_row_split("auto")
@@ -1122,7 +1123,8 @@ def main(argv=None):
         kernel_timing=("GPU span of each g-SpMM call between two events on the launch stream "
                        "(every launch of the call and its output's zero fill), summed per step"
                        if dev.type == "cuda" else "host wall time per step"),
-        kernel="gspmm_sum_kernel<copy_u> (rank 0%s)" % (
+        kernel="gspmm_sum_kernel<copy_u>%s (rank 0%s)" % (
+            " + gspmm_sweep_stream_kernel" if nsw else "",
             ", every segment of the pipelined partition" if dist.is_initialized() else
             ", every block launch and short-row tier of one call" if blocks else ""),
         traffic_source=None if pmc is None else
