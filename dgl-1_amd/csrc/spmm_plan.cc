@@ -96,6 +96,8 @@ SweepPolicy& sweep_ref() {
     if (e && (std::strcmp(e, "0") == 0 || std::strcmp(e, "off") == 0)) q.on = 0;
     const char* pc = std::getenv("DGLHIP_SWEEP_ACCUM_PER_CU");
     if (pc) q.accum_per_cu = std::max(0, std::atoi(pc));
+    const char* lg = std::getenv("DGLHIP_SWEEP_LAG");
+    if (lg) q.lag = std::max(0, std::atoi(lg));
     const char* tm = std::getenv("DGLHIP_SWEEP_ACCUM_TABLE_MIN");  // bytes
     if (tm) q.accum_table_min = std::max<int64_t>(0, std::atoll(tm));
     const char* ms = std::getenv("DGLHIP_SWEEP_ACCUM_MIN_SLOTS");
