@@ -131,7 +131,7 @@ def build_parser():
                     help="nccl (= RCCL) for runs; gloo lets several ranks share one GPU "
                          "to rehearse the multi-rank path")
     ap.add_argument("--no-model-legs", action="store_true",
-                    help="N=1: skip the configs[2]-[4] model legs (gat, gat_pubmed, sage, rgcn)")
+                    help="N=1: skip the model legs (gcn_reddit, gat, sage, gat_pubmed, rgcn)")
     ap.add_argument("--no-strong-leg", action="store_true",
                     help="N>1: skip the fixed-graph (strong scaling) Reddit block")
     ap.add_argument("--emulate-strong", action="store_true",
@@ -1275,6 +1275,10 @@ def main(argv=None):
             not args.no_model_legs and not on_cpu and not args.dist_rehearsal):
         import bench_models as bm
         want = not args.no_cpu_baseline
+        legs.run("gcn_reddit", lambda: None, lambda _: bm.gcn_reddit_leg(
+            g, dev, kernel, gather_peak, algorithmic_bytes, sample, cpu=want),
+            collective=False)
+        _release(dev)
         legs.run("gat", lambda: None, lambda _: bm.gat_layer_leg(
             g, dev, kernel, gather_peak, sample, cpu=want), collective=False)
         legs.run("sage", lambda: None, lambda _: bm.sage_leg(

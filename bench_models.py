@@ -114,6 +114,169 @@ def roof(bytes_, ms, peak, source, kernel_name, **extra):
     return r
 
 
+# -- GCN on the Reddit-shaped graph (configs[1]) -------------------------------
+GCN_IN, GCN_HIDDEN, GCN_CLASSES = 602, 128, 41
+
+
+def gcn_reddit_data(n, dev, seed=7):
+    """configs[1]'s synthetic node data at the graph's size: 602-wide
+    features (Reddit's embedding width), 41 classes, 66 % training nodes."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(seed)
+    feats = 0.1 * torch.randn(n, GCN_IN, generator=gen, device=dev)
+    labels = torch.randint(0, GCN_CLASSES, (n,), generator=gen, device=dev)
+    mask = (torch.rand(n, generator=gen, device=dev) < 0.66).nonzero(as_tuple=True)[0]
+    return feats, labels, mask
+
+
+def gcn_norm(g, dev):
+    """gcn_spmv.py:138-143: in-degree^-1/2 (self-loops already in the graph)."""
+    norm = torch.pow(g.in_degrees().float(), -0.5)
+    norm[torch.isinf(norm)] = 0
+    return norm.unsqueeze(1).to(dev)
+
+
+def gcn_reddit_leg(g, dev, kernel, gather_peak, algorithmic_bytes, sample, epochs=10, warmup=3,
+                   cpu=True, dropout=0.5):
+    """configs[1]: the example's 2-layer GCN (602 -> 128 -> 41, dropout 0.5 ahead
+    of the second layer, Adam; examples/gcn/gcn_spmv.py, the reference's
+    examples/pytorch/gcn/gcn_spmv.py:45-62,136-143,168-182) for full-graph
+    epochs on the headline graph (self-loops included): forward, cross-entropy
+    over the training nodes, backward, Adam. Eager, and one replayed HIP graph
+    per epoch (the example's --hip-graph)."""
+    gcn = example("gcn/gcn_spmv.py")
+    n, E = g.number_of_nodes(), g.number_of_edges()
+    feats, labels, mask = gcn_reddit_data(n, dev)
+    lab = labels.index_select(0, mask)
+    saved = {k: g.ndata[k] for k in ("h",) if k in g.ndata}
+    g.ndata["norm"] = gcn_norm(g, dev)
+    try:
+        def build(capturable=False):
+            torch.manual_seed(0)
+            m = gcn.GCN(g, GCN_IN, GCN_HIDDEN, GCN_CLASSES, 1, F.relu, dropout).to(dev)
+            return m, torch.optim.Adam(m.parameters(), lr=1e-2, weight_decay=5e-4,
+                                       capturable=capturable, fused=True)
+        model, opt = build()
+        model.train()
+
+        def epoch():
+            logits = model(feats)
+            loss = F.cross_entropy(logits.index_select(0, mask), lab)
+            opt.zero_grad(set_to_none=True)
+            loss.backward()
+            opt.step()
+        ms, kms, launches = wall_steps(epoch, epochs, warmup, dev, kernel)
+        # the same epoch captured once and replayed
+        gmodel, gopt = build(capturable=True)
+        gmodel.train()
+
+        def gepoch():
+            gopt.zero_grad(set_to_none=True)
+            F.cross_entropy(gmodel(feats).index_select(0, mask), lab).backward()
+            gopt.step()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                gepoch()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        gopt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph, stream=side):
+            gepoch()
+        gms = call_ms(graph.replay, epochs, dev)
+        del graph, gmodel, gopt
+        # the aggregations alone: layer 1 (F = 128, the headline product) and
+        # layer 2 (F = 41, rows padded to 48 floats by the plan)
+        adj = g.sparse_adjacency(dev)
+        h128 = torch.rand(n, GCN_HIDDEN, device=dev)
+        h41 = torch.rand(n, GCN_CLASSES, device=dev)
+        a128 = call_ms(lambda: kernel.gspmm(adj, "copy_u", "sum", h128), epochs, dev)
+        a41 = call_ms(lambda: kernel.gspmm(adj, "copy_u", "sum", h41), epochs, dev)
+        blocks = kernel.blocked_schedule(adj, h128)
+        peak, src_ = gather_peak(n * GCN_HIDDEN * 4, blocks)
+        del h128, h41
+    finally:
+        g.ndata.pop("norm", None)
+        for k in ("h",):
+            g.ndata.pop(k, None)
+        g.ndata.update(saved)
+    res = {"value": E / (gms * 1e-3), "unit": "edges/s per epoch (HIP graph)",
+           "ms_per_epoch": ms, "ms_per_epoch_hip_graph": gms, "kernel_ms": kms,
+           "launches_per_epoch": launches, "epochs": epochs, "warmup": warmup,
+           "aggregation_ms": {"layer1_f128": a128, "layer2_f41": a41},
+           "config": "configs[1]: 2-layer GCN %d-%d-%d (examples/gcn/gcn_spmv.py: dense Linear, "
+                     "norm, update_all(copy_src, sum), norm, bias, ReLU; dropout %.1f ahead of "
+                     "layer 2), full graph = the headline graph (%d nodes, %d edges incl. "
+                     "self-loops), random features, 41 classes, 66 %% training nodes, "
+                     "cross-entropy + backward + Adam per epoch; eager and one replayed HIP "
+                     "graph" % (GCN_IN, GCN_HIDDEN, GCN_CLASSES, dropout, n, E),
+           "roofline": roof(algorithmic_bytes(E, n, GCN_HIDDEN), a128, peak, src_,
+                            "layer 1's aggregation: g-SpMM copy_u + sum, F = 128 (%d launches "
+                            "per call); per epoch 4 aggregations run (F = 128 and 41, forward "
+                            "and transposed)" % max(blocks, 1)),
+           "cpu_baseline": None}
+    if cpu and sample is not None:
+        res["cpu_baseline"] = gcn_reddit_cpu(sample, n, dropout)
+    return res
+
+
+def gcn_reddit_cpu(sample, n, dropout, target_edges=2_000_000, epochs=2):
+    """The reference's epoch on the host: gcn_spmv.py:45-62,168-182 with its
+    backend's products (torch.sparse.mm on the uncoalesced COO adjacency,
+    python/dgl/backend/pytorch/tensor.py:45-51,145-146) written out in torch,
+    over the in-edges of the first rows of the headline's CPU sample (about
+    ``target_edges``, sources over all ``n`` nodes; every node keeps its
+    Linear and its loss term)."""
+    rows, d, s = sample
+    cum = torch.cumsum(torch.bincount(d, minlength=rows), 0)
+    r1 = min(int(torch.searchsorted(cum, torch.tensor(target_edges))) + 1, rows)
+    sel = d < r1
+    d, s = d[sel], s[sel]
+    e = int(s.numel())
+    A = torch.sparse_coo_tensor(torch.stack([d, s]), torch.ones(e), (n, n))
+    deg = torch.bincount(d, minlength=n).float()
+    norm = torch.pow(deg, -0.5)
+    norm[torch.isinf(norm)] = 0
+    norm = norm.unsqueeze(1)
+    feats, labels, mask = gcn_reddit_data(n, torch.device("cpu"))
+    torch.manual_seed(0)
+    w1 = torch.nn.Parameter(torch.empty(GCN_IN, GCN_HIDDEN).uniform_(-0.088, 0.088))
+    b1 = torch.nn.Parameter(torch.zeros(GCN_HIDDEN))
+    w2 = torch.nn.Parameter(torch.empty(GCN_HIDDEN, GCN_CLASSES).uniform_(-0.156, 0.156))
+    b2 = torch.nn.Parameter(torch.zeros(GCN_CLASSES))
+    opt = torch.optim.Adam([w1, b1, w2, b2], lr=1e-2, weight_decay=5e-4)
+
+    def layer(h, w, b, act, p):
+        if p:
+            h = F.dropout(h, p)
+        h = torch.mm(h, w) * norm
+        h = torch.sparse.mm(A, h) * norm + b
+        return F.relu(h) if act else h
+
+    def once():
+        logits = layer(layer(feats, w1, b1, True, 0.0), w2, b2, False, dropout)
+        loss = F.cross_entropy(logits[mask], labels[mask])
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    once()
+    t = 0.0
+    for _ in range(epochs):
+        t0 = time.perf_counter()
+        once()
+        t += time.perf_counter() - t0
+    ms = t / epochs * 1e3
+    return {"value": e / (ms * 1e-3), "unit": "edges/s per epoch", "ms_per_epoch": ms,
+            "cores": _threads(), "kind": "reference",
+            "sample": "the reference's GCN epoch (gcn_spmv.py:45-62,168-182: torch.mm, norm, "
+                      "torch.sparse.mm on the uncoalesced COO adjacency, norm, bias, ReLU; "
+                      "dropout %.1f; cross-entropy, backward, Adam) on the in-edges of the first "
+                      "%d rows of the headline graph (%d edges, sources over all %d nodes; the "
+                      "dense layers over all %d nodes), %d epochs after one warm-up, torch %d "
+                      "threads" % (dropout, r1, e, n, n, epochs, _threads())}
+
+
 # -- GAT layer on the Reddit-shaped graph: 8 heads x 16 ------------------------
 def gat_fwd_bytes(E, n, H, D, stored, logits_read=True):
     """Fused GAT forward (kernel.gat_aggregate): per edge the gathered feature

@@ -59,11 +59,11 @@ void register_kernel_functions() {
   //  arg_out|null, row_order|null, stream)
   // (msg, reduce, indptr, indices, eid|null, ufeat|null, efeat|null, out,
   //  arg_out|null, row_order|null, stream[, plan|null[, edge_layout]]):
-  // the product on the plan's schedule — the plan made by
-  // dglhip._CAPI_SpmmPlanCreate for this CSR, or one built for the call (the
-  // schedule's structures then cost their build every call: a caller that
-  // runs the product repeatedly keeps a plan, as the reference keeps its
-  // adjacency per context, graph_index.py:537-585). eid: the CSR's edge ids
+  // the product on the plan's schedule when a plan made by
+  // dglhip._CAPI_SpmmPlanCreate for this CSR is passed (a caller that runs
+  // the product repeatedly keeps one, as the reference keeps its adjacency
+  // per context, graph_index.py:537-585); without one, a single launch over
+  // the CSR (no schedule build, no host sync; capturable). eid: the CSR's edge ids
   // (edge_layout BY_EID, the default; NULL = identity) or a per-slot map of
   // efeat rows (BY_MAP); efeat rows by slot with BY_SLOT.
   register_global("dglhip._CAPI_GSpMM", [](const Args& a, RetValue*) {
@@ -112,6 +112,39 @@ void register_kernel_functions() {
     std::unique_ptr<SpmmPlan> own;
     SpmmPlan* plan = static_cast<SpmmPlan*>(plan_h);
     hipStream_t s = static_cast<hipStream_t>(dev ? stream_or_current(stream, out) : nullptr);
+    // No plan: the product is one launch (dglhip_gspmm_device / _strided /
+    // _host), with no host sync, no allocation and no schedule build, so a
+    // plan-less call costs what it did before plans existed and can be
+    // captured into a HIP graph. Only a strided operand on the host, or a
+    // row_order listing a subset of the rows, still takes a plan made for
+    // the call.
+    const bool full_order = !order || numel(order) == rows;
+    if (!plan && full_order && (dev || ldu == 0)) {
+      DGLHIP_CHECK(emode >= DGLHIP_EDGE_BY_SLOT && emode <= DGLHIP_EDGE_BY_MAP,
+                   "unknown edge layout " << emode);
+      const int64_t* erow = emode == DGLHIP_EDGE_BY_SLOT ? nullptr : I64(eid, "eid");
+      DGLHIP_CHECK(!ef || erow || emode == DGLHIP_EDGE_BY_SLOT,
+                   "edge layout " << emode << " needs eid");
+      const float* u = static_cast<const float*>(ufp);
+      int rc;
+      if (!dev) {
+        rc = dglhip_gspmm_host(msg, red, rows, F, I64(indptr, "indptr"), I32(indices, "indices"),
+                               erow, u, F32(ef, "efeat"), elen, F32(out, "out"),
+                               I64(arg, "arg_out"), 0);
+      } else if (ldu != 0 && ldu != F) {
+        DGLHIP_CHECK(!arg, "a strided operand takes no arg_out (sum / mean reducers)");
+        rc = dglhip_gspmm_strided_device(msg, red, rows, F, ldu, I64(indptr, "indptr"),
+                                         I32(indices, "indices"), erow, u, F32(ef, "efeat"),
+                                         elen, F32(out, "out"), I32(order, "row_order"), s);
+      } else {
+        rc = dglhip_gspmm_device(msg, red, rows, F, I64(indptr, "indptr"),
+                                 I32(indices, "indices"), erow, u, F32(ef, "efeat"), elen,
+                                 F32(out, "out"), I64(arg, "arg_out"), I32(order, "row_order"),
+                                 s);
+      }
+      throw_last(rc);
+      return;
+    }
     if (plan) {
       DGLHIP_CHECK(plan->on_device() == dev && (!dev || plan->device_id() == out->device_id),
                    "the plan lives on another device");

@@ -5,27 +5,46 @@ python/dgl/backend/pytorch/tensor.py:45-51,145-146.
 
 It is plain ctypes over the C-ABI (include/dgl_hip.h) and torch — nothing
 from this engine's Python package — so it drops into the reference as it
-stands. The adjacency the reference builds once and caches per context
-(GraphIndex.adjacency_matrix, python/dgl/graph_index.py:537-585, whose
-``idx`` already lives on the context) becomes, on its first product on a
-device, a CSR built on that device (dglhip_coo_to_csr_device) and its launch
-plan (dglhip_spmm_plan_create); every later ``spmm`` on that matrix runs the
-plan (dglhip_spmm_plan_run): the source-blocked schedule, the heavy-row
-split and the short-row tiers, with no per-call upload, sort or host sync.
-Whether the values are the adjacency's ones (copy_src) or edge weights
-(src_mul_edge) is decided once, when the matrix is made. The backward of
-``spmm`` with respect to the dense operand is the product over the
-transposed CSR (built on first use), as torch.sparse.mm's autograd does.
-Results equal torch.sparse.mm on the same uncoalesced COO bit for bit
-(tests/test_hip_tensor_binding.py).
+stands.
+
+Structure and values are kept apart. The structure (the COO index) is what
+the reference builds once and caches per context
+(GraphIndex.adjacency_matrix, python/dgl/graph_index.py:537-585); on its
+first product on a device it becomes a CSR built on that device
+(dglhip_coo_to_csr_device) plus its launch plan (dglhip_spmm_plan_create),
+one per orientation. That structure is cached on the index tensor itself
+(a weak map keyed by the tensor's identity and version), so the per-call
+rebuild of SPMVWithDataExecutor.run
+(python/dgl/runtime/ir/executor.py:544-548: ``sparse_matrix_indices`` of the
+cached adjacency, then ``sparse_matrix(A_data, spidx, shape)``) finds the
+same CSRs and plans: no sort, no plan build, no host sync on the second call.
+
+The values are per matrix: the adjacency's ones (copy_src: the plan's copy_u
+product) or edge weights (src_mul_edge: u_mul_e by edge id). Which one is
+decided without a device sync except for the first matrix made on an index
+(that is the adjacency itself, once per graph and device); a weighted product
+whose weights happen to be ones gives the copy_u bits anyway
+(fma(1, h, acc) == acc + h).
+
+Autograd follows torch.sparse.mm on ``th.sparse_coo_tensor(idx, data)``
+(tensor.py:45-51,145-146):
+  * dY = A^T dC, the product over the transposed CSR (same bits as torch's
+    CPU kernel on the uncoalesced COO, DESIGN.md §2);
+  * d(data)[e] = <dC[idx[0, e]], Y[idx[1, e]]> for every COO position e,
+    duplicates included (torch gives every duplicate the full dot), the
+    g-SDDMM dot (dglhip_gsddmm_device, fp32, features in order) over whichever
+    orientation walks the edge ids more nearly in order (a*b == b*a, so both
+    give the same bits).
 """
 import ctypes
 import os
+import weakref
 
 import torch as th
 
 _vp, _i64, _int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int
 _EDGE_BY_EID = 1
+_SDDMM_DOT = 0
 
 
 def _load():
@@ -47,6 +66,10 @@ def _load():
                                               _vp, ctypes.POINTER(_i64)]),
         "dglhip_spmm_plan_run": (_int, [_vp, _int, _int, _i64, _vp, _i64, _i64, _vp, _i64, _int,
                                         _vp, _vp, _vp, _vp, _i64, _vp]),
+        "dglhip_gsddmm_device": (_int, [_int, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                        _vp]),
+        "dglhip_gsddmm_host": (_int, [_int, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      _int]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -55,6 +78,10 @@ def _load():
 
 
 _lib = _load()
+
+# How many CSR + plan builds this process has made (a test reads it to show
+# that the executor's per-call rebuild reuses the cached structure).
+builds = 0
 
 
 def _check(rc):
@@ -70,10 +97,19 @@ def _p(t):
     return None if t is None else t.data_ptr()
 
 
+def _dense_f32(y):
+    # torch.sparse.mm raises on a dense operand of another dtype; so do we,
+    # rather than read its bytes as float32
+    if y.dtype != th.float32:
+        raise RuntimeError("expected scalar type Float but found %s" % y.dtype)
+    return y.contiguous()
+
+
 class _CSR(object):
     """One orientation of the matrix on one device: CSR arrays + launch plan."""
 
     def __init__(self, rows, cols, r, c, dev):
+        global builds
         nnz = r.numel()
         self.num_rows, self.num_cols = rows, cols
         self.indptr = th.empty(rows + 1, dtype=th.int64, device=dev)
@@ -96,15 +132,31 @@ class _CSR(object):
                                             _p(self.indices) if nnz else None, None, None,
                                             _stream(dev), ctypes.byref(h)))
         self.plan = h.value
+        self._loc = None
+        builds += 1
 
     def __del__(self):
-        if getattr(self, "plan", None):
-            _lib.dglhip_spmm_plan_free(self.plan)
-            self.plan = None
+        plan, self.plan = getattr(self, "plan", None), None
+        if plan and _lib is not None:  # module globals may be gone at interpreter shutdown
+            try:
+                _lib.dglhip_spmm_plan_free(plan)
+            except Exception:  # noqa: BLE001 - never raise from a finaliser
+                pass
+
+    @property
+    def eid_locality(self):
+        """Fraction of consecutive slots whose COO positions are consecutive:
+        how sequential per-edge stores at out[eid] are along this CSR (one
+        reduction + sync, once per CSR)."""
+        if self._loc is None:
+            n = self.eid.numel()
+            self._loc = 1.0 if n < 2 else \
+                float((self.eid[1:] == self.eid[:-1] + 1).sum().item()) / (n - 1)
+        return self._loc
 
     def product(self, y, weights):
         """out = A y (u_mul_e with the weights by edge id, else copy_u), sum."""
-        y = y.contiguous()
+        y = _dense_f32(y)
         dev, F = y.device, y.shape[1]
         msg, elen = (1, 1) if weights is not None else (0, 0)
         out = th.empty(self.num_rows, F, dtype=th.float32, device=dev)
@@ -118,29 +170,97 @@ class _CSR(object):
                                          None, _p(ws), nb.value, _stream(dev)))
         return out
 
+    def edge_dot(self, lhs, rhs, nnz):
+        """out[eid[k]] = <lhs[row of k], rhs[indices[k]]> (fp32, features in
+        order) for every slot k: one value per COO position."""
+        lhs, rhs = _dense_f32(lhs), _dense_f32(rhs)
+        dev, F = lhs.device, lhs.shape[1]
+        out = th.empty(nnz, dtype=th.float32, device=dev)
+        if nnz == 0:
+            return out
+        args = (_SDDMM_DOT, self.num_rows, F, 1, _p(self.indptr), _p(self.indices), _p(self.eid),
+                _p(lhs), _p(rhs), _p(out))
+        if dev.type == "cuda":
+            _check(_lib.dglhip_gsddmm_device(*(args + (_stream(dev),))))
+        else:
+            _check(_lib.dglhip_gsddmm_host(*(args + (0,))))
+        return out
+
+
+class _Structure(object):
+    """The per-device CSRs (both orientations) of one COO index; shared by
+    every matrix made on that index tensor."""
+
+    def __init__(self, idx, shape):
+        # the index itself is not held: the cache entry must not keep its key alive
+        self.shape, self.version = shape, idx._version
+        self.nnz = int(idx.shape[1])
+        self.dev = {}
+
+    def csr(self, idx, dev, transpose=False):
+        key = (str(dev), transpose)
+        if key not in self.dev:
+            r, c = (idx[1], idx[0]) if transpose else (idx[0], idx[1])
+            rows, cols = (self.shape[1], self.shape[0]) if transpose else self.shape
+            self.dev[key] = _CSR(rows, cols, r, c, dev)
+        return self.dev[key]
+
+
+# id(idx) -> (weakref to idx, _Structure); an entry leaves with its tensor.
+_structures = {}
+
+
+def _drop(key, ref):
+    hit = _structures.get(key)
+    if hit is not None and hit[0] is ref:
+        del _structures[key]
+
+
+def _structure_of(idx, shape):
+    """(structure, new): the cached structure of this index tensor, or a new
+    one when the tensor is new, has been written in place or is used with
+    another shape."""
+    key = id(idx)
+    hit = _structures.get(key)
+    if hit is not None and hit[0]() is idx:
+        st = hit[1]
+        if st.version == idx._version and st.shape == shape:
+            return st, False
+    st = _Structure(idx, shape)
+    ref = weakref.ref(idx, lambda r, k=key: _drop(k, r))
+    _structures[key] = (ref, st)
+    return st, True
+
 
 class HipSparseMatrix(object):
     """What sparse_matrix returns: the COO (index, values, shape) as the
-    reference passes it, plus per-device CSRs and plans built on first use."""
+    reference passes it; its CSRs and plans live on the index's structure."""
 
     def __init__(self, data, idx, shape):
         self.idx, self.data, self.shape = idx, data, (int(shape[0]), int(shape[1]))
-        # ones (the adjacency: copy_src) or edge weights (src_mul_edge),
-        # decided once per matrix, not per product
-        self.weights = None if bool((data == 1).all()) else data.reshape(-1).float().contiguous()
-        self._dev = {}
+        self._st, new = _structure_of(idx, self.shape)
+        if data.dim() != 1 or data.shape[0] != self._st.nnz:
+            data = data.reshape(-1)
+            if data.shape[0] != self._st.nnz:
+                raise RuntimeError("sparse_matrix: %d values for %d indices"
+                                   % (data.shape[0], self._st.nnz))
+        # ones (the adjacency: copy_src) or edge weights (src_mul_edge). Only
+        # the first matrix on an index pays a value check (a host sync); a
+        # rebuild on a cached index (SPMVWithDataExecutor) is taken as weighted
+        # without one, and so is data that asks for a gradient.
+        if data.requires_grad or not new:
+            self.ones = False
+        else:
+            self.ones = bool((data == 1).all())
 
     def csr(self, dev, transpose=False):
-        key = (str(dev), transpose)
-        if key not in self._dev:
-            r, c = (self.idx[1], self.idx[0]) if transpose else (self.idx[0], self.idx[1])
-            rows, cols = (self.shape[1], self.shape[0]) if transpose else self.shape
-            self._dev[key] = _CSR(rows, cols, r, c, dev)
-        return self._dev[key]
+        return self._st.csr(self.idx, dev, transpose)
 
-    def weights_on(self, dev):
-        w = self.weights
-        return None if w is None else w.to(dev)
+    def weights_on(self, dev, data=None):
+        if self.ones:
+            return None
+        w = self.data if data is None else data
+        return w.detach().reshape(-1).to(dev, th.float32).contiguous()
 
     def _indices(self):
         return self.idx
@@ -148,14 +268,33 @@ class HipSparseMatrix(object):
 
 class _HipSpMM(th.autograd.Function):
     @staticmethod
-    def forward(ctx, mat, y):
+    def forward(ctx, mat, data, y):
         ctx.mat = mat
-        return mat.csr(y.device).product(y, mat.weights_on(y.device))
+        w = mat.weights_on(y.device, data)
+        ctx.save_for_backward(y, w if w is not None else th.empty(0))
+        ctx.data_shape, ctx.data_dtype = data.shape, data.dtype
+        return mat.csr(y.device).product(y, w)
 
     @staticmethod
-    def backward(ctx, dy):
+    def backward(ctx, dc):
         mat = ctx.mat
-        return None, mat.csr(dy.device, transpose=True).product(dy, mat.weights_on(dy.device))
+        y, w = ctx.saved_tensors
+        w = None if mat.ones else w
+        dc = dc.contiguous()
+        dy = dd = None
+        if ctx.needs_input_grad[2]:
+            dy = mat.csr(dc.device, transpose=True).product(dc, w)
+        if ctx.needs_input_grad[1]:
+            fwd = mat.csr(dc.device)
+            bwd = mat.csr(dc.device, transpose=True)
+            # stores at out[eid] along the orientation whose slots walk the
+            # COO positions more nearly in order (the same bits either way)
+            if bwd.eid_locality > max(0.5, 2.0 * fwd.eid_locality):
+                dd = bwd.edge_dot(y, dc, mat._st.nnz)
+            else:
+                dd = fwd.edge_dot(dc, y, mat._st.nnz)
+            dd = dd.reshape(ctx.data_shape).to(ctx.data_dtype)
+        return None, dd, dy
 
 
 def get_preferred_sparse_format():
@@ -174,4 +313,4 @@ def sparse_matrix_indices(spmat):
 
 
 def spmm(x, y):
-    return _HipSpMM.apply(x, y)
+    return _HipSpMM.apply(x, x.data, y)

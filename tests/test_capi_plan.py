@@ -98,8 +98,9 @@ def test_capi_gspmm_host_with_plan():
         _free(plan)
 
 
-def test_capi_gspmm_without_plan_builds_one():
-    """No plan argument: the call makes one for itself (same bits)."""
+def test_capi_gspmm_without_plan_is_one_launch():
+    """No plan argument: one launch over the CSR, no schedule built (same
+    bits as the planned product)."""
     n, m = 800, 20_000
     src, dst = _graph(n, m, 5)
     csr = kernel.build_csr(n, n, torch.from_numpy(dst), torch.from_numpy(src),
@@ -173,6 +174,35 @@ def _events_ms(fn, iters):
     e.record()
     e.synchronize()
     return s.elapsed_time(e) / iters
+
+
+@pytest.mark.gpu
+def test_capi_gspmm_without_plan_under_stream_capture(cuda):
+    """A plan-less dglhip._CAPI_GSpMM enqueues one kernel and nothing else (no
+    allocation, no host sync), so it can be captured into a HIP graph: the
+    replayed graph gives the oracle's bits, and so does a replay after the
+    operand is overwritten in place."""
+    n, m, F = 5000, 200_000, 64
+    src, dst = _graph(n, m, 11)
+    csr = kernel.build_csr(n, n, torch.from_numpy(dst).to(cuda), torch.from_numpy(src).to(cuda),
+                           kernel.ORDER_EID, cuda)
+    gen = torch.Generator(device=cuda).manual_seed(12)
+    H = torch.rand(n, F, generator=gen, device=cuda)
+    out = torch.empty(n, F, device=cuda)
+    graph = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        with torch.cuda.graph(graph, stream=side):
+            _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, csr.indptr, csr.indices, None, H, None,
+                             out, None, None, ("handle", side.cuda_stream))
+    ip, ix, pos = O.coo_to_csr(n, dst, src)
+    for _ in range(2):
+        out.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), O.spmm_csr(ip, ix, pos, H.cpu().numpy()))
+        H.copy_(torch.rand(n, F, generator=gen, device=cuda))
 
 
 @pytest.mark.gpu

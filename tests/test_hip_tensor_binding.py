@@ -43,9 +43,9 @@ def test_binding_matches_torch_sparse_mm_host(weighted):
     ref.backward(dc)
     assert torch.equal(y.grad, y_ref.grad)
     # the matrix's CSR and plan are made once (per orientation and device)
-    assert set(mat._dev) == {("cpu", False), ("cpu", True)}
+    assert set(mat._st.dev) == {("cpu", False), ("cpu", True)}
     B.spmm(mat, y.detach())
-    assert len(mat._dev) == 2
+    assert len(mat._st.dev) == 2
     if not weighted:
         assert np.array_equal(out.detach().numpy(), O.spmm_coo(n, dst, src, y.detach().numpy()))
 
@@ -98,3 +98,136 @@ def test_binding_on_device_blocked_and_bit_exact():
     _, launches = kernel.timing_read()
     kernel.timing_enable(False)
     assert launches >= 2
+
+
+def _executor_spmv_with_data(adj, a_data, h):
+    """SPMVWithDataExecutor.run's sequence
+    (/root/reference/python/dgl/runtime/ir/executor.py:535-566) on a cached
+    adjacency ``adj``: its index, a matrix rebuilt on it with the edge data,
+    then spmm."""
+    if a_data.dim() > 1:
+        a_data = a_data.squeeze(1)
+    spidx = B.sparse_matrix_indices(adj)
+    spa, _ = B.sparse_matrix(a_data, spidx, adj.shape)
+    return B.spmm(spa, h)
+
+
+def _dot_bound(row, col, dc, h):
+    """float64 per-edge dot and its Σ|dc·h| (the fp32 dot's condition bound)."""
+    return O.sddmm_dot(row, col, dc, h), O.sddmm_dot(row, col, np.abs(dc), np.abs(h))
+
+
+@pytest.mark.parametrize("dup,sorted_src", [(False, True), (True, True), (False, False)])
+def test_spmv_with_data_sequence_host(dup, sorted_src):
+    """The executor's src_mul_edge sequence, twice, on the host, with a
+    learnable (E, 1) edge weight: output and dH equal torch.sparse.mm on the
+    same COO bit for bit, d(weights) is torch's value gradient (every
+    duplicate gets the full dot) within 1e-5 of the float64 dot, and the
+    second call builds nothing. Source-sorted edges take the transposed
+    walk for the weight gradient, unsorted ones the forward walk."""
+    n, m, F = 600, 15_000, 20
+    src, dst = _coo(n, m, 5, sorted_src)
+    if dup:  # multigraph: repeated (dst, src) pairs stay separate COO positions
+        src[1::7], dst[1::7] = src[0::7][:len(src[1::7])], dst[0::7][:len(dst[1::7])]
+    idx = torch.from_numpy(np.stack([dst, src]))
+    adj, _ = B.sparse_matrix(torch.ones(m), ("coo", idx), (n, n))
+    assert adj.ones
+    gen = torch.Generator().manual_seed(6)
+    for call in range(2):
+        before = B.builds
+        w = torch.rand(m, 1, generator=gen).requires_grad_(True)
+        h = torch.randn(n, F, generator=gen).requires_grad_(True)
+        dc = torch.randn(n, F, generator=gen)
+        out = _executor_spmv_with_data(adj, w, h)
+        out.backward(dc)
+        w_ref = w.detach().clone().requires_grad_(True)
+        h_ref = h.detach().clone().requires_grad_(True)
+        ref = torch.sparse.mm(torch.sparse_coo_tensor(idx, w_ref.squeeze(1), (n, n)), h_ref)
+        ref.backward(dc)
+        assert torch.equal(out, ref)
+        assert torch.equal(h.grad, h_ref.grad)
+        assert w.grad.shape == (m, 1)
+        want, mag = _dot_bound(dst, src, dc.numpy(), h.detach().numpy())
+        got = w.grad.squeeze(1).numpy()
+        assert np.all(np.abs(got - want) <= 1e-5 * mag + 1e-30)
+        assert np.allclose(got, w_ref.grad.squeeze(1).numpy(), rtol=1e-5, atol=1e-5 * np.abs(want).max())
+        if call == 1:
+            assert B.builds == before  # the cached adjacency's CSRs and plans
+    # a weight that asks for no gradient gets none; the dense operand still does
+    h = torch.randn(n, F, generator=gen).requires_grad_(True)
+    _executor_spmv_with_data(adj, torch.rand(m, generator=gen), h).sum().backward()
+    assert h.grad is not None
+
+
+def test_binding_rejects_non_float32_dense():
+    """torch.sparse.mm raises on a dense operand of another dtype; so does
+    the binding (it never reads float64 bytes as float32)."""
+    idx = torch.tensor([[0, 1], [1, 0]])
+    mat, _ = B.sparse_matrix(torch.ones(2), ("coo", idx), (2, 2))
+    with pytest.raises(RuntimeError):
+        B.spmm(mat, torch.ones(2, 3, dtype=torch.float64))
+
+
+def test_structure_cache_follows_the_index_tensor():
+    """The CSR cache is keyed by the index tensor itself: a new index (or
+    one written in place) builds anew, and the entry leaves with its tensor."""
+    import gc
+    idx = torch.tensor([[0, 1, 1], [1, 0, 1]])
+    y = torch.ones(2, 4)
+    mat, _ = B.sparse_matrix(torch.ones(3), ("coo", idx), (2, 2))
+    B.spmm(mat, y)
+    b0 = B.builds
+    B.spmm(B.sparse_matrix(torch.rand(3), B.sparse_matrix_indices(mat), (2, 2))[0], y)
+    assert B.builds == b0
+    idx[1, 2] = 0  # in-place write: the cached CSR no longer describes it
+    out = B.spmm(B.sparse_matrix(torch.ones(3), ("coo", idx), (2, 2))[0], y)
+    assert B.builds == b0 + 1 and torch.equal(out, torch.tensor([[1.] * 4, [2.] * 4]))
+    key = id(idx)
+    del mat, idx
+    gc.collect()
+    assert key not in B._structures
+
+
+@pytest.mark.gpu
+def test_spmv_with_data_sequence_reddit_device():
+    """The executor's SPMV_WITH_DATA sequence twice on the full Reddit-shaped
+    graph (232,965 nodes, 114.8M edges, F = 128) on the MI355X, with
+    ``A_data.requires_grad``: output and dH equal the oracle's weighted fma
+    chains bit for bit, d(A_data) is within 1e-5·Σ|dC·H| of the float64 dot
+    (a seeded sample of 2M edges plus both ends), and the second call builds
+    no CSR, sort or plan."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from dgl import data
+    dev = torch.device("cuda", 0)
+    src, dst, n = data.reddit_like(scale=1, seed=0, device=dev)
+    idx = torch.stack([dst, src])
+    m, F = src.numel(), 128
+    adj, _ = B.sparse_matrix(torch.ones(m, device=dev), ("coo", idx), (n, n))
+    s_np, d_np = src.cpu().numpy(), dst.cpu().numpy()
+    fwd = O.coo_to_csr(n, d_np, s_np)
+    bwd = O.coo_to_csr(n, s_np, d_np)
+    gen = torch.Generator(device=dev).manual_seed(7)
+    rng = np.random.default_rng(7)
+    sample = np.concatenate([[0, m - 1], rng.integers(0, m, 2_000_000)])
+    for call in range(2):
+        before = B.builds
+        w = (torch.rand(m, 1, generator=gen, device=dev)).requires_grad_(True)
+        h = (torch.rand(n, F, generator=gen, device=dev) * 2 - 1).requires_grad_(True)
+        dc = torch.rand(n, F, generator=gen, device=dev) * 2 - 1
+        out = _executor_spmv_with_data(adj, w, h)
+        out.backward(dc)
+        torch.cuda.synchronize()
+        if call == 1:
+            assert B.builds == before
+        else:
+            assert B.builds == before + 2  # forward + transpose, once
+        w_np = w.detach().squeeze(1).cpu().numpy()
+        h_np, dc_np = h.detach().cpu().numpy(), dc.cpu().numpy()
+        assert np.array_equal(out.detach().cpu().numpy(),
+                              O.spmm_csr(*fwd, h_np, val=w_np, num_threads=16))
+        assert np.array_equal(h.grad.cpu().numpy(),
+                              O.spmm_csr(*bwd, dc_np, val=w_np, num_threads=16))
+        got = w.grad.squeeze(1).cpu().numpy()[sample]
+        want, mag = _dot_bound(d_np[sample], s_np[sample], dc_np, h_np)
+        assert np.all(np.abs(got - want) <= 1e-5 * mag + 1e-30)
