@@ -513,7 +513,8 @@ std::shared_ptr<Cuts> SpmmPlan::cuts_for(int B, hipStream_t s) {
   return c;
 }
 
-std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStream_t s) {
+std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, int mode, hipStream_t s) {
+  const bool accum = mode == 2;
   const SweepPolicy sp = sweep_policy();
   constexpr int RPW = 19;  // rows per wave of the 128-float sweep kernel
   if (!sp.on || !on_device() || nnz_ == 0 || nnz_ >= (int64_t(1) << 31) || R_ == 0) return nullptr;
@@ -528,7 +529,15 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStr
   if (nnz_ < (accum ? sp.accum_min_slots : 128) * std::max<int64_t>(num_nonempty_, 1))
     return nullptr;
   const int B = static_cast<int>(want);
-  const int key = B * 2 + (accum ? 1 : 0);
+  // the layout is dealt over the waves one launch of THE kernel that will run
+  // holds (its mode and the current gathers-in-flight knob decide its
+  // occupancy), so that geometry is part of the key: a knob changed after
+  // the plan was built gets a layout of its own instead of a mismatch
+  const int per_cu = accum ? sp.accum_per_cu : 0;
+  int64_t wpl = 0;
+  DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry_mode(RPW, per_cu, mode, &wpl) == 0 && wpl > 0,
+               DGLGetLastError());
+  const std::tuple<int, int, int64_t> key(B, mode, wpl);
   std::lock_guard<std::mutex> lk(mu_);
   auto hit = sweeps_.find(key);
   if (hit != sweeps_.end()) return hit->second;
@@ -538,10 +547,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, bool accum, hipStr
     return nullptr;
   }
   auto sw = std::make_shared<SweepPlan>();
-  sw->per_cu = accum ? sp.accum_per_cu : 0;
-  int64_t wpl = 0;
-  DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry(RPW, sw->per_cu, &wpl) == 0 && wpl > 0,
-               DGLGetLastError());
+  sw->per_cu = per_cu;
   sw->B = B;
   sw->rows_per_wave = RPW;
   sw->accum = accum;
@@ -853,7 +859,9 @@ Decision decide(SpmmPlan& plan, const RunArgs& a, hipStream_t s) {
       a.ufeat && !a.efeat && !strided && a.F == 128) {
     // tables past the L2-sized blocked schedule's range: the source sweep
     // (running sums in LDS, no per-block pass over out)
-    d.sw = plan.sweep(a.F * 4, a.red == DGLHIP_REDUCE_SUM_ACCUM, s);
+    d.sw = plan.sweep(a.F * 4,
+                      a.red == DGLHIP_REDUCE_SUM_ACCUM ? 2 : (a.red == DGLHIP_REDUCE_MEAN ? 1 : 0),
+                      s);
     if (d.sw) {
       d.path = PATH_SWEEP;
       return d;

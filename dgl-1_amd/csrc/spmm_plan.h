@@ -200,7 +200,8 @@ class SpmmPlan {
   const int64_t* plan_eidmap(BlockedPlan& bp, const int64_t* eid, hipStream_t s);
 
   // the sweep plan for row_bytes (nullptr when it does not apply)
-  std::shared_ptr<SweepPlan> sweep(int64_t row_bytes, bool accum, hipStream_t s);
+  // mode: the stream kernel's (0 sum, 1 mean, 2 sum continuing out)
+  std::shared_ptr<SweepPlan> sweep(int64_t row_bytes, int mode, hipStream_t s);
 
   int64_t heavy_threshold() const;  // split_threshold on this CSR and part
   SplitPlan& split_plan(int64_t threshold, bool skip_empty, int64_t chunk, hipStream_t s);
@@ -237,7 +238,8 @@ class SpmmPlan {
   std::map<int, std::shared_ptr<BlockSplit>> splits_;
   std::map<int, std::shared_ptr<BlockedPlan>> blocked_;
   std::map<int, std::shared_ptr<Cuts>> cuts_;
-  std::map<int, std::shared_ptr<SweepPlan>> sweeps_;
+  // (blocks, kernel mode, waves per launch) -> layout (nullptr: none fits)
+  std::map<std::tuple<int, int, int64_t>, std::shared_ptr<SweepPlan>> sweeps_;
   std::map<std::tuple<int64_t, bool, int64_t>, SplitPlan> split_plans_;
   std::map<int64_t, Tiers> tiers_;
 };

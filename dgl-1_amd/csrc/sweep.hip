@@ -72,6 +72,12 @@ __device__ __noinline__ bool sweep_wait(const int* arrive, const int* started, i
   return false;
 }
 
+// Waits that ran out of polls (sweep_wait returned false), over every launch
+// on this device since the last reset; read through
+// dglhip_sweep_barrier_expiries. One vector atomic per expiry (lane 0 of the
+// wave that gave up), none on the waits that succeed.
+__device__ unsigned long long g_sweep_expired = 0;
+
 __device__ __forceinline__ int32_t lane_of(int32_t v, int j) {
   return __builtin_amdgcn_readlane(v, j);
 }
@@ -229,7 +235,12 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
   };
   bool waiting = true;
   auto wait_for = [&](int b) {
-    if (sync && waiting && b >= lag) waiting = sweep_wait(arrive, started, b - lag, max_spin);
+    if (sync && waiting && b >= lag) {
+      waiting = sweep_wait(arrive, started, b - lag, max_spin);
+      if (!waiting && lane == 0)
+        __hip_atomic_fetch_add(&g_sweep_expired, 1ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
   };
   int32_t row = -1, deg = 0;
   if (lane < RPW && wv < waves_total) {
@@ -430,14 +441,39 @@ int dglhip_set_sweep_unroll(int unroll) {
   API_END();
 }
 
-int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int per_cu,
-                                       int64_t* waves_per_launch) {
+int dglhip_sweep_barrier_expiries(int reset, int64_t* out) {
+  API_BEGIN();
+  DGLHIP_CHECK(out, "null output");
+  unsigned long long v = 0;
+  HIP_CALL(hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_sweep_expired), sizeof(v), 0,
+                               hipMemcpyDeviceToHost));
+  *out = static_cast<int64_t>(v);
+  if (reset) {
+    const unsigned long long zero = 0;
+    HIP_CALL(hipMemcpyToSymbol(HIP_SYMBOL(g_sweep_expired), &zero, sizeof(zero), 0,
+                               hipMemcpyHostToDevice));
+  }
+  API_END();
+}
+
+int dglhip_gspmm_sweep_stream_geometry_mode(int rows_per_wave, int per_cu, int mode,
+                                            int64_t* waves_per_launch) {
   API_BEGIN();
   DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
   DGLHIP_CHECK(per_cu >= 0, "workgroups per CU " << per_cu);
-  *waves_per_launch = rows_per_wave == 10 ? sweep_waves_per_launch(stream_kernel<10>(0), per_cu)
-                                          : sweep_waves_per_launch(stream_kernel<19>(0), per_cu);
+  DGLHIP_CHECK(mode >= 0 && mode <= 2, "mode " << mode);
+  DGLHIP_CHECK(waves_per_launch, "null output");
+  // the kernel dglhip_gspmm_sweep_stream_device launches for this mode at the
+  // current gathers-in-flight knob
+  *waves_per_launch = rows_per_wave == 10
+                          ? sweep_waves_per_launch(stream_kernel<10>(mode), per_cu)
+                          : sweep_waves_per_launch(stream_kernel<19>(mode), per_cu);
   API_END();
+}
+
+int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int per_cu,
+                                       int64_t* waves_per_launch) {
+  return dglhip_gspmm_sweep_stream_geometry_mode(rows_per_wave, per_cu, 0, waves_per_launch);
 }
 
 int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,

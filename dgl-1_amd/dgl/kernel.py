@@ -157,6 +157,15 @@ def sweep_schedule():
             "accum_min_slots": ams.value, "accum_per_cu": apc.value}
 
 
+def sweep_barrier_expiries(reset=False):
+    """Waits of the accumulating sweep's soft barrier that ran out of polls
+    (max_spin) on the current device since the last reset (a synchronous read;
+    ``reset`` zeroes the count after reading). Results never depend on them."""
+    v = ctypes.c_int64()
+    check_call(LIB.dglhip_sweep_barrier_expiries(1 if reset else 0, ctypes.byref(v)))
+    return int(v.value)
+
+
 def set_sweep_schedule(**changes):
     """Change the source-sweep knobs; returns the old ones (for restoring).
     A plan keeps the sweep layouts it built; the choice is made per call."""
@@ -1573,7 +1582,9 @@ def distmult_score(h, w_rel, subj, rel, obj):
     and relation vectors ``w_rel`` (the reference's calc_score,
     examples/pytorch/rgcn/link_predict.py:50-55) in one kernel; differentiable
     in h and w_rel with deterministic gradients (see _DistMult). Indices out of
-    range give NaN scores."""
+    range raise IndexError, as the torch formulation's index_select does
+    (one min/max reduction per call; skipped under HIP-graph capture, where
+    the kernel still turns them into NaN scores and never reads past h)."""
     dev = h.device
     idx = [t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
            for t in (subj, rel, obj)]
@@ -1581,6 +1592,13 @@ def distmult_score(h, w_rel, subj, rel, obj):
         raise DGLError("distmult_score: subj, rel, obj lengths differ")
     if w_rel.shape[1:] != h.shape[1:] or h.dim() != 2:
         raise DGLError("distmult_score: h and w_rel must be 2-D of one width")
+    if idx[0].numel() and not (dev.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+        lo_hi = torch.stack([torch.stack([t.min(), t.max()]) for t in idx]).tolist()
+        for (lo, hi), bound, what in zip(lo_hi, (h.shape[0], w_rel.shape[0], h.shape[0]),
+                                         ("subj", "rel", "obj")):
+            if lo < 0 or hi >= bound:
+                raise IndexError("distmult_score: %s ids span [%d, %d], out of range for %d rows"
+                                 % (what, lo, hi, bound))
     return _DistMult.apply(_f32c(h), _f32c(w_rel), *idx)
 
 
@@ -2235,10 +2253,11 @@ def gat_logits(ft, attn_l, attn_r):
     el, er = _GATLogits.apply(ftc, al, ar)
     el, er = el.view(N, H, 1), er.view(N, H, 1)
     # what the aggregation may recompute el from: this ft (data, shape,
-    # version) and attn_l's values at this call; el's own version too (an
-    # in-place change of el voids the tag)
+    # version, and the tensor itself, held weakly: once it is freed its
+    # address may come back as another tensor's) and attn_l's values at this
+    # call; el's own version too (an in-place change of el voids the tag)
     el._dglhip_logits = (ftc.data_ptr(), tuple(ftc.shape), ftc._version, el._version,
-                         al.detach().clone())
+                         al.detach().clone(), weakref.ref(ftc))
     return el, er
 
 
@@ -2248,8 +2267,8 @@ def _logits_source(el, ft):
     tag = getattr(el, "_dglhip_logits", None)
     if tag is None or not ft.is_cuda or tuple(ft.shape[1:]) != (8, 16):
         return None
-    ptr_, shape, version, el_version, al = tag
-    if (ft.data_ptr() != ptr_ or tuple(ft.shape) != shape or ft._version != version or
-            el._version != el_version):
+    ptr_, shape, version, el_version, al, ref = tag
+    if (ref() is None or ft.data_ptr() != ptr_ or tuple(ft.shape) != shape or
+            ft._version != version or el._version != el_version):
         return None
     return al if al.device == ft.device else None

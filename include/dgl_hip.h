@@ -606,6 +606,12 @@ int dglhip_gspmm_sweep_device(int64_t num_rows, int64_t feat_len, const int64_t*
  * of the geometry's waves per launch for the same rows_per_wave and per_cu. rows_per_wave 10 or 19;
  * feat_len 128. */
 int dglhip_gspmm_sweep_stream_geometry(int rows_per_wave, int per_cu, int64_t* waves_per_launch);
+/* The same for the kernel of a given mode (0 sum, 1 mean, 2 sum continuing
+ * out) at the current dglhip_set_sweep_unroll: the geometry the launch of
+ * dglhip_gspmm_sweep_stream_device with that mode checks its layout against
+ * (the plain entry above is mode 0). */
+int dglhip_gspmm_sweep_stream_geometry_mode(int rows_per_wave, int per_cu, int mode,
+                                            int64_t* waves_per_launch);
 int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      const int32_t* row_order, const int32_t* counts,
                                      int num_blocks, const int64_t* seg_beg, const int32_t* lay,
@@ -630,6 +636,12 @@ int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, in
 int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes, int* lag,
                               int* max_spin, int64_t* accum_table_min,
                               int64_t* accum_min_slots, int* accum_per_cu);
+/* The accumulating sweep's soft barrier (sweep_wait in csrc/sweep.hip) gives
+ * up after max_spin polls; results never depend on it. This reads how many
+ * waits ran out on the current device since the last reset (one count per
+ * wave that stopped waiting), synchronously; reset != 0 zeroes it after the
+ * read. New design: no reference counterpart. */
+int dglhip_sweep_barrier_expiries(int reset, int64_t* out);
 int dglhip_set_sweep_per_cu(int per_cu);
 int dglhip_set_sweep_unroll(int unroll);
 

@@ -81,11 +81,23 @@ def test_distmult_only_one_grad_and_empty(device):
     assert dh3 is None or not dh3.any()
 
 
-def test_distmult_out_of_range_is_nan():
+@pytest.mark.parametrize("device", DEVICES)
+def test_distmult_out_of_range_raises(device):
+    """Out-of-range subject, relation or object ids raise IndexError at the
+    call, as index_select in the torch formulation does, rather
+    than surfacing later as a NaN loss; the kernel itself never reads past
+    its tables (NaN for such a position)."""
+    dev = _dev(device)
+    for which, bad in ((0, "s"), (1, "r"), (2, "o"), (1, "neg")):
+        h, w, s, r, o = _case(n=10, hub=False)
+        t = [s, r, o][which]
+        t[4] = -1 if bad == "neg" else (w.shape[0] if which == 1 else h.shape[0])
+        with pytest.raises(IndexError):
+            kernel.distmult_score(h.to(dev), w.to(dev), s.to(dev), r.to(dev), o.to(dev))
     h, w, s, r, o = _case(n=10, hub=False)
     s[4] = h.shape[0]
     r[6] = -1
-    sc = kernel.distmult_score(h, w, s, r, o)
+    sc = kernel._DistMult.apply(h, w, s, r, o)  # the kernel without the check
     assert torch.isnan(sc[4]) and torch.isnan(sc[6])
     assert torch.isfinite(sc[[0, 1, 2, 3, 5, 7, 8, 9]]).all()
 

@@ -630,3 +630,18 @@ def test_gat_logits_tag_follows_versions():
     el2, _ = kernel.gat_logits(ft, al, ar)
     el2.mul_(1.0)
     assert el2._version != el2._dglhip_logits[3]
+
+
+def test_gat_logits_tag_dies_with_its_ft():
+    """The tag holds its ft weakly: once that ft is freed, a new
+    tensor at the same address, shape and version 0 no longer matches."""
+    import gc
+    ft = torch.randn(50, 8, 16)
+    al, ar = torch.randn(8, 16, 1), torch.randn(8, 16, 1)
+    with torch.no_grad():
+        el, _ = kernel.gat_logits(ft, al, ar)
+    ref = el._dglhip_logits[5]
+    assert ref() is ft
+    del ft
+    gc.collect()
+    assert ref() is None

@@ -194,16 +194,23 @@ def test_plan_takes_the_sweep_for_large_tables():
         assert np.array_equal(res[True][0].numpy(), ref)
         for a, b in zip(res[True], res[False]):
             assert torch.equal(a, b)
-        # the C-ABI route (DGLFuncCall, a plan made for the call) takes it too
+        # the C-ABI route (DGLFuncCall with a plan handle) takes it too; a
+        # plan-less call is one launch, the same bits
         kernel.set_sweep_schedule(on=True)
         from dgl import _ffi
         fwd = adj.fwd
-        out = torch.full((n_src, 128), float("nan"), device=dev)
         stream = ("handle", torch.cuda.current_stream().cuda_stream)
-        _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, fwd.indptr, fwd.indices, None, H.to(dev),
-                         None, out, None, fwd.row_order, stream)
-        torch.cuda.synchronize()
-        assert np.array_equal(out.cpu().numpy(), ref)
+        plan = _ffi.call_packed("dglhip._CAPI_SpmmPlanCreate", fwd.indptr, fwd.indices, n_src,
+                                fwd.row_order, stream)
+        try:
+            for extra in ((("handle", plan),), ()):
+                out = torch.full((n_src, 128), float("nan"), device=dev)
+                _ffi.call_packed("dglhip._CAPI_GSpMM", 0, 0, fwd.indptr, fwd.indices, None,
+                                 H.to(dev), None, out, None, fwd.row_order, stream, *extra)
+                torch.cuda.synchronize()
+                assert np.array_equal(out.cpu().numpy(), ref)
+        finally:
+            _ffi.call_packed("dglhip._CAPI_SpmmPlanFree", ("handle", plan))
         rnd = rng.permutation(m)
         adj_r = kernel.from_coo(n_src, n_src, torch.from_numpy(dst[rnd]).to(dev),
                                 torch.from_numpy(src[rnd]).to(dev), kernel.ORDER_EID, dev)
@@ -254,4 +261,100 @@ def test_accumulating_sweep_continues_the_chains():
         torch.cuda.synchronize()
         assert torch.equal(out.cpu(), res[1])
     finally:
+        kernel.set_sweep_schedule(**old)
+
+
+def test_accumulating_sweep_beside_an_occupying_kernel():
+    """The default multi-GPU configuration runs the accumulating sweep's soft
+    barrier (sweep_wait: it waits only for workgroups that have begun, and
+    gives up after max_spin polls) beside RCCL kernels that hold CUs. Here a
+    stream of 8192^2 GEMMs on a second stream holds the CUs while the sweep
+    runs on the first: the oracle's bits (the sweep-off chains), bounded wall
+    time, and the count of waits that ran out, read through the C-ABI. With
+    max_spin = 1 waits do run out (the counter counts) and the bits stay."""
+    import time
+    dev = _dev()
+    n_src, n_dst, m = 240_000, 24_000, 6_000_000   # 123 MB source table
+    rng = np.random.default_rng(31)
+    src = rng.integers(0, n_src, m)
+    dst = rng.integers(0, n_dst, m)
+    o = np.lexsort((dst, src))
+    src, dst = src[o], dst[o]
+    csr = kernel.build_csr(n_dst, n_src, torch.from_numpy(dst).to(dev),
+                           torch.from_numpy(src).to(dev), kernel.ORDER_EID, dev)
+    h = torch.randn(n_src, 128, generator=torch.Generator().manual_seed(32)).to(dev)
+    base = torch.randn(n_dst, 128, generator=torch.Generator().manual_seed(33)).to(dev)
+    old = kernel.set_sweep_schedule(accum_table_min=32 << 20, block_bytes=2 << 20)
+    try:
+        path, _ = csr.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, 128, 0, n_src)
+        assert path == kernel.PLAN_PATH_SWEEP
+        kernel.set_sweep_schedule(on=False)
+        want = base.clone()
+        kernel.gspmm_into(csr, want, h, accumulate=True)
+        torch.cuda.synchronize()
+        kernel.set_sweep_schedule(on=True)
+        a = torch.randn(8192, 8192, device=dev)
+        side = torch.cuda.Stream(dev)
+        counts = {}
+        for spin in (old["max_spin"], 1):
+            kernel.set_sweep_schedule(max_spin=spin)
+            kernel.sweep_barrier_expiries(reset=True)
+            outs = [base.clone() for _ in range(4)]
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(12):
+                    a = torch.mm(a, a) * 1e-4
+            for out in outs:  # enqueued while the GEMMs hold the CUs
+                kernel.gspmm_into(csr, out, h, accumulate=True)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            counts[spin] = kernel.sweep_barrier_expiries()
+            print("max_spin %d: %d waits ran out over 4 calls beside the GEMMs, %.3f s"
+                  % (spin, counts[spin], wall))
+            assert wall < 30.0
+            for out in outs:
+                assert torch.equal(out, want)
+        assert counts[1] > 0
+    finally:
+        kernel.set_sweep_schedule(**old)
+
+
+def test_sweep_layout_follows_the_kernel_knobs():
+    """The cached sweep layout is dealt over the waves one launch of the
+    kernel that runs holds; a gathers-in-flight knob changed after the plan
+    was built (its occupancy may differ) gets a layout of its own rather than
+    a geometry mismatch at launch: same bits at 16 and 32
+    gathers in flight, sum and the accumulating mode."""
+    dev = _dev()
+    n_src, n_dst, m = 120_000, 12_000, 2_000_000
+    rng = np.random.default_rng(41)
+    src = rng.integers(0, n_src, m)
+    dst = rng.integers(0, n_dst, m)
+    o = np.lexsort((dst, src))
+    src, dst = src[o], dst[o]
+    csr = kernel.build_csr(n_dst, n_src, torch.from_numpy(dst).to(dev),
+                           torch.from_numpy(src).to(dev), kernel.ORDER_EID, dev)
+    h = torch.randn(n_src, 128, generator=torch.Generator().manual_seed(42)).to(dev)
+    base = torch.randn(n_dst, 128, generator=torch.Generator().manual_seed(43)).to(dev)
+    ref = O.spmm_coo(n_dst, dst, src, h.cpu().numpy())
+    old = kernel.set_sweep_schedule(table_min=32 << 20, accum_table_min=32 << 20,
+                                    block_bytes=2 << 20)
+    try:
+        res = {}
+        for unroll in (16, 32, 16):
+            check_call(LIB.dglhip_set_sweep_unroll(unroll))
+            out = torch.full((n_dst, 128), float("nan"), device=dev)
+            kernel.gspmm_into(csr, out, h)
+            acc = base.clone()
+            kernel.gspmm_into(csr, acc, h, accumulate=True)
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), ref), unroll
+            res.setdefault("acc", acc.cpu())
+            assert torch.equal(acc.cpu(), res["acc"]), unroll
+        path, _ = csr.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, 128, 0, n_src)
+        assert path == kernel.PLAN_PATH_SWEEP
+    finally:
+        check_call(LIB.dglhip_set_sweep_unroll(16))
         kernel.set_sweep_schedule(**old)

@@ -27,6 +27,7 @@ import collections
 import csv
 import json
 import os
+import re
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -55,6 +56,9 @@ def run(args):
 
     fb()  # builds the transposed CSR and its plan
     torch.cuda.synchronize()
+    # marker: parse counts only the dispatches after the last spin kernel
+    # (the timed calls; not the graph build, the sort or the plan's call)
+    torch.cuda._sleep(1000)
     plan = kernel._block_plan(adj.bwd, torch.empty(2, 128, device=dev), 128,
                               kernel._GAT_BWD_BLOCK_BYTES)
     info = {"nodes": n, "edges": adj.fwd.nnz, "calls": args.calls,
@@ -69,19 +73,35 @@ def run(args):
     print(json.dumps({"launches_per_call": len(info["blocks"]), "calls": args.calls + 1}))
 
 
+def kernel_key(full):
+    """The kernel's own name from a demangled signature: namespaces (the
+    anonymous one included), template arguments and parameters dropped."""
+    s = full.replace("(anonymous namespace)", "anon").replace("void ", "").strip()
+    s = re.split(r"[(<]", s, maxsplit=1)[0]
+    return s.split("::")[-1]
+
+
 def parse(args):
     info = json.load(open(args.plan))
     blocks = info["blocks"]
-    calls = info["calls"] + 1  # the plan-building call ran under the profiler too
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
+    marked = True
     for path in args.csvs:
         with open(path) as f:
-            for r in csv.DictReader(f):
-                name = r["Kernel_Name"].split("(")[0].split("<")[0].replace("void ", "")
-                name = name.replace("dglhip::", "")
-                per[name][r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[name].add((path, r["Dispatch_Id"]))
+            rows = list(csv.DictReader(f))
+        marks = [int(r["Dispatch_Id"]) for r in rows if "spin_kernel" in r["Kernel_Name"]]
+        start = max(marks) if marks else -1
+        marked = marked and bool(marks)
+        for r in rows:
+            if int(r["Dispatch_Id"]) <= start:
+                continue
+            name = kernel_key(r["Kernel_Name"])
+            per[name][r["Counter_Name"]] += float(r["Counter_Value"])
+            disp[name].add((path, r["Dispatch_Id"]))
+    # with the marker only the timed calls are counted; an old capture
+    # without one also holds the plan-building call
+    calls = info["calls"] if marked else info["calls"] + 1
     slots = sum(b["slots"] for b in blocks)
     items = sum(b["items"] for b in blocks)
     first = blocks[0]["items"] if blocks else 0
@@ -90,7 +110,9 @@ def parse(args):
              "pair_operand_lines": slots * 2,
              "g_store_partial_lines": slots,
              "row_pass_lines": (items - first) * 4 + items * 4}
-    res = {"model_per_call": model, "kernels": {}}
+    res = {"model_per_call": model, "calls_counted": calls,
+           "window": "dispatches after the spin-kernel marker (the timed calls only)"
+           if marked else "every dispatch (no marker in the capture)", "kernels": {}}
     for name, cs in per.items():
         res["kernels"][name] = {"dispatches_per_call": len(disp[name]) / float(calls),
                                 "per_call": {k: v / calls for k, v in cs.items()}}

@@ -48,7 +48,10 @@ for s in $STEPS; do
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run \
         --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-train-leg --no-cpu-baseline --no-model-legs \
         > gpurun_out/prof.json 2> gpurun_out/prof.log
-      rc=$?; tail -1 gpurun_out/prof.log; cat gpurun_out/prof.json; [ $rc -eq 0 ] || exit $rc ;;
+      rc=$?; tail -1 gpurun_out/prof.log; cat gpurun_out/prof.json; [ $rc -eq 0 ] || exit $rc
+      # the same trace over the timed steps alone (bench.py's spin-kernel markers)
+      python tools/window_stats.py gpurun_out/prof/run_kernel_trace.csv --window 0 \
+        --out gpurun_out/prof/timed_kernel_stats.csv || exit $? ;;
     dist)
       # rehearse the multi-rank bench path: 2 ranks sharing the one GPU over gloo
       timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
@@ -145,6 +148,27 @@ for s in $STEPS; do
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
       rc=$?; tail -4 gpurun_out/rmat.err; cat gpurun_out/rmat.json; [ $rc -eq 0 ] || exit $rc ;;
+    gatsplit)
+      # the GAT backward's L2 hits / misses and EA requests over the timed calls (tools/gat_bwd_split.py)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -s KILL 240 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d gpurun_out/gsa -o run \
+        --output-format csv -- python tools/gat_bwd_split.py run --out gpurun_out/gat_plan.json > gpurun_out/gsa.log 2>&1 &&
+      timeout -s KILL 240 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d gpurun_out/gsb -o run \
+        --output-format csv -- python tools/gat_bwd_split.py run --out gpurun_out/gat_plan.json > gpurun_out/gsb.log 2>&1 &&
+      python tools/gat_bwd_split.py parse gpurun_out/gat_plan.json gpurun_out/gsa/run_counter_collection.csv \
+        gpurun_out/gsb/run_counter_collection.csv --out gpurun_out/gat_bwd_l2_split.json > /dev/null
+      rc=$?; tail -2 gpurun_out/gsb.log; [ $rc -eq 0 ] || exit $rc ;;
+    gatvariants)
+      # GAT 8 x 16 fwd + bwd per backward variant (VARIANTS="0 3"), interleaved rounds
+      timeout -k 10 400 python -u tools/gat_bwd_variants.py --variants ${VARIANTS:-0} --rounds ${ROUNDS:-3} \
+        --out gpurun_out/gat_bwd_variants.json > gpurun_out/gat_bwd_variants.log 2>&1
+      rc=$?; tail -3 gpurun_out/gat_bwd_variants.log; [ $rc -eq 0 ] || exit $rc ;;
+    benchlegs)
+      # the N = 1 line without the PMC passes, the RMAT legs and the CPU baselines (model legs timed)
+      timeout -k 10 600 python bench.py --no-traffic --no-rmat-leg --no-sage-rmat-leg --no-cpu-baseline \
+        ${BENCH_ARGS:-} > gpurun_out/benchlegs.json 2> gpurun_out/benchlegs.err
+      rc=$?; tail -3 gpurun_out/benchlegs.err; [ $rc -eq 0 ] || exit $rc
+      python tools/bench_summary.py gpurun_out/benchlegs.json ;;
     pmc)
       for c in FETCH_SIZE WRITE_SIZE; do
         timeout -k 10 600 rocprofv3 --pmc $c -d gpurun_out/pmc_$c -o run --output-format csv \
