@@ -319,13 +319,19 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
   int64_t xoff = 0, yoff = 0;
   float dq = 0.0f;
   int objq = 0;
+  // positions grouped by row: 2n (subjects, then objects) for dh, n for dw;
+  // a grouping that points past them (a malformed ptr / order) reads nothing
+  // and gives NaN, as an out-of-range id does
+  const int64_t m = task == 0 ? 2 * n : n;
   if (lane < cnt) {
-    const int64_t p = order[beg + lane];
+    const int64_t k = beg + lane;
+    const int64_t p = k >= 0 && k < m ? order[k] : -1;
+    const bool inside = p >= 0 && p < m;
     const bool obj = task == 0 && p >= n;
     const int64_t i = obj ? p - n : p;
-    const int64_t si = s[i], ri = r[i], oi = o[i];
-    const bool ok = si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes && ri >= 0 &&
-                    ri < num_rels;
+    const int64_t si = inside ? s[i] : -1, ri = inside ? r[i] : -1, oi = inside ? o[i] : -1;
+    const bool ok = inside && si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes &&
+                    ri >= 0 && ri < num_rels;
     dq = ok ? ds[i] : __builtin_nanf("");
     objq = obj ? 1 : 0;
     xoff = ok ? (obj ? si : oi) * F : 0;

@@ -480,7 +480,9 @@ def build_csr(num_rows, num_cols, row, col, order=ORDER_EID, device=None, schedu
     if device.type == "cuda":
         row = _upload(row, device).contiguous()
         col = _upload(col, device).contiguous()
-        if nnz and validate:
+        # (no host sync is possible while a HIP graph is being captured: a
+        # captured build takes its edges as validated by whoever filled them)
+        if nnz and validate and not torch.cuda.is_current_stream_capturing():
             b = torch.stack([row.min(), col.min(), row.max(), col.max()]).cpu().tolist()
             if min(b[0], b[1]) < 0 or b[2] >= num_rows or b[3] >= num_cols:
                 raise DGLError("edge endpoints out of range for a %dx%d matrix"
@@ -1506,6 +1508,30 @@ def set_typed_block_width(slices):
     check_call(LIB.dglhip_set_typed_block_width(int(slices)))
 
 
+_DEBUG_GROUPS = os.environ.get("DGLHIP_DEBUG_GROUPS", "0") not in ("", "0")
+
+
+def _check_groups(ptr_, order, idx, num_rows):
+    """DGLHIP_DEBUG_GROUPS=1: check a position grouping on the host before a
+    kernel walks it (one sync; skipped under HIP-graph capture)."""
+    if idx.is_cuda and torch.cuda.is_current_stream_capturing():
+        return
+    p, o, ix = ptr_.cpu(), order.cpu().long(), idx.cpu()
+    m = ix.numel()
+    problems = []
+    if p.numel() != num_rows + 1 or int(p[0]) != 0 or int(p[-1]) != m:
+        problems.append("ptr ends %s..%s for %d positions" % (p[:1].tolist(), p[-1:].tolist(), m))
+    if bool((p[1:] < p[:-1]).any()):
+        problems.append("ptr not monotone")
+    if m and (int(o.min()) < 0 or int(o.max()) >= m or
+              not torch.equal(torch.sort(o)[0], torch.arange(m))):
+        problems.append("order is not a permutation of the positions")
+    if m and (int(ix.min()) < 0 or int(ix.max()) >= num_rows):
+        problems.append("ids span [%d, %d] for %d rows" % (int(ix.min()), int(ix.max()), num_rows))
+    if problems:
+        raise DGLError("malformed position grouping: " + "; ".join(problems))
+
+
 def _position_groups(idx, num_rows):
     """Positions of ``idx`` grouped by row in increasing position, no host
     sync: (ptr int64[R+1], order int32[m]). On a device, the library's CSR
@@ -1561,6 +1587,8 @@ class _DistMult(torch.autograd.Function):
                 continue
             ix = idx()
             ptr_, order = _position_groups(ix, rows)
+            if _DEBUG_GROUPS:
+                _check_groups(ptr_, order, ix, rows)
             out = torch.empty(rows, F, dtype=torch.float32, device=h.device)
             common = (n, h.shape[0], w.shape[0])
             tail = (ptr(order), ptr(s), ptr(r), ptr(o), ptr(ds), ptr(h), ptr(w), ptr(out))
@@ -1582,24 +1610,41 @@ def distmult_score(h, w_rel, subj, rel, obj):
     and relation vectors ``w_rel`` (the reference's calc_score,
     examples/pytorch/rgcn/link_predict.py:50-55) in one kernel; differentiable
     in h and w_rel with deterministic gradients (see _DistMult). Indices out of
-    range raise IndexError, as the torch formulation's index_select does
-    (one min/max reduction per call; skipped under HIP-graph capture, where
-    the kernel still turns them into NaN scores and never reads past h)."""
+    range raise IndexError, as the torch formulation's index_select does: ids
+    given on the host are checked there before they move; ids already on a
+    device are checked when ``set_validate_indices(True)`` (or
+    DGLHIP_VALIDATE_INDICES=1) asks for it, with one min/max reduction and a
+    host sync per call. Unchecked, the kernel never reads past its tables: an
+    out-of-range position scores NaN and adds nothing to the gradients."""
     dev = h.device
-    idx = [t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous()
-           for t in (subj, rel, obj)]
-    if not (idx[0].numel() == idx[1].numel() == idx[2].numel()):
-        raise DGLError("distmult_score: subj, rel, obj lengths differ")
     if w_rel.shape[1:] != h.shape[1:] or h.dim() != 2:
         raise DGLError("distmult_score: h and w_rel must be 2-D of one width")
-    if idx[0].numel() and not (dev.type == "cuda" and torch.cuda.is_current_stream_capturing()):
-        lo_hi = torch.stack([torch.stack([t.min(), t.max()]) for t in idx]).tolist()
+    trip = [torch.as_tensor(t) for t in (subj, rel, obj)]
+    if not (trip[0].numel() == trip[1].numel() == trip[2].numel()):
+        raise DGLError("distmult_score: subj, rel, obj lengths differ")
+    on_host = all(t.device.type == "cpu" for t in trip)
+    if trip[0].numel() and (on_host or (_VALIDATE_INDICES and not (
+            dev.type == "cuda" and torch.cuda.is_current_stream_capturing()))):
+        lo_hi = torch.stack([torch.stack([t.min(), t.max()]).to(torch.int64)
+                             for t in trip]).tolist()
         for (lo, hi), bound, what in zip(lo_hi, (h.shape[0], w_rel.shape[0], h.shape[0]),
                                          ("subj", "rel", "obj")):
             if lo < 0 or hi >= bound:
                 raise IndexError("distmult_score: %s ids span [%d, %d], out of range for %d rows"
                                  % (what, lo, hi, bound))
+    idx = [t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous() for t in trip]
     return _DistMult.apply(_f32c(h), _f32c(w_rel), *idx)
+
+
+_VALIDATE_INDICES = os.environ.get("DGLHIP_VALIDATE_INDICES", "0") not in ("", "0")
+
+
+def set_validate_indices(on):
+    """Check device-resident index arguments (distmult_score's triples) on
+    the host before launching (one sync per call); returns the old setting."""
+    global _VALIDATE_INDICES
+    old, _VALIDATE_INDICES = _VALIDATE_INDICES, bool(on)
+    return old
 
 
 def _typed_items(rowptr, nnz):

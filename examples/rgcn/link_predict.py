@@ -99,8 +99,8 @@ class RGCNBlockLayer(nn.Module):
             g.update_all(msg, fn.sum(msg="msg", out="h"))
             agg = g.ndata.pop("h") * norm.unsqueeze(1)
         else:  # fused typed-edge g-SpMM
-            agg = kernel.typed_block_spmm(g.sparse_adjacency(h.device), h, self.weight,
-                                          etype) * norm.unsqueeze(1)
+            adj = g if isinstance(g, kernel.SparseAdj) else g.sparse_adjacency(h.device)
+            agg = kernel.typed_block_spmm(adj, h, self.weight, etype) * norm.unsqueeze(1)
         out = agg + loop
         return self.activation(out) if self.activation else out
 

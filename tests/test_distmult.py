@@ -88,12 +88,21 @@ def test_distmult_out_of_range_raises(device):
     than surfacing later as a NaN loss; the kernel itself never reads past
     its tables (NaN for such a position)."""
     dev = _dev(device)
-    for which, bad in ((0, "s"), (1, "r"), (2, "o"), (1, "neg")):
-        h, w, s, r, o = _case(n=10, hub=False)
-        t = [s, r, o][which]
-        t[4] = -1 if bad == "neg" else (w.shape[0] if which == 1 else h.shape[0])
-        with pytest.raises(IndexError):
-            kernel.distmult_score(h.to(dev), w.to(dev), s.to(dev), r.to(dev), o.to(dev))
+    old = kernel.set_validate_indices(True)  # device-resident ids: checked on request
+    try:
+        for which, bad in ((0, "s"), (1, "r"), (2, "o"), (1, "neg")):
+            h, w, s, r, o = _case(n=10, hub=False)
+            t = [s, r, o][which]
+            t[4] = -1 if bad == "neg" else (w.shape[0] if which == 1 else h.shape[0])
+            with pytest.raises(IndexError):
+                kernel.distmult_score(h.to(dev), w.to(dev), s.to(dev), r.to(dev), o.to(dev))
+            # host-resident ids are checked whatever the setting
+            kernel.set_validate_indices(False)
+            with pytest.raises(IndexError):
+                kernel.distmult_score(h.to(dev), w.to(dev), s, r, o)
+            kernel.set_validate_indices(True)
+    finally:
+        kernel.set_validate_indices(old)
     h, w, s, r, o = _case(n=10, hub=False)
     s[4] = h.shape[0]
     r[6] = -1

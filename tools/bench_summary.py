@@ -21,8 +21,9 @@ def main(path):
             continue
         rr = v.get("roofline") or {}
         extra = ""
-        if "ms_per_epoch_hip_graph" in v:
-            extra = ", HIP graph %.3f ms" % v["ms_per_epoch_hip_graph"]
+        for key in ("ms_per_epoch_hip_graph", "ms_per_step_hip_graph"):
+            if key in v:
+                extra = ", HIP graph %.3f ms" % v[key]
         print("%-14s %.3f ms%s, kernel %s ms, frac %s" % (
             k, ms, extra, v.get("kernel_ms", v.get("kernel_ms_rank0")), rr.get("frac")))
 
