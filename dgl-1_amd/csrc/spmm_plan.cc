@@ -516,7 +516,8 @@ std::shared_ptr<Cuts> SpmmPlan::cuts_for(int B, hipStream_t s) {
 std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, int mode, hipStream_t s) {
   const bool accum = mode == 2;
   const SweepPolicy sp = sweep_policy();
-  constexpr int RPW = 19;  // rows per wave of the 128-float sweep kernel
+  int RPW = 19;  // rows per wave of the 128-float sweep kernel (dglhip_set_sweep_rows)
+  DGLHIP_CHECK(dglhip_get_sweep_rows(&RPW) == 0, DGLGetLastError());
   if (!sp.on || !on_device() || nnz_ == 0 || nnz_ >= (int64_t(1) << 31) || R_ == 0) return nullptr;
   const auto lh = span(s);
   const int64_t table = (lh.second - lh.first) * row_bytes;
@@ -537,7 +538,7 @@ std::shared_ptr<SweepPlan> SpmmPlan::sweep(int64_t row_bytes, int mode, hipStrea
   int64_t wpl = 0;
   DGLHIP_CHECK(dglhip_gspmm_sweep_stream_geometry_mode(RPW, per_cu, mode, &wpl) == 0 && wpl > 0,
                DGLGetLastError());
-  const std::tuple<int, int, int64_t> key(B, mode, wpl);
+  const std::tuple<int, int, int64_t, int> key(B, mode, wpl, RPW);
   std::lock_guard<std::mutex> lk(mu_);
   auto hit = sweeps_.find(key);
   if (hit != sweeps_.end()) return hit->second;

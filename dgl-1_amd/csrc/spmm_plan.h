@@ -238,8 +238,9 @@ class SpmmPlan {
   std::map<int, std::shared_ptr<BlockSplit>> splits_;
   std::map<int, std::shared_ptr<BlockedPlan>> blocked_;
   std::map<int, std::shared_ptr<Cuts>> cuts_;
-  // (blocks, kernel mode, waves per launch) -> layout (nullptr: none fits)
-  std::map<std::tuple<int, int, int64_t>, std::shared_ptr<SweepPlan>> sweeps_;
+  // (blocks, kernel mode, waves per launch, rows per wave) -> layout
+  // (nullptr: none fits)
+  std::map<std::tuple<int, int, int64_t, int>, std::shared_ptr<SweepPlan>> sweeps_;
   std::map<std::tuple<int64_t, bool, int64_t>, SplitPlan> split_plans_;
   std::map<int64_t, Tiers> tiers_;
 };

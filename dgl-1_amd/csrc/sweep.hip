@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdlib>
 
 #include "gspmm_impl.h"
 
@@ -199,8 +200,21 @@ __global__ __launch_bounds__(256) void gspmm_sweep_kernel(
 // for source-monotone chains (each row's block-b slots contiguous in slot
 // order), which the layout builder checks.
 // MODE 0 sum, 1 mean, 2 sum continuing every row's chain from its value in
-// out (the pipelined multi-GPU segments' SUM_ACCUM)
-template <int VEC, int RPW, int UNROLL, int MODE>
+// out (the pipelined multi-GPU segments' SUM_ACCUM).
+// RR (r06): the wave's last RR rows keep their running sums in registers
+// (two floats per lane per row: a pair of RR-wide register vectors indexed
+// by the wave-uniform row, GPR indexing mode, no scratch) and the first
+// RPW - RR in LDS, so a CU holds RPW rows per wave instead of the LDS's
+// share: fewer launches (row generations) re-sweep the source blocks.
+template <int RR>
+struct RegRows {
+  typedef float T __attribute__((ext_vector_type(RR)));
+  T x, y;
+};
+template <>
+struct RegRows<0> {};
+
+template <int VEC, int RPW, int UNROLL, int MODE, int RR = 0>
 __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     int64_t num_rows, int64_t waves_total, int64_t wave_base,
     const int32_t* __restrict__ row_order, const int32_t* __restrict__ counts, int nblocks,
@@ -209,7 +223,10 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     float* __restrict__ out, int* __restrict__ arrive, int lag, int max_spin) {
   typedef typename Vec<VEC>::T V;
   constexpr int F = 64 * VEC;
-  __shared__ float sums[kSweepWaves * RPW * F];
+  constexpr int RL = RPW - RR;  // rows whose sums live in LDS
+  static_assert(RR == 0 || VEC == 2, "register rows hold two floats per lane");
+  static_assert(RPW <= 64 && RL >= 1, "a lane describes each row of the wave");
+  __shared__ float sums[kSweepWaves * RL * F];
   const int lane = threadIdx.x & 63;
   const int w = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   const int64_t wv = wave_base + int64_t(blockIdx.x) * kSweepWaves + w;
@@ -256,10 +273,33 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     for (int b = 0; b < nblocks; ++b) arrive_at(b);
     return;
   }
-  float* my = sums + w * RPW * F;
+  float* my = sums + w * RL * F;
+  RegRows<RR> reg;
+  if constexpr (RR > 0) reg.x = reg.y = 0.0f;
+  // row j's running sum: LDS for j < RL, registers past it (j is wave-uniform)
+  auto get = [&](int j) -> V {
+    if constexpr (RR > 0) {
+      if (j >= RL) {
+        V v;
+        v.x = reg.x[j - RL];
+        v.y = reg.y[j - RL];
+        return v;
+      }
+    }
+    return ldv<VEC>(my + j * F + f0);
+  };
+  auto put = [&](int j, V v) {
+    if constexpr (RR > 0) {
+      if (j >= RL) {
+        reg.x[j - RL] = v.x;
+        reg.y[j - RL] = v.y;
+        return;
+      }
+    }
+    stv<VEC>(my + j * F + f0, v);
+  };
   for (int j = 0; j < nrows; ++j)
-    stv<VEC>(my + j * F + f0, MODE == 2 ? ldv<VEC>(out + int64_t(lane_of(row, j)) * F + f0)
-                                        : Vec<VEC>::zero());
+    put(j, MODE == 2 ? ldv<VEC>(out + int64_t(lane_of(row, j)) * F + f0) : Vec<VEC>::zero());
   int32_t cnt_next = row >= 0 ? counts[int64_t(row) * nblocks] : 0;
   int64_t base_next = seg_beg[wv * nblocks];
   for (int b = 0; b < nblocks; ++b) {
@@ -288,7 +328,7 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
     const uint64_t live = __ballot(cnt > 0);
     int j = __builtin_ctzll(live);
     int32_t rend = lane_of(incl, j);
-    V acc = ldv<VEC>(my + j * F + f0);
+    V acc = get(j);
     for (int32_t t = 0; t < total; t += UNROLL) {
       const int rem = min(UNROLL, total - t);
       V s[UNROLL];
@@ -305,21 +345,21 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
       for (int u = 0; u < UNROLL; ++u) {
         if (u < rem) {
           if (t + u == rend) {
-            stv<VEC>(my + j * F + f0, acc);
+            put(j, acc);
             j = __builtin_ctzll(live & (~0ull << (j + 1)));
             rend = lane_of(incl, j);
-            acc = ldv<VEC>(my + j * F + f0);
+            acc = get(j);
           }
           acc += s[u];
         }
       }
     }
-    stv<VEC>(my + j * F + f0, acc);
+    put(j, acc);
   }
   arrive_at(nblocks - 1);
   for (int j = 0; j < nrows; ++j) {
     const int32_t r = lane_of(row, j);
-    V acc = ldv<VEC>(my + j * F + f0);
+    V acc = get(j);
     if (MODE == 1) {
       const int32_t d = lane_of(deg, j);
       if (d > 1) acc = acc / Vec<VEC>::splat(static_cast<float>(d));
@@ -329,6 +369,14 @@ __global__ __launch_bounds__(256) void gspmm_sweep_stream_kernel(
 }
 
 int g_sweep_per_cu = 0;  // study knob: workgroups per CU of a launch (0: occupancy)
+// rows per wave the plan lays the streamed sweep out for (19: all in LDS;
+// 35 / 51: 16 / 32 more in registers, 124 VGPRs at 51, still 4 waves per
+// SIMD: emulated N = 8 rank 7.15 -> 6.90 ms); DGLHIP_SWEEP_ROWS
+int g_sweep_rows = [] {
+  const char* e = std::getenv("DGLHIP_SWEEP_ROWS");
+  const int v = e ? std::atoi(e) : 0;
+  return (v == 10 || v == 19 || v == 35 || v == 51) ? v : 51;
+}();
 int g_sweep_unroll = 16;  // study knob: row gathers in flight per wave (16 or 32)
 
 template <typename K>
@@ -343,16 +391,34 @@ int64_t sweep_waves_per_launch(K kern, int cap = 0) {
   return int64_t(cus) * per_cu * kSweepWaves;
 }
 
-template <int RPW, int U>
+template <int RPW, int U, int RR>
 auto stream_kernel_u(int mode) {
-  return mode == 2 ? gspmm_sweep_stream_kernel<2, RPW, U, 2>
-         : mode == 1 ? gspmm_sweep_stream_kernel<2, RPW, U, 1>
-                     : gspmm_sweep_stream_kernel<2, RPW, U, 0>;
+  return mode == 2 ? gspmm_sweep_stream_kernel<2, RPW, U, 2, RR>
+         : mode == 1 ? gspmm_sweep_stream_kernel<2, RPW, U, 1, RR>
+                     : gspmm_sweep_stream_kernel<2, RPW, U, 0, RR>;
 }
 
-template <int RPW>
+template <int RPW, int RR = 0>
 auto stream_kernel(int mode) {
-  return g_sweep_unroll == 32 ? stream_kernel_u<RPW, 32>(mode) : stream_kernel_u<RPW, 16>(mode);
+  return g_sweep_unroll == 32 ? stream_kernel_u<RPW, 32, RR>(mode)
+                              : stream_kernel_u<RPW, 16, RR>(mode);
+}
+
+// rows per wave of the streamed kernel: 10 or 19 in LDS; 19 in LDS plus 16
+// or 32 in registers (35, 51)
+bool stream_rows_ok(int rows_per_wave) {
+  return rows_per_wave == 10 || rows_per_wave == 19 || rows_per_wave == 35 ||
+         rows_per_wave == 51;
+}
+
+template <typename Fn>
+auto with_stream_kernel(int rows_per_wave, int mode, Fn fn) {
+  switch (rows_per_wave) {
+    case 10: return fn(stream_kernel<10>(mode));
+    case 35: return fn(stream_kernel<35, 16>(mode));
+    case 51: return fn(stream_kernel<51, 32>(mode));
+    default: return fn(stream_kernel<19>(mode));
+  }
 }
 
 template <int VEC, int RPW, bool MEAN>
@@ -434,6 +500,20 @@ int dglhip_set_sweep_per_cu(int per_cu) {
   API_END();
 }
 
+int dglhip_set_sweep_rows(int rows_per_wave) {
+  API_BEGIN();
+  DGLHIP_CHECK(stream_rows_ok(rows_per_wave), "rows per wave " << rows_per_wave);
+  g_sweep_rows = rows_per_wave;
+  API_END();
+}
+
+int dglhip_get_sweep_rows(int* rows_per_wave) {
+  API_BEGIN();
+  DGLHIP_CHECK(rows_per_wave, "null output");
+  *rows_per_wave = g_sweep_rows;
+  API_END();
+}
+
 int dglhip_set_sweep_unroll(int unroll) {
   API_BEGIN();
   DGLHIP_CHECK(unroll == 16 || unroll == 32, "gathers in flight " << unroll);
@@ -459,15 +539,14 @@ int dglhip_sweep_barrier_expiries(int reset, int64_t* out) {
 int dglhip_gspmm_sweep_stream_geometry_mode(int rows_per_wave, int per_cu, int mode,
                                             int64_t* waves_per_launch) {
   API_BEGIN();
-  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
+  DGLHIP_CHECK(stream_rows_ok(rows_per_wave), "rows per wave " << rows_per_wave);
   DGLHIP_CHECK(per_cu >= 0, "workgroups per CU " << per_cu);
   DGLHIP_CHECK(mode >= 0 && mode <= 2, "mode " << mode);
   DGLHIP_CHECK(waves_per_launch, "null output");
   // the kernel dglhip_gspmm_sweep_stream_device launches for this mode at the
   // current gathers-in-flight knob
-  *waves_per_launch = rows_per_wave == 10
-                          ? sweep_waves_per_launch(stream_kernel<10>(mode), per_cu)
-                          : sweep_waves_per_launch(stream_kernel<19>(mode), per_cu);
+  *waves_per_launch = with_stream_kernel(
+      rows_per_wave, mode, [&](auto kern) { return sweep_waves_per_launch(kern, per_cu); });
   API_END();
 }
 
@@ -484,11 +563,11 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                                      int64_t arrive_len, int lag, int max_spin, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
-  DGLHIP_CHECK(rows_per_wave == 10 || rows_per_wave == 19, "rows per wave " << rows_per_wave);
+  DGLHIP_CHECK(stream_rows_ok(rows_per_wave), "rows per wave " << rows_per_wave);
   DGLHIP_CHECK(num_rows >= 0 && num_rows < (int64_t(1) << 31) && num_blocks >= 1, "sizes");
   DGLHIP_CHECK(mode >= 0 && mode <= 2 && per_cu >= 0, "mode " << mode << ", per_cu " << per_cu);
   if (num_rows == 0) return 0;
-  auto kern = rows_per_wave == 10 ? stream_kernel<10>(mode) : stream_kernel<19>(mode);
+  with_stream_kernel(rows_per_wave, mode, [&](auto kern) {
   const int64_t wpl = sweep_waves_per_launch(kern, per_cu);
   DGLHIP_CHECK(waves_total % wpl == 0 && waves_total * rows_per_wave >= num_rows,
                "layout for " << waves_total << " waves, launches hold " << wpl);
@@ -509,6 +588,8 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
                          lag > 0 ? arrive + l * per_launch : nullptr, lag, max_spin);
     });
   }
+  return 0;
+  });
   API_END();
 }
 

@@ -134,6 +134,8 @@ def _load():
         "dglhip_gspmm_sweep_stream_geometry": (_c_int, [_c_int, _c_int, _vp]),
         "dglhip_set_sweep_per_cu": (_c_int, [_c_int]),
         "dglhip_sweep_barrier_expiries": (_c_int, [_c_int, _vp]),
+        "dglhip_set_sweep_rows": (_c_int, [_c_int]),
+        "dglhip_get_sweep_rows": (_c_int, [_vp]),
         "dglhip_set_sweep_schedule": (_c_int, [_c_int, _c_i64, _c_i64, _c_int, _c_int, _c_i64,
                                                _c_i64, _c_int]),
         "dglhip_get_sweep_schedule": (_c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -643,6 +643,12 @@ int dglhip_get_sweep_schedule(int* on, int64_t* table_min, int64_t* block_bytes,
  * read. New design: no reference counterpart. */
 int dglhip_sweep_barrier_expiries(int reset, int64_t* out);
 int dglhip_set_sweep_per_cu(int per_cu);
+/* Rows per wave the plan lays the streamed sweep out for: 19 (running sums
+ * in LDS), 35 or 51 (19 in LDS, 16 or 32 more in registers: a CU holds more
+ * rows, so fewer launches re-sweep the source blocks; 51 is the default), 10.
+ * Process-wide; env DGLHIP_SWEEP_ROWS. Same bits at every setting. */
+int dglhip_set_sweep_rows(int rows_per_wave);
+int dglhip_get_sweep_rows(int* rows_per_wave);
 int dglhip_set_sweep_unroll(int unroll);
 
 /* The max reducer of dglhip_gspmm_device over row ranges: row r's slots are

@@ -118,11 +118,12 @@ def _study_tool():
 
 
 @pytest.mark.parametrize("lag", [0, 2])
-@pytest.mark.parametrize("rpw", [10, 19])
+@pytest.mark.parametrize("rpw", [10, 19, 35, 51])
 def test_sweep_stream_bits(lag, rpw):
     """The streamed layout (rows' block runs back to back per wave) and its
     soft barrier: the oracle's bits, sum and mean, with and without the
-    barrier; a random-order graph has no such layout."""
+    barrier; a random-order graph has no such layout. 35 and 51 rows per
+    wave hold 16 / 32 of them in registers (r06)."""
     dev = _dev()
     n, m = 50_000, 1_500_000
     src, dst = _graph(n, m, 7, "sorted")
@@ -323,10 +324,11 @@ def test_accumulating_sweep_beside_an_occupying_kernel():
 
 def test_sweep_layout_follows_the_kernel_knobs():
     """The cached sweep layout is dealt over the waves one launch of the
-    kernel that runs holds; a gathers-in-flight knob changed after the plan
-    was built (its occupancy may differ) gets a layout of its own rather than
-    a geometry mismatch at launch: same bits at 16 and 32
-    gathers in flight, sum and the accumulating mode."""
+    kernel that runs holds; a gathers-in-flight or rows-per-wave knob changed
+    after the plan was built (its occupancy may differ) gets a layout of its
+    own rather than a geometry mismatch at launch: same bits at
+    16 and 32 gathers in flight and at 19, 35 and 51 rows per wave (16 / 32
+    of them in registers), sum and the accumulating mode."""
     dev = _dev()
     n_src, n_dst, m = 120_000, 12_000, 2_000_000
     rng = np.random.default_rng(41)
@@ -341,20 +343,24 @@ def test_sweep_layout_follows_the_kernel_knobs():
     ref = O.spmm_coo(n_dst, dst, src, h.cpu().numpy())
     old = kernel.set_sweep_schedule(table_min=32 << 20, accum_table_min=32 << 20,
                                     block_bytes=2 << 20)
+    rows0 = ctypes.c_int()
+    check_call(LIB.dglhip_get_sweep_rows(ctypes.byref(rows0)))
     try:
         res = {}
-        for unroll in (16, 32, 16):
+        for unroll, rows in ((16, 19), (32, 19), (16, 51), (16, 35), (32, 51), (16, 19)):
             check_call(LIB.dglhip_set_sweep_unroll(unroll))
+            check_call(LIB.dglhip_set_sweep_rows(rows))
             out = torch.full((n_dst, 128), float("nan"), device=dev)
             kernel.gspmm_into(csr, out, h)
             acc = base.clone()
             kernel.gspmm_into(csr, acc, h, accumulate=True)
             torch.cuda.synchronize()
-            assert np.array_equal(out.cpu().numpy(), ref), unroll
+            assert np.array_equal(out.cpu().numpy(), ref), (unroll, rows)
             res.setdefault("acc", acc.cpu())
-            assert torch.equal(acc.cpu(), res["acc"]), unroll
+            assert torch.equal(acc.cpu(), res["acc"]), (unroll, rows)
         path, _ = csr.plan.schedule(kernel.MSG_COPY_U, kernel.RED_SUM_ACCUM, 128, 0, n_src)
         assert path == kernel.PLAN_PATH_SWEEP
     finally:
         check_call(LIB.dglhip_set_sweep_unroll(16))
+        check_call(LIB.dglhip_set_sweep_rows(rows0.value))
         kernel.set_sweep_schedule(**old)

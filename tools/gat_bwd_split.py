@@ -114,7 +114,9 @@ def parse(args):
            "window": "dispatches after the spin-kernel marker (the timed calls only)"
            if marked else "every dispatch (no marker in the capture)", "kernels": {}}
     for name, cs in per.items():
-        res["kernels"][name] = {"dispatches_per_call": len(disp[name]) / float(calls),
+        # each capture (one per counter pass) holds every dispatch once
+        res["kernels"][name] = {"dispatches_per_call":
+                                len(disp[name]) / float(calls * len(args.csvs)),
                                 "per_call": {k: v / calls for k, v in cs.items()}}
     bt = res["kernels"].get("gat_backward_t_kernel", {}).get("per_call", {})
     if "TCC_HIT_sum" in bt and "TCC_MISS_sum" in bt:
