@@ -968,9 +968,8 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
   const void* uf = a.ufeat;
   if (d.pad) {
     char* up = ws.take(d.ws_pad);
-    const int64_t rb = a.F * 4;
-    hip_ok(hipMemcpy2DAsync(up, d.ld * 4, a.ufeat, rb, rb, a.urows, hipMemcpyDeviceToDevice, s),
-           "padded rows copy");
+    plan_pad_rows_device(a.urows, a.F, d.ld, static_cast<const float*>(a.ufeat),
+                         reinterpret_cast<float*>(up), s);
     uf = up;
   }
   if (d.path == PATH_SWEEP) {

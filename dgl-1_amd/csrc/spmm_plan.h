@@ -301,6 +301,8 @@ void plan_gather_vals_device(int64_t n, const int64_t* rows, const float* vals, 
                              hipStream_t s);
 // out[rows[i], :] = 0 for i < n
 void plan_zero_rows_device(int64_t n, const int32_t* rows, int64_t F, float* out, hipStream_t s);
+void plan_pad_rows_device(int64_t n, int64_t F, int64_t ld, const float* src, float* dst,
+                          hipStream_t s);
 // out[r, f] = out[r, f] / max(deg r, 1) (IEEE division, torch.div's bits)
 void plan_div_degree_device(int64_t R, int64_t F, const int64_t* indptr, float* out,
                             hipStream_t s);
