@@ -132,6 +132,8 @@ def build_parser():
                          "to rehearse the multi-rank path")
     ap.add_argument("--no-model-legs", action="store_true",
                     help="N=1: skip the model legs (gcn_reddit, gat, sage, gat_pubmed, rgcn)")
+    ap.add_argument("--model-legs", default=None,
+                    help="N=1: run only these model legs (comma list; a profiling aid)")
     ap.add_argument("--no-strong-leg", action="store_true",
                     help="N>1: skip the fixed-graph (strong scaling) Reddit block")
     ap.add_argument("--emulate-strong", action="store_true",
@@ -1292,6 +1294,13 @@ def main(argv=None):
             not args.no_model_legs and not on_cpu and not args.dist_rehearsal):
         import bench_models as bm
         want = not args.no_cpu_baseline
+        only = set(args.model_legs.split(",")) if args.model_legs else None
+        if only is not None:
+            legs_run = legs.run
+
+            def run_selected(name, *a, **k):
+                return legs_run(name, *a, **k) if name in only else None
+            legs.run = run_selected
         legs.run("gcn_reddit", lambda: None, lambda _: bm.gcn_reddit_leg(
             g, dev, kernel, gather_peak, algorithmic_bytes, sample, cpu=want),
             collective=False)

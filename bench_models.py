@@ -71,14 +71,23 @@ def wall_steps(step, steps, warmup, dev, kernel):
     _sync(dev)
     with _no_gc():
         kernel.timing_enable(True)
+        _marker(dev)  # tools/window_stats.py: this region's kernels
+        _sync(dev)
         t0 = time.perf_counter()
         for _ in range(steps):
             step()
         _sync(dev)
         el = time.perf_counter() - t0
+        _marker(dev)
     kms, launches = kernel.timing_read()
     kernel.timing_enable(False)
     return el / steps * 1e3, kms / steps, launches // max(steps, 1)
+
+
+def _marker(dev):
+    """A one-wave spin kernel outside the timed region (bench._window_marker)."""
+    if dev.type == "cuda":
+        torch.cuda._sleep(1)
 
 
 def call_ms(fn, iters, dev):

@@ -148,6 +148,16 @@ for s in $STEPS; do
       timeout -k 10 900 python bench.py --workload rmat --rmat-scale ${RMAT_SCALE:-26} --steps 5 \
         --warmup 2 > gpurun_out/rmat.json 2> gpurun_out/rmat.err
       rc=$?; tail -4 gpurun_out/rmat.err; cat gpurun_out/rmat.json; [ $rc -eq 0 ] || exit $rc ;;
+    legprof)
+      # one model leg under the kernel trace (LEG=gcn_reddit): its timed epochs' kernels alone
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/legprof -o run \
+        --output-format csv -- python bench.py --no-traffic --no-rmat-leg --no-sage-rmat-leg \
+        --no-train-leg --no-one-launch-leg --no-cpu-baseline --model-legs ${LEG:-gcn_reddit} \
+        > gpurun_out/legprof.json 2> gpurun_out/legprof.log
+      rc=$?; tail -1 gpurun_out/legprof.log; [ $rc -eq 0 ] || exit $rc
+      python tools/window_stats.py gpurun_out/legprof/run_kernel_trace.csv --window 1 \
+        --out gpurun_out/legprof/leg_timed_kernel_stats.csv || exit $? ;;
     gatsplit)
       # the GAT backward's L2 hits / misses and EA requests over the timed calls (tools/gat_bwd_split.py)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
