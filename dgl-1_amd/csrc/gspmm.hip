@@ -21,6 +21,8 @@
 //  * Rows are launched in degree-descending order (row_order) so the longest
 //    sequential chains start first and the tail is short.
 
+#include <cstdlib>
+
 #include "gspmm_impl.h"
 
 namespace dglhip {
@@ -450,6 +452,101 @@ int g_gather_buf = 2;
 int g_row_pol = 2;
 int g_sddmm_alt = 0;
 
+// ---------------------------------------------------------------------------
+// Narrow rows, two slots per gather (r06): copy_u + sum over the blocked
+// schedule's items when a source row is at most 64 floats (F = 41 at its
+// 48-float padded stride: GCN's output layer). The one-row-per-wave kernel
+// gathers such a row with 48 of 64 lanes one slot per instruction; here the
+// wave's halves gather consecutive slots k and k + 1 of the same item (lane
+// 32h + j holds floats 2j, 2j + 1 of slot k + h), and the lower half adds
+// them in slot order: acc = (acc + s_k) + s_{k+1}, the second operand brought
+// down through the LDS crossbar (ds_bpermute). Every output element is the one-launch kernel's
+// chain (same additions, same order), so the bits are unchanged; the gather
+// instructions per slot halve. The column ids stay scalar (both slots' ids
+// through the scalar cache, a select per half), the rows are read through one
+// buffer descriptor over the whole table (32-bit lane offsets).
+// ---------------------------------------------------------------------------
+int g_pair_slots = [] {
+  const char* e = std::getenv("DGLHIP_PAIR_SLOTS");
+  return e ? std::atoi(e) : 1;
+}();
+
+__device__ __forceinline__ float upper_half(float v, int from) {
+  // lanes 0..31 receive lanes 32..63's values (ds_bpermute: the LDS
+  // crossbar, no LDS storage; ``from`` = the source lane's byte address)
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(v)));
+}
+
+template <int UNROLL, bool ACCUM>
+__global__ __launch_bounds__(256) void gspmm_pair_items_kernel(
+    int64_t num_items, int64_t F, int64_t ld, int64_t table_bytes,
+    const int32_t* __restrict__ item_rows, const int64_t* __restrict__ item_ptr,
+    const int32_t* __restrict__ indices, const float* __restrict__ ufeat,
+    float* __restrict__ out) {
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const int64_t it = block_linear() * 4 +
+                     __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  if (it >= num_items) return;
+  const int lane = threadIdx.x & 63, half = lane >> 5;
+  const int64_t f0 = int64_t(lane & 31) * 2;
+  const bool active = f0 < F;  // f0 + 1 may be a padding float (ld even > F)
+  auto uni64 = [](int64_t x) {  // a wave-uniform 64-bit value, said so
+    return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int32_t(x >> 32)))) << 32) |
+                   uint32_t(__builtin_amdgcn_readfirstlane(int32_t(x))));
+  };
+  const int64_t row = __builtin_amdgcn_readfirstlane(item_rows[it]);
+  const int64_t beg = uni64(item_ptr[it]), end = uni64(item_ptr[it + 1]);
+  const __amdgpu_buffer_rsrc_t tab = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(ufeat), 0, static_cast<int>(table_bytes), 0x00020000);
+  const uint32_t foff = static_cast<uint32_t>(f0 * 4);
+  const uint32_t rowb = static_cast<uint32_t>(ld * 4);
+  const int from = ((lane + 32) & 63) * 4;
+  float* orow = out + row * F;
+  float ax = (ACCUM && half == 0 && active) ? orow[f0] : 0.0f;
+  float ay = (ACCUM && half == 0 && f0 + 1 < F) ? orow[f0 + 1] : 0.0f;
+  // one loop for full and partial batches: rem is wave-uniform, so the
+  // predicates are scalar branches (a separate predicated tail batch doubled
+  // the live registers: 126 against 42 VGPRs)
+  for (int64_t k = beg; k < end; k += 2 * UNROLL) {
+    const int64_t rem = end - k;
+    float vx[UNROLL], vy[UNROLL];
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j) {
+      if (2 * j < rem) {
+        const int32_t ca = indices[k + 2 * j];
+        const int32_t cb = 2 * j + 1 < rem ? indices[k + 2 * j + 1] : ca;
+        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(
+            tab, static_cast<uint32_t>(half ? cb : ca) * rowb + foff, 0, 0);
+        vx[j] = __uint_as_float(w.x);
+        vy[j] = __uint_as_float(w.y);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < UNROLL; ++j) {
+      if (2 * j < rem) {
+        const float wx = upper_half(vx[j], from), wy = upper_half(vy[j], from);
+        ax += vx[j];  // slot k + 2j (this half's own)
+        ay += vy[j];
+        if (2 * j + 1 < rem) {  // then slot k + 2j + 1 (the upper half's)
+          ax += wx;
+          ay += wy;
+        }
+      }
+    }
+  }
+  if (half == 0 && active) {
+    orow[f0] = ax;
+    if (f0 + 1 < F) orow[f0 + 1] = ay;
+  }
+}
+
+// the paired kernel's shapes: copy_u, rows of <= 64 floats at an even stride,
+// a table the 32-bit buffer offsets span
+static bool pair_items_ok(int msg_op, int64_t F, int64_t ld, int64_t num_src_bytes) {
+  return g_pair_slots && msg_op == DGLHIP_MSG_COPY_U && F >= 16 && ld <= 64 && ld % 2 == 0 &&
+         num_src_bytes > 0 && num_src_bytes < (int64_t(1) << 31);
+}
+
 static void dispatch_sum(int msg_op, bool mean, const SumLaunch& a, hipStream_t stream) {
   const int em = edge_mode(a.elen, a.F);
   if (msg_op == DGLHIP_MSG_COPY_U_BF16) {
@@ -651,6 +748,46 @@ int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
               out, item_rows, item_ptr, item_ptr + 1, accumulate != 0, false, ufeat_ld};
   dispatch_sum(msg_op, false, a, stream);
   API_END();
+}
+
+int dglhip_gspmm_pair_items_ok(int msg_op, int64_t feat_len, int64_t ufeat_ld,
+                               int64_t num_src_rows) {
+  const int64_t ld = ufeat_ld ? ufeat_ld : feat_len;
+  return pair_items_ok(msg_op, feat_len, ld, num_src_rows * ld * 4) ? 1 : 0;
+}
+
+int dglhip_gspmm_pair_items_device(int64_t num_items, int64_t feat_len, int64_t ufeat_ld,
+                                   int64_t num_src_rows, const int32_t* item_rows,
+                                   const int64_t* item_ptr, int accumulate,
+                                   const int32_t* indices, const float* ufeat, float* out,
+                                   void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  const int64_t ld = ufeat_ld ? ufeat_ld : feat_len;
+  DGLHIP_CHECK(num_items >= 0 && feat_len >= 0 && num_src_rows >= 0, "negative size");
+  DGLHIP_CHECK(pair_items_ok(DGLHIP_MSG_COPY_U, feat_len, ld, num_src_rows * ld * 4),
+               "paired gathers take copy_u rows of 16..64 floats at an even stride <= 64 "
+               "over a table under 2 GiB (F " << feat_len << ", stride " << ld << ")");
+  if (num_items == 0 || feat_len == 0) return 0;
+  DGLHIP_CHECK(item_rows && item_ptr && indices && ufeat && out, "null argument");
+  const dim3 grid = grid_1d((num_items + 3) / 4);
+  const int64_t bytes = num_src_rows * ld * 4;
+  timed_launch(stream, [&] {
+    if (accumulate)
+      hipLaunchKernelGGL((gspmm_pair_items_kernel<16, true>), grid, dim3(256), 0, stream,
+                         num_items, feat_len, ld, bytes, item_rows, item_ptr, indices, ufeat,
+                         out);
+    else
+      hipLaunchKernelGGL((gspmm_pair_items_kernel<16, false>), grid, dim3(256), 0, stream,
+                         num_items, feat_len, ld, bytes, item_rows, item_ptr, indices, ufeat,
+                         out);
+  });
+  API_END();
+}
+
+int dglhip_set_pair_slots(int on) {
+  g_pair_slots = on ? 1 : 0;
+  return 0;
 }
 
 int dglhip_gspmm_max_ranges_device(int msg_op, int64_t num_rows, int64_t feat_len,

@@ -1015,8 +1015,19 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
       }
     }
     const int64_t ldk = d.ld;
+    const bool paired = a.msg == DGLHIP_MSG_COPY_U &&
+                        dglhip_gspmm_pair_items_ok(a.msg, a.F, ldk, a.urows) == 1;
     for (size_t i = 0; i < bp.launches.size(); ++i) {
       const BlockItems& it = bp.launches[i];
+      if (paired) {  // narrow rows: two slots per gather, the same chains
+        DGLHIP_CHECK(dglhip_gspmm_pair_items_device(
+                         it.n_items, a.F, ldk, a.urows, it.rows.data<int32_t>(),
+                         it.ptr.data<int64_t>(), (i == 0 && first_writes) ? 0 : 1,
+                         bp.indices.data<int32_t>(), static_cast<const float*>(uf), a.out,
+                         s) == 0,
+                     DGLGetLastError());
+        continue;
+      }
       DGLHIP_CHECK(dglhip_gspmm_items_device(
                        a.msg, it.n_items, a.F, it.rows.data<int32_t>(), it.ptr.data<int64_t>(),
                        (i == 0 && first_writes) ? 0 : 1, bp.indices.data<int32_t>(),

@@ -135,6 +135,8 @@ def _load():
         "dglhip_set_sweep_per_cu": (_c_int, [_c_int]),
         "dglhip_sweep_barrier_expiries": (_c_int, [_c_int, _vp]),
         "dglhip_set_sweep_rows": (_c_int, [_c_int]),
+        "dglhip_set_pair_slots": (_c_int, [_c_int]),
+        "dglhip_gspmm_pair_items_ok": (_c_int, [_c_int, _c_i64, _c_i64, _c_i64]),
         "dglhip_get_sweep_rows": (_c_int, [_vp]),
         "dglhip_set_sweep_schedule": (_c_int, [_c_int, _c_i64, _c_i64, _c_int, _c_int, _c_i64,
                                                _c_i64, _c_int]),

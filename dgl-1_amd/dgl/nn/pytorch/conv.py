@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from ... import function as fn
 from ... import kernel
 from ...base import DGLError
-from .linear import NodeLinear, sage_dense
+from .linear import NodeLinear, sage_dense, bias_add
 
 __all__ = ["GraphConv", "GATConv", "SAGEConv", "RelGraphConv"]
 
@@ -57,7 +57,7 @@ class GraphConv(nn.Module):
             deg = g.in_degrees().float().clamp(min=1).to(dev).unsqueeze(1)
             rst = rst * (deg.pow(-0.5) if self.norm == "both" else 1.0 / deg)
         if self.bias is not None:
-            rst = rst + self.bias
+            rst = bias_add(rst, self.bias)
         return self.activation(rst) if self.activation else rst
 
 

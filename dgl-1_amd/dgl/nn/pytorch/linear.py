@@ -25,7 +25,7 @@ import torch.nn as nn
 
 from ..._handoff import GradHandoff, is_output, output_ref, take
 
-__all__ = ["NodeLinear", "sage_dense"]
+__all__ = ["NodeLinear", "sage_dense", "bias_add"]
 
 _ROWS_PER_CHUNK = 1 << 16
 _SMALL_ROWS_PER_CHUNK = 1 << 11
@@ -101,6 +101,38 @@ class _NodeLinearFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _given_colsum(ctx, dy)
         return dx, dw, db
+
+
+class _BiasAddFn(torch.autograd.Function):
+    """h + bias over node rows, whose bias gradient is the chunked column sum
+    (_colsum) instead of torch's reduction over the node dimension (r06: the
+    2-layer GCN's bias gradient over 232,965 x 128 took 1.16 ms of a 15.8 ms
+    epoch in torch's reduce kernel)."""
+
+    @staticmethod
+    def forward(ctx, h, bias):
+        ctx.bias_shape = bias.shape
+        return h + bias
+
+    @staticmethod
+    def backward(ctx, dy):
+        db = None
+        if ctx.needs_input_grad[1]:
+            d2 = dy.reshape(-1, dy.shape[-1]) if dy.dim() != 2 else dy
+            db = _colsum(d2.contiguous()).reshape(ctx.bias_shape)
+        return (dy if ctx.needs_input_grad[0] else None), db
+
+
+def bias_add(h, bias):
+    """``h + bias`` for a bias broadcast over the rows of a node tensor
+    (bias of h's trailing width); the same values, and a bias gradient summed
+    in row chunks (fp32 summation tolerance against torch's reduction, whose
+    association is implementation-defined too)."""
+    if bias is None:
+        return h
+    if not (h.is_cuda and h.dim() >= 2 and bias.dim() == 1 and bias.shape[0] == h.shape[-1]):
+        return h + bias
+    return _BiasAddFn.apply(h, bias)
 
 
 def _mm_t(x, w):

@@ -24,6 +24,7 @@ import dgl  # noqa: E402
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph  # noqa: E402
 from dgl.data import load_data  # noqa: E402
+from dgl.nn.pytorch import bias_add  # noqa: E402
 
 
 class GCNLayer(nn.Module):
@@ -49,7 +50,7 @@ class GCNLayer(nn.Module):
         h = self.g.ndata.pop("h")
         h = h * self.g.ndata["norm"]          # destination-degree normalisation
         if self.bias is not None:
-            h = h + self.bias
+            h = bias_add(h, self.bias)        # h + bias; its gradient a chunked column sum
         if self.activation:
             h = self.activation(h)
         return h

@@ -571,6 +571,25 @@ int dglhip_gspmm_items_device(int msg_op, int64_t num_items, int64_t feat_len,
                               int64_t ufeat_ld, const float* efeat, int64_t efeat_len,
                               float* out, void* stream);
 
+/* Narrow rows, two slots per gather (r06): the same items as
+ * dglhip_gspmm_items_device (copy_u + sum, item i = row item_rows[i] over
+ * slots [item_ptr[i], item_ptr[i + 1]), accumulate continuing the chains)
+ * for source rows of 16..64 floats at an even stride ufeat_ld <= 64 (0 =
+ * feat_len) over a table of num_src_rows rows under 2 GiB. The wave's halves
+ * gather consecutive slots and the lower half adds them in slot order, so the
+ * results equal dglhip_gspmm_items_device's bit for bit with half the gather
+ * instructions. _ok: 1 when a shape qualifies (and the knob is on). */
+int dglhip_gspmm_pair_items_ok(int msg_op, int64_t feat_len, int64_t ufeat_ld,
+                               int64_t num_src_rows);
+int dglhip_gspmm_pair_items_device(int64_t num_items, int64_t feat_len, int64_t ufeat_ld,
+                                   int64_t num_src_rows, const int32_t* item_rows,
+                                   const int64_t* item_ptr, int accumulate,
+                                   const int32_t* indices, const float* ufeat, float* out,
+                                   void* stream);
+/* Knob: the plan's blocked copy_u + sum takes the paired kernel where it
+ * qualifies (1, the default; env DGLHIP_PAIR_SLOTS=0 turns it off). */
+int dglhip_set_pair_slots(int on);
+
 /* Source-swept copy_u + sum (mean != 0: mean) of fp32 rows of feat_len = 64,
  * 128 or 256 floats over the CSR (indptr, indices), every row of out
  * written. Each wave keeps rows_per_wave rows' running sums in LDS for a

@@ -145,6 +145,60 @@ def test_blocked_device_bits(F, reduce):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("F", [16, 32, 41, 48, 64])
+def test_paired_narrow_rows_same_bits(F):
+    """Narrow source rows (<= 64 floats at an even stride: F = 41 runs at its
+    48-float padded stride) take the paired kernel on the blocked schedule
+    (dglhip_gspmm_pair_items_device: the wave's halves gather consecutive
+    slots, the lower half adds them in slot order). Forward, the transposed
+    backward, mean and a continued (SUM_ACCUM) product equal the one-row-
+    per-wave kernel bit for bit, and the oracle's chains; rows of 1, 2 and 3
+    slots and odd tails included."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    from dgl._ffi import LIB, check_call
+    dev = torch.device("cuda", 0)
+    n, m = 120_000, 8_000_000
+    src, dst = _graph(n, m, 5, True)
+    # a few rows with 1..3 slots in the source-major order (short items)
+    src = np.concatenate([src, [7, 8, 9, 10, 11, 12]]).astype(np.int64)
+    dst = np.concatenate([dst, [n - 1, n - 2, n - 2, n - 3, n - 3, n - 3]]).astype(np.int64)
+    o = np.lexsort((dst, src))
+    src, dst = src[o], dst[o]
+    g = dgl.DGLGraph((torch.from_numpy(src), torch.from_numpy(dst)))
+    gen = torch.Generator().manual_seed(6)
+    H = torch.randn(n, F, generator=gen)
+    G = torch.randn(n, F, generator=gen)
+    base = torch.randn(n, F, generator=gen)
+    adj = g.sparse_adjacency(dev)
+    ld = kernel.padded_width(F)
+    assert LIB.dglhip_gspmm_pair_items_ok(0, F, ld, n) == 1
+
+    def run(pair):
+        check_call(LIB.dglhip_set_pair_slots(pair))
+        try:
+            h = H.to(dev).requires_grad_(True)
+            g.ndata["h"] = h
+            g.update_all(fn.copy_src("h", "m"), fn.sum("m", "o"))
+            g.ndata["o"].backward(G.to(dev))
+            g.update_all(fn.copy_src("h", "m"), fn.mean("m", "mo"))
+            acc = base.to(dev).clone()
+            kernel.gspmm_into(adj.fwd, acc, H.to(dev), accumulate=True)
+            torch.cuda.synchronize()
+            return [g.ndata["o"].detach().cpu(), h.grad.cpu(), g.ndata["mo"].cpu(), acc.cpu()]
+        finally:
+            check_call(LIB.dglhip_set_pair_slots(1))
+    # small tables: blocks of 2 MiB so that every width takes the blocked schedule
+    with kernel.scheduled(block_table_min=0, block_bytes=2 << 20):
+        assert kernel._block_plan(adj.fwd, H.to(dev), F) is not None
+        paired, single = run(1), run(0)
+    for a, b in zip(paired, single):
+        assert torch.equal(a, b)
+    assert np.array_equal(paired[0].numpy(), O.spmm_coo(n, dst, src, H.numpy()))
+    assert np.array_equal(paired[1].numpy(), O.spmm_coo(n, src, dst, G.numpy()))
+
+
+@pytest.mark.gpu
 def test_random_order_graph_keeps_one_launch():
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
