@@ -468,7 +468,7 @@ int g_sddmm_alt = 0;
 // ---------------------------------------------------------------------------
 int g_pair_slots = [] {
   const char* e = std::getenv("DGLHIP_PAIR_SLOTS");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 0;
 }();
 
 __device__ __forceinline__ float upper_half(float v, int from) {
@@ -477,19 +477,25 @@ __device__ __forceinline__ float upper_half(float v, int from) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(from, __float_as_int(v)));
 }
 
-template <int UNROLL, bool ACCUM>
+// VEC floats per lane (2: rows of <= 64 floats; 4: rows of <= 128, the
+// headline's F = 128, 16-B gathers); RP: the running rows' cache policy of
+// the one-slot kernel (load_out / store_out: non-temporal loads, sc1 stores
+// by default), so the two kernels treat the blocked schedule's passes alike.
+template <int VEC, int UNROLL, bool ACCUM, int RP>
 __global__ __launch_bounds__(256) void gspmm_pair_items_kernel(
     int64_t num_items, int64_t F, int64_t ld, int64_t table_bytes,
     const int32_t* __restrict__ item_rows, const int64_t* __restrict__ item_ptr,
     const int32_t* __restrict__ indices, const float* __restrict__ ufeat,
     float* __restrict__ out) {
-  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  typedef typename Vec<VEC>::T V;
+  typedef unsigned int uvec __attribute__((ext_vector_type(VEC)));
   const int64_t it = block_linear() * 4 +
                      __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
   if (it >= num_items) return;
   const int lane = threadIdx.x & 63, half = lane >> 5;
-  const int64_t f0 = int64_t(lane & 31) * 2;
-  const bool active = f0 < F;  // f0 + 1 may be a padding float (ld even > F)
+  const int64_t f0 = int64_t(lane & 31) * VEC;
+  const bool active = f0 < F;  // the lane's last floats may be row padding (ld > F)
+  const bool in_row = f0 < ld;  // lanes past the row read nothing (no next-row lines)
   auto uni64 = [](int64_t x) {  // a wave-uniform 64-bit value, said so
     return int64_t((uint64_t(uint32_t(__builtin_amdgcn_readfirstlane(int32_t(x >> 32)))) << 32) |
                    uint32_t(__builtin_amdgcn_readfirstlane(int32_t(x))));
@@ -502,48 +508,77 @@ __global__ __launch_bounds__(256) void gspmm_pair_items_kernel(
   const uint32_t rowb = static_cast<uint32_t>(ld * 4);
   const int from = ((lane + 32) & 63) * 4;
   float* orow = out + row * F;
-  float ax = (ACCUM && half == 0 && active) ? orow[f0] : 0.0f;
-  float ay = (ACCUM && half == 0 && f0 + 1 < F) ? orow[f0 + 1] : 0.0f;
+  // whole-vector running rows where the row holds them (F a multiple of VEC)
+  const bool vec_out = F % VEC == 0;
+  float a[VEC];
+  if (ACCUM && half == 0 && active && vec_out) {
+    const V v = load_out<VEC, RP>(orow, f0);
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) a[c] = v[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < VEC; ++c) a[c] = (ACCUM && half == 0 && f0 + c < F) ? orow[f0 + c] : 0.0f;
+  }
   // one loop for full and partial batches: rem is wave-uniform, so the
   // predicates are scalar branches (a separate predicated tail batch doubled
-  // the live registers: 126 against 42 VGPRs)
+  // the live registers: 126 against 42 VGPRs at VEC 2)
   for (int64_t k = beg; k < end; k += 2 * UNROLL) {
     const int64_t rem = end - k;
-    float vx[UNROLL], vy[UNROLL];
+    float v[UNROLL][VEC];
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
       if (2 * j < rem) {
         const int32_t ca = indices[k + 2 * j];
         const int32_t cb = 2 * j + 1 < rem ? indices[k + 2 * j + 1] : ca;
-        const u32x2 w = __builtin_amdgcn_raw_buffer_load_b64(
-            tab, static_cast<uint32_t>(half ? cb : ca) * rowb + foff, 0, 0);
-        vx[j] = __uint_as_float(w.x);
-        vy[j] = __uint_as_float(w.y);
+        const uint32_t off = static_cast<uint32_t>(half ? cb : ca) * rowb + foff;
+        uvec w = uvec(0u);
+        if (in_row) {
+          if constexpr (VEC == 4) w = __builtin_amdgcn_raw_buffer_load_b128(tab, off, 0, 0);
+          else w = __builtin_amdgcn_raw_buffer_load_b64(tab, off, 0, 0);
+        }
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) v[j][c] = __uint_as_float(w[c]);
       }
     }
 #pragma unroll
     for (int j = 0; j < UNROLL; ++j) {
       if (2 * j < rem) {
-        const float wx = upper_half(vx[j], from), wy = upper_half(vy[j], from);
-        ax += vx[j];  // slot k + 2j (this half's own)
-        ay += vy[j];
-        if (2 * j + 1 < rem) {  // then slot k + 2j + 1 (the upper half's)
-          ax += wx;
-          ay += wy;
+        float w[VEC];
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) w[c] = upper_half(v[j][c], from);
+#pragma unroll
+        for (int c = 0; c < VEC; ++c) a[c] += v[j][c];  // slot k + 2j (this half's own)
+        if (2 * j + 1 < rem) {                           // then slot k + 2j + 1
+#pragma unroll
+          for (int c = 0; c < VEC; ++c) a[c] += w[c];
         }
       }
     }
   }
   if (half == 0 && active) {
-    orow[f0] = ax;
-    if (f0 + 1 < F) orow[f0 + 1] = ay;
+    if (vec_out) {
+      V v;
+#pragma unroll
+      for (int c = 0; c < VEC; ++c) v[c] = a[c];
+      store_out<VEC, RP>(orow, f0, v);
+    } else {
+#pragma unroll
+      for (int c = 0; c < VEC; ++c)
+        if (f0 + c < F) orow[f0 + c] = a[c];
+    }
   }
 }
 
 // the paired kernel's shapes: copy_u, rows of <= 64 floats at an even stride,
 // a table the 32-bit buffer offsets span
+static int pair_vec(int64_t F, int64_t ld) {
+  if (F >= 16 && ld <= 64 && ld % 2 == 0) return 2;
+  if (g_pair_slots >= 2 && F > 64 && ld <= 128 && ld % 4 == 0) return 4;
+  return 0;
+}
+
 static bool pair_items_ok(int msg_op, int64_t F, int64_t ld, int64_t num_src_bytes) {
-  return g_pair_slots && msg_op == DGLHIP_MSG_COPY_U && F >= 16 && ld <= 64 && ld % 2 == 0 &&
+  return g_pair_slots && msg_op == DGLHIP_MSG_COPY_U && pair_vec(F, ld) != 0 &&
          num_src_bytes > 0 && num_src_bytes < (int64_t(1) << 31);
 }
 
@@ -772,21 +807,32 @@ int dglhip_gspmm_pair_items_device(int64_t num_items, int64_t feat_len, int64_t 
   DGLHIP_CHECK(item_rows && item_ptr && indices && ufeat && out, "null argument");
   const dim3 grid = grid_1d((num_items + 3) / 4);
   const int64_t bytes = num_src_rows * ld * 4;
+  // 32 slots (16 gathers) in flight per wave at VEC 2; 16 slots (8 gathers
+  // of 16 B: 44 VGPRs, where 16 took 76) at VEC 4, the one-slot kernel's 16
+#define DGLHIP_PAIR(VEC, ACC, RPV)                                                            \
+  hipLaunchKernelGGL((gspmm_pair_items_kernel<VEC, VEC == 4 ? 8 : 16, ACC, RPV>), grid,       \
+                     dim3(256), 0, stream, num_items, feat_len, ld, bytes, item_rows,         \
+                     item_ptr, indices, ufeat, out)
+  const int vec = pair_vec(feat_len, ld);
   timed_launch(stream, [&] {
-    if (accumulate)
-      hipLaunchKernelGGL((gspmm_pair_items_kernel<16, true>), grid, dim3(256), 0, stream,
-                         num_items, feat_len, ld, bytes, item_rows, item_ptr, indices, ufeat,
-                         out);
-    else
-      hipLaunchKernelGGL((gspmm_pair_items_kernel<16, false>), grid, dim3(256), 0, stream,
-                         num_items, feat_len, ld, bytes, item_rows, item_ptr, indices, ufeat,
-                         out);
+    // the running rows as the one-slot kernel treats them (g_row_pol; the
+    // first launch only stores: sc1, as policy 4)
+    if (vec == 4) {
+      if (!accumulate) DGLHIP_PAIR(4, false, 4);
+      else if (g_row_pol == 2) DGLHIP_PAIR(4, true, 2);
+      else DGLHIP_PAIR(4, true, 0);
+    } else {
+      if (accumulate) DGLHIP_PAIR(2, true, 0);
+      else DGLHIP_PAIR(2, false, 0);
+    }
   });
+#undef DGLHIP_PAIR
   API_END();
 }
 
 int dglhip_set_pair_slots(int on) {
-  g_pair_slots = on ? 1 : 0;
+  // 0 off, 1 rows of <= 64 floats, 2 also rows of <= 128 (16-B gathers)
+  g_pair_slots = on < 0 ? 0 : (on > 2 ? 2 : on);
   return 0;
 }
 

@@ -334,6 +334,15 @@ __device__ __forceinline__ void store_out(float* row, int64_t f0, typename Vec<V
                                           0, 16);
     return;
   }
+  if ((RP == 2 || RP == 3 || RP == 4) && VEC == 4) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(row, 0, 0x7fffffff,
+                                                                       0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u32x4*>(&v), r,
+                                           static_cast<uint32_t>(f0 * int64_t(sizeof(float))),
+                                           0, 16);
+    return;
+  }
   stv<VEC>(row + f0, v);
 }
 

@@ -587,7 +587,9 @@ int dglhip_gspmm_pair_items_device(int64_t num_items, int64_t feat_len, int64_t 
                                    const int32_t* indices, const float* ufeat, float* out,
                                    void* stream);
 /* Knob: the plan's blocked copy_u + sum takes the paired kernel where it
- * qualifies (1, the default; env DGLHIP_PAIR_SLOTS=0 turns it off). */
+ * qualifies: 0 never (the default: measured slower), 1 rows
+ * of <= 64 floats, 2 also rows of <= 128 (16-B gathers); env
+ * DGLHIP_PAIR_SLOTS. */
 int dglhip_set_pair_slots(int on);
 
 /* Source-swept copy_u + sum (mean != 0: mean) of fp32 rows of feat_len = 64,

@@ -145,15 +145,17 @@ def test_blocked_device_bits(F, reduce):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F", [16, 32, 41, 48, 64])
-def test_paired_narrow_rows_same_bits(F):
+@pytest.mark.parametrize("F,level", [(16, 1), (32, 1), (41, 1), (48, 1), (64, 1), (96, 2),
+                                     (128, 2)])
+def test_paired_narrow_rows_same_bits(F, level):
     """Narrow source rows (<= 64 floats at an even stride: F = 41 runs at its
     48-float padded stride) take the paired kernel on the blocked schedule
     (dglhip_gspmm_pair_items_device: the wave's halves gather consecutive
     slots, the lower half adds them in slot order). Forward, the transposed
     backward, mean and a continued (SUM_ACCUM) product equal the one-row-
     per-wave kernel bit for bit, and the oracle's chains; rows of 1, 2 and 3
-    slots and odd tails included."""
+    slots and odd tails included. Level 2 of the knob also pairs rows of up
+    to 128 floats (16-B gathers, the headline's F = 128)."""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     from dgl._ffi import LIB, check_call
@@ -172,7 +174,11 @@ def test_paired_narrow_rows_same_bits(F):
     base = torch.randn(n, F, generator=gen)
     adj = g.sparse_adjacency(dev)
     ld = kernel.padded_width(F)
-    assert LIB.dglhip_gspmm_pair_items_ok(0, F, ld, n) == 1
+    check_call(LIB.dglhip_set_pair_slots(level))
+    try:
+        assert LIB.dglhip_gspmm_pair_items_ok(0, F, ld, n) == 1
+    finally:
+        check_call(LIB.dglhip_set_pair_slots(0))
 
     def run(pair):
         check_call(LIB.dglhip_set_pair_slots(pair))
@@ -187,11 +193,11 @@ def test_paired_narrow_rows_same_bits(F):
             torch.cuda.synchronize()
             return [g.ndata["o"].detach().cpu(), h.grad.cpu(), g.ndata["mo"].cpu(), acc.cpu()]
         finally:
-            check_call(LIB.dglhip_set_pair_slots(1))
+            check_call(LIB.dglhip_set_pair_slots(0))
     # small tables: blocks of 2 MiB so that every width takes the blocked schedule
-    with kernel.scheduled(block_table_min=0, block_bytes=2 << 20):
+    with kernel.scheduled(block_table_min=0, block_bytes=2 << 20, block_min_row_bytes=0):
         assert kernel._block_plan(adj.fwd, H.to(dev), F) is not None
-        paired, single = run(1), run(0)
+        paired, single = run(level), run(0)
     for a, b in zip(paired, single):
         assert torch.equal(a, b)
     assert np.array_equal(paired[0].numpy(), O.spmm_coo(n, dst, src, H.numpy()))
