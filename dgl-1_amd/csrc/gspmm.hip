@@ -573,7 +573,6 @@ __global__ __launch_bounds__(256) void gspmm_pair_items_kernel(
 // a table the 32-bit buffer offsets span
 static int pair_vec(int64_t F, int64_t ld) {
   if (F >= 16 && ld <= 64 && ld % 2 == 0) return 2;
-  if (g_pair_slots >= 2 && F > 64 && ld <= 128 && ld % 4 == 0) return 4;
   return 0;
 }
 
@@ -817,22 +816,17 @@ int dglhip_gspmm_pair_items_device(int64_t num_items, int64_t feat_len, int64_t 
   timed_launch(stream, [&] {
     // the running rows as the one-slot kernel treats them (g_row_pol; the
     // first launch only stores: sc1, as policy 4)
-    if (vec == 4) {
-      if (!accumulate) DGLHIP_PAIR(4, false, 4);
-      else if (g_row_pol == 2) DGLHIP_PAIR(4, true, 2);
-      else DGLHIP_PAIR(4, true, 0);
-    } else {
-      if (accumulate) DGLHIP_PAIR(2, true, 0);
-      else DGLHIP_PAIR(2, false, 0);
-    }
+    (void)vec;  // 2: rows of <= 64 floats (a VEC 4 form for 128-float rows measured
+                // 4.58 vs 3.75 ms on the headline and was dropped)
+    if (accumulate) DGLHIP_PAIR(2, true, 0);
+    else DGLHIP_PAIR(2, false, 0);
   });
 #undef DGLHIP_PAIR
   API_END();
 }
 
 int dglhip_set_pair_slots(int on) {
-  // 0 off, 1 rows of <= 64 floats, 2 also rows of <= 128 (16-B gathers)
-  g_pair_slots = on < 0 ? 0 : (on > 2 ? 2 : on);
+  g_pair_slots = on ? 1 : 0;
   return 0;
 }
 

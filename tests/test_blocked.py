@@ -145,8 +145,7 @@ def test_blocked_device_bits(F, reduce):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("F,level", [(16, 1), (32, 1), (41, 1), (48, 1), (64, 1), (96, 2),
-                                     (128, 2)])
+@pytest.mark.parametrize("F,level", [(16, 1), (32, 1), (41, 1), (48, 1), (64, 1)])
 def test_paired_narrow_rows_same_bits(F, level):
     """Narrow source rows (<= 64 floats at an even stride: F = 41 runs at its
     48-float padded stride) take the paired kernel on the blocked schedule
@@ -154,8 +153,8 @@ def test_paired_narrow_rows_same_bits(F, level):
     slots, the lower half adds them in slot order). Forward, the transposed
     backward, mean and a continued (SUM_ACCUM) product equal the one-row-
     per-wave kernel bit for bit, and the oracle's chains; rows of 1, 2 and 3
-    slots and odd tails included. Level 2 of the knob also pairs rows of up
-    to 128 floats (16-B gathers, the headline's F = 128)."""
+    slots and odd tails included. (A study kernel, off by default: it
+    measured slower)"""
     if not torch.cuda.is_available():
         pytest.skip("no ROCm device")
     from dgl._ffi import LIB, check_call

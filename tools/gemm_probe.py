@@ -1,0 +1,52 @@
+"""The GCN's dense products at configs[1]'s shapes on each BLAS backend torch
+offers on ROCm (hipBLASLt, rocBLAS): forward X·W (232,965 x 602 x 128), the
+weight gradient Xᵀ·dA, and layer 2's (x 128 x 41) pair; ms per call by
+events.
+
+  python tools/gemm_probe.py
+"""
+import json
+
+import torch
+
+
+def ms(fn, iters=20):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    n = 232965
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(n, 602, generator=g, device=dev)
+    w1 = torch.randn(602, 128, generator=g, device=dev)
+    da1 = torch.randn(n, 128, generator=g, device=dev)
+    h1 = torch.randn(n, 128, generator=g, device=dev)
+    w2 = torch.randn(128, 41, generator=g, device=dev)
+    da2 = torch.randn(n, 41, generator=g, device=dev)
+    res = {}
+    for lib in ("cublaslt", "cublas"):
+        try:
+            torch.backends.cuda.preferred_blas_library(lib)
+        except Exception as err:  # noqa: BLE001
+            res[lib] = str(err)
+            continue
+        r = {"fwd1 x@w1": ms(lambda: torch.mm(x, w1)),
+             "dw1 x^T@da1": ms(lambda: torch.mm(x.t(), da1)),
+             "fwd2 h1@w2": ms(lambda: torch.mm(h1, w2)),
+             "dw2 h1^T@da2": ms(lambda: torch.mm(h1.t(), da2)),
+             "dh1 da2@w2^T": ms(lambda: torch.mm(da2, w2.t()))}
+        res[lib] = r
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

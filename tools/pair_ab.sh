@@ -1,9 +1,9 @@
 #!/bin/bash
-# Paired-slot gathers (DGLHIP_PAIR_SLOTS 0 / 1 / 2) on the GCN leg's F = 41
+# Paired-slot gathers (DGLHIP_PAIR_SLOTS 0 / 1) on the GCN leg's F = 41
 # aggregation and the headline F = 128 step, one bench process per setting.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pair_ab
-for P in ${PAIRS:-0 1 2 0}; do
+for P in ${PAIRS:-0 1 0}; do
   out=gpurun_out/pair_ab/p$P.json
   DGLHIP_PAIR_SLOTS=$P timeout -k 10 400 python bench.py --no-traffic --no-rmat-leg \
     --no-sage-rmat-leg --no-train-leg --no-one-launch-leg --no-cpu-baseline \
