@@ -65,12 +65,14 @@ def _no_gc():
 
 def wall_steps(step, steps, warmup, dev, kernel):
     """(wall ms per step, library kernel ms per step) over ``steps`` steps
-    after ``warmup``; kernel ms from the library's per-launch events."""
+    after ``warmup``; kernel ms from the library's per-launch events, taken
+    over ``steps`` further steps: the event pairs and their lock cost host
+    time on every launch (≈0.5 ms of an R-GCN step, r06), so the wall-clock
+    steps run without them."""
     for _ in range(warmup):
         step()
     _sync(dev)
     with _no_gc():
-        kernel.timing_enable(True)
         _marker(dev)  # tools/window_stats.py: this region's kernels
         _sync(dev)
         t0 = time.perf_counter()
@@ -79,8 +81,14 @@ def wall_steps(step, steps, warmup, dev, kernel):
         _sync(dev)
         el = time.perf_counter() - t0
         _marker(dev)
-    kms, launches = kernel.timing_read()
-    kernel.timing_enable(False)
+        kernel.timing_enable(True)
+        try:
+            for _ in range(steps):
+                step()
+            _sync(dev)
+            kms, launches = kernel.timing_read()
+        finally:
+            kernel.timing_enable(False)
     return el / steps * 1e3, kms / steps, launches // max(steps, 1)
 
 
@@ -549,6 +557,15 @@ def rgcn_leg(dev, kernel, gather_peak, steps=20, warmup=3, cpu=True):
     outside the timer."""
     import tools.rgcn_step as rs
     args = rs.lp.parser().parse_args([])
+    prev_blas = rs.lp.select_blas(args.blas) if dev.type == "cuda" else None
+    try:
+        return _rgcn_leg(rs, args, dev, kernel, gather_peak, steps, warmup, cpu)
+    finally:
+        if prev_blas is not None:
+            rs.lp.select_blas(prev_blas)
+
+
+def _rgcn_leg(rs, args, dev, kernel, gather_peak, steps, warmup, cpu):
     raw = rs.make_samples(args, warmup + steps)
     samples = [rs.to_dev(s, dev) for s in raw]
     model, opt = rs.build_model(args, dev)
@@ -561,10 +578,10 @@ def rgcn_leg(dev, kernel, gather_peak, steps=20, warmup=3, cpu=True):
         if gg.number_of_nodes() < len(uniq):
             gg.add_nodes(len(uniq) - gg.number_of_nodes())
         graphs.append(gg)
-    it = iter(range(warmup + steps))
+    it = iter(range(1 << 30))
 
-    def step():
-        i = next(it)
+    def step():  # the samples in turn (wall_steps' kernel-time pass reuses them)
+        i = next(it) % len(samples)
         uniq, _, _, rel, norm, smp, lab = samples[i]
         h = model(graphs[i], uniq, rel, norm)
         loss = model.loss(h, smp, lab)
@@ -582,7 +599,7 @@ def rgcn_leg(dev, kernel, gather_peak, steps=20, warmup=3, cpu=True):
                      "entities, 237 relations x 2 directions, 272,115 triples), %d-edge sampled "
                      "graph per step, 2 block layers of 100 bases 5x5 (500 hidden), DistMult, "
                      "Adam; graph sampling and DGLGraph build outside the timer (the "
-                     "reference's)" % E,
+                     "reference's); dense products on %s" % (E, args.blas),
            "typed_block_kernels": kt,
            "roofline": roof(kt["forward"]["bytes"], kt["forward"]["ms"], peak, src_,
                             "typed_block_spmm forward (chunked items + combine)",

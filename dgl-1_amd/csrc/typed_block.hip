@@ -31,6 +31,7 @@
 
 #include <rocprim/device/device_scan.hpp>
 
+#include <cstdlib>
 #include <type_traits>
 
 #include "../../include/dgl_hip.h"
@@ -248,6 +249,273 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_kernel(
       if (q < cnt) acc = __builtin_fmaf(rel_norm ? nrm[q] * x[q] : x[q], g[q], acc);
   }
   (single ? dw + r * wr : partial + it * wr)[rem] = acc;
+}
+
+// ---- Relation-major messages (r06) -----------------------------------------
+// The destination-major kernel above loads, per slot and per 64 outputs, the
+// source row's si values and the relation's si weight columns: ten 4-byte
+// gathers per lane for every slot at R-GCN's 5 x 5 blocks, each weight gather
+// spanning ~11 cache lines, and every wave resolves its item and slots before
+// the first of them (0.10 ms per call for a 30,000-edge sample against a few
+// MB of data). Split in two, with the same per-element arithmetic:
+//   messages: one workgroup per item of the relation-major grouping (a chunk
+//     of one relation's edges); the relation's weight columns are loaded once
+//     into registers (thread t: outputs t + 256 q), PB source rows at a time
+//     are staged whole in LDS, and m_e[j] = fma chain over i of
+//     row[b*si+i] * W[r, b, i, j] (the chain above, from 0) is stored at the
+//     edge's forward slot: msg[slot * Fo + j];
+//   sum: the destination-major items as above, but a slot's contribution is
+//     one coalesced read of its message row: acc = fma(norm_e, m_e, acc) in
+//     slot order, chunked rows' partials combined in chunk order.
+// Bits: the same m_e and the same accumulation order as
+// typed_block_spmm_kernel, so the same outputs (test_typed_block.py).
+constexpr int kMsgRows = 8;  // source rows staged per step of a message workgroup
+
+template <int SI, int QO, int RI>
+__global__ __launch_bounds__(256) void typed_block_msg_kernel(
+    int64_t num_items, int64_t num_rels, int64_t nb, int64_t so,
+    const int64_t* __restrict__ rel_ptr, const int64_t* __restrict__ item_ptr,
+    const int32_t* __restrict__ item_rel, const int32_t* __restrict__ pos_row,
+    const int64_t* __restrict__ pos_slot, const float* __restrict__ ufeat,
+    const float* __restrict__ weight, float* __restrict__ msg) {
+  extern __shared__ float rows[];  // kMsgRows x Fi
+  const int64_t it = block_linear();
+  if (it >= num_items) return;  // the whole workgroup
+  int64_t r, beg, end;
+  bool single;
+  if (!item_range(it, num_rels, rel_ptr, item_ptr, item_rel, &r, &beg, &end, &single)) return;
+  const int t = threadIdx.x;
+  const int64_t Fi = nb * SI, Fo = nb * so, wr = nb * SI * so;
+  float w[QO][SI];
+  int xo[QO];
+  bool act[QO];
+#pragma unroll
+  for (int q = 0; q < QO; ++q) {
+    const int64_t j = t + 256 * q;
+    act[q] = j < Fo;
+    const int64_t b = act[q] ? j / so : 0, jj = act[q] ? j - b * so : 0;
+    xo[q] = static_cast<int>(b * SI);
+#pragma unroll
+    for (int i = 0; i < SI; ++i) w[q][i] = weight[r * wr + b * SI * so + i * so + jj];
+  }
+  for (int64_t k = beg; k < end; k += kMsgRows) {
+    const int64_t cnt = end - k;  // uniform
+    float v[kMsgRows][RI];
+#pragma unroll
+    for (int p = 0; p < kMsgRows; ++p) {
+      const int64_t row = pos_row[p < cnt ? k + p : k];  // idle p re-read a valid row
+#pragma unroll
+      for (int ri = 0; ri < RI; ++ri) {
+        const int64_t f = t + 256 * ri;
+        v[p][ri] = f < Fi ? ufeat[row * Fi + f] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kMsgRows; ++p)
+#pragma unroll
+      for (int ri = 0; ri < RI; ++ri) {
+        const int64_t f = t + 256 * ri;
+        if (f < Fi) rows[p * Fi + f] = v[p][ri];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < kMsgRows; ++p) {
+      if (p < cnt) {
+        const int64_t slot = pos_slot[k + p];
+        const float* rp = rows + p * Fi;
+#pragma unroll
+        for (int q = 0; q < QO; ++q) {
+          float m = 0.0f;
+#pragma unroll
+          for (int i = 0; i < SI; ++i) m = __builtin_fmaf(rp[xo[q] + i], w[q][i], m);
+          if (act[q]) msg[slot * Fo + t + 256 * q] = m;
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// out[row] (or the item's partial) = fma(norm_e, msg[mrow(e)], acc) over the
+// item's slots in slot order, mrow = slot_map[slot] or the slot itself. One
+// wave per (item, 64 * T outputs); G slots' message rows in flight.
+template <int T>
+__global__ __launch_bounds__(256) void typed_msg_sum_kernel(
+    int64_t num_items, int64_t num_rows, int64_t npass, int64_t Fo,
+    const int64_t* __restrict__ indptr, const int64_t* __restrict__ item_ptr,
+    const int32_t* __restrict__ item_row, const int64_t* __restrict__ slot_map,
+    const float* __restrict__ slot_norm, const float* __restrict__ msg,
+    float* __restrict__ out, float* __restrict__ partial) {
+  constexpr int G = T >= 4 ? 4 : 8;
+  const int64_t wave = block_linear() * (blockDim.x >> 6) +
+                       __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
+  const int64_t it = wave / npass, pass = wave - it * npass;
+  if (it >= num_items) return;
+  int64_t row, beg, end;
+  bool single;
+  if (!item_range(it, num_rows, indptr, item_ptr, item_row, &row, &beg, &end, &single)) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t f0 = pass * 64 * T + lane;
+  float acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = 0.0f;
+  auto batch = [&](int64_t k, auto gb_tag) {
+    constexpr int GB = decltype(gb_tag)::value;
+    const int64_t cnt = end - k;  // wave-uniform
+    float mv[GB][T], nrm[GB];
+#pragma unroll
+    for (int q = 0; q < GB; ++q) {
+      const int64_t kk = q < cnt ? k + q : end - 1;  // a valid slot for idle q
+      const int64_t mr = slot_map ? slot_map[kk] : kk;
+      nrm[q] = slot_norm ? slot_norm[kk] : 1.0f;
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+        const int64_t f = f0 + 64 * t;
+        mv[q][t] = f < Fo ? msg[mr * Fo + f] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < GB; ++q)
+      if (q < cnt)
+#pragma unroll
+        for (int t = 0; t < T; ++t) acc[t] = __builtin_fmaf(nrm[q], mv[q][t], acc[t]);
+  };
+  constexpr int G2 = G / 2, G4 = G / 4;
+  for (int64_t k = beg; k < end; k += G) {
+    if (end - k <= G4) {
+      batch(k, std::integral_constant<int, G4>());
+      break;
+    }
+    if (end - k <= G2) {
+      batch(k, std::integral_constant<int, G2>());
+      break;
+    }
+    batch(k, std::integral_constant<int, G>());
+  }
+  float* dst = single ? out + row * Fo : partial + it * Fo;
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int64_t f = f0 + 64 * t;
+    if (f < Fo) dst[f] = acc[t];
+  }
+}
+
+// dW over item `it` as typed_block_wgrad_kernel computes it (the same chain
+// per weight element, acc = fma(norm * x, g, acc) in position order), with
+// the positions' source and gradient rows staged whole in LDS, kMsgRows at a
+// time, instead of two 4-byte gathers per (position, weight element): one
+// workgroup per item, thread t owning weight elements t + 256 q.
+template <int QW, int RI, int RO>
+__global__ __launch_bounds__(256) void typed_block_wgrad_lds_kernel(
+    int64_t num_items, int64_t num_rels, int64_t nb, int64_t si, int64_t so,
+    const int64_t* __restrict__ rel_ptr, const int64_t* __restrict__ item_ptr,
+    const int32_t* __restrict__ item_rel, const int32_t* __restrict__ rel_src,
+    const int32_t* __restrict__ rel_dst, const float* __restrict__ rel_norm,
+    const float* __restrict__ ufeat, const float* __restrict__ dout, float* __restrict__ dw,
+    float* __restrict__ partial) {
+  extern __shared__ float stage[];  // kMsgRows x Fi source rows, kMsgRows x Fo, kMsgRows norms
+  const int64_t it = block_linear();
+  if (it >= num_items) return;
+  int64_t r, beg, end;
+  bool single;
+  if (!item_range(it, num_rels, rel_ptr, item_ptr, item_rel, &r, &beg, &end, &single)) return;
+  const int t = threadIdx.x;
+  const int64_t wr = nb * si * so, Fi = nb * si, Fo = nb * so;
+  float* xs = stage;
+  float* gs = stage + kMsgRows * Fi;
+  float* ns = gs + kMsgRows * Fo;
+  int xo[QW], go[QW];
+  float acc[QW];
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const int64_t e = t + 256 * q;
+    const int64_t ec = e < wr ? e : 0;
+    const int64_t b = ec / (si * so), i = (ec / so) % si, j = ec % so;
+    xo[q] = static_cast<int>(b * si + i);
+    go[q] = static_cast<int>(b * so + j);
+    acc[q] = 0.0f;
+  }
+  for (int64_t k = beg; k < end; k += kMsgRows) {
+    const int64_t cnt = end - k;
+    float xv[kMsgRows][RI], gv[kMsgRows][RO];
+#pragma unroll
+    for (int p = 0; p < kMsgRows; ++p) {
+      const int64_t kk = p < cnt ? k + p : k;
+      const int64_t s = rel_src[kk], d = rel_dst[kk];
+#pragma unroll
+      for (int ri = 0; ri < RI; ++ri) {
+        const int64_t f = t + 256 * ri;
+        xv[p][ri] = f < Fi ? ufeat[s * Fi + f] : 0.0f;
+      }
+#pragma unroll
+      for (int ro = 0; ro < RO; ++ro) {
+        const int64_t f = t + 256 * ro;
+        gv[p][ro] = f < Fo ? dout[d * Fo + f] : 0.0f;
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kMsgRows; ++p) {
+#pragma unroll
+      for (int ri = 0; ri < RI; ++ri) {
+        const int64_t f = t + 256 * ri;
+        if (f < Fi) xs[p * Fi + f] = xv[p][ri];
+      }
+#pragma unroll
+      for (int ro = 0; ro < RO; ++ro) {
+        const int64_t f = t + 256 * ro;
+        if (f < Fo) gs[p * Fo + f] = gv[p][ro];
+      }
+    }
+    // the batch's norms staged too (read per position below, not one global
+    // round trip each)
+    if (t < kMsgRows) ns[t] = rel_norm && t < cnt ? rel_norm[k + t] : 1.0f;
+    __syncthreads();
+    // one position at a time: its 2 * QW LDS reads (unrolled over positions
+    // the compiler hoists all of them, 256 VGPRs at QW = 12)
+    const int pc = cnt < kMsgRows ? static_cast<int>(cnt) : kMsgRows;
+#pragma unroll 1
+    for (int p = 0; p < pc; ++p) {
+      {
+        const float nrm = ns[p];
+#pragma unroll
+        for (int q = 0; q < QW; ++q) {
+          const float x = xs[p * Fi + xo[q]];
+          acc[q] = __builtin_fmaf(rel_norm ? nrm * x : x, gs[p * Fo + go[q]], acc[q]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* dst = single ? dw + r * wr : partial + it * wr;
+#pragma unroll
+  for (int q = 0; q < QW; ++q) {
+    const int64_t e = t + 256 * q;
+    if (e < wr) dst[e] = acc[q];
+  }
+}
+
+// 0: the one-kernel forms above; 1 (default): messages + sum, and the
+// LDS-staged dW (DGLHIP_TYPED_MESSAGES; dglhip_set_typed_block_messages).
+// configs[4] step, r06: forward 0.116 -> 0.078 ms, dH 0.122 -> 0.079, dW
+// 0.110 -> 0.063 per layer (gpurun_out rgcn_leg0/1).
+int g_typed_msg = -1;
+
+int typed_msg_level() {
+  if (g_typed_msg < 0) {
+    const char* s = std::getenv("DGLHIP_TYPED_MESSAGES");
+    g_typed_msg = s && *s ? std::atoi(s) : 1;
+  }
+  return g_typed_msg;
+}
+
+int round_up_q(int64_t n) {  // 1, 2, 4, 8, 12 or 16 (0: too wide)
+  if (n <= 1) return 1;
+  if (n <= 2) return 2;
+  if (n <= 4) return 4;
+  if (n <= 8) return 8;
+  if (n <= 12) return 12;
+  if (n <= 16) return 16;
+  return 0;
 }
 
 // DistMult decoder (R-GCN link prediction, the reference's calc_score:
@@ -481,6 +749,102 @@ int dglhip_typed_block_spmm_device(int64_t num_rows, int64_t num_items, int64_t 
   API_END();
 }
 
+int dglhip_typed_block_msg_ok(int64_t num_blocks, int64_t in_block, int64_t out_block) {
+  const bool known = in_block == 1 || in_block == 2 || in_block == 4 || in_block == 5 ||
+                     in_block == 8 || in_block == 16;
+  return typed_msg_level() >= 1 && known && num_blocks > 0 && out_block > 0 &&
+                 num_blocks * in_block <= 1024 && num_blocks * out_block <= 1024
+             ? 1
+             : 0;
+}
+
+int dglhip_set_typed_block_messages(int on) {
+  g_typed_msg = on ? 1 : 0;
+  return 0;
+}
+
+int dglhip_typed_block_msg_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
+                                  int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
+                                  const int64_t* item_ptr, const int32_t* item_rel,
+                                  const int32_t* pos_row, const int64_t* pos_slot,
+                                  const float* ufeat, const float* weight, float* msg,
+                                  void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rels >= 0 && num_items >= 0 && num_blocks > 0 && in_block > 0 &&
+                   out_block > 0, "bad sizes");
+  const int64_t Fi = num_blocks * in_block, Fo = num_blocks * out_block;
+  DGLHIP_CHECK(Fi <= 1024 && Fo <= 1024, "message rows of " << Fi << " -> " << Fo
+                                                             << " features: at most 1024");
+  if (num_rels == 0 || num_items == 0) return 0;
+  DGLHIP_CHECK(rel_ptr && item_ptr && item_rel && pos_row && pos_slot && ufeat && weight && msg,
+               "null pointer argument");
+  DGLHIP_CHECK(num_items <= 0x7fffffff, "grid too large");
+  const int Q = (Fi > 512 || Fo > 512) ? 4 : 2;
+  const size_t lds = size_t(kMsgRows) * size_t(Fi) * sizeof(float);
+#define DGLHIP_MSG(S, QQ)                                                                     \
+  hipLaunchKernelGGL((typed_block_msg_kernel<S, QQ, QQ>), grid_1d(num_items), dim3(256), lds, \
+                     stream, num_items, num_rels, num_blocks, out_block, rel_ptr, item_ptr,   \
+                     item_rel, pos_row, pos_slot, ufeat, weight, msg)
+#define DGLHIP_MSGQ(S)                 \
+  if (Q == 4) DGLHIP_MSG(S, 4);        \
+  else DGLHIP_MSG(S, 2);
+  timed_launch(stream, [&] {
+    switch (in_block) {
+      case 1: DGLHIP_MSGQ(1); break;
+      case 2: DGLHIP_MSGQ(2); break;
+      case 4: DGLHIP_MSGQ(4); break;
+      case 5: DGLHIP_MSGQ(5); break;
+      case 8: DGLHIP_MSGQ(8); break;
+      case 16: DGLHIP_MSGQ(16); break;
+      default: DGLHIP_CHECK(false, "message kernel for block width " << in_block);
+    }
+  });
+#undef DGLHIP_MSGQ
+#undef DGLHIP_MSG
+  API_END();
+}
+
+int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t feat_len,
+                                const int64_t* indptr, const int64_t* item_ptr,
+                                const int32_t* item_row, int64_t num_heavy,
+                                const int32_t* heavy_row, const int64_t* slot_map,
+                                const float* slot_norm, const float* msg, float* out,
+                                float* partial, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && num_items >= 0 && num_heavy >= 0 && feat_len > 0, "bad sizes");
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(indptr && item_ptr && item_row && msg && out, "null pointer argument");
+  DGLHIP_CHECK(num_heavy == 0 || partial, "chunked rows need their partials");
+  const int64_t n64 = (feat_len + 63) / 64;
+  const int T = n64 >= 8 ? 8 : (n64 >= 4 ? 4 : (n64 >= 2 ? 2 : 1));
+  const int64_t npass = (feat_len + 64 * T - 1) / (64 * T);
+  const int64_t waves = num_items * npass;
+  DGLHIP_CHECK((waves + 3) / 4 <= 0x7fffffff, "grid too large");
+#define DGLHIP_MS(TT)                                                                           \
+  hipLaunchKernelGGL((typed_msg_sum_kernel<TT>), grid_1d((waves + 3) / 4), dim3(256), 0, stream, \
+                     num_items, num_rows, npass, feat_len, indptr, item_ptr, item_row, slot_map,  \
+                     slot_norm, msg, out, partial)
+  timed_launch(stream, [&] {
+    switch (T) {
+      case 8: DGLHIP_MS(8); break;
+      case 4: DGLHIP_MS(4); break;
+      case 2: DGLHIP_MS(2); break;
+      default: DGLHIP_MS(1); break;
+    }
+  });
+#undef DGLHIP_MS
+  if (num_heavy > 0) {
+    const int64_t total = num_heavy * feat_len;
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                         stream, num_heavy, feat_len, heavy_row, item_ptr, partial, out);
+    });
+  }
+  API_END();
+}
+
 int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
                                     int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
                                     const int64_t* item_ptr, const int32_t* item_rel,
@@ -499,12 +863,40 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
   DGLHIP_CHECK(num_heavy == 0 || partial, "chunked relations need their partials");
   const int64_t total = num_items * wr;
   DGLHIP_CHECK((total + 255) / 256 <= 0x7fffffff, "grid too large");
-  timed_launch(stream, [&] {
-    hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
-                       stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr,
-                       item_ptr,
-                       item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight, partial);
-  });
+  const int64_t Fi = num_blocks * in_block, Fo = num_blocks * out_block;
+  const int qw = round_up_q((wr + 255) / 256);
+  if (typed_msg_level() >= 1 && qw > 0 && Fi <= 1024 && Fo <= 1024 && rel_src && rel_dst) {
+    // staged rows (r06): one workgroup per item
+    const int R = (Fi > 512 || Fo > 512) ? 4 : 2;
+    const size_t lds = size_t(kMsgRows) * size_t(Fi + Fo + 1) * sizeof(float);
+#define DGLHIP_WG(QQ, RR)                                                                        \
+  hipLaunchKernelGGL((typed_block_wgrad_lds_kernel<QQ, RR, RR>), grid_1d(num_items), dim3(256),   \
+                     lds, stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr, \
+                     item_ptr, item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight,       \
+                     partial)
+#define DGLHIP_WGR(QQ)             \
+  if (R == 4) DGLHIP_WG(QQ, 4);    \
+  else DGLHIP_WG(QQ, 2);
+    timed_launch(stream, [&] {
+      switch (qw) {
+        case 1: DGLHIP_WGR(1); break;
+        case 2: DGLHIP_WGR(2); break;
+        case 4: DGLHIP_WGR(4); break;
+        case 8: DGLHIP_WGR(8); break;
+        case 12: DGLHIP_WGR(12); break;
+        default: DGLHIP_WGR(16); break;
+      }
+    });
+#undef DGLHIP_WGR
+#undef DGLHIP_WG
+  } else {
+    timed_launch(stream, [&] {
+      hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                         stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr,
+                         item_ptr, item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight,
+                         partial);
+    });
+  }
   if (num_heavy > 0) {
     const int64_t t2 = num_heavy * wr;
     timed_launch(stream, [&] {

@@ -97,6 +97,11 @@ def _load():
         "dglhip_typed_block_wgrad_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
                                             [_vp] * 9),
         "dglhip_typed_block_wgrad_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),
+        "dglhip_typed_block_msg_ok": (_c_int, [_c_i64] * 3),
+        "dglhip_set_typed_block_messages": (_c_int, [_c_int]),
+        "dglhip_typed_block_msg_device": (_c_int, [_c_i64] * 5 + [_vp] * 9),
+        "dglhip_typed_msg_sum_device": (_c_int, [_c_i64] * 3 + [_vp] * 3 + [_c_i64] +
+                                        [_vp] * 7),
         "dglhip_gsddmm_attention_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                     ctypes.c_float, ctypes.c_float,
                                                     ctypes.c_float, _c_int, _vp, _vp]),

@@ -1053,7 +1053,8 @@ def _fwd_slot_of_bwd(adj):
     m = getattr(adj, "_bwd_fslot", None)
     if m is None:
         fwd, bwd = adj.fwd, adj.bwd
-        if fwd.slot_eid is None:  # forward slots already run in edge-id order
+        # (the identity check is a host sync: used only when already made)
+        if fwd._slot_eid is None:  # forward slots known to run in edge-id order
             m = bwd.eid
         else:
             inv = torch.empty_like(fwd.eid)
@@ -1697,6 +1698,51 @@ def _run_typed_block(csr, ufeat2, weight, slot_rel, slot_norm, nb, si, so):
     return out
 
 
+def set_typed_block_messages(on):
+    """The typed-block g-SpMM as relation-major messages + a slot-order sum,
+    and its weight gradient with LDS-staged rows (csrc/typed_block.hip, r06),
+    instead of the one-kernel forms; the same bits."""
+    check_call(LIB.dglhip_set_typed_block_messages(1 if on else 0))
+
+
+def _typed_msg_ok(nb, si, so):
+    return LIB.dglhip_typed_block_msg_ok(nb, si, so) == 1
+
+
+def _relation_groups(adj, etype, num_rels):
+    g = getattr(adj, "_rel_groups", None)
+    if g is None or not g.matches(etype):
+        g = adj._rel_groups = _RelationGroups(adj.fwd, etype, num_rels)
+    return g
+
+
+def _run_typed_msg(csr, slot_map, groups, pos_row, ufeat2, weight, slot_norm, nb, si, so):
+    """out = the typed-block g-SpMM over ``csr`` in two launches: every edge's
+    message (blockdiag(weight[r]) applied to ufeat2[pos_row]) stored at its
+    forward slot, walked relation-major; then each row's sum over its slots,
+    reading message ``slot_map[k]`` (None: k) for slot k."""
+    dev = ufeat2.device
+    Fo = nb * so
+    R = groups.ptr.numel() - 1
+    msg = torch.empty(max(csr.nnz, 1), Fo, dtype=torch.float32, device=dev)
+    g_ptr, g_rel = groups.items
+    stream = _stream_of(dev)
+    check_call(LIB.dglhip_typed_block_msg_device(
+        R, g_rel.numel(), nb, si, so, ptr(groups.ptr), ptr(g_ptr), ptr(g_rel), ptr(pos_row),
+        ptr(groups.slot), ptr(ufeat2), ptr(weight), ptr(msg), stream))
+    items = csr._plans.get("typed_items")
+    if items is None:
+        items = csr._plans["typed_items"] = _typed_items(csr.indptr, csr.nnz)
+    item_ptr, item_row = items
+    out = torch.empty(csr.num_rows, Fo, dtype=torch.float32, device=dev)
+    part = torch.empty(item_row.numel(), Fo, dtype=torch.float32, device=dev)
+    check_call(LIB.dglhip_typed_msg_sum_device(
+        csr.num_rows, item_row.numel(), Fo, ptr(csr.indptr), ptr(item_ptr), ptr(item_row),
+        csr.num_rows, None, ptr(slot_map), ptr(slot_norm), ptr(msg), ptr(out), ptr(part),
+        stream))
+    return out
+
+
 def _slot_values(csr, etype, enorm):
     """The per-edge relation (int32) and norm in ``csr``'s slot order."""
     rel = etype.index_select(0, csr.eid).to(torch.int32)
@@ -1735,8 +1781,13 @@ class _TypedBlock(torch.autograd.Function):
     @staticmethod
     def forward(ctx, adj, etype, num_rels, ufeat2, weight, enorm):
         R, nb, si, so = weight.shape
-        rel, nrm = _slot_values(adj.fwd, etype, enorm)
-        out = _run_typed_block(adj.fwd, ufeat2, weight, rel, nrm, nb, si, so)
+        if ufeat2.is_cuda and _typed_msg_ok(nb, si, so):
+            g = _relation_groups(adj, etype, R)
+            nrm = None if enorm is None else enorm.index_select(0, adj.fwd.eid)
+            out = _run_typed_msg(adj.fwd, None, g, g.src, ufeat2, weight, nrm, nb, si, so)
+        else:
+            rel, nrm = _slot_values(adj.fwd, etype, enorm)
+            out = _run_typed_block(adj.fwd, ufeat2, weight, rel, nrm, nb, si, so)
         ctx.adj, ctx.num_rels = adj, num_rels
         ctx.save_for_backward(etype, ufeat2, weight, enorm)
         return out
@@ -1750,12 +1801,18 @@ class _TypedBlock(torch.autograd.Function):
         du = dw = None
         if ctx.needs_input_grad[3]:
             wt = weight.transpose(2, 3).contiguous()  # (R, nb, so, si)
-            rel, nrm = _slot_values(adj.bwd, etype, enorm)
-            du = _run_typed_block(adj.bwd, dout, wt, rel, nrm, nb, so, si)
+            if dout.is_cuda and _typed_msg_ok(nb, so, si):
+                # messages Wt[r] dout[dst] at the forward slots, read along the
+                # transpose
+                g = _relation_groups(adj, etype, R)
+                nrm = None if enorm is None else enorm.index_select(0, adj.bwd.eid)
+                du = _run_typed_msg(adj.bwd, _fwd_slot_of_bwd(adj), g, g.dst, dout, wt, nrm,
+                                    nb, so, si)
+            else:
+                rel, nrm = _slot_values(adj.bwd, etype, enorm)
+                du = _run_typed_block(adj.bwd, dout, wt, rel, nrm, nb, so, si)
         if ctx.needs_input_grad[4]:
-            g = getattr(adj, "_rel_groups", None)
-            if g is None or not g.matches(etype):
-                g = adj._rel_groups = _RelationGroups(adj.fwd, etype, R)
+            g = _relation_groups(adj, etype, R)
             fwd_nrm = None if enorm is None else enorm.index_select(0, adj.fwd.eid)
             nrm = None if fwd_nrm is None else fwd_nrm.index_select(0, g.slot)
             dw = torch.empty_like(weight)

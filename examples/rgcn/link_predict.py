@@ -137,8 +137,22 @@ class LinkPredict(nn.Module):
         return F.binary_cross_entropy_with_logits(score, labels) + self.reg * reg
 
 
+def select_blas(name):
+    """The dense products' BLAS library on ROCm ("rocblas" or "hipblaslt";
+    returns the previous one). The step's Linear GEMMs are small (11,816 x
+    500 x 500) and the step is host-bound: rocBLAS enqueues one in ≈7 µs
+    against hipBLASLt's ≈18 (profiles/r05/host_costs.txt), 0.3 ms per step
+    here (tools/rgcn_host_study.py, r06)."""
+    old = torch.backends.cuda.preferred_blas_library()
+    torch.backends.cuda.preferred_blas_library({"rocblas": "cublas",
+                                                "hipblaslt": "cublaslt"}[name])
+    return "rocblas" if old == torch._C._BlasBackend.Cublas else "hipblaslt"
+
+
 def run(args):
     device = torch.device("cpu") if args.gpu < 0 else torch.device("cuda", args.gpu)
+    if device.type == "cuda":
+        select_blas(args.blas)
     triplets = synthetic_kg(args.num_entities, args.num_rels, args.num_triples, args.seed)
     rng = np.random.default_rng(args.seed)
     torch.manual_seed(args.seed)
@@ -189,6 +203,8 @@ def parser():
     p.add_argument("--num-rels", type=int, default=237)
     p.add_argument("--num-triples", type=int, default=272115)
     p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--blas", choices=["rocblas", "hipblaslt"], default="rocblas",
+                   help="BLAS library of the dense products (select_blas)")
     return p
 
 

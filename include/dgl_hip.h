@@ -925,6 +925,35 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
                                   const int32_t* rel_dst, const float* rel_norm,
                                   const float* ufeat, const float* dout, float* dweight,
                                   int num_threads);
+/* The typed-block g-SpMM in two launches (r06), the same bits as
+ * dglhip_typed_block_spmm_device:
+ *   messages: msg[pos_slot[p] * Fo + b*so + j] = fma chain over i of
+ *     ufeat[pos_row[p], b*si + i] * weight[r, b, i, j] (from 0), for every
+ *     position p of the relation-major grouping (rel_ptr[R+1], chunked as
+ *     items item_ptr / item_rel; pos_row = each position's operand row,
+ *     pos_slot = the forward-CSR slot its message goes to; Fi, Fo <= 1024,
+ *     in_block 1, 2, 4, 5, 8 or 16);
+ *   sum: out[row] = fma(slot_norm[k], msg[slot_map[k]], acc) over the CSR
+ *     row's slots k in order (slot_map NULL: the slot itself; slot_norm NULL:
+ *     1), rows of several items combined as in the one-kernel form.
+ * dglhip_typed_block_msg_ok: 1 when the message path is on (the default;
+ * dglhip_set_typed_block_messages / env DGLHIP_TYPED_MESSAGES) and takes
+ * these widths. The same switch moves dglhip_typed_block_wgrad_device to its
+ * LDS-staged form (same bits). */
+int dglhip_typed_block_msg_ok(int64_t num_blocks, int64_t in_block, int64_t out_block);
+int dglhip_set_typed_block_messages(int on);
+int dglhip_typed_block_msg_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
+                                  int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
+                                  const int64_t* item_ptr, const int32_t* item_rel,
+                                  const int32_t* pos_row, const int64_t* pos_slot,
+                                  const float* ufeat, const float* weight, float* msg,
+                                  void* stream);
+int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t feat_len,
+                                const int64_t* indptr, const int64_t* item_ptr,
+                                const int32_t* item_row, int64_t num_heavy,
+                                const int32_t* heavy_row, const int64_t* slot_map,
+                                const float* slot_norm, const float* msg, float* out,
+                                float* partial, void* stream);
 
 /* The typed-block entries' item list from a CSR-like ptr[num_rows+1]: item_ptr
  * [num_rows+1] (row r has max(1, ceil(deg / DGLHIP_TYPED_CHUNK)) items) and

@@ -92,10 +92,13 @@ def test_typed_block_device_matches_host_bits(shape):
     assert int(torch.bincount(etype).min()) > kernel.TYPED_CHUNK
     for nm in (norm, None):
         outs, grads, wgrads = [], [], []
-        # the host, then the device at 8 output slices per wave and at 1
-        # (the default)
-        for dev, width in (("cpu", 8), ("cuda", 8), ("cuda", 1)):
+        # the host, then the device's one-kernel forms at 8 output slices per
+        # wave and at 1, then the relation-major messages + slot-order sum and
+        # the LDS-staged weight gradient (r06; block widths outside the
+        # message kernel's set fall back per direction)
+        for dev, width, msgs in (("cpu", 8, 0), ("cuda", 8, 0), ("cuda", 1, 0), ("cuda", 1, 1)):
             kernel.set_typed_block_width(width)
+            kernel.set_typed_block_messages(msgs)
             try:
                 adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
                 h1 = h.detach().to(dev).clone().requires_grad_(True)
@@ -105,13 +108,29 @@ def test_typed_block_device_matches_host_bits(shape):
                 out.backward(G.to(dev))
             finally:
                 kernel.set_typed_block_width(1)
+                kernel.set_typed_block_messages(_MSG_DEFAULT)
             outs.append(out.detach().cpu())
             grads.append(h1.grad.cpu())
             wgrads.append(W1.grad.cpu())
-        for k in (1, 2):
+        for k in (1, 2, 3):
             assert torch.equal(outs[0], outs[k])
             assert torch.equal(grads[0], grads[k])
             assert torch.equal(wgrads[0], wgrads[k])
+
+
+_MSG_DEFAULT = 1
+
+
+def test_typed_block_messages_take_rgcn_widths():
+    """The message path covers configs[4]'s 100 blocks of 5 x 5 both ways
+    (and rejects widths its kernels are not built for)."""
+    kernel.set_typed_block_messages(1)
+    try:
+        assert kernel._typed_msg_ok(100, 5, 5)
+        assert not kernel._typed_msg_ok(3, 7, 9)
+        assert not kernel._typed_msg_ok(300, 5, 5)  # rows past 1024 features
+    finally:
+        kernel.set_typed_block_messages(_MSG_DEFAULT)
 
 
 def _example():

@@ -1,4 +1,4 @@
-"""The GCN's dense products at configs[1]'s shapes on each BLAS backend torch
+"""The GCN's dense products at configs[1]'s shapes (and R-GCN's 11,816 x 500 x 500) on each BLAS backend torch
 offers on ROCm (hipBLASLt, rocBLAS): forward X·W (232,965 x 602 x 128), the
 weight gradient Xᵀ·dA, and layer 2's (x 128 x 41) pair; ms per call by
 events.
@@ -22,6 +22,19 @@ def ms(fn, iters=20):
     return s.elapsed_time(e) / iters
 
 
+def host_us(fn, iters=200):
+    """Host time per call while the GPU keeps up (enqueue only)."""
+    import time
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    t = (time.perf_counter() - t0) / iters * 1e6
+    torch.cuda.synchronize()
+    return t
+
+
 def main():
     dev = torch.device("cuda", 0)
     n = 232965
@@ -32,6 +45,9 @@ def main():
     h1 = torch.randn(n, 128, generator=g, device=dev)
     w2 = torch.randn(128, 41, generator=g, device=dev)
     da2 = torch.randn(n, 41, generator=g, device=dev)
+    hr = torch.randn(11816, 500, generator=g, device=dev)
+    wr = torch.randn(500, 500, generator=g, device=dev)
+    sm = torch.randn(64, 64, generator=g, device=dev)
     res = {}
     for lib in ("cublaslt", "cublas"):
         try:
@@ -43,7 +59,11 @@ def main():
              "dw1 x^T@da1": ms(lambda: torch.mm(x.t(), da1)),
              "fwd2 h1@w2": ms(lambda: torch.mm(h1, w2)),
              "dw2 h1^T@da2": ms(lambda: torch.mm(h1.t(), da2)),
-             "dh1 da2@w2^T": ms(lambda: torch.mm(da2, w2.t()))}
+             "dh1 da2@w2^T": ms(lambda: torch.mm(da2, w2.t())),
+             "rgcn h@W (11816x500x500)": ms(lambda: torch.mm(hr, wr)),
+             "rgcn h^T@d": ms(lambda: torch.mm(hr.t(), hr)),
+             "host_us rgcn h@W": host_us(lambda: torch.mm(hr, wr)),
+             "host_us small 64x64": host_us(lambda: torch.mm(sm, sm))}
         res[lib] = r
     print(json.dumps(res, indent=1))
 

@@ -161,6 +161,8 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     kernel.set_typed_block_width(args.typed_width)
+    if dev.type == "cuda":
+        lp.select_blas(args.blas)
     sync = torch.cuda.synchronize if dev.type == "cuda" else (lambda: None)
     raw = make_samples(args, args.warmup + args.steps)
     samples = [to_dev(s, dev) for s in raw]
