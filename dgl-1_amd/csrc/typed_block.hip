@@ -197,10 +197,12 @@ __global__ __launch_bounds__(256) void typed_block_spmm_kernel(
 // out[row] = ((p0 + p1) + p2) ... over the row's items in order, for the
 // rows (or relations) of several items: one thread per (row, element).
 // heavy_row NULL: every row, those of one item skipped.
+// row_scale (optional): out[row] = that sum * row_scale[row] (the R-GCN
+// layer's 1 / in-degree, one rounding as `agg * norm` has it)
 __global__ __launch_bounds__(256) void typed_block_combine_kernel(
     int64_t num_heavy, int64_t F, const int32_t* __restrict__ heavy_row,
     const int64_t* __restrict__ item_ptr, const float* __restrict__ partial,
-    float* __restrict__ out) {
+    float* __restrict__ out, const float* __restrict__ row_scale = nullptr) {
   const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
   if (idx >= num_heavy * F) return;
   const int64_t h = idx / F, f = idx - h * F;
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(256) void typed_block_combine_kernel(
   if (i1 - i0 <= 1) return;
   float s = partial[i0 * F + f];
   for (int64_t i = i0 + 1; i < i1; ++i) s = s + partial[i * F + f];
-  out[r * F + f] = s;
+  out[r * F + f] = row_scale ? s * row_scale[r] : s;
 }
 
 // dW[r, b, i, j] over item `it` (a chunk of relation r's edges, relation-major
@@ -277,7 +279,8 @@ __global__ __launch_bounds__(256) void typed_block_msg_kernel(
     const int64_t* __restrict__ rel_ptr, const int64_t* __restrict__ item_ptr,
     const int32_t* __restrict__ item_rel, const int32_t* __restrict__ pos_row,
     const int64_t* __restrict__ pos_slot, const float* __restrict__ ufeat,
-    const float* __restrict__ weight, float* __restrict__ msg) {
+    const float* __restrict__ row_scale, const float* __restrict__ weight, int wtrans,
+    float* __restrict__ msg) {
   extern __shared__ float rows[];  // kMsgRows x Fi
   const int64_t it = block_linear();
   if (it >= num_items) return;  // the whole workgroup
@@ -296,7 +299,8 @@ __global__ __launch_bounds__(256) void typed_block_msg_kernel(
     const int64_t b = act[q] ? j / so : 0, jj = act[q] ? j - b * so : 0;
     xo[q] = static_cast<int>(b * SI);
 #pragma unroll
-    for (int i = 0; i < SI; ++i) w[q][i] = weight[r * wr + b * SI * so + i * so + jj];
+    for (int i = 0; i < SI; ++i)  // wtrans: weight is (R, nb, so, SI), read as its transpose
+      w[q][i] = weight[r * wr + b * SI * so + (wtrans ? jj * SI + i : i * so + jj)];
   }
   for (int64_t k = beg; k < end; k += kMsgRows) {
     const int64_t cnt = end - k;  // uniform
@@ -304,10 +308,14 @@ __global__ __launch_bounds__(256) void typed_block_msg_kernel(
 #pragma unroll
     for (int p = 0; p < kMsgRows; ++p) {
       const int64_t row = pos_row[p < cnt ? k + p : k];  // idle p re-read a valid row
+      // a scaled operand row (the backward's dout * norm[dst]) as torch's
+      // product rounds it
+      const float sc = row_scale ? row_scale[row] : 1.0f;
 #pragma unroll
       for (int ri = 0; ri < RI; ++ri) {
         const int64_t f = t + 256 * ri;
-        v[p][ri] = f < Fi ? ufeat[row * Fi + f] : 0.0f;
+        const float x = f < Fi ? ufeat[row * Fi + f] : 0.0f;
+        v[p][ri] = row_scale ? x * sc : x;
       }
     }
 #pragma unroll
@@ -345,7 +353,8 @@ __global__ __launch_bounds__(256) void typed_msg_sum_kernel(
     const int64_t* __restrict__ indptr, const int64_t* __restrict__ item_ptr,
     const int32_t* __restrict__ item_row, const int64_t* __restrict__ slot_map,
     const float* __restrict__ slot_norm, const float* __restrict__ msg,
-    float* __restrict__ out, float* __restrict__ partial) {
+    const float* __restrict__ row_scale, float* __restrict__ out,
+    float* __restrict__ partial) {
   constexpr int G = T >= 4 ? 4 : 8;
   const int64_t wave = block_linear() * (blockDim.x >> 6) +
                        __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x >> 6));
@@ -393,10 +402,11 @@ __global__ __launch_bounds__(256) void typed_msg_sum_kernel(
     batch(k, std::integral_constant<int, G>());
   }
   float* dst = single ? out + row * Fo : partial + it * Fo;
+  const float sc = row_scale && single ? row_scale[row] : 1.0f;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int64_t f = f0 + 64 * t;
-    if (f < Fo) dst[f] = acc[t];
+    if (f < Fo) dst[f] = row_scale && single ? acc[t] * sc : acc[t];
   }
 }
 
@@ -411,7 +421,8 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_lds_kernel(
     const int64_t* __restrict__ rel_ptr, const int64_t* __restrict__ item_ptr,
     const int32_t* __restrict__ item_rel, const int32_t* __restrict__ rel_src,
     const int32_t* __restrict__ rel_dst, const float* __restrict__ rel_norm,
-    const float* __restrict__ ufeat, const float* __restrict__ dout, float* __restrict__ dw,
+    const float* __restrict__ ufeat, const float* __restrict__ dout,
+    const float* __restrict__ dout_scale, float* __restrict__ dw,
     float* __restrict__ partial) {
   extern __shared__ float stage[];  // kMsgRows x Fi source rows, kMsgRows x Fo, kMsgRows norms
   const int64_t it = block_linear();
@@ -447,10 +458,12 @@ __global__ __launch_bounds__(256) void typed_block_wgrad_lds_kernel(
         const int64_t f = t + 256 * ri;
         xv[p][ri] = f < Fi ? ufeat[s * Fi + f] : 0.0f;
       }
+      const float dsc = dout_scale ? dout_scale[d] : 1.0f;
 #pragma unroll
       for (int ro = 0; ro < RO; ++ro) {
         const int64_t f = t + 256 * ro;
-        gv[p][ro] = f < Fo ? dout[d * Fo + f] : 0.0f;
+        const float g = f < Fo ? dout[d * Fo + f] : 0.0f;
+        gv[p][ro] = dout_scale ? g * dsc : g;
       }
     }
 #pragma unroll
@@ -563,6 +576,25 @@ __global__ __launch_bounds__(256) void distmult_score_kernel(
 // item; the batches then only gather rows, at row bases read from lane q
 // (wave-uniform), G positions in flight.
 static_assert(kChunk == 64, "one position per lane");
+
+// The fused loss's gradient inputs (all null / 0: ds given): ds_i =
+// (sigmoid(score_i) - label_i) * (g * inv_n), the BCE-with-logits mean's
+// gradient, and the regulariser's term reg_coef * g * base[row] added to
+// every output row (base = h for dh, w for dw).
+constexpr int64_t kLossChunks = 512;  // blocks summing h^2 (and w^2) in the fused loss
+
+struct LossGrad {
+  const float* score;
+  const float* labels;
+  const float* g;
+  float inv_n;
+  float reg_coef;
+  __device__ __forceinline__ float dscore(int64_t i) const {
+    const float x = score[i];
+    return (1.0f / (1.0f + expf(-x)) - labels[i]) * (g[0] * inv_n);
+  }
+  __device__ __forceinline__ float reg_scale() const { return g ? g[0] * reg_coef : 0.0f; }
+};
 template <int T>
 __global__ __launch_bounds__(256) void distmult_grad_kernel(
     int task, int64_t num_items, int64_t num_rows, int64_t npass, int64_t F, int64_t n,
@@ -571,7 +603,7 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
     const int32_t* __restrict__ order, const int64_t* __restrict__ s,
     const int64_t* __restrict__ r, const int64_t* __restrict__ o,
     const float* __restrict__ ds, const float* __restrict__ h, const float* __restrict__ w,
-    float* __restrict__ out, float* __restrict__ partial) {
+    float* __restrict__ out, float* __restrict__ partial, const LossGrad lg) {
 #pragma clang fp contract(off)
   constexpr int G = 4;
   const int64_t wave = block_linear() * 4 +
@@ -600,7 +632,7 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
     const int64_t si = inside ? s[i] : -1, ri = inside ? r[i] : -1, oi = inside ? o[i] : -1;
     const bool ok = inside && si >= 0 && si < num_nodes && oi >= 0 && oi < num_nodes &&
                     ri >= 0 && ri < num_rels;
-    dq = ok ? ds[i] : __builtin_nanf("");
+    dq = ok ? (lg.labels ? lg.dscore(i) : ds[i]) : __builtin_nanf("");
     objq = obj ? 1 : 0;
     xoff = ok ? (obj ? si : oi) * F : 0;
     yoff = ok ? (task == 1 ? si * F : ri * F) : 0;
@@ -637,11 +669,117 @@ __global__ __launch_bounds__(256) void distmult_grad_kernel(
     }
   }
   float* dst = single ? out + row * F : partial + it * F;
+  // the regulariser's term on rows of one item (chunked rows: at the combine)
+  const float rc = single ? lg.reg_scale() : 0.0f;
+  const float* base = task == 0 ? h : w;
 #pragma unroll
   for (int t = 0; t < T; ++t) {
     const int64_t f = f0 + 64 * t;
-    if (f < F) dst[f] = acc[t];
+    if (f < F) dst[f] = lg.reg_coef != 0.0f && single ? acc[t] + rc * base[row * F + f] : acc[t];
   }
+}
+
+// out[row] = ((p0 + p1) + ...) over the row's items, + the regulariser's term
+// (DistMult loss gradient, rows of several items)
+__global__ __launch_bounds__(256) void distmult_combine_kernel(
+    int64_t num_rows, int64_t F, const int64_t* __restrict__ item_ptr,
+    const float* __restrict__ partial, const float* __restrict__ base, const LossGrad lg,
+    float* __restrict__ out) {
+  const int64_t idx = block_linear() * blockDim.x + threadIdx.x;
+  if (idx >= num_rows * F) return;
+  const int64_t r = idx / F, f = idx - r * F;
+  const int64_t i0 = item_ptr[r], i1 = item_ptr[r + 1];
+  if (i1 - i0 <= 1) return;
+  float s = partial[i0 * F + f];
+  for (int64_t i = i0 + 1; i < i1; ++i) s = s + partial[i * F + f];
+  out[r * F + f] = lg.reg_coef != 0.0f ? s + lg.reg_scale() * base[r * F + f] : s;
+}
+
+// The link-prediction loss of the R-GCN example in two launches
+// (examples/pytorch/rgcn/link_predict.py get_loss: BCE-with-logits of the
+// DistMult scores, mean over the samples, + reg * (mean(h^2) + mean(w^2))):
+// partials — blocks [0, nb_s): 4 samples each, a wave per sample scoring it
+// as distmult_score_kernel does (the same bits) and its BCE term; blocks
+// [nb_s, nb_s + nb_h): sums of h^2 over contiguous chunks; then the w^2
+// chunks — then one block adding each kind's partials in block order.
+__device__ __forceinline__ float bce_with_logits(float x, float y) {
+  // (1 - y) * x + log(1 + exp(-x)), stably: max(x, 0) - x * y + log1p(exp(-|x|))
+  return fmaxf(x, 0.0f) - x * y + log1pf(expf(-fabsf(x)));
+}
+
+__device__ __forceinline__ float block_sum_256(float v, float* red) {
+  // a fixed tree: the same order at every call
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = v + __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  const float s = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(256) void distmult_loss_partials_kernel(
+    int64_t n, int64_t F, int64_t num_nodes, int64_t num_rels, const int64_t* __restrict__ s,
+    const int64_t* __restrict__ r, const int64_t* __restrict__ o, const float* __restrict__ h,
+    const float* __restrict__ w, const float* __restrict__ labels, int64_t nb_s, int64_t nb_h,
+    int64_t nb_w, float* __restrict__ score, float* __restrict__ partial) {
+  __shared__ float red[4];
+  const int64_t b = block_linear();
+  const int lane = threadIdx.x & 63;
+  float v = 0.0f;
+  if (b < nb_s) {
+    const int64_t i = b * 4 + (threadIdx.x >> 6);
+    if (i < n) {
+      const int64_t si = s[i], ri = r[i], oi = o[i];
+      float sc;
+      if (si < 0 || si >= num_nodes || oi < 0 || oi >= num_nodes || ri < 0 || ri >= num_rels) {
+        sc = __builtin_nanf("");
+      } else {
+#pragma clang fp contract(off)
+        const float* a = h + si * F;
+        const float* bb = w + ri * F;
+        const float* c = h + oi * F;
+        float acc = 0.0f;
+        for (int64_t f = lane; f < F; f += 64) acc = acc + (a[f] * bb[f]) * c[f];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) acc = acc + __shfl_xor(acc, off, 64);
+        sc = acc;
+      }
+      if (lane == 0) {
+        score[i] = sc;
+        v = bce_with_logits(sc, labels[i]);
+      }
+    }
+  } else {
+    const bool hb = b < nb_s + nb_h;
+    const float* x = hb ? h : w;
+    const int64_t elems = hb ? num_nodes * F : num_rels * F;
+    const int64_t nbk = hb ? nb_h : nb_w, k = hb ? b - nb_s : b - nb_s - nb_h;
+    const int64_t chunk = (elems + nbk - 1) / nbk;
+    const int64_t e0 = k * chunk, e1 = e0 + chunk < elems ? e0 + chunk : elems;
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) v = __builtin_fmaf(x[e], x[e], v);
+  }
+  const float tot = block_sum_256(v, red);
+  if (threadIdx.x == 0) partial[b] = tot;
+}
+
+__global__ __launch_bounds__(256) void distmult_loss_final_kernel(
+    int64_t n, int64_t h_elems, int64_t w_elems, int64_t nb_s, int64_t nb_h, int64_t nb_w,
+    float reg, const float* __restrict__ partial, float* __restrict__ loss) {
+  __shared__ float red[4];
+  float sums[3];
+  const int64_t beg[3] = {0, nb_s, nb_s + nb_h}, cnt[3] = {nb_s, nb_h, nb_w};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float v = 0.0f;
+    for (int64_t j = threadIdx.x; j < cnt[k]; j += 256) v = v + partial[beg[k] + j];
+    sums[k] = block_sum_256(v, red);
+  }
+  if (threadIdx.x == 0)
+    loss[0] = sums[0] / float(n) +
+              reg * (sums[1] / float(h_elems > 0 ? h_elems : 1) +
+                     sums[2] / float(w_elems > 0 ? w_elems : 1));
 }
 
 // The chunked item list (kernel._typed_items): items per row, scanned by
@@ -767,7 +905,8 @@ int dglhip_typed_block_msg_device(int64_t num_rels, int64_t num_items, int64_t n
                                   int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
                                   const int64_t* item_ptr, const int32_t* item_rel,
                                   const int32_t* pos_row, const int64_t* pos_slot,
-                                  const float* ufeat, const float* weight, float* msg,
+                                  const float* ufeat, const float* row_scale,
+                                  const float* weight, int weight_transposed, float* msg,
                                   void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
@@ -785,7 +924,8 @@ int dglhip_typed_block_msg_device(int64_t num_rels, int64_t num_items, int64_t n
 #define DGLHIP_MSG(S, QQ)                                                                     \
   hipLaunchKernelGGL((typed_block_msg_kernel<S, QQ, QQ>), grid_1d(num_items), dim3(256), lds, \
                      stream, num_items, num_rels, num_blocks, out_block, rel_ptr, item_ptr,   \
-                     item_rel, pos_row, pos_slot, ufeat, weight, msg)
+                     item_rel, pos_row, pos_slot, ufeat, row_scale, weight,                  \
+                     weight_transposed, msg)
 #define DGLHIP_MSGQ(S)                 \
   if (Q == 4) DGLHIP_MSG(S, 4);        \
   else DGLHIP_MSG(S, 2);
@@ -809,8 +949,9 @@ int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t fea
                                 const int64_t* indptr, const int64_t* item_ptr,
                                 const int32_t* item_row, int64_t num_heavy,
                                 const int32_t* heavy_row, const int64_t* slot_map,
-                                const float* slot_norm, const float* msg, float* out,
-                                float* partial, void* stream_) {
+                                const float* slot_norm, const float* msg,
+                                const float* row_scale, float* out, float* partial,
+                                void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rows >= 0 && num_items >= 0 && num_heavy >= 0 && feat_len > 0, "bad sizes");
@@ -825,7 +966,7 @@ int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t fea
 #define DGLHIP_MS(TT)                                                                           \
   hipLaunchKernelGGL((typed_msg_sum_kernel<TT>), grid_1d((waves + 3) / 4), dim3(256), 0, stream, \
                      num_items, num_rows, npass, feat_len, indptr, item_ptr, item_row, slot_map,  \
-                     slot_norm, msg, out, partial)
+                     slot_norm, msg, row_scale, out, partial)
   timed_launch(stream, [&] {
     switch (T) {
       case 8: DGLHIP_MS(8); break;
@@ -839,19 +980,22 @@ int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t fea
     const int64_t total = num_heavy * feat_len;
     timed_launch(stream, [&] {
       hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
-                         stream, num_heavy, feat_len, heavy_row, item_ptr, partial, out);
+                         stream, num_heavy, feat_len, heavy_row, item_ptr, partial, out,
+                         row_scale);
     });
   }
   API_END();
 }
 
-int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
-                                    int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
-                                    const int64_t* item_ptr, const int32_t* item_rel,
-                                    int64_t num_heavy, const int32_t* heavy_rel,
-                                    const int32_t* rel_src, const int32_t* rel_dst,
-                                    const float* rel_norm, const float* ufeat, const float* dout,
-                                    float* dweight, float* partial, void* stream_) {
+int dglhip_typed_block_wgrad_scaled_device(int64_t num_rels, int64_t num_items,
+                                           int64_t num_blocks, int64_t in_block,
+                                           int64_t out_block, const int64_t* rel_ptr,
+                                           const int64_t* item_ptr, const int32_t* item_rel,
+                                           int64_t num_heavy, const int32_t* heavy_rel,
+                                           const int32_t* rel_src, const int32_t* rel_dst,
+                                           const float* rel_norm, const float* ufeat,
+                                           const float* dout, const float* dout_scale,
+                                           float* dweight, float* partial, void* stream_) {
   API_BEGIN();
   hipStream_t stream = static_cast<hipStream_t>(stream_);
   DGLHIP_CHECK(num_rels >= 0 && num_items >= 0 && num_heavy >= 0 && num_blocks >= 0 &&
@@ -872,8 +1016,8 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
 #define DGLHIP_WG(QQ, RR)                                                                        \
   hipLaunchKernelGGL((typed_block_wgrad_lds_kernel<QQ, RR, RR>), grid_1d(num_items), dim3(256),   \
                      lds, stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr, \
-                     item_ptr, item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dweight,       \
-                     partial)
+                     item_ptr, item_rel, rel_src, rel_dst, rel_norm, ufeat, dout, dout_scale,    \
+                     dweight, partial)
 #define DGLHIP_WGR(QQ)             \
   if (R == 4) DGLHIP_WG(QQ, 4);    \
   else DGLHIP_WG(QQ, 2);
@@ -890,6 +1034,7 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
 #undef DGLHIP_WGR
 #undef DGLHIP_WG
   } else {
+    DGLHIP_CHECK(dout_scale == nullptr, "a scaled dout needs the staged weight gradient");
     timed_launch(stream, [&] {
       hipLaunchKernelGGL(typed_block_wgrad_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
                          stream, num_items, num_rels, num_blocks, in_block, out_block, rel_ptr,
@@ -905,6 +1050,19 @@ int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t
     });
   }
   API_END();
+}
+
+int dglhip_typed_block_wgrad_device(int64_t num_rels, int64_t num_items, int64_t num_blocks,
+                                    int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
+                                    const int64_t* item_ptr, const int32_t* item_rel,
+                                    int64_t num_heavy, const int32_t* heavy_rel,
+                                    const int32_t* rel_src, const int32_t* rel_dst,
+                                    const float* rel_norm, const float* ufeat, const float* dout,
+                                    float* dweight, float* partial, void* stream_) {
+  return dglhip_typed_block_wgrad_scaled_device(num_rels, num_items, num_blocks, in_block,
+                                                out_block, rel_ptr, item_ptr, item_rel,
+                                                num_heavy, heavy_rel, rel_src, rel_dst, rel_norm,
+                                                ufeat, dout, nullptr, dweight, partial, stream_);
 }
 
 int64_t dglhip_typed_items_workspace_bytes(int64_t num_rows) {
@@ -977,22 +1135,27 @@ int dglhip_distmult_score_device(int64_t num_samples, int64_t feat_len, int64_t 
   API_END();
 }
 
-int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, int64_t feat_len,
-                                int64_t num_samples, int64_t num_nodes, int64_t num_rels,
-                                const int64_t* ptr, const int64_t* item_ptr,
-                                const int32_t* item_row, const int32_t* order,
-                                const int64_t* subj, const int64_t* rel, const int64_t* obj,
-                                const float* dscore, const float* h, const float* w_rel,
-                                float* out, float* partial, void* stream_) {
-  API_BEGIN();
-  hipStream_t stream = static_cast<hipStream_t>(stream_);
+}  // extern "C"
+
+namespace dglhip {
+namespace {
+
+int distmult_grad_launch(int task, int64_t num_rows, int64_t num_items, int64_t feat_len,
+                         int64_t num_samples, int64_t num_nodes, int64_t num_rels,
+                         const int64_t* ptr, const int64_t* item_ptr, const int32_t* item_row,
+                         const int32_t* order, const int64_t* subj, const int64_t* rel,
+                         const int64_t* obj, const float* dscore, const LossGrad& lg,
+                         const float* h, const float* w_rel, float* out, float* partial,
+                         hipStream_t stream) {
   DGLHIP_CHECK(task == 0 || task == 1, "unknown DistMult gradient task " << task);
   DGLHIP_CHECK(num_rows >= 0 && num_items >= 0 && feat_len >= 0 && num_samples >= 0,
                "bad sizes");
   if (num_rows == 0 || feat_len == 0) return 0;
   DGLHIP_CHECK(ptr && item_ptr && item_row && out && partial, "null pointer argument");
-  DGLHIP_CHECK(num_samples == 0 || (order && subj && rel && obj && dscore && h && w_rel),
+  DGLHIP_CHECK(num_samples == 0 || (order && subj && rel && obj && (dscore || lg.labels) && h &&
+                                    w_rel),
                "null pointer argument");
+  DGLHIP_CHECK(!lg.labels || (lg.score && lg.g), "loss gradient without scores or its scale");
   // features per lane: up to 8 (F = 500: one wave covers the row)
   const int64_t lanes64 = (feat_len + 63) / 64;
   const int T = lanes64 >= 8 ? 8 : (lanes64 >= 4 ? 4 : (lanes64 >= 2 ? 2 : 1));
@@ -1003,7 +1166,7 @@ int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, i
   hipLaunchKernelGGL(distmult_grad_kernel<TT>, grid_1d((waves + 3) / 4), dim3(256), 0, stream, \
                      task, num_items, num_rows, npass, feat_len, num_samples, num_nodes,      \
                      num_rels, ptr, item_ptr, item_row, order, subj, rel, obj, dscore, h,     \
-                     w_rel, out, partial)
+                     w_rel, out, partial, lg)
   timed_launch(stream, [&] {
     switch (T) {
       case 8: DGLHIP_DM(8); break;
@@ -1015,9 +1178,87 @@ int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, i
 #undef DGLHIP_DM
   const int64_t total = num_rows * feat_len;
   timed_launch(stream, [&] {
-    hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
-                       stream, num_rows, feat_len, nullptr, item_ptr, partial, out);
+    if (lg.reg_coef != 0.0f)
+      hipLaunchKernelGGL(distmult_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                         stream, num_rows, feat_len, item_ptr, partial, task == 0 ? h : w_rel,
+                         lg, out);
+    else
+      hipLaunchKernelGGL(typed_block_combine_kernel, grid_1d((total + 255) / 256), dim3(256), 0,
+                         stream, num_rows, feat_len, nullptr, item_ptr, partial, out);
   });
+  return 0;
+}
+
+}  // namespace
+}  // namespace dglhip
+
+extern "C" {
+
+int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, int64_t feat_len,
+                                int64_t num_samples, int64_t num_nodes, int64_t num_rels,
+                                const int64_t* ptr, const int64_t* item_ptr,
+                                const int32_t* item_row, const int32_t* order,
+                                const int64_t* subj, const int64_t* rel, const int64_t* obj,
+                                const float* dscore, const float* h, const float* w_rel,
+                                float* out, float* partial, void* stream_) {
+  API_BEGIN();
+  const LossGrad lg{nullptr, nullptr, nullptr, 0.0f, 0.0f};
+  distmult_grad_launch(task, num_rows, num_items, feat_len, num_samples, num_nodes, num_rels,
+                       ptr, item_ptr, item_row, order, subj, rel, obj, dscore, lg, h, w_rel, out,
+                       partial, static_cast<hipStream_t>(stream_));
+  API_END();
+}
+
+int64_t dglhip_distmult_loss_workspace_floats(int64_t num_samples, int64_t num_nodes,
+                                              int64_t num_rels, int64_t feat_len) {
+  (void)num_nodes;
+  (void)num_rels;
+  (void)feat_len;
+  return (num_samples + 3) / 4 + 2 * kLossChunks;
+}
+
+int dglhip_distmult_loss_fwd_device(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                                    int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                                    const int64_t* obj, const float* h, const float* w_rel,
+                                    const float* labels, float reg, float* score, float* loss,
+                                    float* workspace, int64_t workspace_floats, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_samples > 0 && feat_len > 0 && num_nodes > 0 && num_rels > 0, "bad sizes");
+  DGLHIP_CHECK(subj && rel && obj && h && w_rel && labels && score && loss && workspace,
+               "null pointer argument");
+  const int64_t nb_s = (num_samples + 3) / 4, nb_h = kLossChunks, nb_w = kLossChunks;
+  DGLHIP_CHECK(workspace_floats >= nb_s + nb_h + nb_w, "workspace too small");
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(distmult_loss_partials_kernel, grid_1d(nb_s + nb_h + nb_w), dim3(256), 0,
+                       stream, num_samples, feat_len, num_nodes, num_rels, subj, rel, obj, h,
+                       w_rel, labels, nb_s, nb_h, nb_w, score, workspace);
+  });
+  timed_launch(stream, [&] {
+    hipLaunchKernelGGL(distmult_loss_final_kernel, dim3(1), dim3(256), 0, stream, num_samples,
+                       num_nodes * feat_len, num_rels * feat_len, nb_s, nb_h, nb_w, reg,
+                       workspace, loss);
+  });
+  API_END();
+}
+
+int dglhip_distmult_loss_grad_device(int task, int64_t num_rows, int64_t num_items,
+                                     int64_t feat_len, int64_t num_samples, int64_t num_nodes,
+                                     int64_t num_rels, const int64_t* ptr, const int64_t* item_ptr,
+                                     const int32_t* item_row, const int32_t* order,
+                                     const int64_t* subj, const int64_t* rel, const int64_t* obj,
+                                     const float* score, const float* labels, const float* g,
+                                     float reg, const float* h, const float* w_rel, float* out,
+                                     float* partial, void* stream_) {
+  API_BEGIN();
+  DGLHIP_CHECK(score && labels && g, "null pointer argument");
+  const int64_t elems = (task == 0 ? num_nodes : num_rels) * feat_len;
+  // d/dx of reg * mean(x^2): 2 * reg / elems * x
+  const LossGrad lg{score, labels, g, 1.0f / float(num_samples > 0 ? num_samples : 1),
+                    elems > 0 ? 2.0f * reg / float(elems) : 0.0f};
+  distmult_grad_launch(task, num_rows, num_items, feat_len, num_samples, num_nodes, num_rels,
+                       ptr, item_ptr, item_row, order, subj, rel, obj, nullptr, lg, h, w_rel,
+                       out, partial, static_cast<hipStream_t>(stream_));
   API_END();
 }
 

@@ -91,17 +91,31 @@ def _load():
         "dglhip_distmult_score_host": (_c_int, [_c_i64] * 4 + [_vp] * 6 + [_c_int]),
         "dglhip_distmult_grad_device": (_c_int, [_c_int] + [_c_i64] * 6 + [_vp] * 13),
         "dglhip_distmult_grad_host": (_c_int, [_c_int] + [_c_i64] * 5 + [_vp] * 9 + [_c_int]),
+        "dglhip_distmult_loss_workspace_floats": (_c_i64, [_c_i64] * 4),
+        "dglhip_distmult_loss_fwd_device": (_c_int, [_c_i64] * 4 + [_vp] * 6 + [_c_float] +
+                                            [_vp] * 3 + [_c_i64, _vp]),
+        "dglhip_distmult_loss_grad_device": (_c_int, [_c_int] + [_c_i64] * 6 + [_vp] * 10 +
+                                             [_c_float] + [_vp] * 5),
         "dglhip_typed_block_spmm_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
                                            [_vp] * 9),
         "dglhip_typed_block_spmm_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),
         "dglhip_typed_block_wgrad_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
                                             [_vp] * 9),
         "dglhip_typed_block_wgrad_host": (_c_int, [_c_i64] * 4 + [_vp] * 7 + [_c_int]),
+        "dglhip_group_positions_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
+        "dglhip_group_positions_device": (_c_int, [_c_i64, _c_i64, _vp, _c_i64] + [_vp] * 5 +
+                                          [_c_i64, _vp]),
+        "dglhip_relation_groups_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
+        "dglhip_relation_groups_device": (_c_int, [_c_i64] * 3 + [_vp] * 4 + [_c_i64] +
+                                          [_vp] * 7 + [_c_i64, _vp]),
         "dglhip_typed_block_msg_ok": (_c_int, [_c_i64] * 3),
         "dglhip_set_typed_block_messages": (_c_int, [_c_int]),
-        "dglhip_typed_block_msg_device": (_c_int, [_c_i64] * 5 + [_vp] * 9),
+        "dglhip_typed_block_msg_device": (_c_int, [_c_i64] * 5 + [_vp] * 8 + [_c_int] +
+                                          [_vp] * 2),
         "dglhip_typed_msg_sum_device": (_c_int, [_c_i64] * 3 + [_vp] * 3 + [_c_i64] +
-                                        [_vp] * 7),
+                                        [_vp] * 8),
+        "dglhip_typed_block_wgrad_scaled_device": (_c_int, [_c_i64] * 5 + [_vp] * 3 + [_c_i64] +
+                                                   [_vp] * 10),
         "dglhip_gsddmm_attention_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _vp, _vp,
                                                     ctypes.c_float, ctypes.c_float,
                                                     ctypes.c_float, _c_int, _vp, _vp]),

@@ -594,6 +594,16 @@ def from_coo(num_rows, num_cols, row, col, order=ORDER_EID, device=None, validat
     device) recover it from the forward CSR."""
     row = torch.as_tensor(row, dtype=torch.int64)
     col = torch.as_tensor(col, dtype=torch.int64)
+    dev = torch.device(device) if device is not None else row.device
+    if (dev.type == "cuda" and row.device.type == "cpu" and col.device.type == "cpu" and
+            row.numel() == col.numel() and 2 * row.numel() * 8 <= _PINNED_UPLOAD_MAX):
+        # both endpoint arrays in one pinned copy, shared by the forward build
+        # and the transpose's (was four uploads per sampled graph, r06)
+        both = torch.empty(2, row.numel(), dtype=torch.int64, pin_memory=True)
+        both[0].copy_(row)
+        both[1].copy_(col)
+        both = both.to(dev, non_blocking=True)
+        row, col = both[0], both[1]
     fwd = build_csr(num_rows, num_cols, row, col, order, device, validate=validate)
     coo = [row, col]
 
@@ -1533,6 +1543,28 @@ def _check_groups(ptr_, order, idx, num_rows):
         raise DGLError("malformed position grouping: " + "; ".join(problems))
 
 
+def _position_groups_items(idx, num_rows):
+    """_position_groups on a device with the typed-block item list over it,
+    in one library call (dglhip_group_positions_device: ≈80 µs of host time
+    as a CSR build plus _typed_items, r06): (ptr, order, item_ptr, item_row)."""
+    dev = idx.device
+    m = idx.numel()
+    R = max(int(num_rows), 1)
+    bound = R + -(-m // TYPED_CHUNK)
+    nb = LIB.dglhip_group_positions_workspace_bytes(R, m)
+    if nb < 0:
+        check_call(-1)
+    ptr_ = torch.empty(R + 1, dtype=torch.int64, device=dev)
+    order = torch.empty(max(m, 1), dtype=torch.int32, device=dev)[:m]
+    item_ptr = torch.empty(R + 1, dtype=torch.int64, device=dev)
+    item_row = torch.empty(bound, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(int(nb), 1), dtype=torch.uint8, device=dev)
+    check_call(LIB.dglhip_group_positions_device(
+        R, m, ptr(idx.contiguous()), bound, ptr(ptr_), ptr(order), ptr(item_ptr),
+        ptr(item_row), ptr(ws), int(nb), _stream_of(dev)))
+    return ptr_, order, item_ptr, item_row
+
+
 def _position_groups(idx, num_rows):
     """Positions of ``idx`` grouped by row in increasing position, no host
     sync: (ptr int64[R+1], order int32[m]). On a device, the library's CSR
@@ -1541,10 +1573,7 @@ def _position_groups(idx, num_rows):
     and scan (a quarter of the launches); the same arrays."""
     m = idx.numel()
     if idx.is_cuda and m:
-        pos = torch.arange(m, dtype=torch.int64, device=idx.device)
-        c = build_csr(num_rows, m, idx, pos, ORDER_EID, idx.device, schedule=False,
-                      validate=False)
-        return c.indptr, c.indices
+        return _position_groups_items(idx, num_rows)[:2]
     order = torch.sort(idx, stable=True)[1].to(torch.int32)
     counts = torch.zeros(num_rows, dtype=torch.int64, device=idx.device).scatter_add_(
         0, idx, torch.ones_like(idx))
@@ -1587,14 +1616,19 @@ class _DistMult(torch.autograd.Function):
             if not need:
                 continue
             ix = idx()
-            ptr_, order = _position_groups(ix, rows)
+            if h.is_cuda and ix.numel():
+                ptr_, order, item_ptr, item_row = _position_groups_items(ix, rows)
+            else:
+                ptr_, order = _position_groups(ix, rows)
+                item_ptr = item_row = None
             if _DEBUG_GROUPS:
                 _check_groups(ptr_, order, ix, rows)
             out = torch.empty(rows, F, dtype=torch.float32, device=h.device)
             common = (n, h.shape[0], w.shape[0])
             tail = (ptr(order), ptr(s), ptr(r), ptr(o), ptr(ds), ptr(h), ptr(w), ptr(out))
             if h.is_cuda:
-                item_ptr, item_row = _typed_items(ptr_, ix.numel())
+                if item_ptr is None:
+                    item_ptr, item_row = _typed_items(ptr_, ix.numel())
                 part = torch.empty(item_row.numel(), F, dtype=torch.float32, device=h.device)
                 check_call(LIB.dglhip_distmult_grad_device(
                     task, rows, item_row.numel(), F, *common, ptr(ptr_), ptr(item_ptr),
@@ -1617,6 +1651,11 @@ def distmult_score(h, w_rel, subj, rel, obj):
     DGLHIP_VALIDATE_INDICES=1) asks for it, with one min/max reduction and a
     host sync per call. Unchecked, the kernel never reads past its tables: an
     out-of-range position scores NaN and adds nothing to the gradients."""
+    return _DistMult.apply(_f32c(h), _f32c(w_rel), *_distmult_ids(h, w_rel, subj, rel, obj))
+
+
+def _distmult_ids(h, w_rel, subj, rel, obj):
+    """The triples' ids as int64 on h's device, checked (distmult_score)."""
     dev = h.device
     if w_rel.shape[1:] != h.shape[1:] or h.dim() != 2:
         raise DGLError("distmult_score: h and w_rel must be 2-D of one width")
@@ -1633,16 +1672,90 @@ def distmult_score(h, w_rel, subj, rel, obj):
             if lo < 0 or hi >= bound:
                 raise IndexError("distmult_score: %s ids span [%d, %d], out of range for %d rows"
                                  % (what, lo, hi, bound))
-    idx = [t.to(device=dev, dtype=torch.int64).reshape(-1).contiguous() for t in trip]
-    return _DistMult.apply(_f32c(h), _f32c(w_rel), *idx)
+    # one stacking copy (the triples usually arrive as the columns of one
+    # (n, 3) sample tensor: three strided views) instead of three
+    ids = torch.stack([t.to(device=dev, dtype=torch.int64).reshape(-1) for t in trip])
+    return [ids[0], ids[1], ids[2]]
+
+
+class _DistMultLoss(torch.autograd.Function):
+    """distmult_link_loss on a device: the loss and the scores in two
+    launches, the gradients as _DistMult's chains with the BCE gradient formed
+    in the kernel and the regulariser's term added to every row
+    (dglhip_distmult_loss_*)."""
+
+    @staticmethod
+    def forward(ctx, h, w, s, r, o, labels, reg):
+        n, F = s.numel(), h.shape[1]
+        dev = h.device
+        score = torch.empty(n, dtype=torch.float32, device=dev)
+        loss = torch.empty((), dtype=torch.float32, device=dev)
+        nws = LIB.dglhip_distmult_loss_workspace_floats(n, h.shape[0], w.shape[0], F)
+        ws = torch.empty(max(int(nws), 1), dtype=torch.float32, device=dev)
+        check_call(LIB.dglhip_distmult_loss_fwd_device(
+            n, F, h.shape[0], w.shape[0], ptr(s), ptr(r), ptr(o), ptr(h), ptr(w), ptr(labels),
+            float(reg), ptr(score), ptr(loss), ptr(ws), int(nws), _stream_of(dev)))
+        ctx.save_for_backward(h, w, s, r, o, labels, score)
+        ctx.reg = float(reg)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w, s, r, o, labels, score = ctx.saved_tensors
+        g = g.detach().to(torch.float32).reshape(1).contiguous()
+        n, F = s.numel(), h.shape[1]
+        dev = h.device
+        grads = [None, None]
+        for task, (need, rows, idx) in enumerate(
+                ((ctx.needs_input_grad[0], h.shape[0], lambda: torch.cat([s, o])),
+                 (ctx.needs_input_grad[1], w.shape[0], lambda: r))):
+            if not need:
+                continue
+            ptr_, order, item_ptr, item_row = _position_groups_items(idx(), rows)
+            out = torch.empty(rows, F, dtype=torch.float32, device=dev)
+            part = torch.empty(item_row.numel(), F, dtype=torch.float32, device=dev)
+            check_call(LIB.dglhip_distmult_loss_grad_device(
+                task, rows, item_row.numel(), F, n, h.shape[0], w.shape[0], ptr(ptr_),
+                ptr(item_ptr), ptr(item_row), ptr(order), ptr(s), ptr(r), ptr(o), ptr(score),
+                ptr(labels), ptr(g), ctx.reg, ptr(h), ptr(w), ptr(out), ptr(part),
+                _stream_of(dev)))
+            grads[task] = out
+        return grads[0], grads[1], None, None, None, None, None
+
+
+def distmult_link_loss(h, w_rel, subj, rel, obj, labels, reg):
+    """The R-GCN link-prediction loss (the reference's get_loss,
+    examples/pytorch/rgcn/link_predict.py:57-66):
+
+        F.binary_cross_entropy_with_logits(distmult_score(h, w_rel, subj, rel, obj), labels)
+            + reg * (h.pow(2).mean() + w_rel.pow(2).mean())
+
+    On a ROCm device one forward launch pair and the decoder's gradient
+    launches (the BCE and regulariser gradients formed inside them) instead of
+    about twenty small kernels; values within fp32 rounding of that
+    expression (its sums associate differently). Ids are checked as
+    distmult_score checks them."""
+    ids = _distmult_ids(h, w_rel, subj, rel, obj)
+    labels = torch.as_tensor(labels)
+    if (h.is_cuda and h.dtype == torch.float32 and w_rel.dtype == torch.float32 and
+            ids[0].numel() > 0 and h.numel() > 0):
+        lab = labels.to(device=h.device, dtype=torch.float32).reshape(-1).contiguous()
+        if lab.numel() != ids[0].numel():
+            raise DGLError("distmult_link_loss: %d labels for %d triples"
+                           % (lab.numel(), ids[0].numel()))
+        return _DistMultLoss.apply(_f32c(h), _f32c(w_rel), *ids, lab, float(reg))
+    score = _DistMult.apply(_f32c(h), _f32c(w_rel), *ids)
+    return (torch.nn.functional.binary_cross_entropy_with_logits(score, labels.to(score)) +
+            reg * (h.pow(2).mean() + w_rel.pow(2).mean()))
 
 
 _VALIDATE_INDICES = os.environ.get("DGLHIP_VALIDATE_INDICES", "0") not in ("", "0")
 
 
 def set_validate_indices(on):
-    """Check device-resident index arguments (distmult_score's triples) on
-    the host before launching (one sync per call); returns the old setting."""
+    """Check device-resident index arguments (distmult_score's triples,
+    typed_block_spmm's relations) on the host before launching (one sync per
+    call); returns the old setting. Host-resident ones are always checked."""
     global _VALIDATE_INDICES
     old, _VALIDATE_INDICES = _VALIDATE_INDICES, bool(on)
     return old
@@ -1716,11 +1829,13 @@ def _relation_groups(adj, etype, num_rels):
     return g
 
 
-def _run_typed_msg(csr, slot_map, groups, pos_row, ufeat2, weight, slot_norm, nb, si, so):
+def _run_typed_msg(csr, slot_map, groups, pos_row, ufeat2, weight, slot_norm, nb, si, so,
+                   operand_scale=None, out_scale=None, weight_transposed=False):
     """out = the typed-block g-SpMM over ``csr`` in two launches: every edge's
-    message (blockdiag(weight[r]) applied to ufeat2[pos_row]) stored at its
-    forward slot, walked relation-major; then each row's sum over its slots,
-    reading message ``slot_map[k]`` (None: k) for slot k."""
+    message (blockdiag(weight[r]) applied to ufeat2[pos_row], that row scaled
+    by ``operand_scale[pos_row]`` when given) stored at its forward slot,
+    walked relation-major; then each row's sum over its slots, reading message
+    ``slot_map[k]`` (None: k) for slot k, times ``out_scale[row]``."""
     dev = ufeat2.device
     Fo = nb * so
     R = groups.ptr.numel() - 1
@@ -1729,7 +1844,8 @@ def _run_typed_msg(csr, slot_map, groups, pos_row, ufeat2, weight, slot_norm, nb
     stream = _stream_of(dev)
     check_call(LIB.dglhip_typed_block_msg_device(
         R, g_rel.numel(), nb, si, so, ptr(groups.ptr), ptr(g_ptr), ptr(g_rel), ptr(pos_row),
-        ptr(groups.slot), ptr(ufeat2), ptr(weight), ptr(msg), stream))
+        ptr(groups.slot), ptr(ufeat2), ptr(operand_scale), ptr(weight),
+        1 if weight_transposed else 0, ptr(msg), stream))
     items = csr._plans.get("typed_items")
     if items is None:
         items = csr._plans["typed_items"] = _typed_items(csr.indptr, csr.nnz)
@@ -1738,8 +1854,8 @@ def _run_typed_msg(csr, slot_map, groups, pos_row, ufeat2, weight, slot_norm, nb
     part = torch.empty(item_row.numel(), Fo, dtype=torch.float32, device=dev)
     check_call(LIB.dglhip_typed_msg_sum_device(
         csr.num_rows, item_row.numel(), Fo, ptr(csr.indptr), ptr(item_ptr), ptr(item_row),
-        csr.num_rows, None, ptr(slot_map), ptr(slot_norm), ptr(msg), ptr(out), ptr(part),
-        stream))
+        csr.num_rows, None, ptr(slot_map), ptr(slot_norm), ptr(msg), ptr(out_scale), ptr(out),
+        ptr(part), stream))
     return out
 
 
@@ -1757,16 +1873,44 @@ class _RelationGroups(object):
     and the chunked items (_typed_items)."""
 
     def __init__(self, fwd, etype, num_rels):
-        rel_of_slot = etype.index_select(0, fwd.eid)
-        rel = build_csr(num_rels, max(fwd.num_cols, 1), rel_of_slot, fwd.indices.long(),
-                        ORDER_EID, fwd.device, schedule=False)
-        self.ptr = rel.indptr
-        self.src = rel.indices
-        self.slot = rel.eid  # forward slot of each relation-major position
-        self.dst = fwd.row_ids().index_select(0, self.slot).to(torch.int32)
-        self.items = _typed_items(self.ptr, fwd.nnz) if fwd.device.type == "cuda" else None
+        # relations are checked where they were given (typed_block_spmm: host
+        # ids always, device ids on request), not with a sync here; the
+        # grouping never stores outside its arrays for any value
+        if fwd.device.type == "cuda":
+            self._build_device(fwd, etype, num_rels)
+        else:
+            rel_of_slot = etype.index_select(0, fwd.eid)
+            rel = build_csr(num_rels, max(fwd.num_cols, 1), rel_of_slot, fwd.indices.long(),
+                            ORDER_EID, fwd.device, schedule=False, validate=False)
+            self.ptr = rel.indptr
+            self.src = rel.indices
+            self.slot = rel.eid  # forward slot of each relation-major position
+            self.dst = fwd.row_ids().index_select(0, self.slot).to(torch.int32)
+            self.items = None
         self.etype = etype  # the relations it was built for (held: see matches)
         self.version = etype._version
+
+    def _build_device(self, fwd, etype, num_rels):
+        """The same arrays in one library call (dglhip_relation_groups_device:
+        ≈100 µs of host time as a CSR build, gathers, repeat_interleave and
+        the item list, r06)."""
+        dev, nnz, R = fwd.device, fwd.nnz, max(int(num_rels), 1)
+        bound = R + -(-nnz // TYPED_CHUNK)
+        nb = LIB.dglhip_relation_groups_workspace_bytes(R, nnz)
+        if nb < 0:
+            check_call(-1)
+        self.ptr = torch.empty(R + 1, dtype=torch.int64, device=dev)
+        self.src = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+        self.slot = torch.empty(max(nnz, 1), dtype=torch.int64, device=dev)[:nnz]
+        self.dst = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)[:nnz]
+        item_ptr = torch.empty(R + 1, dtype=torch.int64, device=dev)
+        item_rel = torch.empty(bound, dtype=torch.int32, device=dev)
+        ws = torch.empty(max(int(nb), 1), dtype=torch.uint8, device=dev)
+        check_call(LIB.dglhip_relation_groups_device(
+            R, fwd.num_rows, nnz, ptr(etype), ptr(fwd.indptr), ptr(fwd.indices), ptr(fwd.eid),
+            bound, ptr(self.ptr), ptr(self.src), ptr(self.slot), ptr(self.dst), ptr(item_ptr),
+            ptr(item_rel), ptr(ws), int(nb), _stream_of(dev)))
+        self.items = (item_ptr, item_rel)
 
     def matches(self, etype):
         # typed_block_spmm hands a new 1-D view of the relations at every call
@@ -1777,38 +1921,47 @@ class _RelationGroups(object):
                 self.etype.data_ptr() == etype.data_ptr() and self.version == etype._version)
 
 
+def _typed_scale_fused(dev, nb, si, so):
+    """A destination row scale rides in the message path's kernels (forward
+    sum, dH messages, staged dW) for these widths on a device."""
+    return (dev.type == "cuda" and _typed_msg_ok(nb, si, so) and _typed_msg_ok(nb, so, si) and
+            nb * si * so <= 4096)
+
+
 class _TypedBlock(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, adj, etype, num_rels, ufeat2, weight, enorm):
+    def forward(ctx, adj, etype, num_rels, ufeat2, weight, enorm, row_scale=None):
         R, nb, si, so = weight.shape
         if ufeat2.is_cuda and _typed_msg_ok(nb, si, so):
             g = _relation_groups(adj, etype, R)
             nrm = None if enorm is None else enorm.index_select(0, adj.fwd.eid)
-            out = _run_typed_msg(adj.fwd, None, g, g.src, ufeat2, weight, nrm, nb, si, so)
+            out = _run_typed_msg(adj.fwd, None, g, g.src, ufeat2, weight, nrm, nb, si, so,
+                                 out_scale=row_scale)
         else:
+            assert row_scale is None  # typed_block_spmm scales outside otherwise
             rel, nrm = _slot_values(adj.fwd, etype, enorm)
             out = _run_typed_block(adj.fwd, ufeat2, weight, rel, nrm, nb, si, so)
         ctx.adj, ctx.num_rels = adj, num_rels
-        ctx.save_for_backward(etype, ufeat2, weight, enorm)
+        ctx.save_for_backward(etype, ufeat2, weight, enorm, row_scale)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        etype, ufeat2, weight, enorm = ctx.saved_tensors
+        etype, ufeat2, weight, enorm, row_scale = ctx.saved_tensors
         adj = ctx.adj
         R, nb, si, so = weight.shape
         dout = dout.contiguous()
         du = dw = None
         if ctx.needs_input_grad[3]:
-            wt = weight.transpose(2, 3).contiguous()  # (R, nb, so, si)
             if dout.is_cuda and _typed_msg_ok(nb, so, si):
                 # messages Wt[r] dout[dst] at the forward slots, read along the
-                # transpose
+                # transpose (the weight read transposed in the kernel)
                 g = _relation_groups(adj, etype, R)
                 nrm = None if enorm is None else enorm.index_select(0, adj.bwd.eid)
-                du = _run_typed_msg(adj.bwd, _fwd_slot_of_bwd(adj), g, g.dst, dout, wt, nrm,
-                                    nb, so, si)
+                du = _run_typed_msg(adj.bwd, _fwd_slot_of_bwd(adj), g, g.dst, dout, weight, nrm,
+                                    nb, so, si, operand_scale=row_scale, weight_transposed=True)
             else:
+                wt = weight.transpose(2, 3).contiguous()  # (R, nb, so, si)
                 rel, nrm = _slot_values(adj.bwd, etype, enorm)
                 du = _run_typed_block(adj.bwd, dout, wt, rel, nrm, nb, so, si)
         if ctx.needs_input_grad[4]:
@@ -1820,18 +1973,18 @@ class _TypedBlock(torch.autograd.Function):
                 item_ptr, item_rel = g.items
                 part = torch.empty(item_rel.numel(), nb * si * so, dtype=torch.float32,
                                    device=dout.device)
-                check_call(LIB.dglhip_typed_block_wgrad_device(
+                check_call(LIB.dglhip_typed_block_wgrad_scaled_device(
                     R, item_rel.numel(), nb, si, so, ptr(g.ptr), ptr(item_ptr), ptr(item_rel),
                     R, None, ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2), ptr(dout),
-                    ptr(dw), ptr(part), _stream_of(dout.device)))
+                    ptr(row_scale), ptr(dw), ptr(part), _stream_of(dout.device)))
             else:
                 check_call(LIB.dglhip_typed_block_wgrad_host(
                     R, nb, si, so, ptr(g.ptr), ptr(g.src), ptr(g.dst), ptr(nrm), ptr(ufeat2),
                     ptr(dout), ptr(dw), 0))
-        return None, None, None, du, dw, None
+        return None, None, None, du, dw, None, None
 
 
-def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
+def typed_block_spmm(adj, ufeat, weight, etype, enorm=None, row_scale=None):
     """R-GCN block-diagonal message passing in one kernel:
     out[v] = sum_{e=(u->v)} enorm[e] * blockdiag(weight[etype[e]]) applied to ufeat[u].
 
@@ -1840,12 +1993,25 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
     weight : (num_rels, nb, si, so) float32 (autograd)
     etype  : (num_edges,) int64 relation of each edge id
     enorm  : optional (num_edges,) float32 per-edge scale (not differentiated)
+    row_scale : optional (num_rows,) float32 scale of each output row (not
+             differentiated): the value of ``out * row_scale.unsqueeze(1)`` —
+             the R-GCN layer's 1 / in-degree, rounded as that product is —
+             applied inside the kernels when the message path runs (no
+             elementwise pass either way, r06), else by that product
     """
     dev = ufeat.device
     adj = adj.to(dev)
     R, nb, si, so = weight.shape
     if ufeat.shape[1] != nb * si:
         raise DGLError("ufeat width %d != num_blocks * in_block %d" % (ufeat.shape[1], nb * si))
+    etype = torch.as_tensor(etype)
+    if etype.numel() and (etype.device.type == "cpu" or (
+            _VALIDATE_INDICES and not (dev.type == "cuda" and
+                                       torch.cuda.is_current_stream_capturing()))):
+        lo, hi = torch.stack([etype.min(), etype.max()]).tolist()
+        if lo < 0 or hi >= R:
+            raise IndexError("typed_block_spmm: relations span [%d, %d], out of range for %d "
+                             "relation weights" % (lo, hi, R))
     etype = etype.to(device=dev, dtype=torch.int64).contiguous().reshape(-1)
     en = None if enorm is None else _f32c(enorm.to(dev).reshape(-1).detach())
     # one relation (and norm) per edge id: the kernels gather them by edge id
@@ -1853,7 +2019,15 @@ def typed_block_spmm(adj, ufeat, weight, etype, enorm=None):
     if etype.numel() != E or (en is not None and en.numel() != E):
         raise DGLError("typed_block_spmm: %d edges but etype has %d and enorm %s entries"
                        % (E, etype.numel(), "no" if en is None else en.numel()))
-    return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en)
+    if row_scale is None:
+        return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en)
+    rs = _f32c(torch.as_tensor(row_scale).to(dev).reshape(-1).detach())
+    if rs.numel() != adj.fwd.num_rows:
+        raise DGLError("typed_block_spmm: row_scale has %d entries for %d rows"
+                       % (rs.numel(), adj.fwd.num_rows))
+    if _typed_scale_fused(dev, nb, si, so):
+        return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en, rs)
+    return _TypedBlock.apply(adj, etype, R, _f32c(ufeat), _f32c(weight), en) * rs.unsqueeze(1)
 
 
 # ---------------------------------------------------------------------------

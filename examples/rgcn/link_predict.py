@@ -100,7 +100,9 @@ class RGCNBlockLayer(nn.Module):
             agg = g.ndata.pop("h") * norm.unsqueeze(1)
         else:  # fused typed-edge g-SpMM
             adj = g if isinstance(g, kernel.SparseAdj) else g.sparse_adjacency(h.device)
-            agg = kernel.typed_block_spmm(adj, h, self.weight, etype) * norm.unsqueeze(1)
+            # (the 1 / in-degree scale rides in the kernels: the bits of
+            # `typed_block_spmm(...) * norm.unsqueeze(1)`)
+            agg = kernel.typed_block_spmm(adj, h, self.weight, etype, row_scale=norm)
         out = agg + loop
         return self.activation(out) if self.activation else out
 
@@ -118,7 +120,14 @@ class LinkPredict(nn.Module):
         self.udf = udf
 
     def forward(self, g, node_ids, etype, norm):
-        h = self.emb(node_ids)
+        if self.udf:
+            h = self.emb(node_ids)
+        else:
+            # the sample's entities are unique (np.unique), so the lookup's
+            # gradient is one row per entity: index_select's backward (a zero
+            # fill and a collision-free index_add) gives the bits of
+            # nn.Embedding's sort-based backward in 2 launches instead of ~8
+            h = self.emb.weight.index_select(0, node_ids)
         for layer in self.layers:
             h = layer(g, h, etype, norm)
         return h
@@ -130,11 +139,12 @@ class LinkPredict(nn.Module):
         if self.udf:
             s = h[samples[:, 0]] * self.w_relation[samples[:, 1]] * h[samples[:, 2]]
             score = s.sum(1)
-        else:
-            score = kernel.distmult_score(h, self.w_relation, samples[:, 0], samples[:, 1],
-                                          samples[:, 2])
-        reg = h.pow(2).mean() + self.w_relation.pow(2).mean()
-        return F.binary_cross_entropy_with_logits(score, labels) + self.reg * reg
+            reg = h.pow(2).mean() + self.w_relation.pow(2).mean()
+            return F.binary_cross_entropy_with_logits(score, labels) + self.reg * reg
+        # the same loss as one engine op: scores, BCE and the regulariser in
+        # two launches forward, their gradients inside the decoder's
+        return kernel.distmult_link_loss(h, self.w_relation, samples[:, 0], samples[:, 1],
+                                         samples[:, 2], labels, self.reg)
 
 
 def select_blas(name):

@@ -935,7 +935,12 @@ int dglhip_typed_block_wgrad_host(int64_t num_rels, int64_t num_blocks,
  *     in_block 1, 2, 4, 5, 8 or 16);
  *   sum: out[row] = fma(slot_norm[k], msg[slot_map[k]], acc) over the CSR
  *     row's slots k in order (slot_map NULL: the slot itself; slot_norm NULL:
- *     1), rows of several items combined as in the one-kernel form.
+ *     1), rows of several items combined as in the one-kernel form, times
+ *     row_scale[row] when given (one rounding, as torch's `agg * norm`).
+ * A message's operand row may be scaled too (row_scale of the message entry:
+ * ufeat[row] * row_scale[row], the backward's dout * norm), and the weight
+ * given as (R, nb, out_block, in_block) and read transposed
+ * (weight_transposed = 1: the backward's blocks without a transposed copy). 
  * dglhip_typed_block_msg_ok: 1 when the message path is on (the default;
  * dglhip_set_typed_block_messages / env DGLHIP_TYPED_MESSAGES) and takes
  * these widths. The same switch moves dglhip_typed_block_wgrad_device to its
@@ -946,14 +951,28 @@ int dglhip_typed_block_msg_device(int64_t num_rels, int64_t num_items, int64_t n
                                   int64_t in_block, int64_t out_block, const int64_t* rel_ptr,
                                   const int64_t* item_ptr, const int32_t* item_rel,
                                   const int32_t* pos_row, const int64_t* pos_slot,
-                                  const float* ufeat, const float* weight, float* msg,
+                                  const float* ufeat, const float* row_scale,
+                                  const float* weight, int weight_transposed, float* msg,
                                   void* stream);
 int dglhip_typed_msg_sum_device(int64_t num_rows, int64_t num_items, int64_t feat_len,
                                 const int64_t* indptr, const int64_t* item_ptr,
                                 const int32_t* item_row, int64_t num_heavy,
                                 const int32_t* heavy_row, const int64_t* slot_map,
-                                const float* slot_norm, const float* msg, float* out,
-                                float* partial, void* stream);
+                                const float* slot_norm, const float* msg,
+                                const float* row_scale, float* out, float* partial,
+                                void* stream);
+/* The weight gradient with dout's rows scaled (dout[dst] * dout_scale[dst],
+ * rounded as torch's product; NULL: unscaled, as
+ * dglhip_typed_block_wgrad_device) on the message path's staged kernel. */
+int dglhip_typed_block_wgrad_scaled_device(int64_t num_rels, int64_t num_items,
+                                           int64_t num_blocks, int64_t in_block,
+                                           int64_t out_block, const int64_t* rel_ptr,
+                                           const int64_t* item_ptr, const int32_t* item_rel,
+                                           int64_t num_heavy, const int32_t* heavy_rel,
+                                           const int32_t* rel_src, const int32_t* rel_dst,
+                                           const float* rel_norm, const float* ufeat,
+                                           const float* dout, const float* dout_scale,
+                                           float* dweight, float* partial, void* stream);
 
 /* The typed-block entries' item list from a CSR-like ptr[num_rows+1]: item_ptr
  * [num_rows+1] (row r has max(1, ceil(deg / DGLHIP_TYPED_CHUNK)) items) and
@@ -964,6 +983,30 @@ int64_t dglhip_typed_items_workspace_bytes(int64_t num_rows);
 int dglhip_typed_items_device(int64_t num_rows, const int64_t* ptr, int64_t bound,
                               int64_t* item_ptr, int32_t* item_row, void* workspace,
                               int64_t workspace_bytes, void* stream);
+
+/* Groupings of the typed-block and DistMult kernels, each one call (r06):
+ *   positions: ptr[num_rows+1] and order[m] = the positions k of idx[m]
+ *     grouped by idx[k], ascending k within a group (a stable sort; ids
+ *     outside [0, num_rows) are clamped into it: check them first), and the
+ *     item list over ptr as dglhip_typed_items_device makes it (bound >=
+ *     num_rows + ceil(m / DGLHIP_TYPED_CHUNK));
+ *   relations: the forward CSR's slots grouped by relation, etype[fwd_eid[s]]
+ *     for slot s, ascending slot within a relation: ptr[num_rels+1], and per
+ *     relation-major position the slot, its column (src) and its row (dst),
+ *     with the item list over ptr (item_ptr / item_rel).
+ * No host sync; workspace of the *_workspace_bytes size. */
+int64_t dglhip_group_positions_workspace_bytes(int64_t num_rows, int64_t m);
+int dglhip_group_positions_device(int64_t num_rows, int64_t m, const int64_t* idx,
+                                  int64_t bound, int64_t* ptr, int32_t* order,
+                                  int64_t* item_ptr, int32_t* item_row, void* workspace,
+                                  int64_t workspace_bytes, void* stream);
+int64_t dglhip_relation_groups_workspace_bytes(int64_t num_rels, int64_t nnz);
+int dglhip_relation_groups_device(int64_t num_rels, int64_t fwd_rows, int64_t nnz,
+                                  const int64_t* etype, const int64_t* fwd_indptr,
+                                  const int32_t* fwd_indices, const int64_t* fwd_eid,
+                                  int64_t bound, int64_t* ptr, int32_t* src, int64_t* slot,
+                                  int32_t* dst, int64_t* item_ptr, int32_t* item_rel,
+                                  void* workspace, int64_t workspace_bytes, void* stream);
 
 /* DistMult decoder of R-GCN link prediction (the reference's calc_score,
  * examples/pytorch/rgcn/link_predict.py:50-55: s = h[subj] * w_rel[rel] *
@@ -996,6 +1039,31 @@ int dglhip_distmult_grad_device(int task, int64_t num_rows, int64_t num_items, i
                                 const int64_t* subj, const int64_t* rel, const int64_t* obj,
                                 const float* dscore, const float* h, const float* w_rel,
                                 float* out, float* partial, void* stream);
+/* The R-GCN example's link-prediction loss fused (r06; the reference's
+ * get_loss, examples/pytorch/rgcn/link_predict.py: BCE-with-logits of the
+ * DistMult scores averaged over the samples, + reg * (mean(h^2) +
+ * mean(w_rel^2))): loss[0] and score[num_samples] (the bits of
+ * dglhip_distmult_score_device) in two launches, workspace of
+ * dglhip_distmult_loss_workspace_floats floats. Its gradients: the entry
+ * above with dscore = (sigmoid(score) - labels) * (g[0] / num_samples) formed
+ * in the kernel, and 2 * reg * g[0] / (rows * feat_len) * h (task 0) or
+ * * w_rel (task 1) added to every output row; g = the loss's upstream
+ * gradient on the device (no host read). */
+int64_t dglhip_distmult_loss_workspace_floats(int64_t num_samples, int64_t num_nodes,
+                                              int64_t num_rels, int64_t feat_len);
+int dglhip_distmult_loss_fwd_device(int64_t num_samples, int64_t feat_len, int64_t num_nodes,
+                                    int64_t num_rels, const int64_t* subj, const int64_t* rel,
+                                    const int64_t* obj, const float* h, const float* w_rel,
+                                    const float* labels, float reg, float* score, float* loss,
+                                    float* workspace, int64_t workspace_floats, void* stream);
+int dglhip_distmult_loss_grad_device(int task, int64_t num_rows, int64_t num_items,
+                                     int64_t feat_len, int64_t num_samples, int64_t num_nodes,
+                                     int64_t num_rels, const int64_t* ptr, const int64_t* item_ptr,
+                                     const int32_t* item_row, const int32_t* order,
+                                     const int64_t* subj, const int64_t* rel, const int64_t* obj,
+                                     const float* score, const float* labels, const float* g,
+                                     float reg, const float* h, const float* w_rel, float* out,
+                                     float* partial, void* stream);
 int dglhip_distmult_grad_host(int task, int64_t num_rows, int64_t feat_len, int64_t num_samples,
                               int64_t num_nodes, int64_t num_rels, const int64_t* ptr,
                               const int32_t* order, const int64_t* subj, const int64_t* rel,

@@ -124,3 +124,43 @@ def test_distmult_host_equals_device():
         res.append([sc.detach().cpu(), g[0].cpu(), g[1].cpu()])
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("device", DEVICES)
+@pytest.mark.parametrize("F", [500, 37])
+def test_distmult_link_loss_matches_float64(device, F):
+    """kernel.distmult_link_loss (the example's get_loss: BCE-with-logits of
+    the scores, mean, + reg * (mean(h^2) + mean(w^2))) — fused on a device,
+    the torch expression on the host — against float64: the loss within 1e-5
+    of its terms' magnitudes, the scores with distmult_score's bits, every
+    gradient element within 1e-5 of its Σ|terms| (hub rows of several chunks
+    and rows no triple touches included)."""
+    dev = _dev(device)
+    h, w, s, r, o = _case(F=F, N=900)  # rows past 700 see no triple
+    s, o = s % 700, o % 700
+    labels = (torch.arange(s.numel()) % 2).float()
+    reg = 0.01
+    h1, w1 = h.clone().to(dev).requires_grad_(True), w.clone().to(dev).requires_grad_(True)
+    loss = kernel.distmult_link_loss(h1, w1, s.to(dev), r.to(dev), o.to(dev), labels.to(dev), reg)
+    loss.backward()
+    h2, w2 = h.double().requires_grad_(True), w.double().requires_grad_(True)
+    score = (h2[s] * w2[r] * h2[o]).sum(1)
+    ref = (torch.nn.functional.binary_cross_entropy_with_logits(score, labels.double()) +
+           reg * (h2.pow(2).mean() + w2.pow(2).mean()))
+    ref.backward()
+    with torch.no_grad():
+        mag_s = (h2[s] * w2[r] * h2[o]).abs().sum(1)
+        lmag = (mag_s + 1.0).mean() + reg * (h2.pow(2).mean() + w2.pow(2).mean())
+    assert abs(float(loss) - float(ref)) <= 1e-5 * float(lmag)
+    # gradient bounds: the same chains over magnitudes
+    ha, wa = h.double().abs().requires_grad_(True), w.double().abs().requires_grad_(True)
+    with torch.no_grad():
+        # |sigmoid| + |label|: the Σ|terms| of the BCE gradient's subtraction
+        # (saturated logits cancel it)
+        ds = (torch.sigmoid(score) + labels.double()) / s.numel()
+    lm = (ds * (ha[s] * wa[r] * ha[o]).sum(1)).sum() + reg * (ha.pow(2).mean() +
+                                                             wa.pow(2).mean())
+    lm.backward()
+    for got, want, bound in ((h1.grad, h2.grad, ha.grad), (w1.grad, w2.grad, wa.grad)):
+        err = (got.double().cpu() - want).abs()
+        assert bool((err <= 1e-5 * bound + 1e-30).all()), float((err / (bound + 1e-30)).max())

@@ -242,7 +242,8 @@ def _rgcn_magnitude_bounds(model, params64, h64, loss64, uniq, src, dst, rel, no
         h = h64
         wr = params64["w_relation"]
         score = (h[samples[:, 0]] * wr[samples[:, 1]] * h[samples[:, 2]]).sum(1)
-        dscore = ((torch.sigmoid(score) - labels) / score.numel()).abs()
+        # |sigmoid| + |label|: the Σ|terms| of the BCE gradient's subtraction
+        dscore = (torch.sigmoid(score) + labels) / score.numel()
     # the ReLU's active elements, from the real float64 forward
     active = []
     with torch.no_grad():

@@ -194,3 +194,69 @@ def test_typed_block_fb15k_shape(device):
             err = (got - want).abs()
             assert bool((err <= 1e-5 * bound + 1e-30).all()), \
                 float((err / (1e-5 * bound + 1e-30)).max())
+
+
+@pytest.mark.gpu
+def test_groupings_device_match_host():
+    """The one-call device groupings (relation-major slots for the typed-block
+    kernels, positions by id for DistMult, each with its item list) equal the
+    host builds: a CSR over the keys, the gathers and kernel._typed_items."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    rng = np.random.default_rng(11)
+    n, m, R = 500, 9000, 37
+    p = 1.0 / np.arange(1, n + 1) ** 1.1
+    dst = torch.from_numpy(rng.choice(n, size=m, p=p / p.sum()))
+    src = torch.from_numpy(rng.integers(0, n, m))
+    etype = torch.from_numpy(rng.integers(0, R, m))
+    etype[:300] = 5  # one relation of several chunks
+    host = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, "cpu")
+    dev = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, "cuda")
+    gh = kernel._RelationGroups(host.fwd, etype, R)
+    gd = kernel._RelationGroups(dev.fwd, etype.cuda(), R)
+    for a, b in ((gh.ptr, gd.ptr), (gh.src, gd.src), (gh.slot, gd.slot), (gh.dst, gd.dst)):
+        assert torch.equal(a, b.cpu())
+    ip, ir = kernel._typed_items(gh.ptr, m)
+    assert torch.equal(ip, gd.items[0].cpu()) and torch.equal(ir, gd.items[1].cpu())
+    for rows, ids in ((n, torch.cat([src, dst])), (R, etype), (n, torch.zeros(5, dtype=torch.int64))):
+        ph, oh = kernel._position_groups(ids, rows)
+        pd, od, ipd, ird = kernel._position_groups_items(ids.cuda(), rows)
+        assert torch.equal(ph, pd.cpu()) and torch.equal(oh, od.cpu())
+        iph, irh = kernel._typed_items(ph, ids.numel())
+        assert torch.equal(iph, ipd.cpu()) and torch.equal(irh, ird.cpu())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(11, 4, 3, 5), (20, 100, 5, 5), (6, 3, 7, 9)])
+def test_typed_block_row_scale_bits(shape):
+    """row_scale inside the message path's kernels (the forward sum's store,
+    the dH messages' and dW's staged dout rows) gives the bits of
+    ``typed_block_spmm(...) * scale.unsqueeze(1)`` with torch's product and
+    its backward, on the host; widths outside the message kernels take that
+    product themselves."""
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    R, nb, si, so = shape
+    rng = np.random.default_rng(7 + sum(shape))
+    n, m = 400, 9000
+    p = 1.0 / np.arange(1, n + 1) ** 1.1
+    dst = torch.from_numpy(rng.choice(n, size=m, p=p / p.sum()))
+    src = torch.from_numpy(rng.integers(0, n, m))
+    etype = torch.from_numpy(rng.integers(0, R, m))
+    scale = torch.from_numpy(rng.uniform(0.01, 1, n).astype(np.float32))
+    h = torch.randn(n, nb * si)
+    W = torch.randn(R, nb, si, so) * 0.3
+    G = torch.randn(n, nb * so)
+    res = []
+    for dev in ("cpu", "cuda"):
+        adj = kernel.from_coo(n, n, dst, src, kernel.ORDER_EID, dev)
+        h1 = h.detach().to(dev).clone().requires_grad_(True)
+        W1 = W.detach().to(dev).clone().requires_grad_(True)
+        if dev == "cpu":
+            out = kernel.typed_block_spmm(adj, h1, W1, etype) * scale.unsqueeze(1)
+        else:
+            out = kernel.typed_block_spmm(adj, h1, W1, etype.cuda(), row_scale=scale.cuda())
+        out.backward(G.to(dev))
+        res.append((out.detach().cpu(), h1.grad.cpu(), W1.grad.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

@@ -158,6 +158,16 @@ for s in $STEPS; do
       rc=$?; tail -1 gpurun_out/legprof.log; [ $rc -eq 0 ] || exit $rc
       python tools/window_stats.py gpurun_out/legprof/run_kernel_trace.csv --window 1 \
         --out gpurun_out/legprof/leg_timed_kernel_stats.csv || exit $? ;;
+    rgcnlegs)
+      # the R-GCN leg alone, REPEAT times (process-to-process spread), then its host study
+      for i in $(seq ${REPEAT:-3}); do
+        timeout -k 10 300 python bench.py --no-traffic --no-rmat-leg --no-sage-rmat-leg --no-train-leg \
+          --no-one-launch-leg --no-cpu-baseline --model-legs rgcn > gpurun_out/rgcn_leg_$i.json 2> gpurun_out/rgcn_leg_$i.err
+        rc=$?; [ $rc -eq 0 ] || { tail -3 gpurun_out/rgcn_leg_$i.err; exit $rc; }
+        python -c "import json; d=json.load(open('gpurun_out/rgcn_leg_$i.json'))['rgcn']; print('rgcn', d['ms_per_step'], d['kernel_ms'], d['launches_per_step'])"
+      done
+      timeout -k 10 400 python -u tools/rgcn_host_study.py --blas rocblas --out gpurun_out/rgcn_host.json > gpurun_out/rgcn_host.log 2>&1
+      rc=$?; tail -1 gpurun_out/rgcn_host.log; [ $rc -eq 0 ] || exit $rc ;;
     gatsplit)
       # the GAT backward's L2 hits / misses and EA requests over the timed calls (tools/gat_bwd_split.py)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -4,7 +4,7 @@ Per BLAS library (torch.backends.cuda.preferred_blas_library): host enqueue
 ms per step (no sync inside the steps), ms to completion, and the top ops by
 self CPU time (torch.profiler, CPU activity only).
 
-  python tools/rgcn_host_study.py --blas default cublas --out gpurun_out/rgcn_host.json
+  python tools/rgcn_host_study.py --blas hipblaslt rocblas --out gpurun_out/rgcn_host.json
 """
 import argparse
 import json
@@ -21,7 +21,7 @@ import tools.rgcn_step as rs  # noqa: E402
 
 def measure(blas, steps, top):
     if blas != "default":
-        torch.backends.cuda.preferred_blas_library(blas)
+        rs.lp.select_blas(blas)  # "rocblas" / "hipblaslt"
     args = rs.lp.parser().parse_args([])
     dev = torch.device("cuda", 0)
     raw = rs.make_samples(args, 5 + 3 * steps)
@@ -49,12 +49,39 @@ def measure(blas, steps, top):
             rs.one_step(model, opt, s, args)
         torch.cuda.synchronize()
     rows = sorted(prof.key_averages(), key=lambda e: -e.self_cpu_time_total)[:top]
+    # host syncs torch sees (set_sync_debug_mode), one step
+    import warnings
+    syncs = []
+    torch.cuda.set_sync_debug_mode("warn")
+    try:
+        with warnings.catch_warnings(record=True) as caught:
+            warnings.simplefilter("always")
+            rs.one_step(model, opt, samples[5], args)
+        for w in caught:
+            syncs.append(str(w.message)[:120])
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    # Python-level host time by function (cProfile, tottime)
+    import cProfile
+    import pstats
+    pr = cProfile.Profile()
+    pr.enable()
+    for s in samples[5:5 + steps]:
+        rs.one_step(model, opt, s, args)
+    torch.cuda.synchronize()
+    pr.disable()
+    st = pstats.Stats(pr)
+    funcs = sorted(st.stats.items(), key=lambda kv: -kv[1][2])[:top]
+    py = [{"func": "%s:%d(%s)" % (os.path.basename(k[0]), k[1], k[2]),
+           "tottime_us_per_step": v[2] / steps * 1e6, "cumtime_us_per_step": v[3] / steps * 1e6,
+           "calls_per_step": v[1] / steps} for k, v in funcs]
     ops = [{"name": e.key, "self_us_per_step": e.self_cpu_time_total / steps,
             "total_us_per_step": e.cpu_time_total / steps, "calls_per_step": e.count / steps}
            for e in rows]
     return {"blas": blas, "host_enqueue_ms": t_enq, "to_completion_ms": t_all,
             "phase_ms": {"graph": phases[0], "forward": phases[1], "backward": phases[2]},
-            "top_self_cpu": ops}
+            "top_self_cpu": ops, "syncs_one_step": syncs, "cprofile_top": py}
 
 
 def main():
