@@ -270,7 +270,11 @@ class _LazyLib(object):
         return self._lib
 
     def __getattr__(self, name):
-        return getattr(self._get(), name)
+        fn = getattr(self._get(), name)
+        # kept on the instance: later lookups skip this hook (≈40 library
+        # calls per R-GCN step went through it)
+        setattr(self, name, fn)
+        return fn
 
     @property
     def loaded(self):
