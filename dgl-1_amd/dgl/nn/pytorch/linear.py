@@ -25,7 +25,7 @@ import torch.nn as nn
 
 from ..._handoff import GradHandoff, is_output, output_ref, take
 
-__all__ = ["NodeLinear", "sage_dense", "bias_add"]
+__all__ = ["NodeLinear", "sage_dense", "bias_add", "dense_mm"]
 
 _ROWS_PER_CHUNK = 1 << 16
 _SMALL_ROWS_PER_CHUNK = 1 << 11
@@ -35,6 +35,12 @@ def _splitk_tn(a, b):
     """aᵀ·b for tall a (n, p), b (n, q): split-K over row chunks, summed in order."""
     n = a.shape[0]
     chunks = min(256, n // _ROWS_PER_CHUNK)
+    if 1 < chunks < 32:
+        # a few 64K-row chunks leave too few tiles for 256 CUs: 2K-row chunks
+        # (r06, GCN on the 232,965-row graph: the 602 x 128 weight gradient
+        # 0.83 -> 0.34 ms, the 128 x 41 one 0.42 -> 0.06 ms against torch's
+        # unsplit GEMM; tools/gemm_probe.py, profiles/r06/gemm_probe_splitk.json)
+        chunks = min(256, n // _SMALL_ROWS_PER_CHUNK)
     if chunks <= 1:
         # below two 64K-row chunks: 2K-row chunks, so a small output still gets
         # workgroups (Pubmed's 19,717 x 500 -> 64 x 500 weight gradient ran on
@@ -101,6 +107,34 @@ class _NodeLinearFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = _given_colsum(ctx, dy)
         return dx, dw, db
+
+
+class _DenseMMFn(torch.autograd.Function):
+    """x·w (w: in x out, the GCN layer's weight layout) whose weight gradient
+    xᵀ·dy is the split-K product (_splitk_tn) instead of autograd's one GEMM
+    with K = the node count (too few output tiles to fill the chip)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return torch.mm(x, w)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = dy.mm(w.t()) if ctx.needs_input_grad[0] else None
+        dw = _splitk_tn(x.contiguous(), dy) if ctx.needs_input_grad[1] else None
+        return dx, dw
+
+
+def dense_mm(x, w):
+    """``torch.mm(x, w)`` for node-row inputs, with the weight gradient over
+    the node dimension split into row chunks (summed in chunk order; fp32
+    summation tolerance against torch's)."""
+    if x.dim() != 2 or w.dim() != 2 or not (x.requires_grad or w.requires_grad):
+        return torch.mm(x, w)
+    return _DenseMMFn.apply(x, w)
 
 
 class _BiasAddFn(torch.autograd.Function):

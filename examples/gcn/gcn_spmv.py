@@ -24,7 +24,7 @@ import dgl  # noqa: E402
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph  # noqa: E402
 from dgl.data import load_data  # noqa: E402
-from dgl.nn.pytorch import bias_add  # noqa: E402
+from dgl.nn.pytorch import bias_add, dense_mm  # noqa: E402
 
 
 class GCNLayer(nn.Module):
@@ -43,7 +43,9 @@ class GCNLayer(nn.Module):
     def forward(self, h):
         if self.dropout is not None:
             h = self.dropout(h)
-        h = torch.mm(h, self.weight)          # dense Linear: MFMA via torch/hipBLASLt
+        # dense Linear: MFMA via torch/hipBLASLt; its weight gradient split
+        # over row chunks (one GEMM with K = 232,965 filled 20 of 256 CUs)
+        h = dense_mm(h, self.weight)
         h = h * self.g.ndata["norm"]          # source-degree normalisation
         self.g.ndata["h"] = h
         self.g.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))  # g-SpMM

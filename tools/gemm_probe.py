@@ -65,6 +65,22 @@ def main():
              "host_us rgcn h@W": host_us(lambda: torch.mm(hr, wr)),
              "host_us small 64x64": host_us(lambda: torch.mm(sm, sm))}
         res[lib] = r
+    # the weight gradients as split-K batched GEMMs (row chunks, partials summed)
+    def splitk(a, b, chunks):
+        n = a.shape[0]
+        k = n // chunks
+        m = k * chunks
+        out = torch.bmm(a[:m].reshape(chunks, k, a.shape[1]).transpose(1, 2),
+                        b[:m].reshape(chunks, k, b.shape[1])).sum(0)
+        if m < n:
+            out = out + a[m:].t().matmul(b[m:])
+        return out
+    torch.backends.cuda.preferred_blas_library("cublaslt")
+    sk = {}
+    for c in (8, 16, 32, 64, 128, 256):
+        sk["dw1 chunks %d" % c] = ms(lambda: splitk(x, da1, c))
+        sk["dw2 chunks %d" % c] = ms(lambda: splitk(h1, da2, c))
+    res["splitk_hipblaslt"] = sk
     print(json.dumps(res, indent=1))
 
 
