@@ -102,6 +102,8 @@ SweepPolicy& sweep_ref() {
     if (tm) q.accum_table_min = std::max<int64_t>(0, std::atoll(tm));
     const char* ms = std::getenv("DGLHIP_SWEEP_ACCUM_MIN_SLOTS");
     if (ms) q.accum_min_slots = std::max<int64_t>(0, std::atoll(ms));
+    const char* bb = std::getenv("DGLHIP_SWEEP_BLOCK_BYTES");  // a study knob
+    if (bb && std::atoll(bb) >= (int64_t(1) << 20)) q.block_bytes = std::atoll(bb);
     return q;
   }();
   return p;
