@@ -177,3 +177,28 @@ def test_sage_dense_matches_unfused(dims):
                                        rtol=1e-5, atol=1e-5)
     finally:
         L._ROWS_PER_CHUNK = old
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("n,k,m", [(232965, 41, 24), (20000, 64, 41), (3000, 16, 8), (100, 8, 4)])
+def test_dense_mm_splitk_weight_gradient(device, n, k, m):
+    """nn.pytorch.dense_mm: torch.mm's value; its weight gradient xᵀ·dy
+    summed over 2K-row chunks (the split-K product) within 1e-5 of float64
+    per element, relative to Σ|x·dy| (the chunking only reassociates)."""
+    from dgl.nn.pytorch import dense_mm
+    if device == "cuda" and not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    gen = torch.Generator().manual_seed(n + k)
+    x = torch.randn(n, k, generator=gen).to(device).requires_grad_(True)
+    w = torch.randn(k, m, generator=gen).to(device).requires_grad_(True)
+    dy = torch.randn(n, m, generator=gen).to(device)
+    y = dense_mm(x, w)
+    assert torch.equal(y.detach(), torch.mm(x.detach(), w.detach()))
+    y.backward(dy)
+    x64, dy64 = x.detach().double().cpu(), dy.double().cpu()
+    want = x64.t() @ dy64
+    bound = x64.abs().t() @ dy64.abs()
+    err = (w.grad.double().cpu() - want).abs()
+    assert bool((err <= 1e-5 * bound + 1e-30).all()), float((err / (bound + 1e-30)).max())
+    wdx = dy64 @ w.detach().double().cpu().t()
+    assert torch.allclose(x.grad.double().cpu(), wdx, rtol=1e-4, atol=1e-4)
