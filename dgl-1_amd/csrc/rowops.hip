@@ -103,6 +103,69 @@ __global__ __launch_bounds__(kThreads) void div_rows_tiled_kernel(
   }
 }
 
+// The node-row epilogue of a GCN layer after its aggregation (r06):
+//   out = act(x * row_scale[r] + bias), act = ReLU or none,
+// the value of torch's `x * norm`, `+ bias`, `relu` (each rounding once, in
+// that order; ReLU as torch's clamp_min: NaN kept, max(v, 0) otherwise), in
+// one pass instead of three. Its backward, one pass: d_pre = out <= 0 ? 0 :
+// dout (torch's threshold_backward on the ReLU's result) or dout, dx = d_pre *
+// row_scale[r], and each workgroup's column sums of d_pre over its rows (in
+// row order) for the bias gradient.
+__global__ __launch_bounds__(kThreads) void node_epilogue_fwd_kernel(
+    int64_t total, int64_t F, const float* __restrict__ x, const float* __restrict__ row_scale,
+    const float* __restrict__ bias, int relu, float* __restrict__ out) {
+#pragma clang fp contract(off)
+  for (int64_t i = block_linear() * kThreads + threadIdx.x; i < total;
+       i += int64_t(gridDim.x) * gridDim.y * kThreads) {
+    const int64_t r = i / F, f = i - r * F;
+    float v = x[i];
+    if (row_scale) v = v * row_scale[r];
+    if (bias) v = v + bias[f];
+    if (relu) v = __builtin_isnan(v) ? v : fmaxf(v, 0.0f);
+    out[i] = v;
+  }
+}
+
+constexpr int kEpiRows = 128;  // rows per workgroup of the backward (one column sum each)
+
+template <int CPT>
+__global__ __launch_bounds__(kThreads) void node_epilogue_bwd_kernel(
+    int64_t n, int64_t F, const float* __restrict__ dout, const float* __restrict__ out,
+    const float* __restrict__ row_scale, int relu, float* __restrict__ dx,
+    float* __restrict__ col_partial) {
+#pragma clang fp contract(off)
+  const int64_t part = block_linear();
+  const int64_t r0 = part * kEpiRows;
+  if (r0 >= n) return;
+  const int64_t r1 = r0 + kEpiRows < n ? r0 + kEpiRows : n;
+  float acc[CPT];
+  int64_t col[CPT];
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    acc[c] = 0.0f;
+    col[c] = threadIdx.x + int64_t(c) * blockDim.x;
+  }
+#pragma unroll 8
+  for (int64_t r = r0; r < r1; ++r) {
+    const float sc = row_scale ? row_scale[r] : 1.0f;
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      if (col[c] < F) {
+        const int64_t i = r * F + col[c];
+        float d = dout[i];
+        if (relu) d = out[i] <= 0.0f ? 0.0f : d;
+        acc[c] = acc[c] + d;
+        dx[i] = row_scale ? d * sc : d;
+      }
+    }
+  }
+  if (col_partial) {
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+      if (col[c] < F) col_partial[part * F + col[c]] = acc[c];
+  }
+}
+
 }  // namespace
 
 }  // namespace dglhip
@@ -141,6 +204,48 @@ int dglhip_div_rows_device(int64_t num_rows, int64_t feat_len, const float* x, i
                        ldx, divisor, out, ldo);
   }
   DGLHIP_CHECK(hipGetLastError() == hipSuccess, "row division launch failed");
+  API_END();
+}
+
+int64_t dglhip_node_epilogue_parts(int64_t num_rows) {
+  return num_rows > 0 ? (num_rows + kEpiRows - 1) / kEpiRows : 0;
+}
+
+int dglhip_node_epilogue_fwd_device(int64_t num_rows, int64_t feat_len, const float* x,
+                                    const float* row_scale, const float* bias, int relu,
+                                    float* out, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 1, "bad sizes");
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(x && out, "null pointer argument");
+  const int64_t total = num_rows * feat_len;
+  const int64_t blocks = std::min<int64_t>((total + kThreads - 1) / kThreads, int64_t(1) << 20);
+  hipLaunchKernelGGL(node_epilogue_fwd_kernel, grid_1d(blocks), dim3(kThreads), 0, stream,
+                     total, feat_len, x, row_scale, bias, relu, out);
+  DGLHIP_CHECK(hipGetLastError() == hipSuccess, "node epilogue launch failed");
+  API_END();
+}
+
+int dglhip_node_epilogue_bwd_device(int64_t num_rows, int64_t feat_len, const float* dout,
+                                    const float* out, const float* row_scale, int relu,
+                                    float* dx, float* col_partial, void* stream_) {
+  API_BEGIN();
+  hipStream_t stream = static_cast<hipStream_t>(stream_);
+  DGLHIP_CHECK(num_rows >= 0 && feat_len >= 1 && feat_len <= 4 * kThreads,
+               "1.." << 4 * kThreads << " columns, got " << feat_len);
+  if (num_rows == 0) return 0;
+  DGLHIP_CHECK(dout && dx && (!relu || out), "null pointer argument");
+  const int64_t parts = dglhip_node_epilogue_parts(num_rows);
+  const int cpt = feat_len <= kThreads ? 1 : (feat_len <= 2 * kThreads ? 2 : 4);
+#define DGLHIP_EPI(C)                                                                        \
+  hipLaunchKernelGGL(node_epilogue_bwd_kernel<C>, grid_1d(parts), dim3(kThreads), 0, stream, \
+                     num_rows, feat_len, dout, out, row_scale, relu, dx, col_partial)
+  if (cpt == 1) DGLHIP_EPI(1);
+  else if (cpt == 2) DGLHIP_EPI(2);
+  else DGLHIP_EPI(4);
+#undef DGLHIP_EPI
+  DGLHIP_CHECK(hipGetLastError() == hipSuccess, "node epilogue backward launch failed");
   API_END();
 }
 

@@ -25,7 +25,7 @@ import torch.nn as nn
 
 from ..._handoff import GradHandoff, is_output, output_ref, take
 
-__all__ = ["NodeLinear", "sage_dense", "bias_add", "dense_mm"]
+__all__ = ["NodeLinear", "sage_dense", "bias_add", "dense_mm", "node_epilogue"]
 
 _ROWS_PER_CHUNK = 1 << 16
 _SMALL_ROWS_PER_CHUNK = 1 << 11
@@ -126,6 +126,67 @@ class _DenseMMFn(torch.autograd.Function):
         dx = dy.mm(w.t()) if ctx.needs_input_grad[0] else None
         dw = _splitk_tn(x.contiguous(), dy) if ctx.needs_input_grad[1] else None
         return dx, dw
+
+
+class _NodeEpilogueFn(torch.autograd.Function):
+    """act(x * row_scale + bias) in one pass each way (rowops.hip,
+    dglhip_node_epilogue_*): the bits of torch's three operations; the bias
+    gradient from the backward kernel's per-128-row column sums, summed in
+    order."""
+
+    @staticmethod
+    def forward(ctx, x, row_scale, bias, relu):
+        from ... import _ffi, kernel
+        n, F = x.shape
+        out = torch.empty_like(x)
+        _ffi.check_call(_ffi.LIB.dglhip_node_epilogue_fwd_device(
+            n, F, _ffi.ptr(x), _ffi.ptr(row_scale), _ffi.ptr(bias), 1 if relu else 0,
+            _ffi.ptr(out), kernel._stream_of(x.device)))
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(out if relu else None, row_scale)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from ... import _ffi, kernel
+        out, row_scale = ctx.saved_tensors
+        dout = dout.contiguous()
+        n, F = dout.shape
+        dx = torch.empty_like(dout)
+        parts = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            parts = torch.empty(max(int(_ffi.LIB.dglhip_node_epilogue_parts(n)), 1), F,
+                                dtype=torch.float32, device=dout.device)
+        _ffi.check_call(_ffi.LIB.dglhip_node_epilogue_bwd_device(
+            n, F, _ffi.ptr(dout), _ffi.ptr(out), _ffi.ptr(row_scale), 1 if ctx.relu else 0,
+            _ffi.ptr(dx), _ffi.ptr(parts), kernel._stream_of(dout.device)))
+        db = parts.sum(0) if parts is not None else None
+        return dx, None, db, None
+
+
+def node_epilogue(x, row_scale=None, bias=None, activation=None):
+    """``activation(x * row_scale + bias)`` over node rows (the GCN layer's
+    destination normalisation, bias and ReLU after its aggregation):
+    ``row_scale`` (n,) or (n, 1), not differentiated; ``bias`` (F,);
+    ``activation`` None or ReLU. On a ROCm device one kernel forward and one
+    backward with the same forward bits and input gradient as the three torch
+    operations (the bias gradient within fp32 summation tolerance); otherwise
+    those operations."""
+    relu = activation in (torch.relu, torch.nn.functional.relu)
+    fused = (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and
+             (activation is None or relu) and x.shape[1] <= 1024 and
+             (row_scale is None or (row_scale.numel() == x.shape[0] and
+                                    row_scale.dtype == torch.float32)) and
+             (bias is None or (bias.dim() == 1 and bias.numel() == x.shape[1] and
+                               bias.dtype == torch.float32)))
+    if not fused:
+        h = x if row_scale is None else x * row_scale.reshape(-1, 1)
+        if bias is not None:
+            h = bias_add(h, bias)
+        return activation(h) if activation else h
+    rs = None if row_scale is None else row_scale.detach().reshape(-1).contiguous()
+    return _NodeEpilogueFn.apply(x.contiguous(), rs, bias, relu)
 
 
 def dense_mm(x, w):

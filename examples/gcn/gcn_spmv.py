@@ -24,7 +24,7 @@ import dgl  # noqa: E402
 import dgl.function as fn  # noqa: E402
 from dgl import DGLGraph  # noqa: E402
 from dgl.data import load_data  # noqa: E402
-from dgl.nn.pytorch import bias_add, dense_mm  # noqa: E402
+from dgl.nn.pytorch import dense_mm, node_epilogue  # noqa: E402
 
 
 class GCNLayer(nn.Module):
@@ -50,12 +50,9 @@ class GCNLayer(nn.Module):
         self.g.ndata["h"] = h
         self.g.update_all(fn.copy_src(src="h", out="m"), fn.sum(msg="m", out="h"))  # g-SpMM
         h = self.g.ndata.pop("h")
-        h = h * self.g.ndata["norm"]          # destination-degree normalisation
-        if self.bias is not None:
-            h = bias_add(h, self.bias)        # h + bias; its gradient a chunked column sum
-        if self.activation:
-            h = self.activation(h)
-        return h
+        # destination-degree normalisation, + bias, activation: one pass each
+        # way on the device (the bits of `h * norm`, `+ bias`, `relu`)
+        return node_epilogue(h, self.g.ndata["norm"], self.bias, self.activation)
 
 
 class GCN(nn.Module):

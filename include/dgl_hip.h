@@ -400,6 +400,21 @@ int64_t dglhip_node_linear_dgrad_workspace_floats(int64_t in_feats);
  * [feat_len, ldo) may be overwritten (with zeros). */
 int dglhip_div_rows_device(int64_t num_rows, int64_t feat_len, const float* x, int64_t ldx,
                            const float* divisor, float* out, int64_t ldo, void* stream);
+/* The node-row epilogue of a GCN layer after its aggregation (r06): out =
+ * act(x * row_scale[r] + bias[f]) over num_rows x feat_len packed rows,
+ * act = ReLU (relu = 1; torch's clamp_min: NaN kept) or none, each operation
+ * rounded as torch's separate `*`, `+` and relu; row_scale / bias may be
+ * NULL. Backward: d_pre = relu ? (out <= 0 ? 0 : dout) : dout, dx = d_pre *
+ * row_scale[r], and col_partial[p, f] = the sum of d_pre over rows [128 p,
+ * 128 p + 128) in row order (dglhip_node_epilogue_parts(num_rows) parts; NULL:
+ * not wanted): the bias gradient is their sum over p. */
+int64_t dglhip_node_epilogue_parts(int64_t num_rows);
+int dglhip_node_epilogue_fwd_device(int64_t num_rows, int64_t feat_len, const float* x,
+                                    const float* row_scale, const float* bias, int relu,
+                                    float* out, void* stream);
+int dglhip_node_epilogue_bwd_device(int64_t num_rows, int64_t feat_len, const float* dout,
+                                    const float* out, const float* row_scale, int relu,
+                                    float* dx, float* col_partial, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* Weighted softmax cross-entropy over node rows (csrc/node_loss.hip): the   */

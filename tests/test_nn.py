@@ -202,3 +202,45 @@ def test_dense_mm_splitk_weight_gradient(device, n, k, m):
     assert bool((err <= 1e-5 * bound + 1e-30).all()), float((err / (bound + 1e-30)).max())
     wdx = dy64 @ w.detach().double().cpu().t()
     assert torch.allclose(x.grad.double().cpu(), wdx, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("F", [128, 41, 300])
+@pytest.mark.parametrize("relu", [True, False])
+def test_node_epilogue_bits_of_torch(F, relu):
+    """nn.pytorch.node_epilogue on the device (one kernel each way) against
+    torch's `x * norm`, `+ bias`, `relu` on the same device: the output and
+    the input gradient bit for bit (zeros, -0.0, NaN and rows of scale 0
+    included), the bias gradient within 1e-5 of Σ|d_pre|."""
+    from dgl.nn.pytorch import node_epilogue
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm device")
+    dev = torch.device("cuda", 0)
+    gen = torch.Generator().manual_seed(F)
+    n = 5000
+    x = torch.randn(n, F, generator=gen)
+    x[0, :4] = torch.tensor([0.0, -0.0, float("nan"), 1e-30])
+    norm = torch.rand(n, 1, generator=gen)
+    norm[7] = 0.0
+    bias = torch.randn(F, generator=gen)
+    dout = torch.randn(n, F, generator=gen)
+    act = torch.nn.functional.relu if relu else None
+    res = []
+    for fused in (True, False):
+        x1 = x.to(dev).requires_grad_(True)
+        b1 = bias.to(dev).requires_grad_(True)
+        nd = norm.to(dev)
+        if fused:
+            out = node_epilogue(x1, nd, b1, act)
+        else:
+            out = x1 * nd + b1
+            out = act(out) if act else out
+        out.backward(dout.to(dev))
+        res.append((out.detach().cpu(), x1.grad.cpu(), b1.grad.cpu()))
+    (o1, g1, b1g), (o2, g2, b2g) = res
+    assert torch.equal(o1.nan_to_num(7.0), o2.nan_to_num(7.0))
+    assert torch.equal(torch.signbit(o1), torch.signbit(o2))
+    assert torch.equal(g1.nan_to_num(7.0), g2.nan_to_num(7.0))
+    d_pre = torch.where(o2 > 0, dout, torch.zeros(())) if relu else dout
+    bound = d_pre.double().abs().sum(0)
+    assert bool(((b1g.double() - b2g.double()).abs() <= 1e-5 * bound + 1e-30).all())
