@@ -798,6 +798,17 @@ struct RunArgs {
 
 enum Path { PATH_HOST = 0, PATH_ROWS = 1, PATH_BLOCKED = 2, PATH_MAX_BLOCKED = 3, PATH_SWEEP = 4 };
 
+// mean_add on the blocked schedule (DGLHIP_BLOCKED_MEAN_ADD;
+// dglhip_set_blocked_mean_add). Off by default: built late in r06 and not yet
+// measured on the box (the GPU pool was unavailable), so the one-launch
+// schedule stays the default until its bits and time are checked.
+int g_blocked_mean_add = [] {
+  const char* e = std::getenv("DGLHIP_BLOCKED_MEAN_ADD");
+  return e && *e ? std::atoi(e) : 0;
+}();
+
+inline bool blocked_mean_add() { return g_blocked_mean_add != 0; }
+
 struct Decision {
   Path path = PATH_ROWS;
   std::shared_ptr<BlockedPlan> bp;
@@ -808,7 +819,10 @@ struct Decision {
   int64_t split = 0;
   // workspace pieces (bytes, 256-B aligned offsets)
   int64_t ws_pad = 0, ws_vals = 0, ws_map = 0, ws_partial = 0;
-  int64_t total() const { return ws_pad + ws_vals + ws_map + ws_partial; }
+  // mean_add on the blocked schedule: the running sums' own rows (out holds
+  // the value the mean is added to)
+  int64_t ws_sums = 0;
+  int64_t total() const { return ws_pad + ws_vals + ws_map + ws_partial + ws_sums; }
 };
 
 inline int64_t align256(int64_t b) { return (b + 255) / 256 * 256; }
@@ -870,10 +884,18 @@ Decision decide(SpmmPlan& plan, const RunArgs& a, hipStream_t s) {
       return d;
     }
   }
-  if (sumlike && a.ufeat && ((cu && !a.efeat) || (a.msg == DGLHIP_MSG_U_MUL_E && a.efeat))) {
+  // out + mean (GraphSAGE's narrowing layer, kernel.gspmm_mean_add): the
+  // blocked chains run into rows of their own, then one pass adds sum / deg
+  // to out (r06: the same bits as the one-launch store, 3.4 -> ~2.1 ms at F = 41
+  // on the headline graph)
+  const bool mean_add = blocked_mean_add() && a.red == DGLHIP_REDUCE_MEAN_ACCUM &&
+                        a.msg == DGLHIP_MSG_COPY_U && !a.efeat;
+  if ((sumlike || mean_add) && a.ufeat &&
+      ((cu && !a.efeat) || (a.msg == DGLHIP_MSG_U_MUL_E && a.efeat))) {
     d.bp = plan.blocked(ld_in * elem, p.block_bytes, s);
     if (d.bp) {
       d.path = PATH_BLOCKED;
+      if (mean_add) d.ws_sums = align256(plan.num_rows() * a.F * 4);
       if (!strided && fp32u && pad_rows(p, a.msg, DGLHIP_REDUCE_SUM, a.F, a.urows)) {
         d.pad = true;
         d.ld = padded_width(a.F);
@@ -990,8 +1012,10 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
   if (d.path == PATH_BLOCKED) {
     BlockedPlan& bp = *d.bp;
     const bool first_writes = a.red != DGLHIP_REDUCE_SUM_ACCUM;
+    // mean_add: the chains in their own rows, added to out at the end
+    float* sums = d.ws_sums ? reinterpret_cast<float*>(ws.take(d.ws_sums)) : a.out;
     if (first_writes && bp.n_absent)
-      plan_zero_rows_device(bp.n_absent, bp.absent.data<int32_t>(), a.F, a.out, s);
+      plan_zero_rows_device(bp.n_absent, bp.absent.data<int32_t>(), a.F, sums, s);
     const float* ev = nullptr;     // edge values in plan order (scalar weights)
     const int64_t* erows = nullptr;  // or their rows per plan slot
     if (a.msg == DGLHIP_MSG_U_MUL_E) {
@@ -1025,7 +1049,7 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
         DGLHIP_CHECK(dglhip_gspmm_pair_items_device(
                          it.n_items, a.F, ldk, a.urows, it.rows.data<int32_t>(),
                          it.ptr.data<int64_t>(), (i == 0 && first_writes) ? 0 : 1,
-                         bp.indices.data<int32_t>(), static_cast<const float*>(uf), a.out,
+                         bp.indices.data<int32_t>(), static_cast<const float*>(uf), sums,
                          s) == 0,
                      DGLGetLastError());
         continue;
@@ -1035,11 +1059,12 @@ void run_planned(SpmmPlan& plan, const RunArgs& a, const Decision& d, void* work
                        (i == 0 && first_writes) ? 0 : 1, bp.indices.data<int32_t>(),
                        ev ? nullptr : erows, static_cast<const float*>(uf), ldk,
                        ev ? ev : (a.msg == DGLHIP_MSG_U_MUL_E ? a.efeat : nullptr),
-                       elen, a.out, s) == 0,
+                       elen, sums, s) == 0,
                    DGLGetLastError());
     }
     if (a.red == DGLHIP_REDUCE_MEAN) plan_div_degree_device(plan.num_rows(), a.F, plan.indptr(),
                                                             a.out, s);
+    if (d.ws_sums) plan_add_mean_device(plan.num_rows(), a.F, plan.indptr(), sums, a.out, s);
     return;
   }
   if (d.path == PATH_MAX_BLOCKED) {
@@ -1168,6 +1193,12 @@ int spmm_plan_path(SpmmPlan& plan, int msg, int red, int64_t F, int64_t ldu, int
 using namespace dglhip;
 
 extern "C" {
+
+int dglhip_set_blocked_mean_add(int on) {
+  const int old = g_blocked_mean_add;
+  g_blocked_mean_add = on ? 1 : 0;
+  return old;
+}
 
 int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
                               int max_spin, int64_t accum_table_min, int64_t accum_min_slots,

@@ -306,5 +306,9 @@ void plan_pad_rows_device(int64_t n, int64_t F, int64_t ld, const float* src, fl
 // out[r, f] = out[r, f] / max(deg r, 1) (IEEE division, torch.div's bits)
 void plan_div_degree_device(int64_t R, int64_t F, const int64_t* indptr, float* out,
                             hipStream_t s);
+// out[r, f] = out[r, f] + sums[r, f] / deg r (division when deg > 1) for rows
+// with in-edges: the blocked schedule's mean_add (DGLHIP_REDUCE_MEAN_ACCUM)
+void plan_add_mean_device(int64_t R, int64_t F, const int64_t* indptr, const float* sums,
+                          float* out, hipStream_t s);
 
 }  // namespace dglhip

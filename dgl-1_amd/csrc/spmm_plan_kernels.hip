@@ -207,6 +207,26 @@ __global__ __launch_bounds__(256) void div_degree_kernel(int64_t R, int64_t F,
   for (int64_t f = threadIdx.x & 63; f < F; f += 64) o[f] = o[f] / div;
 }
 
+// out[r] = out[r] + sums[r] / deg r for rows with in-edges (the one-launch
+// mean_add store: the chain, divided when deg > 1, added to out; rows without
+// in-edges keep out)
+__global__ __launch_bounds__(256) void add_mean_kernel(int64_t R, int64_t F,
+                                                       const int64_t* __restrict__ indptr,
+                                                       const float* __restrict__ sums,
+                                                       float* __restrict__ out) {
+  const int64_t r = block_linear() * 4 + (threadIdx.x >> 6);
+  if (r >= R) return;
+  const int64_t d = indptr[r + 1] - indptr[r];
+  if (d == 0) return;
+  const float div = static_cast<float>(d);
+  const float* sr = sums + r * F;
+  float* o = out + r * F;
+  for (int64_t f = threadIdx.x & 63; f < F; f += 64) {
+    const float m = d > 1 ? sr[f] / div : sr[f];
+    o[f] = o[f] + m;
+  }
+}
+
 // rows of F floats into rows padded to ld floats (the plan's line-aligned
 // copy of a narrow source table): element-parallel, reads in order. (A 2-D
 // hipMemcpy2DAsync of the same rows ran at ~0.25 TB/s: 155 us for F = 41 on
@@ -304,6 +324,13 @@ void plan_div_degree_device(int64_t R, int64_t F, const int64_t* indptr, float* 
   if (R == 0 || F == 0) return;
   hipLaunchKernelGGL(div_degree_kernel, wave_grid(R), dim3(256), 0, s, R, F, indptr, out);
   check_launch("plan mean division");
+}
+
+void plan_add_mean_device(int64_t R, int64_t F, const int64_t* indptr, const float* sums,
+                          float* out, hipStream_t s) {
+  if (R == 0 || F == 0) return;
+  hipLaunchKernelGGL(add_mean_kernel, wave_grid(R), dim3(256), 0, s, R, F, indptr, sums, out);
+  check_launch("plan mean addition");
 }
 
 }  // namespace dglhip

@@ -108,6 +108,7 @@ def _load():
         "dglhip_relation_groups_workspace_bytes": (_c_i64, [_c_i64, _c_i64]),
         "dglhip_relation_groups_device": (_c_int, [_c_i64] * 3 + [_vp] * 4 + [_c_i64] +
                                           [_vp] * 7 + [_c_i64, _vp]),
+        "dglhip_set_blocked_mean_add": (_c_int, [_c_int]),
         "dglhip_node_epilogue_parts": (_c_i64, [_c_i64]),
         "dglhip_node_epilogue_fwd_device": (_c_int, [_c_i64, _c_i64, _vp, _vp, _vp, _c_int, _vp,
                                                      _vp]),

@@ -7,6 +7,8 @@ runtime/degree_bucketing.py:13-84); every check here is against
 (a sum of two terms is the same either way round), forward and backward, on
 every schedule the mean takes: one wave per row, the heavy-row split, the
 short-row tiers and the padded-stride gather, and on the host path."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -130,3 +132,44 @@ def test_sage_dense_add_into_equals_sum(monkeypatch):
         assert len(calls) == (1 if agg is aggregate else 0)
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(os.environ.get("DGLHIP_TEST_BLOCKED_MEAN_ADD", "0") in ("", "0"),
+                    reason="blocked mean_add is off by default until measured on the box "
+                           "(DGLHIP_TEST_BLOCKED_MEAN_ADD=1 runs it)")
+@pytest.mark.parametrize("F,strided", [(41, False), (41, True), (128, False), (16, False)])
+def test_mean_add_blocked_schedule(F, strided):
+    """mean_add on the source-blocked schedule (r06: the chains in rows of
+    their own, sum / deg added to out at the end): the plan takes the blocked
+    path, and values and gradients equal the unfused out + mean bit for bit
+    (padded F = 41 copies, a row-padded view read in place, empty rows)."""
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(11 + F)
+    n = 60_000
+    # uniform rows (a hub row past the heavy-row threshold keeps the one-launch
+    # schedule), some rows empty
+    row, col = _graph(rng, n, 1_500_000, skew=False)
+    keep = row % 17 != 0
+    row, col = row[keep], col[keep]
+    o = np.lexsort((row.numpy(), col.numpy()))  # source-major edge numbering
+    row, col = row[o], col[o]
+    from dgl._ffi import LIB
+    old_knob = LIB.dglhip_set_blocked_mean_add(1)
+    with kernel.scheduled(block_table_min=0, block_bytes=1 << 20, block_min_row_bytes=0,
+                          block_min_slots=1):
+        adj = kernel.from_coo(n, n, row.to(dev), col.to(dev), kernel.ORDER_EID, dev)
+        gen = torch.Generator().manual_seed(F)
+        h = (torch.rand(n, F, generator=gen) * 2 - 1).to(dev)
+        base = torch.randn(n, F, generator=gen).to(dev)
+        if strided:
+            hp = torch.zeros(n, 48, device=dev)
+            hp[:, :F] = h
+            h = hp[:, :F]
+        ldu = h.stride(0) if strided else 0
+        path, launches = adj.fwd.plan.schedule(kernel.MSG_COPY_U, kernel.RED_MEAN_ACCUM, F, ldu, n)
+        try:
+            assert path == kernel.PLAN_PATH_BLOCKED and launches > 1
+            _check(adj, h, base, dev)
+        finally:
+            LIB.dglhip_set_blocked_mean_add(old_knob)
