@@ -799,12 +799,13 @@ struct RunArgs {
 enum Path { PATH_HOST = 0, PATH_ROWS = 1, PATH_BLOCKED = 2, PATH_MAX_BLOCKED = 3, PATH_SWEEP = 4 };
 
 // mean_add on the blocked schedule (DGLHIP_BLOCKED_MEAN_ADD;
-// dglhip_set_blocked_mean_add). Off by default: built late in r06 and not yet
-// measured on the box (the GPU pool was unavailable), so the one-launch
-// schedule stays the default until its bits and time are checked.
+// dglhip_set_blocked_mean_add). On by default since r06's box check: same
+// bits as the one-launch schedule, GraphSAGE-mean Reddit-shaped epoch
+// 15.4 -> 14.2 ms (profiles/r06/sage_blocked_mean_add/). 0 restores the
+// one-launch schedule.
 int g_blocked_mean_add = [] {
   const char* e = std::getenv("DGLHIP_BLOCKED_MEAN_ADD");
-  return e && *e ? std::atoi(e) : 0;
+  return e && *e ? std::atoi(e) : 1;
 }();
 
 inline bool blocked_mean_add() { return g_blocked_mean_add != 0; }

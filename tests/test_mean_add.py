@@ -7,8 +7,6 @@ runtime/degree_bucketing.py:13-84); every check here is against
 (a sum of two terms is the same either way round), forward and backward, on
 every schedule the mean takes: one wave per row, the heavy-row split, the
 short-row tiers and the padded-stride gather, and on the host path."""
-import os
-
 import numpy as np
 import pytest
 import torch
@@ -135,9 +133,6 @@ def test_sage_dense_add_into_equals_sum(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(os.environ.get("DGLHIP_TEST_BLOCKED_MEAN_ADD", "0") in ("", "0"),
-                    reason="blocked mean_add is off by default until measured on the box "
-                           "(DGLHIP_TEST_BLOCKED_MEAN_ADD=1 runs it)")
 @pytest.mark.parametrize("F,strided", [(41, False), (41, True), (128, False), (16, False)])
 def test_mean_add_blocked_schedule(F, strided):
     """mean_add on the source-blocked schedule (r06: the chains in rows of
