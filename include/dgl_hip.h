@@ -668,8 +668,8 @@ int dglhip_gspmm_sweep_stream_device(int64_t num_rows, int64_t waves_total,
  * (DGLHIP_SWEEP_ACCUM_PER_CU). */
 /* mean_add (DGLHIP_REDUCE_MEAN_ACCUM) on the source-blocked schedule: the
  * chains in workspace rows, sum / deg added to out at the end (the
- * one-launch store's bits); 1 on, 0 the one-launch schedule (the default
- * until measured; env DGLHIP_BLOCKED_MEAN_ADD). Returns the previous setting. */
+ * one-launch store's bits); 1 on (the default), 0 the one-launch schedule
+ * (env DGLHIP_BLOCKED_MEAN_ADD). Returns the previous setting. */
 int dglhip_set_blocked_mean_add(int on);
 int dglhip_set_sweep_schedule(int on, int64_t table_min, int64_t block_bytes, int lag,
                               int max_spin, int64_t accum_table_min, int64_t accum_min_slots,
